@@ -1,0 +1,235 @@
+"""Benchmark: candidate-pose scorings/s of the correlative scan matcher.
+
+Workload (BASELINE.json configs[1]): 1081-beam scans against a 2000x2000
+@5 cm probability grid, full 3-level coarse -> fine -> super-fine search
+(sim-YAML windows: 5,070 + 1,331 + 189 = 6,590 candidate poses per scan), every
+beam summed (use_point_size = 1081 -> B = 1081, the "1081-beam" headline of
+SURVEY.md 8d). One step = the whole 3-level match of a batch of scans that is
+already resident in HBM (grid and points uploaded before the timed region);
+the step includes every device launch, the device->host score copies and the
+host finish (std::sort / FindBestCandidate / covariance) of all windows.
+
+Multi-GPU: one process per GPU; each rank matches its own batch (weak scaling,
+no data-path collective — independent scans). Timing: barrier +
+synchronize on both sides of exactly --steps steps, max over ranks.
+
+Roofline: the dominant kernel's algorithmic bytes (4 B per summed beam per
+candidate) over its HIP-event time, measured live on the stream it runs on.
+cpu_baseline: the oracle (single-threaded restatement of the reference) on a
+bounded sample of the same workload, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "roborts-edu-slam_amd"), os.path.join(ROOT, "oracle")]
+
+import numpy as np  # noqa: E402
+
+METRIC = "candidate-pose scorings/sec (1081-beam scan, 2000×2000 grid) at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(world, batch, levels, seconds: float):
+    """Oracle (test infrastructure, CPU restatement) on a bounded sample."""
+    import pyoracle as O
+    m = O.Map(world.grid, world.resolution, world.offset)
+    eye = np.tile(np.eye(3).reshape(1, 9), (1, 1))
+
+    def run(k0, k1):
+        off = batch.offsets[k0:k1 + 1] - batch.offsets[k0]
+        pts = batch.points_cells[batch.offsets[k0]:batch.offsets[k1]]
+        t = time.perf_counter()
+        O.scan_matchers_batch(m, pts, off, levels, batch.init_poses[k0:k1],
+                              np.tile(eye, (k1 - k0, 1)))
+        return time.perf_counter() - t
+
+    probe = run(0, 2) / 2
+    n = int(max(2, min(batch.offsets.size - 1, seconds / max(probe, 1e-6))))
+    dt = run(0, n)
+    per_scan = sum(_window_cands(l) for l in levels)
+    return {"value": n * per_scan / dt, "unit": "scorings/s", "cores": 1, "kind": "port",
+            "sample": f"{n} scans x 3 levels ({n * per_scan} scorings, {dt:.1f} s) single-threaded "
+                      f"oracle/csm_oracle.cpp on {_cpu_model()}"}
+
+
+def _window_cands(p) -> int:
+    import roborts_csm
+    na, ns = roborts_csm.window_dims(p)
+    return na * ns * ns
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scans", type=int, default=4096, help="scans per GPU per step")
+    ap.add_argument("--levels", choices=["headline", "sim"], default="headline",
+                    help="headline: every beam summed (B=1081); sim: reference YAML U=100 (B=109)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC-derived HBM bytes per launch of the dominant kernel (profiles/)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world_size = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    import torch
+    if world_size > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+
+    import roborts_csm
+    from roborts_csm import worlds
+    from roborts_csm.params import SIM_YAML_LEVELS, headline_levels
+
+    levels = headline_levels() if args.levels == "headline" else SIM_YAML_LEVELS
+    world = worlds.make_world(2000, 2000, 0.05, seed=20261015)
+    batch = worlds.make_scan_batch(world, args.scans, seed=1000 + rank)
+
+    ctx = roborts_csm.Context(local_rank)
+    ctx.set_grid(roborts_csm.ScanMatchMap(world.grid, world.resolution, world.offset, 0, 1))
+    ctx.load_scans(batch.points_cells, batch.offsets)
+    poses0 = np.ascontiguousarray(batch.init_poses)
+    covs0 = np.ascontiguousarray(np.tile(np.eye(3).reshape(1, 9), (args.scans, 1)))
+
+    def step():
+        poses, covs = poses0.copy(), covs0.copy()
+        ctx.scan_matchers_loaded(levels, poses, covs)
+        return poses
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_profiling(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        poses = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    stats = ctx.kernel_stats()
+    ctx.set_profiling(False)
+
+    per_scan = sum(_window_cands(l) for l in levels)
+    local_scorings = float(args.scans * per_scan * args.steps)
+    if dist is not None:
+        t = torch.tensor([elapsed, local_scorings], dtype=torch.float64,
+                         device="cuda" if torch.cuda.is_available() else "cpu")
+        e = t[:1].clone()
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        s = t[1:].clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        elapsed, total_scorings = float(e.item()), float(s.item())
+    else:
+        total_scorings = local_scorings
+
+    # single-scan latency (front-end, config 5 shape): one 3-level match
+    lat = []
+    one_pts = batch.points_cells[batch.offsets[0]:batch.offsets[1]]
+    for _ in range(20):
+        pose = poses0[0].copy()
+        cov = np.eye(3).reshape(9).copy()
+        t = time.perf_counter()
+        ctx.scan_matchers(one_pts, levels, pose, cov)
+        lat.append(time.perf_counter() - t)
+    ctx.load_scans(batch.points_cells, batch.offsets)
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    dom = max(stats, key=lambda s: s["total_ms"])
+    avg_ms = dom["total_ms"] / dom["launches"]
+    bytes_per_launch = dom["algorithmic_bytes"] / dom["launches"]
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    kernel_total_ms = sum(s["total_ms"] for s in stats)
+    kernel_scorings = sum(s["scorings"] for s in stats)
+
+    err = np.hypot(*(poses[:, :2] - batch.true_poses[:, :2]).T)
+    out = {
+        "metric": METRIC,
+        "value": total_scorings / elapsed,
+        "unit": "scorings/s",
+        "n_gpus": world_size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded 2000x2000 @5cm wall map with the reference's blur splat; "
+                "ray-cast 1081-beam Hokuyo scans at distinct poses)",
+        "config": {
+            "workload": "config2: 1081-beam scans vs 2000x2000 @5cm fp32 grid, full 3-level "
+                        "coarse->fine->super-fine (sim-YAML windows 5070+1331+189 candidates/scan)",
+            "levels": args.levels,
+            "beams_summed": 1081 if args.levels == "headline" else 109,
+            "scans_per_gpu": args.scans,
+            "scorings_per_scan": per_scan,
+            "parallelism": f"replicas x{world_size} (scan-sharded, no collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom["name"],
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "avg_launch_ms": avg_ms,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+        },
+        "kernel_scorings_per_s": kernel_scorings / (kernel_total_ms * 1e-3) if kernel_total_ms else None,
+        "kernel_share_of_step": kernel_total_ms * 1e-3 / elapsed,
+        "single_scan_latency_ms": float(np.median(lat) * 1e3),
+        "median_pose_error_m": float(np.median(err)),
+        "kernels": stats,
+    }
+    if not args.no_cpu and world_size == 1:
+        out["cpu_baseline"] = cpu_baseline(world, batch, levels, args.cpu_seconds)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,212 @@
+/*
+ * csm.h — C-ABI of the MI355X-native correlative scan matcher.
+ *
+ * This is the drop-in boundary for RoboRTS-Edu-SLAM's hot path, the
+ * correlative (x, y, theta) search of src/scan_match/correlate_scan_matcher.h.
+ * Plain C: POD structs, raw pointers, sizes and int status codes. No C++
+ * exceptions, no torch or Eigen types cross this boundary.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference repository root):
+ *
+ *   csm_param                 CorrelationScanMatchParam  correlate_scan_matcher.h:41-86
+ *   csm_match_type            CorrelationScanMatchType   correlate_scan_matcher.h:34-39
+ *   csm_map_info              GridMapBase geometry       grid_map_base.h:47-71,307-309,371-378
+ *   csm_set_grid              OccuGridMap cell storage read by GetGridProbValue
+ *                                                        occu_grid_map.h:395-397, grid_map_base.h:352-354
+ *   csm_scan_match            BasedCorrelationScanMatch::ScanMatch
+ *                                                        correlate_scan_matcher.h:784-875
+ *   csm_scan_matchers         ScanMatchers::ScanMatch (3-level coarse->fine->super)
+ *                                                        scan_matchers.h:179-289
+ *   csm_score_window          MultiResolutionCorrelateScanMatcher::ScanMatch enumeration +
+ *                             GetResponse + PenalizeResponse, all candidate scores in
+ *                             reference enumeration order (theta, x, y)
+ *                                                        correlate_scan_matcher.h:516-603,637-662,718-745
+ *   csm_best_window           same scoring, reduced on device to (max score, lowest flat index)
+ *                             (large windows / loop-closure shards; no reference counterpart,
+ *                             SURVEY.md 8e)
+ *   csm_bnb_match             BranchAndBoundCorrelateScanMatcher::ScanMatch (FAST type)
+ *                                                        correlate_scan_matcher.h:274-331
+ *
+ * Threading: every entry point locks the context; a context may be shared by
+ * the front-end (ROS callback) thread and the back-end thread exactly like the
+ * reference's shared ScanMatchers (scan_matchers.h:298, slam_processor.cpp:139,292).
+ *
+ * Error convention: 0 = success. The reference logs and returns 0.0 for an
+ * uninitialised map or an empty scan (correlate_scan_matcher.h:792-795); this ABI
+ * does the same (status CSM_OK, *response = 0.0, pose and covariance untouched).
+ * Any other failure returns a non-zero status and csm_last_error() explains it;
+ * the product never silently falls back to a CPU path.
+ */
+#ifndef ROBORTS_CSM_H
+#define ROBORTS_CSM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CSM_ABI_VERSION 1
+
+enum csm_status {
+  CSM_OK = 0,
+  CSM_ERR_INVALID_ARG = 1,
+  CSM_ERR_HIP = 2,
+  CSM_ERR_NO_GRID = 3,
+  CSM_ERR_ALLOC = 4,
+  CSM_ERR_UNSUPPORTED = 5
+};
+
+/* correlate_scan_matcher.h:34-39 */
+enum csm_match_type {
+  CSM_COARSE = 0,
+  CSM_FINE = 1,
+  CSM_SUPER = 2,
+  CSM_FAST = 3
+};
+
+/* CorrelationScanMatchParam (correlate_scan_matcher.h:41-86). Units as in the
+ * reference: sizes/resolutions in metres, angles in radians. */
+typedef struct csm_param {
+  double search_space_size;        /* full window width (m)                  */
+  double search_space_resolution;  /* window step (m)                        */
+  double search_angle_offset;      /* +/- angle half width (rad)             */
+  double search_angle_resolution;  /* angle step (rad)                       */
+  double response_threshold;       /* pose written back only above this      */
+  int32_t use_point_size;          /* U: beam subsampling target             */
+  int32_t max_depth;               /* BnB depth (FAST type only)             */
+  int32_t use_center_penalty;      /* bool                                   */
+  int32_t type;                    /* enum csm_match_type                    */
+} csm_param;
+
+/* Geometry of a ScanMatchMap (GridMapBase, grid_map_base.h:47-71).
+ * world_to_map = Scaling(1/resolution) * Translation(offset). */
+typedef struct csm_map_info {
+  double resolution;    /* cell length used to build the map (m)             */
+  double offset_x;      /* map_offset_ (m)                                   */
+  double offset_y;
+  int32_t size_x;       /* cells                                             */
+  int32_t size_y;
+  int32_t update_index; /* map_update_index_; < 0 means IsMapInit()==false    */
+  int32_t reserved;
+} csm_map_info;
+
+/* Result of an argmax-only search (csm_best_window). flat_index is in the
+ * reference enumeration order ((theta * n_space + x) * n_space + y); ties are
+ * broken by the lowest flat index. */
+typedef struct csm_best {
+  double score;
+  int64_t flat_index;
+  double x, y, angle;   /* candidate pose in map cells / rad                 */
+} csm_best;
+
+/* Per-kernel accounting collected with HIP events on the context's stream
+ * while profiling is on (csm_set_profiling). algorithmic_bytes counts one
+ * fp32 grid read per summed beam per candidate (4*B bytes per scoring). */
+typedef struct csm_kernel_stat {
+  char name[48];
+  int64_t launches;
+  double total_ms;
+  double algorithmic_bytes;
+  double scorings;
+} csm_kernel_stat;
+
+typedef struct csm_ctx csm_ctx;
+
+/* --- lifetime ---------------------------------------------------------- */
+int csm_create(int device, csm_ctx** out);
+int csm_destroy(csm_ctx* ctx);
+const char* csm_last_error(const csm_ctx* ctx);
+int csm_abi_version(void);
+/* Value read for an endpoint outside the grid. The reference reads out of
+ * bounds (UB, grid_map_base.h:352-354); this ABI defines it. Default 0.3f =
+ * kMapUnknownCellProb (slam/slam_processor.h:264). */
+int csm_set_outside_value(csm_ctx* ctx, float value);
+
+/* --- grid residency ------------------------------------------------------ */
+/* Upload a host grid. cells points at the first cell's probability (float);
+ * cell_stride_bytes is 8 for the reference's AoS ProbabilityCell
+ * {float prob_value_; int update_index_;} (grid_map_cell.h:301-328) and 4 for
+ * a packed float grid. Row-major, index y*size_x + x (grid_map_base.h:352-354).
+ * The device copy is keyed on (cells, stride, size, version): a call with an
+ * unchanged key skips the upload. Pass version = -1 to force the upload. */
+int csm_set_grid(csm_ctx* ctx, const void* cells, int64_t cell_stride_bytes,
+                 const csm_map_info* info, int64_t version);
+/* Borrow a packed float grid that already lives in device memory of this
+ * context's device (size_y * size_x floats). The caller keeps it alive. */
+int csm_set_grid_device(csm_ctx* ctx, const float* device_prob,
+                        const csm_map_info* info);
+
+/* --- window geometry ----------------------------------------------------- */
+/* n_angles = floor(2*offset/ares)+1 (correlate_scan_matcher.h:154),
+ * n_space = Round(size/res)+1 (:538). */
+int csm_window_dims(const csm_param* param, int32_t* n_angles, int32_t* n_space);
+
+/* --- drop-in entry points (host buffers) -------------------------------- */
+/* BasedCorrelationScanMatch::ScanMatch. points_xy: n_points (x, y) pairs in
+ * map-cell units, sensor frame (RangeDataContainer after CreateFrom with the
+ * map's 1/resolution, sensor_data_manager.h:99-115). pose: world (x, y, theta)
+ * in/out. cov: row-major 3x3 in/out (partially written per type, :835-858).
+ * argmax_flat (nullable): enumeration index of the candidate std::sort put
+ * first (-1 when the reference's early return applies). */
+int csm_scan_match(csm_ctx* ctx, const double* points_xy, int32_t n_points,
+                   const csm_param* param, double pose[3], double cov[9],
+                   double* response, int64_t* argmax_flat);
+
+/* ScanMatchers::ScanMatch with use_optimize_scan_match = false (both reference
+ * YAMLs) and the grid already sized by the caller's MapSizeCheck:
+ * levels[0..2] = coarse, fine, super-fine params, all matched on the current
+ * grid (scan_matchers.h:238,249,256). use_fine = false runs only the coarse
+ * level. score = mean of the level responses (:281). */
+int csm_scan_matchers(csm_ctx* ctx, const double* points_xy, int32_t n_points,
+                      const csm_param levels[3], int32_t use_fine,
+                      double pose[3], double cov[9], double* score);
+
+/* Batched forms: n_scans independent scans matched on the same grid in one
+ * pass per level. point_offsets has n_scans+1 entries (prefix offsets in
+ * points). poses n_scans*3, covs n_scans*9, responses n_scans. */
+int csm_scan_match_batch(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
+                         const int64_t* point_offsets, const csm_param* param,
+                         double* poses, double* covs, double* responses,
+                         int64_t* argmax_flat);
+int csm_scan_matchers_batch(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
+                            const int64_t* point_offsets, const csm_param levels[3],
+                            int32_t use_fine, double* poses, double* covs,
+                            double* scores);
+
+/* Device-resident scan sets: csm_load_scans uploads a batch of scans once;
+ * csm_scan_matchers_loaded runs the 3-level driver over it (poses/covs/scores
+ * as in csm_scan_matchers_batch). Any other call that takes host points
+ * replaces the loaded set. */
+int csm_load_scans(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
+                   const int64_t* point_offsets);
+int csm_scan_matchers_loaded(csm_ctx* ctx, const csm_param levels[3], int32_t use_fine,
+                             double* poses, double* covs, double* scores);
+
+/* --- measurement ---------------------------------------------------------- */
+/* Turn HIP-event timing of every scoring launch on/off (resets the stats). */
+int csm_set_profiling(csm_ctx* ctx, int32_t on);
+/* Copy up to capacity stats; *count = number of distinct kernels seen. */
+int csm_kernel_stats(csm_ctx* ctx, csm_kernel_stat* out, int32_t capacity, int32_t* count);
+
+/* --- raw scoring --------------------------------------------------------- */
+/* Every candidate score of one window (after the centre penalty when
+ * param->use_center_penalty), in reference enumeration order. center_map is
+ * the window centre in map cells / rad (GetMapCoordsPose of the world pose).
+ * n_out must equal n_angles * n_space^2. */
+int csm_score_window(csm_ctx* ctx, const double* points_xy, int32_t n_points,
+                     const csm_param* param, const double center_map[3],
+                     double* scores_out, int64_t n_out);
+
+/* Argmax-only scoring of one window: max score, lowest flat index on ties.
+ * Intended for windows far larger than the front end's (loop closure). */
+int csm_best_window(csm_ctx* ctx, const double* points_xy, int32_t n_points,
+                    const csm_param* param, const double center_map[3],
+                    csm_best* best);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ROBORTS_CSM_H */

@@ -1,0 +1,871 @@
+// csm_api.cpp — host side of the C-ABI (include/csm.h).
+//
+// Owns the per-context HIP stream and device buffers, turns reference-style
+// calls into batched device windows (csm_internal.hpp), and performs the
+// reference's host finish: std::sort of the candidates, FindBestCandidate,
+// covariance and the world-pose write-back
+// (correlate_scan_matcher.h:606-611, 670-710, 784-1019).
+//
+// Compiled with g++ -O2 -ffp-contract=off (no -march), like the reference's
+// Release build, so every host double expression rounds as the reference's
+// does. The candidate sort is libstdc++'s std::sort on records compared by
+// score only, fed in the reference's enumeration order: the permutation is a
+// function of the comparison outcomes alone, so ties resolve exactly as in the
+// reference (whose Candidate2D records are 40 bytes, ours 16).
+
+#include "csm.h"
+#include "csm_internal.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+using csm::AngleEntry;
+using csm::BestPartial;
+using csm::LevelWork;
+using csm::ScanWork;
+
+namespace {
+
+constexpr double kMaxVariance = 500.0;      // util/slam_util.h:57
+constexpr double kDoubleTolerance = 1e-06;  // util/slam_util.h:59
+constexpr double kResponseFilterTolerance = 1e-2;  // correlate_scan_matcher.h:763
+constexpr int kMaxVarianceUsePointSize = 20;       // correlate_scan_matcher.h:1033
+
+inline bool double_equal(double a, double b, double tol = kDoubleTolerance) {
+  // util::DoubleEqual (util/slam_util.h:70-73)
+  const double d = a - b;
+  return d < 0.0 ? d >= -std::fabs(tol) : d <= std::fabs(tol);
+}
+
+inline double round_half_away(double v) {  // util::Round (util/slam_util.h:75-77)
+  return v >= 0.0 ? std::floor(v + 0.5) : std::ceil(v - 0.5);
+}
+
+// Map geometry as GridMapBase stores it (grid_map_base.h:47-71,307-309).
+struct Geometry {
+  double scale;   // scale_factor_ = 1.0 / resolution
+  double tx, ty;  // translation of world_to_map_ = scale * offset
+  double mres;    // GetCellLength() = 1 / scale_factor_
+  double inv_a;   // diagonal of map_to_world_ (Eigen 2x2 inverse: s * (1 / (s*s)))
+  explicit Geometry(const csm_map_info& m) {
+    scale = 1.0 / m.resolution;
+    tx = scale * m.offset_x;
+    ty = scale * m.offset_y;
+    mres = 1 / scale;
+    const double det = scale * scale - 0.0 * 0.0;
+    inv_a = scale * (1.0 / det);
+  }
+  // GetMapCoordsPose (grid_map_base.h:89-93)
+  void to_map(const double w[3], double out[3]) const {
+    out[0] = scale * w[0] + tx;
+    out[1] = scale * w[1] + ty;
+    out[2] = w[2];
+  }
+  // GetWorldCoordsPose (grid_map_base.h:83-87)
+  void to_world(const double p[3], double out[3]) const {
+    const double ntx = -(inv_a * tx), nty = -(inv_a * ty);
+    out[0] = inv_a * p[0] + ntx;
+    out[1] = inv_a * p[1] + nty;
+    out[2] = p[2];
+  }
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct HostBuf {  // pinned staging for device->host score copies
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// Window dimensions of one level (correlate_scan_matcher.h:154,538).
+struct Dims {
+  int32_t n_angles = 0, n_space = 0;
+  int64_t n_cand = 0;
+};
+
+int window_dims(const csm_param& P, Dims& d) {
+  if (!(P.search_angle_resolution > 0.0) || !(P.search_space_resolution > 0.0) ||
+      !(P.search_angle_offset >= 0.0) || !(P.search_space_size >= 0.0))
+    return CSM_ERR_INVALID_ARG;
+  // serach_angle_size_ = offset*2 (:526); the LUT gets serach_angle_size_/2 (:536)
+  const double half = (P.search_angle_offset * 2) / 2;
+  const double na = std::floor(half * 2 / P.search_angle_resolution) + 1;
+  const double ns = round_half_away(P.search_space_size / P.search_space_resolution) + 1;
+  if (!(na >= 1.0 && na < 1e7 && ns >= 1.0 && ns < 1e7)) return CSM_ERR_INVALID_ARG;
+  d.n_angles = (int32_t)na;
+  d.n_space = (int32_t)ns;
+  d.n_cand = (int64_t)d.n_angles * d.n_space * d.n_space;
+  return CSM_OK;
+}
+
+// Beam subsampling (correlate_scan_matcher.h:561-566); false if the reference
+// would divide by zero or loop forever (use_point_size <= 1 with n >= 2*U).
+bool beam_rule(int n, int use_point_size, int& step, int& use, int& n_used) {
+  use = use_point_size;
+  if (n < 2 * use) {
+    use = n;
+    step = 1;
+  } else {
+    if (use - 1 <= 0) return false;
+    step = n / (use - 1);
+  }
+  if (step <= 0) return false;
+  n_used = (n + step - 1) / step;
+  return true;
+}
+
+// Host plan of one window (a scan at one level, centred on its current pose).
+struct WindowPlan {
+  double center[3];
+  int step = 1, use = 1, n_used = 0, n_points = 0;
+  double x0 = 0, y0 = 0;
+  int64_t angle_off = 0;
+};
+
+struct Entry {
+  double score;
+  int64_t idx;
+};
+
+// Host finish of one window: everything BasedCorrelationScanMatch::ScanMatch
+// does after the scores exist (correlate_scan_matcher.h:606-611, 670-710,
+// 835-869). scores are in enumeration order, penalty already applied.
+double finish_window(const double* scores, const Dims& D, const WindowPlan& W,
+                     const AngleEntry* angles, const csm_param& P, const Geometry& G,
+                     double pose[3], double cov[9], std::vector<Entry>& e,
+                     int64_t* argmax_flat) {
+  const int64_t n = D.n_cand;
+  e.resize((size_t)n);
+  for (int64_t i = 0; i < n; ++i) e[(size_t)i] = Entry{scores[i], i};
+  std::sort(e.begin(), e.end(), [](const Entry& a, const Entry& b) { return a.score > b.score; });
+  if (argmax_flat) *argmax_flat = e[0].idx;
+
+  const double f = P.search_space_resolution / G.mres;
+  const int64_t ns = D.n_space, nss = ns * ns;
+  auto cand_x = [&](int64_t idx) { return W.x0 + (int)((idx / ns) % ns) * f; };
+  auto cand_y = [&](int64_t idx) { return W.y0 + (int)(idx % ns) * f; };
+  auto cand_a = [&](int64_t idx) { return angles[idx / nss].angle; };
+
+  // FindBestCandidate (:670-710)
+  double best_x = cand_x(e[0].idx), best_y = cand_y(e[0].idx), best_a = cand_a(e[0].idx);
+  const double best_score = e[0].score;
+  {
+    double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;
+    int count = 0;
+    for (size_t i = 0; i < e.size(); ++i) {
+      const double sc = e[i].score;
+      if (!double_equal(sc, best_score, kResponseFilterTolerance)) break;
+      const double cx = cand_x(e[i].idx), cy = cand_y(e[i].idx), ca = cand_a(e[i].idx);
+      ax += cx * sc;
+      ay += cy * sc;
+      thx += std::cos(ca) * sc;
+      thy += std::sin(ca) * sc;
+      ssum += sc;
+      count++;
+    }
+    if (count > 1) {
+      ax /= ssum;
+      ay /= ssum;
+      thx /= ssum;
+      thy /= ssum;
+      best_x = ax;
+      best_y = ay;
+      best_a = std::atan2(thy, thx);
+    }
+  }
+
+  const double sres = P.search_space_resolution;
+  const double max_ang_var = 4 * (P.search_angle_resolution * P.search_angle_resolution);  // :801
+
+  auto positional = [&]() {  // ComputePositionalCovariance (:887-956)
+    for (int i = 0; i < 9; ++i) cov[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    if (best_score < kDoubleTolerance) {
+      cov[0] = kMaxVariance;
+      cov[4] = kMaxVariance;
+      cov[8] = max_ang_var;
+      return;
+    }
+    double vxx = 0.0, vxy = 0.0, vyy = 0.0, norm = 0.0;
+    const double bound = std::min(best_score - 0.1, 0.5);
+    int counter = 0;
+    for (size_t i = 0; i < e.size(); ++i) {
+      const double sc = e[i].score;
+      if (!(sc > bound && counter < kMaxVarianceUsePointSize)) break;
+      const double dx = cand_x(e[i].idx) - best_x, dy = cand_y(e[i].idx) - best_y;
+      norm += sc;
+      vxx += (dx * dx * sc);
+      vxy += (dx * dy * sc);
+      vyy += (dy * dy * sc);
+      counter++;
+    }
+    if (norm > kDoubleTolerance) {
+      double xx = vxx / norm, xy = vxy / norm, yy = vyy / norm;
+      const double r = sres / G.mres;
+      const double minv = 0.1 * (r * r);
+      xx = std::max<double>(xx, minv);
+      yy = std::max<double>(yy, minv);
+      const double m2 = G.mres * G.mres;
+      cov[0] = (xx * m2) / best_score;
+      cov[1] = (xy * m2) / best_score;
+      cov[3] = (xy * m2) / best_score;
+      cov[4] = (yy * m2) / best_score;
+      cov[8] = max_ang_var;
+    }
+    if (double_equal(cov[0], 0.0)) cov[0] = kMaxVariance;
+    if (double_equal(cov[4], 0.0)) cov[4] = kMaxVariance;
+  };
+  auto angular = [&]() {  // ComputeAngularCovariance (:965-1019)
+    if (best_score < kDoubleTolerance) {
+      cov[8] = max_ang_var;
+      return;
+    }
+    const double lin_tol = sres / G.mres;
+    double norm = 0.0, acc = 0.0;
+    const double bound = std::min(best_score - 0.1, 0.5);
+    int counter = 0;
+    for (size_t i = 0; i < e.size(); ++i) {
+      const double sc = e[i].score;
+      if (sc >= bound && counter < kMaxVarianceUsePointSize) {
+        const int64_t idx = e[i].idx;
+        if (double_equal(cand_x(idx), best_x, lin_tol) && double_equal(cand_y(idx), best_y, lin_tol)) {
+          const double d = cand_a(idx) - best_a;
+          norm += sc;
+          acc += (d * d * sc);
+          counter++;
+        }
+      }
+    }
+    cov[8] = (norm > kDoubleTolerance) ? acc / norm : 200 * max_ang_var;
+  };
+  switch (P.type) {
+    case CSM_COARSE:
+      positional();
+      angular();
+      break;
+    case CSM_FINE:
+      positional();
+      break;
+    case CSM_SUPER:
+      angular();
+      break;
+    default:
+      break;
+  }
+  const double response = best_score > 1.0 ? 1.0 : best_score;  // :861-863
+  if (response > P.response_threshold) {                        // :866-869
+    const double bp[3] = {best_x, best_y, best_a};
+    G.to_world(bp, pose);
+  }
+  return response;
+}
+
+template <class F>
+void parallel_for(int n, int threads, F&& fn) {
+  if (threads <= 1 || n <= 1) {
+    for (int i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  threads = std::min(threads, n);
+  std::atomic<int> next{0};
+  std::vector<std::thread> pool;
+  pool.reserve(threads - 1);
+  auto worker = [&]() {
+    for (;;) {
+      const int i = next.fetch_add(1);
+      if (i >= n) break;
+      fn(i);
+    }
+  };
+  for (int t = 0; t < threads - 1; ++t) pool.emplace_back(worker);
+  worker();
+  for (auto& t : pool) t.join();
+}
+
+int pick_cpl(int64_t n_cand) {
+  if (n_cand >= 8192) return 4;
+  if (n_cand >= 1024) return 2;
+  return 1;
+}
+
+}  // namespace
+
+struct csm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  float outside = 0.3f;  // kMapUnknownCellProb (slam/slam_processor.h:264)
+  int host_threads = 1;
+
+  csm_map_info info{};
+  bool has_grid = false;
+  const float* d_grid = nullptr;  // owned (grid_buf) or borrowed
+  DevBuf grid_buf;
+  const void* key_cells = nullptr;
+  int64_t key_stride = 0, key_version = -1;
+  int32_t key_sx = -1, key_sy = -1;
+
+  DevBuf pts, scans, angles, scores, partials, best;
+  HostBuf h_scores;
+  std::vector<float> h_pack;
+
+  // scans made resident by csm_load_scans (offsets relative to pts)
+  int32_t loaded_n = -1;
+  std::vector<int64_t> loaded_off;
+
+  // per-kernel HIP-event timing (csm_set_profiling / csm_kernel_stats)
+  bool profiling = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<csm_kernel_stat> stats;
+  void account(const char* name, float ms, double bytes, double scorings) {
+    for (auto& s : stats)
+      if (std::strncmp(s.name, name, sizeof(s.name)) == 0) {
+        s.launches += 1;
+        s.total_ms += ms;
+        s.algorithmic_bytes += bytes;
+        s.scorings += scorings;
+        return;
+      }
+    csm_kernel_stat s{};
+    std::snprintf(s.name, sizeof(s.name), "%s", name);
+    s.launches = 1;
+    s.total_ms = ms;
+    s.algorithmic_bytes = bytes;
+    s.scorings = scorings;
+    stats.push_back(s);
+  }
+
+  int fail(int code, const std::string& msg) {
+    err = msg;
+    return code;
+  }
+  int hip_fail(hipError_t e, const char* what) {
+    err = std::string(what) + ": " + hipGetErrorString(e);
+    return CSM_ERR_HIP;
+  }
+};
+
+namespace {
+
+// Scores windows_n windows of one level on the device. plans[i] describes
+// window i, pts_dev is the batch's points already resident. When best_out is
+// null, every score is copied back into ctx->h_scores (window-major).
+int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
+                const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
+                const std::vector<AngleEntry>& angles, const std::vector<int32_t>& grid_index,
+                BestPartial* best_out) {
+  const int nw = (int)plans.size();
+  if (nw == 0) return CSM_OK;
+  const int cpl = pick_cpl(D.n_cand);
+  const int64_t per_block = (int64_t)csm::kBlock * cpl;
+  const int64_t bps = (D.n_cand + per_block - 1) / per_block;
+  if (bps * nw > INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
+
+  std::vector<ScanWork> sw((size_t)nw);
+  for (int i = 0; i < nw; ++i) {
+    const WindowPlan& W = plans[(size_t)i];
+    ScanWork& s = sw[(size_t)i];
+    s.pts_off = pt_offsets[(size_t)i];
+    s.angle_off = W.angle_off;
+    s.out_off = (int64_t)i * D.n_cand;
+    s.n_used = W.n_used;
+    s.step = W.step;
+    s.divisor = (double)(W.use - 0);
+    s.x0 = W.x0;
+    s.y0 = W.y0;
+    s.cx = W.center[0];
+    s.cy = W.center[1];
+    s.ct = W.center[2];
+    s.grid_sel = 0.f;
+    s.grid_index = grid_index.empty() ? 0 : grid_index[(size_t)i];
+  }
+  LevelWork L{};
+  L.n_angles = D.n_angles;
+  L.n_space = D.n_space;
+  L.n_cand = D.n_cand;
+  L.blocks_per_scan = (int32_t)bps;
+  L.n_scans = nw;
+  L.step_cells = P.search_space_resolution / G.mres;
+  L.use_penalty = P.use_center_penalty ? 1 : 0;
+  L.dist_gain = (P.type == CSM_COARSE) ? 0.4 : 0.2;  // :759-761
+  L.size = P.search_space_size;
+  L.mres = G.mres;
+  L.grid = c->d_grid;
+  L.grid_stride = (int64_t)c->info.size_x * c->info.size_y;
+  L.size_x = c->info.size_x;
+  L.size_y = c->info.size_y;
+  L.outside = c->outside;
+
+  hipError_t e;
+  if ((e = c->scans.ensure(sw.size() * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
+  if ((e = c->angles.ensure(angles.size() * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
+  if ((e = hipMemcpyAsync(c->scans.p, sw.data(), sw.size() * sizeof(ScanWork), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(scans)");
+  if ((e = hipMemcpyAsync(c->angles.p, angles.data(), angles.size() * sizeof(AngleEntry), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(angles)");
+
+  // algorithmic traffic: one fp32 grid read per summed beam per candidate
+  double beams = 0.0;
+  for (const WindowPlan& W : plans) beams += (double)W.n_used;
+  const double alg_bytes = beams * (double)D.n_cand * 4.0;
+  const double scorings = (double)nw * (double)D.n_cand;
+  char kname[48];
+  std::snprintf(kname, sizeof(kname), "%s<%d>", best_out ? "score_best_kernel" : "score_all_kernel", cpl);
+  if (c->profiling && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+
+  if (best_out == nullptr) {
+    const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
+    if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
+    if ((e = c->h_scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scores)");
+    if ((e = csm::launch_score_all(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                   (const AngleEntry*)c->angles.p, (double*)c->scores.p, cpl,
+                                   c->stream)) != hipSuccess)
+      return c->hip_fail(e, "score_all_kernel");
+    if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+    if ((e = hipMemcpyAsync(c->h_scores.p, c->scores.p, bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(scores)");
+  } else {
+    const size_t pbytes = (size_t)nw * (size_t)bps * sizeof(BestPartial);
+    if ((e = c->partials.ensure(pbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(partials)");
+    if ((e = c->best.ensure((size_t)nw * sizeof(BestPartial))) != hipSuccess) return c->hip_fail(e, "hipMalloc(best)");
+    if ((e = csm::launch_score_best(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                    (const AngleEntry*)c->angles.p, (BestPartial*)c->partials.p, cpl,
+                                    c->stream)) != hipSuccess)
+      return c->hip_fail(e, "score_best_kernel");
+    if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+    if ((e = csm::launch_reduce_best((const BestPartial*)c->partials.p, (int32_t)bps, nw,
+                                     (BestPartial*)c->best.p, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "reduce_best_kernel");
+    if ((e = hipMemcpyAsync(best_out, c->best.p, (size_t)nw * sizeof(BestPartial), hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(best)");
+  }
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize");
+  if (c->profiling) {
+    float ms = 0.f;
+    if ((e = hipEventElapsedTime(&ms, c->ev0, c->ev1)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
+    c->account(kname, ms, alg_bytes, scorings);
+  }
+  return CSM_OK;
+}
+
+// Fill a WindowPlan + its AngleEntry rows (AngleSearchLookUpTable::UpdateLookUpTable
+// :154-172 and ScanMatch :538-548) for a window centred at `center` (map coords).
+bool plan_window(const csm_param& P, const Dims& D, const Geometry& G, int n_points,
+                 const double center[3], std::vector<AngleEntry>& angles, WindowPlan& W) {
+  W.center[0] = center[0];
+  W.center[1] = center[1];
+  W.center[2] = center[2];
+  W.n_points = n_points;
+  if (!beam_rule(n_points, P.use_point_size, W.step, W.use, W.n_used)) return false;
+  const double ssize = P.search_space_size;
+  W.x0 = center[0] - (ssize / G.mres) * 0.5;
+  W.y0 = center[1] - (ssize / G.mres) * 0.5;
+  const double offset = (P.search_angle_offset * 2) / 2;
+  const double start = center[2] - offset;
+  W.angle_off = (int64_t)angles.size();
+  for (int a = 0; a < D.n_angles; ++a) {
+    AngleEntry ae;
+    ae.angle = start + a * P.search_angle_resolution;
+    ae.cosine = std::cos(ae.angle);
+    ae.sine = std::sin(ae.angle);
+    angles.push_back(ae);
+  }
+  return true;
+}
+
+int upload_points(csm_ctx* c, const double* pts, int64_t n_total) {
+  c->loaded_n = -1;  // the point buffer is shared with csm_load_scans
+  const size_t bytes = (size_t)std::max<int64_t>(n_total, 1) * 2 * sizeof(double);
+  hipError_t e;
+  if ((e = c->pts.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(points)");
+  if (n_total > 0 &&
+      (e = hipMemcpyAsync(c->pts.p, pts, (size_t)n_total * 2 * sizeof(double), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(points)");
+  return CSM_OK;
+}
+
+bool map_ready(const csm_ctx* c) { return c->has_grid && c->info.update_index >= 0; }
+
+// One level (BasedCorrelationScanMatch::ScanMatch) over a batch of scans.
+// Points must already be uploaded; offsets index them.
+int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
+                double* poses, double* covs, double* responses, int64_t* argmax_flat) {
+  Dims D;
+  int st = window_dims(P, D);
+  if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
+  if (P.type == CSM_FAST) return c->fail(CSM_ERR_UNSUPPORTED, "FAST (branch-and-bound) type not supported by this entry point");
+  const Geometry G(c->info);
+  std::vector<WindowPlan> plans;
+  std::vector<int64_t> pt_off;
+  std::vector<int> scan_of;
+  std::vector<AngleEntry> angles;
+  plans.reserve((size_t)n_scans);
+  for (int s = 0; s < n_scans; ++s) {
+    const int n = (int)(offsets[s + 1] - offsets[s]);
+    responses[s] = 0.0;  // kMinResponse (:1034)
+    if (argmax_flat) argmax_flat[s] = -1;
+    if (!map_ready(c) || n == 0) continue;  // :792-795
+    double center[3];
+    G.to_map(poses + 3 * s, center);
+    WindowPlan W;
+    if (!plan_window(P, D, G, n, center, angles, W))
+      return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+    plans.push_back(W);
+    pt_off.push_back(offsets[s]);
+    scan_of.push_back(s);
+  }
+  st = run_windows(c, P, D, G, plans, pt_off, angles, {}, nullptr);
+  if (st != CSM_OK) return st;
+  const double* h = (const double*)c->h_scores.p;
+  const int nw = (int)plans.size();
+  const int threads = (nw >= 4) ? c->host_threads : 1;
+  parallel_for(nw, threads, [&](int i) {
+    thread_local std::vector<Entry> scratch;
+    const int s = scan_of[(size_t)i];
+    responses[s] = finish_window(h + (size_t)i * (size_t)D.n_cand, D, plans[(size_t)i],
+                                 angles.data() + plans[(size_t)i].angle_off, P, G, poses + 3 * s,
+                                 covs + 9 * s, scratch, argmax_flat ? argmax_flat + s : nullptr);
+  });
+  return CSM_OK;
+}
+
+int check_points(csm_ctx* c, const double* pts, int64_t n_total) {
+  if (n_total < 0) return c->fail(CSM_ERR_INVALID_ARG, "negative point count");
+  if (n_total > 0 && pts == nullptr) return c->fail(CSM_ERR_INVALID_ARG, "null points");
+  return CSM_OK;
+}
+
+int check_offsets(csm_ctx* c, int32_t n_scans, const int64_t* offsets) {
+  if (n_scans < 0 || (n_scans > 0 && offsets == nullptr)) return c->fail(CSM_ERR_INVALID_ARG, "bad scan offsets");
+  for (int s = 0; s < n_scans; ++s)
+    if (offsets[s + 1] < offsets[s] || offsets[s + 1] - offsets[s] > INT32_MAX)
+      return c->fail(CSM_ERR_INVALID_ARG, "scan offsets must be non-decreasing");
+  return CSM_OK;
+}
+
+struct DeviceGuard {
+  explicit DeviceGuard(int d) { (void)hipSetDevice(d); }
+};
+
+}  // namespace
+
+extern "C" {
+
+int csm_abi_version(void) { return CSM_ABI_VERSION; }
+
+int csm_create(int device, csm_ctx** out) {
+  if (!out) return CSM_ERR_INVALID_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return CSM_ERR_HIP;
+  if (hipSetDevice(device) != hipSuccess) return CSM_ERR_HIP;
+  csm_ctx* c = new (std::nothrow) csm_ctx();
+  if (!c) return CSM_ERR_ALLOC;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return CSM_ERR_HIP;
+  }
+  unsigned hw = std::thread::hardware_concurrency();
+  int threads = (int)std::min<unsigned>(hw ? hw : 1, 16);
+  if (const char* env = std::getenv("CSM_HOST_THREADS")) {
+    const int v = std::atoi(env);
+    if (v > 0) threads = v;
+  }
+  c->host_threads = threads;
+  *out = c;
+  return CSM_OK;
+}
+
+int csm_destroy(csm_ctx* c) {
+  if (!c) return CSM_OK;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->grid_buf.release();
+    c->pts.release();
+    c->scans.release();
+    c->angles.release();
+    c->scores.release();
+    c->partials.release();
+    c->best.release();
+    c->h_scores.release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    (void)hipStreamDestroy(c->stream);
+  }
+  delete c;
+  return CSM_OK;
+}
+
+const char* csm_last_error(const csm_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int csm_set_outside_value(csm_ctx* c, float value) {
+  if (!c) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->outside = value;
+  return CSM_OK;
+}
+
+int csm_window_dims(const csm_param* p, int32_t* n_angles, int32_t* n_space) {
+  if (!p) return CSM_ERR_INVALID_ARG;
+  Dims d;
+  const int st = window_dims(*p, d);
+  if (st != CSM_OK) return st;
+  if (n_angles) *n_angles = d.n_angles;
+  if (n_space) *n_space = d.n_space;
+  return CSM_OK;
+}
+
+int csm_set_grid(csm_ctx* c, const void* cells, int64_t stride, const csm_map_info* info,
+                 int64_t version) {
+  if (!c || !info) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (info->size_x <= 0 || info->size_y <= 0 || !(info->resolution > 0.0))
+    return c->fail(CSM_ERR_INVALID_ARG, "grid size and resolution must be positive");
+  if ((int64_t)info->size_x * info->size_y >= ((int64_t)1 << 31))
+    return c->fail(CSM_ERR_INVALID_ARG, "grid larger than 2^31 cells");
+  if (!cells || stride < 4 || stride % 4 != 0) return c->fail(CSM_ERR_INVALID_ARG, "cells must be non-null with a stride that is a multiple of 4 bytes");
+  const bool same = c->has_grid && c->d_grid == c->grid_buf.p && version >= 0 && cells == c->key_cells &&
+                    stride == c->key_stride && version == c->key_version && info->size_x == c->key_sx &&
+                    info->size_y == c->key_sy;
+  c->info = *info;
+  if (same) return CSM_OK;
+  const size_t ncell = (size_t)info->size_x * (size_t)info->size_y;
+  hipError_t e;
+  if ((e = c->grid_buf.ensure(ncell * sizeof(float))) != hipSuccess) return c->hip_fail(e, "hipMalloc(grid)");
+  const float* src = (const float*)cells;
+  if (stride != 4) {
+    c->h_pack.resize(ncell);
+    const char* b = (const char*)cells;
+    for (size_t i = 0; i < ncell; ++i) std::memcpy(&c->h_pack[i], b + i * (size_t)stride, 4);
+    src = c->h_pack.data();
+  }
+  if ((e = hipMemcpyAsync(c->grid_buf.p, src, ncell * sizeof(float), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(grid)");
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(grid)");
+  c->d_grid = (const float*)c->grid_buf.p;
+  c->has_grid = true;
+  c->key_cells = cells;
+  c->key_stride = stride;
+  c->key_version = version;
+  c->key_sx = info->size_x;
+  c->key_sy = info->size_y;
+  return CSM_OK;
+}
+
+int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) {
+  if (!c || !info) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!dev || info->size_x <= 0 || info->size_y <= 0 || !(info->resolution > 0.0))
+    return c->fail(CSM_ERR_INVALID_ARG, "invalid device grid");
+  if ((int64_t)info->size_x * info->size_y >= ((int64_t)1 << 31))
+    return c->fail(CSM_ERR_INVALID_ARG, "grid larger than 2^31 cells");
+  c->info = *info;
+  c->d_grid = dev;
+  c->has_grid = true;
+  c->key_cells = nullptr;
+  c->key_version = -1;
+  return CSM_OK;
+}
+
+int csm_scan_match_batch(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
+                         const csm_param* param, double* poses, double* covs, double* responses,
+                         int64_t* argmax_flat) {
+  if (!c || !param || !poses || !covs || !responses) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st;
+  if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
+  if (n_scans == 0) return CSM_OK;
+  const int64_t n_total = offsets[n_scans] - offsets[0];
+  if ((st = check_points(c, pts, n_total)) != CSM_OK) return st;
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  std::vector<int64_t> off(offsets, offsets + n_scans + 1);
+  for (auto& o : off) o -= offsets[0];
+  if ((st = upload_points(c, pts + 2 * offsets[0], n_total)) != CSM_OK) return st;
+  return match_level(c, n_scans, off.data(), *param, poses, covs, responses, argmax_flat);
+}
+
+int csm_scan_match(csm_ctx* c, const double* pts, int32_t n_points, const csm_param* param,
+                   double pose[3], double cov[9], double* response, int64_t* argmax_flat) {
+  if (!c || !response) return CSM_ERR_INVALID_ARG;
+  const int64_t off[2] = {0, n_points < 0 ? 0 : n_points};
+  if (n_points < 0) return c->fail(CSM_ERR_INVALID_ARG, "negative point count");
+  return csm_scan_match_batch(c, 1, pts, off, param, pose, cov, response, argmax_flat);
+}
+
+int csm_load_scans(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets) {
+  if (!c) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st;
+  c->loaded_n = -1;
+  if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
+  const int64_t n_total = n_scans > 0 ? offsets[n_scans] - offsets[0] : 0;
+  if ((st = check_points(c, pts, n_total)) != CSM_OK) return st;
+  c->loaded_off.assign(offsets, offsets + n_scans + 1);
+  for (auto& o : c->loaded_off) o -= offsets[0];
+  if ((st = upload_points(c, n_total > 0 ? pts + 2 * offsets[0] : pts, n_total)) != CSM_OK) return st;
+  hipError_t e;
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(points)");
+  c->loaded_n = n_scans;
+  return CSM_OK;
+}
+
+int csm_scan_matchers_loaded(csm_ctx* c, const csm_param levels[3], int32_t use_fine, double* poses,
+                             double* covs, double* scores) {
+  if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (c->loaded_n < 0) return c->fail(CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)");
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  const int32_t n_scans = c->loaded_n;
+  if (n_scans == 0) return CSM_OK;
+  // ScanMatchers::ScanMatch (scan_matchers.h:179-289), use_optimize = false:
+  // coarse, then (use_fine) fine and super-fine, pose fed forward in place.
+  std::vector<double> resp((size_t)n_scans, 0.0), sum((size_t)n_scans, 0.0);
+  const int n_levels = use_fine ? 3 : 1;
+  int st;
+  for (int l = 0; l < n_levels; ++l) {
+    if ((st = match_level(c, n_scans, c->loaded_off.data(), levels[l], poses, covs, resp.data(), nullptr)) != CSM_OK)
+      return st;
+    for (int s = 0; s < n_scans; ++s) sum[(size_t)s] += resp[(size_t)s];
+  }
+  for (int s = 0; s < n_scans; ++s) scores[s] = sum[(size_t)s] / n_levels;  // :281
+  return CSM_OK;
+}
+
+int csm_scan_matchers_batch(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
+                            const csm_param levels[3], int32_t use_fine, double* poses, double* covs,
+                            double* scores) {
+  if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
+  const int st = csm_load_scans(c, n_scans, pts, offsets);
+  if (st != CSM_OK) return st;
+  return csm_scan_matchers_loaded(c, levels, use_fine, poses, covs, scores);
+}
+
+int csm_set_profiling(csm_ctx* c, int32_t on) {
+  if (!c) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  hipError_t e;
+  if (on && !c->ev0) {
+    if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
+    if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
+  }
+  c->profiling = on != 0;
+  c->stats.clear();
+  return CSM_OK;
+}
+
+int csm_kernel_stats(csm_ctx* c, csm_kernel_stat* out, int32_t capacity, int32_t* count) {
+  if (!c || !count) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  *count = (int32_t)c->stats.size();
+  for (int32_t i = 0; i < *count && i < capacity && out; ++i) out[i] = c->stats[(size_t)i];
+  return CSM_OK;
+}
+
+int csm_scan_matchers(csm_ctx* c, const double* pts, int32_t n_points, const csm_param levels[3],
+                      int32_t use_fine, double pose[3], double cov[9], double* score) {
+  if (!c || !score) return CSM_ERR_INVALID_ARG;
+  if (n_points < 0) return c->fail(CSM_ERR_INVALID_ARG, "negative point count");
+  const int64_t off[2] = {0, n_points};
+  return csm_scan_matchers_batch(c, 1, pts, off, levels, use_fine, pose, cov, score);
+}
+
+int csm_score_window(csm_ctx* c, const double* pts, int32_t n_points, const csm_param* param,
+                     const double center_map[3], double* scores_out, int64_t n_out) {
+  if (!c || !param || !center_map || !scores_out) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  Dims D;
+  int st = window_dims(*param, D);
+  if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
+  if (n_out != D.n_cand) return c->fail(CSM_ERR_INVALID_ARG, "n_out must equal n_angles * n_space^2");
+  if (n_points <= 0) return c->fail(CSM_ERR_INVALID_ARG, "no points");
+  if ((st = check_points(c, pts, n_points)) != CSM_OK) return st;
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  const Geometry G(c->info);
+  std::vector<WindowPlan> plans(1);
+  std::vector<AngleEntry> angles;
+  if (!plan_window(*param, D, G, n_points, center_map, angles, plans[0]))
+    return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+  if ((st = upload_points(c, pts, n_points)) != CSM_OK) return st;
+  if ((st = run_windows(c, *param, D, G, plans, {0}, angles, {}, nullptr)) != CSM_OK) return st;
+  std::memcpy(scores_out, c->h_scores.p, (size_t)n_out * sizeof(double));
+  return CSM_OK;
+}
+
+int csm_best_window(csm_ctx* c, const double* pts, int32_t n_points, const csm_param* param,
+                    const double center_map[3], csm_best* best) {
+  if (!c || !param || !center_map || !best) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  Dims D;
+  int st = window_dims(*param, D);
+  if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
+  if (n_points <= 0) return c->fail(CSM_ERR_INVALID_ARG, "no points");
+  if ((st = check_points(c, pts, n_points)) != CSM_OK) return st;
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  const Geometry G(c->info);
+  std::vector<WindowPlan> plans(1);
+  std::vector<AngleEntry> angles;
+  if (!plan_window(*param, D, G, n_points, center_map, angles, plans[0]))
+    return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+  if ((st = upload_points(c, pts, n_points)) != CSM_OK) return st;
+  BestPartial bp{};
+  if ((st = run_windows(c, *param, D, G, plans, {0}, angles, {}, &bp)) != CSM_OK) return st;
+  const WindowPlan& W = plans[0];
+  const int64_t ns = D.n_space, nss = ns * ns;
+  best->score = bp.score;
+  best->flat_index = bp.flat;
+  best->x = W.x0 + (int)((bp.flat / ns) % ns) * (param->search_space_resolution / G.mres);
+  best->y = W.y0 + (int)(bp.flat % ns) * (param->search_space_resolution / G.mres);
+  best->angle = angles[(size_t)(bp.flat / nss)].angle;
+  return CSM_OK;
+}
+
+}  // extern "C"

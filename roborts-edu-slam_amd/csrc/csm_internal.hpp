@@ -1,0 +1,74 @@
+// csm_internal.hpp — types shared by the HIP kernels (csm_kernels.hip) and the
+// host side of the C-ABI (csm_api.cpp). Not installed; include/csm.h is the
+// public boundary.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+
+namespace csm {
+
+// One window to search: a scan (its points) at one level, centred on one pose.
+// Everything a lane needs to rebuild its candidate's (x, y, theta) exactly as
+// MultiResolutionCorrelateScanMatcher::ScanMatch does
+// (correlate_scan_matcher.h:536-572) is precomputed on the host.
+struct ScanWork {
+  int64_t pts_off;      // first point of this scan in the batch point array
+  int64_t angle_off;    // first AngleEntry of this window
+  int64_t out_off;      // first output slot (all-scores mode)
+  int32_t n_used;       // B = ceil(N / step): beams summed
+  int32_t step;         // beam stride (:561-566)
+  double divisor;       // use_point_size after the :561 rule
+  double x0, y0;        // search_space_start_x/y (:546-547), map cells
+  double cx, cy, ct;    // window centre (map cells, rad)
+  float grid_sel;       // reserved
+  int32_t grid_index;   // which resident grid (submap) this window reads
+};
+
+// Per-angle data of a window: theta_i = start + i*ares and the host libm
+// cos/sin of it (AngleSearchLookUpTable::UpdateLookUpTable :161-172).
+struct AngleEntry {
+  double angle, cosine, sine;
+};
+
+// Launch-uniform description of one level.
+struct LevelWork {
+  int32_t n_angles;
+  int32_t n_space;
+  int64_t n_cand;          // n_angles * n_space^2 per window
+  int32_t blocks_per_scan;
+  int32_t n_scans;
+  double step_cells;       // space_step_factor = res / map_resolution (:548)
+  int32_t use_penalty;
+  int32_t pad0;
+  double dist_gain;        // kDistancePenaltyGain{Coarse,Fine} (:760-761)
+  double size;             // search_space_size (max_distance_bound of :734)
+  double mres;             // map_resolution (scale_factor of :733)
+  const float* grid;       // packed fp32 grid(s), row-major
+  int64_t grid_stride;     // floats between consecutive grids (submaps)
+  int32_t size_x, size_y;
+  float outside;
+  int32_t pad1;
+};
+
+// Argmax partial: best score of a block and its flat candidate index.
+struct BestPartial {
+  double score;
+  int64_t flat;
+};
+
+constexpr int kBlock = 256;      // 4 waves
+constexpr int kChunk = 1024;     // beams staged in LDS per pass (16 KB)
+
+// Launchers (csm_kernels.hip). All enqueue on `stream` and return hipError_t.
+hipError_t launch_score_all(const LevelWork& L, const ScanWork* d_scans,
+                            const double* d_pts, const AngleEntry* d_angles,
+                            double* d_out, int cpl, hipStream_t stream);
+hipError_t launch_score_best(const LevelWork& L, const ScanWork* d_scans,
+                             const double* d_pts, const AngleEntry* d_angles,
+                             BestPartial* d_partials, int cpl, hipStream_t stream);
+// Reduce per-window partials (blocks_per_scan each) to one BestPartial per window.
+hipError_t launch_reduce_best(const BestPartial* d_partials, int32_t blocks_per_scan,
+                              int32_t n_windows, BestPartial* d_out, hipStream_t stream);
+
+}  // namespace csm

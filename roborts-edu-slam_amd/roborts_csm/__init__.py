@@ -1,0 +1,338 @@
+"""roborts_csm — MI355X-native correlative scan matcher for RoboRTS-Edu-SLAM.
+
+Python mirror of the reference's scan-matching interface, bound to the C-ABI
+of libroborts_csm.so (include/csm.h). Names, argument meaning and error
+behaviour follow the reference:
+
+  ScanMatchMap                 ~ ScanMatchMap = OccuGridMap<ProbabilityCell> (map/slam_map.h:32-34)
+  RangeDataContainer2d         ~ RangeDataContainer<double> (slam/sensor_data_manager.h:87-300)
+  BasedCorrelationScanMatch    ~ correlate_scan_matcher.h:766-1036 (ScanMatch :784-875)
+  ScanMatchers                 ~ scan_match/scan_matchers.h:160-416 (ScanMatch :179-289)
+
+Everything numeric runs in the shared library on the GPU; this module only
+moves arrays. Importing it fails loudly when the library is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Sequence
+
+import numpy as np
+
+from . import _abi
+from ._abi import COARSE, FAST, FINE, SUPER, CsmBest, CsmMapInfo, CsmParam
+from .params import (
+    CONFIG1_PARAM, FAST_PARAM, IN_CLASS_LEVELS, PARAM_CONFIG_LEVELS, SIM_YAML_LEVELS,
+    CorrelationScanMatchParam, headline_levels,
+)
+
+_lib = _abi.load_library()
+
+kMapUnknownCellProb = np.float32(0.3)  # slam/slam_processor.h:264
+
+
+class CsmError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"csm status {status}: {msg}")
+        self.status = status
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _i64ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int64))
+
+
+def _as_param(p) -> CsmParam:
+    if isinstance(p, CsmParam):
+        return p
+    return p.to_c()
+
+
+# ---------------------------------------------------------------------------
+# Data containers (reference data formats either side of the boundary)
+# ---------------------------------------------------------------------------
+
+@dataclass
+class ScanMatchMap:
+    """Probability grid + GridMapBase geometry (map/grid_map_base.h:47-71).
+
+    ``cells`` is either a packed float32 [size_y, size_x] array or the
+    reference's AoS ProbabilityCell layout as a structured array with fields
+    (prob_value_ f4, update_index_ i4) (map/grid_map_cell.h:301-328).
+    """
+
+    cells: np.ndarray
+    resolution: float
+    offset: tuple = (0.0, 0.0)
+    update_index: int = 0
+    version: int = 0
+
+    @property
+    def size_x(self) -> int:
+        return int(self.cells.shape[1])
+
+    @property
+    def size_y(self) -> int:
+        return int(self.cells.shape[0])
+
+    def IsMapInit(self) -> bool:  # grid_map_base.h:373-378
+        return self.update_index >= 0
+
+    def GetCellLength(self) -> float:  # grid_map_base.h:307-309
+        return 1 / (1.0 / self.resolution)
+
+    def info(self) -> CsmMapInfo:
+        return CsmMapInfo(float(self.resolution), float(self.offset[0]), float(self.offset[1]),
+                          self.size_x, self.size_y, int(self.update_index), 0)
+
+    def GetMapCoordsPose(self, pose_world) -> np.ndarray:  # grid_map_base.h:89-93
+        s = 1.0 / self.resolution
+        return np.array([s * pose_world[0] + s * self.offset[0],
+                         s * pose_world[1] + s * self.offset[1], pose_world[2]])
+
+    def GetWorldCoordsPose(self, pose_map) -> np.ndarray:  # grid_map_base.h:83-87
+        s = 1.0 / self.resolution
+        a = s * (1.0 / (s * s - 0.0 * 0.0))
+        return np.array([a * pose_map[0] + -(a * (s * self.offset[0])),
+                         a * pose_map[1] + -(a * (s * self.offset[1])), pose_map[2]])
+
+
+@dataclass
+class RangeDataContainer2d:
+    """Scan endpoints in the sensor frame (slam/sensor_data_manager.h:87-300)."""
+
+    points: np.ndarray = field(default_factory=lambda: np.zeros((0, 2)))
+    sensor_pose: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    scale_factor: float = 1.0
+
+    def CreateFrom(self, other: "RangeDataContainer2d", factor: float) -> "RangeDataContainer2d":
+        """Copy and scale every point by ``factor`` (sensor_data_manager.h:99-115)."""
+        self.scale_factor = factor
+        self.sensor_pose = np.array(other.sensor_pose, dtype=np.float64)
+        self.points = np.ascontiguousarray(other.points, dtype=np.float64) * factor
+        return self
+
+    def GetSize(self) -> int:
+        return int(self.points.shape[0])
+
+    def GetDataPoint(self, i: int) -> np.ndarray:
+        return self.points[i]
+
+
+def cell_points(points_m: np.ndarray, resolution: float) -> np.ndarray:
+    """Metres -> map cells as CreateFrom(range, 1 / resolution) does."""
+    return np.ascontiguousarray(points_m, dtype=np.float64) * (1 / resolution)
+
+
+# ---------------------------------------------------------------------------
+# Context over the C-ABI
+# ---------------------------------------------------------------------------
+
+class Context:
+    """One csm_ctx: a device, a HIP stream, a resident grid."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        st = _lib.csm_create(int(device), C.byref(h))
+        if st != _abi.CSM_OK:
+            raise CsmError(st, f"csm_create(device={device}) failed (no usable HIP device?)")
+        self._h = h
+        self.device = device
+        self._grid_ref = None
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.csm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st: int):
+        if st != _abi.CSM_OK:
+            raise CsmError(st, _lib.csm_last_error(self._h).decode())
+
+    def set_outside_value(self, v: float):
+        self._check(_lib.csm_set_outside_value(self._h, C.c_float(v)))
+
+    def set_grid(self, m: ScanMatchMap, force: bool = False):
+        cells = m.cells
+        if cells.dtype == np.float32:
+            cells = np.ascontiguousarray(cells)
+            stride = 4
+        elif cells.dtype.names and "prob_value_" in cells.dtype.names:
+            cells = np.ascontiguousarray(cells)
+            stride = cells.dtype.itemsize
+        else:
+            raise TypeError("grid cells must be float32 or a ProbabilityCell structured array")
+        self._grid_ref = cells  # keep the host copy alive (key is its address)
+        info = m.info()
+        self._check(_lib.csm_set_grid(self._h, cells.ctypes.data_as(C.c_void_p), stride,
+                                      C.byref(info), -1 if force else int(m.version)))
+
+    def set_grid_device(self, dev_ptr: int, m: ScanMatchMap):
+        info = m.info()
+        self._check(_lib.csm_set_grid_device(self._h, C.c_void_p(dev_ptr), C.byref(info)))
+
+    # -- reference entry points -------------------------------------------
+    def scan_match(self, points_cells: np.ndarray, param, pose: np.ndarray, cov: np.ndarray,
+                   return_argmax: bool = False):
+        """BasedCorrelationScanMatch::ScanMatch; pose/cov updated in place."""
+        pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
+        assert pose.dtype == np.float64 and pose.flags.c_contiguous and pose.size == 3
+        assert cov.dtype == np.float64 and cov.flags.c_contiguous and cov.size == 9
+        p = _as_param(param)
+        resp = C.c_double(0.0)
+        am = C.c_int64(-1)
+        self._check(_lib.csm_scan_match(self._h, _dptr(pts), pts.shape[0], C.byref(p), _dptr(pose),
+                                        _dptr(cov), C.byref(resp), C.byref(am)))
+        return (resp.value, am.value) if return_argmax else resp.value
+
+    def scan_matchers(self, points_cells, levels: Sequence, pose, cov, use_fine: bool = True) -> float:
+        pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
+        lv = (CsmParam * 3)(*[_as_param(l) for l in levels])
+        sc = C.c_double(0.0)
+        self._check(_lib.csm_scan_matchers(self._h, _dptr(pts), pts.shape[0], lv, 1 if use_fine else 0,
+                                           _dptr(pose), _dptr(cov), C.byref(sc)))
+        return sc.value
+
+    def scan_match_batch(self, points: np.ndarray, offsets: np.ndarray, param, poses, covs):
+        """Returns (responses, argmax_flat) for n independent scans."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 2)
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = off.size - 1
+        assert poses.dtype == np.float64 and poses.flags.c_contiguous and poses.size == 3 * n
+        assert covs.dtype == np.float64 and covs.flags.c_contiguous and covs.size == 9 * n
+        resp = np.zeros(n)
+        am = np.full(n, -1, dtype=np.int64)
+        p = _as_param(param)
+        self._check(_lib.csm_scan_match_batch(self._h, n, _dptr(pts), _i64ptr(off), C.byref(p),
+                                              _dptr(poses), _dptr(covs), _dptr(resp), _i64ptr(am)))
+        return resp, am
+
+    def scan_matchers_batch(self, points, offsets, levels, poses, covs, use_fine: bool = True):
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 2)
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = off.size - 1
+        assert poses.dtype == np.float64 and poses.flags.c_contiguous and poses.size == 3 * n
+        assert covs.dtype == np.float64 and covs.flags.c_contiguous and covs.size == 9 * n
+        scores = np.zeros(n)
+        lv = (CsmParam * 3)(*[_as_param(l) for l in levels])
+        self._check(_lib.csm_scan_matchers_batch(self._h, n, _dptr(pts), _i64ptr(off), lv,
+                                                 1 if use_fine else 0, _dptr(poses), _dptr(covs),
+                                                 _dptr(scores)))
+        return scores
+
+    def load_scans(self, points, offsets):
+        """Make a batch of scans device-resident (csm_load_scans)."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 2)
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        self._loaded = (pts, off)
+        self._check(_lib.csm_load_scans(self._h, off.size - 1, _dptr(pts), _i64ptr(off)))
+
+    def scan_matchers_loaded(self, levels, poses, covs, use_fine: bool = True):
+        n = self._loaded[1].size - 1
+        assert poses.dtype == np.float64 and poses.flags.c_contiguous and poses.size == 3 * n
+        assert covs.dtype == np.float64 and covs.flags.c_contiguous and covs.size == 9 * n
+        scores = np.zeros(n)
+        lv = (CsmParam * 3)(*[_as_param(l) for l in levels])
+        self._check(_lib.csm_scan_matchers_loaded(self._h, lv, 1 if use_fine else 0, _dptr(poses),
+                                                  _dptr(covs), _dptr(scores)))
+        return scores
+
+    def set_profiling(self, on: bool = True):
+        self._check(_lib.csm_set_profiling(self._h, 1 if on else 0))
+
+    def kernel_stats(self) -> list[dict]:
+        cnt = C.c_int32(0)
+        self._check(_lib.csm_kernel_stats(self._h, None, 0, C.byref(cnt)))
+        arr = (_abi.CsmKernelStat * max(cnt.value, 1))()
+        self._check(_lib.csm_kernel_stats(self._h, arr, cnt.value, C.byref(cnt)))
+        return [dict(name=a.name.decode(), launches=a.launches, total_ms=a.total_ms,
+                     algorithmic_bytes=a.algorithmic_bytes, scorings=a.scorings) for a in arr[:cnt.value]]
+
+    def score_window(self, points_cells, param, center_map) -> np.ndarray:
+        pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
+        p = _as_param(param)
+        na, ns = window_dims(p)
+        out = np.empty(na * ns * ns)
+        ctr = np.ascontiguousarray(center_map, dtype=np.float64)
+        self._check(_lib.csm_score_window(self._h, _dptr(pts), pts.shape[0], C.byref(p), _dptr(ctr),
+                                          _dptr(out), out.size))
+        return out
+
+    def best_window(self, points_cells, param, center_map) -> CsmBest:
+        pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
+        p = _as_param(param)
+        ctr = np.ascontiguousarray(center_map, dtype=np.float64)
+        b = CsmBest()
+        self._check(_lib.csm_best_window(self._h, _dptr(pts), pts.shape[0], C.byref(p), _dptr(ctr),
+                                         C.byref(b)))
+        return b
+
+
+def window_dims(param) -> tuple[int, int]:
+    p = _as_param(param)
+    na, ns = C.c_int32(), C.c_int32()
+    st = _lib.csm_window_dims(C.byref(p), C.byref(na), C.byref(ns))
+    if st != _abi.CSM_OK:
+        raise CsmError(st, "invalid window parameters")
+    return na.value, ns.value
+
+
+# ---------------------------------------------------------------------------
+# Reference-interface mirror
+# ---------------------------------------------------------------------------
+
+class BasedCorrelationScanMatch:
+    """Mirror of BasedCorrelationScanMatch (correlate_scan_matcher.h:766-1036).
+
+    ScanMatch(map, range_data, param, current_pose, cov_matrix) -> response;
+    current_pose (world, 3) and cov_matrix (3x3) are updated in place exactly
+    where the reference updates them.
+    """
+
+    def __init__(self, context: Context | None = None):
+        self.ctx = context or Context(0)
+
+    def ScanMatch(self, map_: ScanMatchMap, range_data: RangeDataContainer2d, param,
+                  current_pose: np.ndarray, cov_matrix: np.ndarray) -> float:
+        self.ctx.set_grid(map_)
+        return self.ctx.scan_match(range_data.points, param, current_pose, cov_matrix.reshape(-1))
+
+
+class ScanMatchers:
+    """Mirror of ScanMatchers::ScanMatch (scan_matchers.h:179-289) with the
+    correlative levels only (use_optimize_scan_match = false, both YAMLs)."""
+
+    def __init__(self, levels=SIM_YAML_LEVELS, context: Context | None = None):
+        self.levels = tuple(levels)
+        self.ctx = context or Context(0)
+
+    def ScanMatch(self, coarse_range_data, fine_range_data, coarse_map, fine_map,
+                  best_pose: np.ndarray, cov_matrix: np.ndarray, use_fine_scan_match: bool = True) -> float:
+        # every correlative level runs on fine_map with fine_range_data (:238,:249,:256)
+        self.ctx.set_grid(fine_map)
+        return self.ctx.scan_matchers(fine_range_data.points, self.levels, best_pose,
+                                      cov_matrix.reshape(-1), use_fine_scan_match)
+
+
+__all__ = [
+    "Context", "CsmError", "ScanMatchMap", "RangeDataContainer2d", "BasedCorrelationScanMatch",
+    "ScanMatchers", "CorrelationScanMatchParam", "SIM_YAML_LEVELS", "PARAM_CONFIG_LEVELS",
+    "IN_CLASS_LEVELS", "FAST_PARAM", "CONFIG1_PARAM", "headline_levels", "window_dims",
+    "cell_points", "COARSE", "FINE", "SUPER", "FAST", "kMapUnknownCellProb",
+]

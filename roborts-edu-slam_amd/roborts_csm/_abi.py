@@ -1,0 +1,124 @@
+"""ctypes view of include/csm.h (the C-ABI of libroborts_csm.so).
+
+The shared library is the product; this module only binds it. It raises at
+import time when the library is missing: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libroborts_csm.so"))
+
+CSM_OK = 0
+CSM_ERR_INVALID_ARG = 1
+CSM_ERR_HIP = 2
+CSM_ERR_NO_GRID = 3
+CSM_ERR_ALLOC = 4
+CSM_ERR_UNSUPPORTED = 5
+
+COARSE, FINE, SUPER, FAST = 0, 1, 2, 3
+
+# Every function include/csm.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "csm_create", "csm_destroy", "csm_last_error", "csm_abi_version",
+    "csm_set_outside_value", "csm_set_grid", "csm_set_grid_device",
+    "csm_window_dims", "csm_scan_match", "csm_scan_matchers",
+    "csm_scan_match_batch", "csm_scan_matchers_batch", "csm_score_window",
+    "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded",
+    "csm_set_profiling", "csm_kernel_stats",
+)
+
+
+class CsmParam(C.Structure):
+    """csm_param == CorrelationScanMatchParam (correlate_scan_matcher.h:41-86)."""
+
+    _fields_ = [
+        ("search_space_size", C.c_double),
+        ("search_space_resolution", C.c_double),
+        ("search_angle_offset", C.c_double),
+        ("search_angle_resolution", C.c_double),
+        ("response_threshold", C.c_double),
+        ("use_point_size", C.c_int32),
+        ("max_depth", C.c_int32),
+        ("use_center_penalty", C.c_int32),
+        ("type", C.c_int32),
+    ]
+
+
+class CsmMapInfo(C.Structure):
+    _fields_ = [
+        ("resolution", C.c_double),
+        ("offset_x", C.c_double),
+        ("offset_y", C.c_double),
+        ("size_x", C.c_int32),
+        ("size_y", C.c_int32),
+        ("update_index", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+class CsmBest(C.Structure):
+    _fields_ = [
+        ("score", C.c_double),
+        ("flat_index", C.c_int64),
+        ("x", C.c_double),
+        ("y", C.c_double),
+        ("angle", C.c_double),
+    ]
+
+
+class CsmKernelStat(C.Structure):
+    _fields_ = [
+        ("name", C.c_char * 48),
+        ("launches", C.c_int64),
+        ("total_ms", C.c_double),
+        ("algorithmic_bytes", C.c_double),
+        ("scorings", C.c_double),
+    ]
+
+
+_dp = C.POINTER(C.c_double)
+_i64p = C.POINTER(C.c_int64)
+_i32p = C.POINTER(C.c_int32)
+_ctx = C.c_void_p
+
+
+def _bind(lib: C.CDLL) -> C.CDLL:
+    sig = {
+        "csm_create": (C.c_int, [C.c_int, C.POINTER(_ctx)]),
+        "csm_destroy": (C.c_int, [_ctx]),
+        "csm_last_error": (C.c_char_p, [_ctx]),
+        "csm_abi_version": (C.c_int, []),
+        "csm_set_outside_value": (C.c_int, [_ctx, C.c_float]),
+        "csm_set_grid": (C.c_int, [_ctx, C.c_void_p, C.c_int64, C.POINTER(CsmMapInfo), C.c_int64]),
+        "csm_set_grid_device": (C.c_int, [_ctx, C.c_void_p, C.POINTER(CsmMapInfo)]),
+        "csm_window_dims": (C.c_int, [C.POINTER(CsmParam), _i32p, _i32p]),
+        "csm_scan_match": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), _dp, _dp, _dp, _i64p]),
+        "csm_scan_matchers": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), C.c_int32, _dp, _dp, _dp]),
+        "csm_scan_match_batch": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, C.POINTER(CsmParam), _dp, _dp, _dp, _i64p]),
+        "csm_scan_matchers_batch": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, C.POINTER(CsmParam), C.c_int32, _dp, _dp, _dp]),
+        "csm_score_window": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), _dp, _dp, C.c_int64]),
+        "csm_best_window": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), _dp, C.POINTER(CsmBest)]),
+        "csm_load_scans": (C.c_int, [_ctx, C.c_int32, _dp, _i64p]),
+        "csm_scan_matchers_loaded": (C.c_int, [_ctx, C.POINTER(CsmParam), C.c_int32, _dp, _dp, _dp]),
+        "csm_set_profiling": (C.c_int, [_ctx, C.c_int32]),
+        "csm_kernel_stats": (C.c_int, [_ctx, C.POINTER(CsmKernelStat), C.c_int32, _i32p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load libroborts_csm.so; raises OSError when it has not been built."""
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise OSError(
+            f"libroborts_csm.so not found at {p}; build it with "
+            "`make -C roborts-edu-slam_amd` (or __graft_entry__.build())"
+        )
+    return _bind(C.CDLL(p))

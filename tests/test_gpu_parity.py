@@ -1,0 +1,263 @@
+"""GPU parity: the HIP path (through the C-ABI of libroborts_csm.so) against
+the CPU oracle and the committed golden fixtures.
+
+Bar (north star): bit-exact argmax pose index, scores within 1e-6 — this
+implementation is held to bit-exact everywhere (scores, sort order, pose,
+covariance, response), tolerance 0.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import pyoracle as O  # noqa: E402
+
+
+def _param(a):
+    from roborts_csm.params import CorrelationScanMatchParam
+    return CorrelationScanMatchParam(float(a[0]), float(a[1]), float(a[2]), float(a[3]), float(a[4]),
+                                     int(a[5]), int(a[6]), bool(a[7]), int(a[8]))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import roborts_csm
+    c = roborts_csm.Context(0)
+    yield c
+    c.close()
+
+
+def _map(grid, res, off, update_index=0, version=0):
+    import roborts_csm
+    return roborts_csm.ScanMatchMap(grid, float(res), tuple(off), update_index, version)
+
+
+@pytest.fixture(scope="module")
+def f1(golden_dir):
+    return np.load(os.path.join(golden_dir, "f1_config1.npz"))
+
+
+def test_f1_scores_bit_exact(ctx, f1):
+    ctx.set_grid(_map(f1["grid"], f1["resolution"], f1["offset"]), force=True)
+    sc = ctx.score_window(f1["points"], _param(f1["param"]), f1["center"])
+    assert sc.size == 7056
+    assert np.array_equal(sc, f1["scores"])
+
+
+def test_f1_scan_match_bit_exact(ctx, f1):
+    ctx.set_grid(_map(f1["grid"], f1["resolution"], f1["offset"]), force=True)
+    pose = np.array(f1["init_pose"], dtype=np.float64)
+    cov = np.eye(3).reshape(9).copy()
+    r, am = ctx.scan_match(f1["points"], _param(f1["param"]), pose, cov, return_argmax=True)
+    assert am == f1["argmax"]
+    assert r == f1["response"]
+    assert np.array_equal(pose, f1["pose"]) and np.array_equal(cov, f1["cov"])
+
+
+def test_f1_three_level_bit_exact(ctx, f1):
+    from roborts_csm.params import SIM_YAML_LEVELS
+    ctx.set_grid(_map(f1["grid"], f1["resolution"], f1["offset"]), force=True)
+    pose = np.array(f1["init_pose"], dtype=np.float64)
+    cov = np.eye(3).reshape(9).copy()
+    s = ctx.scan_matchers(f1["points"], SIM_YAML_LEVELS, pose, cov)
+    assert s == f1["sim3_score"]
+    assert np.array_equal(pose, f1["sim3_pose"]) and np.array_equal(cov, f1["sim3_cov"])
+
+
+@pytest.mark.parametrize("tag", ["sim", "b1081", "pcfg"])
+def test_f2_levels_bit_exact(ctx, golden_dir, tag):
+    f2 = np.load(os.path.join(golden_dir, "f2_config2_crop.npz"))
+    ctx.set_grid(_map(f2["grid"], f2["resolution"], f2["offset"]), force=True)
+    levels = [_param(a) for a in f2[f"{tag}_levels"]]
+    for li in range(3):
+        sc = ctx.score_window(f2["points"], levels[li], f2[f"{tag}_l{li}_center"])
+        assert np.array_equal(sc, f2[f"{tag}_l{li}_scores"]), (tag, li)
+    pose = np.array(f2["init_pose"], dtype=np.float64)
+    cov = np.eye(3).reshape(9).copy()
+    s = ctx.scan_matchers(f2["points"], levels, pose, cov)
+    assert s == f2[f"{tag}_score"]
+    assert np.array_equal(pose, f2[f"{tag}_pose"]) and np.array_equal(cov, f2[f"{tag}_cov"])
+
+
+def test_f3_ties_bit_exact(ctx, golden_dir):
+    """Whole groups of candidates tie: the winner depends on std::sort's order."""
+    f3 = np.load(os.path.join(golden_dir, "f3_ties.npz"))
+    ctx.set_grid(_map(f3["grid"], f3["resolution"], f3["offset"]), force=True)
+    for tag in ("pen", "nopen", "fine"):
+        p = _param(f3[f"{tag}_param"])
+        pose = np.array(f3["init_pose"], dtype=np.float64)
+        cov = np.eye(3).reshape(9).copy()
+        r, am = ctx.scan_match(f3["points"], p, pose, cov, return_argmax=True)
+        assert am == f3[f"{tag}_argmax"], tag
+        assert r == f3[f"{tag}_response"]
+        assert np.array_equal(pose, f3[f"{tag}_pose"]) and np.array_equal(cov, f3[f"{tag}_cov"])
+
+
+def test_f5_best_window(ctx, golden_dir, f1):
+    f5 = np.load(os.path.join(golden_dir, "f5_large_window.npz"))
+    ctx.set_grid(_map(f1["grid"], f1["resolution"], f1["offset"]), force=True)
+    b = ctx.best_window(f1["points"], _param(f5["param"]), f5["center"])
+    assert b.score == f5["best_score"] and b.flat_index == f5["best_flat"]
+
+
+def test_hostile_grid_bit_exact(ctx, f1):
+    """fp32 values over 30 binades: fp64 sums are order-dependent here, so
+    only the reference beam order reproduces the oracle bit for bit."""
+    from roborts_csm import worlds
+    g = worlds.hostile_grid(400, 400)
+    ctx.set_grid(_map(g, f1["resolution"], f1["offset"]), force=True)
+    m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
+    p = _param(f1["param"])
+    for U in (100, 1000):
+        q = p.with_(use_point_size=U)
+        sc = ctx.score_window(f1["points"], q, f1["center"])
+        ref = O.score_window(m, f1["points"], q, f1["center"], sc.size)
+        assert np.array_equal(sc, ref)
+
+
+def test_aos_cells_upload(ctx, f1):
+    g = f1["grid"]
+    aos = np.zeros(g.shape, dtype=[("prob_value_", "<f4"), ("update_index_", "<i4")])
+    aos["prob_value_"] = g
+    aos["update_index_"] = 7
+    ctx.set_grid(_map(aos, f1["resolution"], f1["offset"]), force=True)
+    sc = ctx.score_window(f1["points"], _param(f1["param"]), f1["center"])
+    assert np.array_equal(sc, f1["scores"])
+
+
+def test_out_of_bounds_endpoints(ctx):
+    """Endpoints beyond the grid read the defined outside value (the reference
+    reads out of bounds: UB). Both sides use the same definition."""
+    rng = np.random.default_rng(5)
+    g = rng.uniform(0.3, 1.0, size=(64, 80)).astype(np.float32)
+    pts = rng.uniform(-120, 120, size=(500, 2))
+    from roborts_csm.params import CONFIG1_PARAM
+    p = CONFIG1_PARAM.with_(use_point_size=400)
+    center = np.array([40.0, 30.0, 0.2])
+    ctx.set_grid(_map(g, 0.05, (0.0, 0.0)), force=True)
+    for outside in (0.3, 0.0, 0.75):
+        ctx.set_outside_value(outside)
+        m = O.Map(g, 0.05, (0.0, 0.0), outside=outside)
+        sc = ctx.score_window(pts, p, center)
+        assert np.array_equal(sc, O.score_window(m, pts, p, center, sc.size))
+    ctx.set_outside_value(0.3)
+
+
+@pytest.mark.parametrize("n,U", [(1, 100), (1, 1), (150, 100), (199, 100), (200, 100), (1081, 541),
+                                 (1081, 540), (1081, 1081), (3000, 5000), (5000, 2)])
+def test_beam_subsampling_edges(ctx, f1, n, U):
+    """The :561-566 rule (step, divisor) at its boundaries, incl. >1 LDS chunk."""
+    rng = np.random.default_rng(n * 7 + U)
+    pts = rng.uniform(-60, 60, size=(n, 2))
+    p = _param(f1["param"]).with_(use_point_size=U)
+    ctx.set_grid(_map(f1["grid"], f1["resolution"], f1["offset"]), force=True)
+    m = O.Map(f1["grid"], float(f1["resolution"]), tuple(f1["offset"]))
+    sc = ctx.score_window(pts, p, f1["center"])
+    assert np.array_equal(sc, O.score_window(m, pts, p, f1["center"], sc.size))
+    pose = np.array(f1["init_pose"], dtype=np.float64)
+    cov = np.eye(3).reshape(9).copy()
+    r, am = ctx.scan_match(pts, p, pose, cov, return_argmax=True)
+    r2, pose2, cov2, am2, _ = O.scan_match(m, pts, p, f1["init_pose"], np.eye(3))
+    assert (r, am) == (r2, am2)
+    assert np.array_equal(pose, pose2) and np.array_equal(cov, cov2)
+
+
+def test_early_returns(ctx, f1):
+    """Uninitialised map or empty scan: response 0, pose/cov untouched (:792-795)."""
+    p = _param(f1["param"])
+    ctx.set_grid(_map(f1["grid"], f1["resolution"], f1["offset"], update_index=-1), force=True)
+    pose = np.array(f1["init_pose"], dtype=np.float64)
+    cov = np.full(9, 7.0)
+    r, am = ctx.scan_match(f1["points"], p, pose, cov, return_argmax=True)
+    assert r == 0.0 and am == -1 and np.array_equal(pose, f1["init_pose"]) and (cov == 7.0).all()
+    ctx.set_grid(_map(f1["grid"], f1["resolution"], f1["offset"]), force=True)
+    r = ctx.scan_match(np.zeros((0, 2)), p, pose, cov)
+    assert r == 0.0 and np.array_equal(pose, f1["init_pose"]) and (cov == 7.0).all()
+
+
+def test_invalid_use_point_size(ctx, f1):
+    import roborts_csm
+    ctx.set_grid(_map(f1["grid"], f1["resolution"], f1["offset"]), force=True)
+    p = _param(f1["param"]).with_(use_point_size=1)
+    with pytest.raises(roborts_csm.CsmError) as e:
+        ctx.scan_match(f1["points"], p, np.array(f1["init_pose"], dtype=np.float64), np.eye(3).reshape(9).copy())
+    assert e.value.status == 1
+
+
+def test_grid_version_cache(ctx, f1):
+    g = np.array(f1["grid"])
+    p = _param(f1["param"])
+    m = _map(g, f1["resolution"], f1["offset"], version=11)
+    ctx.set_grid(m)
+    a = ctx.score_window(f1["points"], p, f1["center"])
+    g[:, :] = np.float32(0.5)          # same buffer, same version -> cached copy is used
+    ctx.set_grid(m)
+    assert np.array_equal(ctx.score_window(f1["points"], p, f1["center"]), a)
+    m.version = 12                     # bump -> re-upload
+    ctx.set_grid(m)
+    b = ctx.score_window(f1["points"], p, f1["center"])
+    assert not np.array_equal(a, b)
+
+
+@pytest.fixture(scope="module")
+def world2000():
+    from roborts_csm import worlds
+    w = worlds.make_world(2000, 2000, 0.05)
+    b = worlds.make_scan_batch(w, 96, seed=99)
+    return w, b
+
+
+@pytest.mark.parametrize("which", ["sim", "headline"])
+def test_batch_three_level_bit_exact(ctx, world2000, which):
+    """BASELINE config 2 shape (1081 beams, 2000x2000 @5 cm), batched 3 levels."""
+    from roborts_csm.params import SIM_YAML_LEVELS, headline_levels
+    w, b = world2000
+    levels = SIM_YAML_LEVELS if which == "sim" else headline_levels()
+    ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+    poses = np.ascontiguousarray(b.init_poses.copy())
+    covs = np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1))
+    s = ctx.scan_matchers_batch(b.points_cells, b.offsets, levels, poses, covs)
+    m = O.Map(w.grid, w.resolution, w.offset)
+    s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells, b.offsets, levels, b.init_poses,
+                                       np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1)))
+    assert np.array_equal(s, s2)
+    assert np.array_equal(poses, p2)
+    assert np.array_equal(covs, c2)
+    # property: the matcher pulls the (0.12, -0.07, 4 deg) init error in
+    err = np.hypot(*(poses[:, :2] - b.true_poses[:, :2]).T)
+    assert np.median(err) < 0.05
+
+
+def test_batch_single_level_matches_single_calls(ctx, world2000):
+    from roborts_csm.params import SIM_YAML_LEVELS
+    w, b = world2000
+    ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+    n = 16
+    poses = np.ascontiguousarray(b.init_poses[:n].copy())
+    covs = np.tile(np.eye(3).reshape(1, 9), (n, 1))
+    r, am = ctx.scan_match_batch(b.points_cells[:b.offsets[n]], b.offsets[:n + 1], SIM_YAML_LEVELS[0], poses, covs)
+    for k in range(n):
+        pose = np.array(b.init_poses[k])
+        cov = np.eye(3).reshape(9).copy()
+        r1, am1 = ctx.scan_match(b.points_cells[b.offsets[k]:b.offsets[k + 1]], SIM_YAML_LEVELS[0], pose, cov,
+                                 return_argmax=True)
+        assert r1 == r[k] and am1 == am[k]
+        assert np.array_equal(pose, poses[k]) and np.array_equal(cov, covs[k])
+
+
+def test_best_window_large_matches_oracle(ctx, world2000):
+    """Argmax-only over a +-2 m / +-180 deg window at full grid size."""
+    from roborts_csm.params import CorrelationScanMatchParam
+    w, b = world2000
+    ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+    p = CorrelationScanMatchParam(2.0, 0.05, math.pi, 0.0349, 0.5, 100, 0, False, 0)
+    m = O.Map(w.grid, w.resolution, w.offset)
+    for k in range(3):
+        pts = b.points_cells[b.offsets[k]:b.offsets[k + 1]]
+        c = O.world_to_map(m, b.init_poses[k])
+        got = ctx.best_window(pts, p, c)
+        s, flat = O.best_window(m, pts, p, c)
+        assert got.score == s and got.flat_index == flat
