@@ -166,52 +166,80 @@ struct Entry {
   int64_t idx;
 };
 
-// Host finish of one window: everything BasedCorrelationScanMatch::ScanMatch
-// does after the scores exist (correlate_scan_matcher.h:606-611, 670-710,
-// 835-869). scores are in enumeration order, penalty already applied.
-double finish_window(const double* scores, const Dims& D, const WindowPlan& W,
-                     const AngleEntry* angles, const csm_param& P, const Geometry& G,
-                     double pose[3], double cov[9], std::vector<Entry>& e,
-                     int64_t* argmax_flat) {
+// Candidate geometry of a window, rebuilt from its flat enumeration index
+// exactly as the reference stored it in Candidate2D (:569,:572, angle :554).
+struct CandGeom {
+  const WindowPlan& W;
+  const AngleEntry* angles;
+  double f;
+  int64_t ns, nss;
+  double x(int64_t idx) const { return W.x0 + (int)((idx / ns) % ns) * f; }
+  double y(int64_t idx) const { return W.y0 + (int)(idx % ns) * f; }
+  const AngleEntry& a(int64_t idx) const { return angles[idx / nss]; }
+};
+
+// Host sort path: std::sort of the window's candidates and the three ordered
+// scans, producing the same FinishOut the device finish kernel produces.
+void host_sort_finish(const double* scores, const Dims& D, const CandGeom& C, const csm_param& P,
+                      const Geometry& G, std::vector<Entry>& e, csm::FinishOut& o) {
   const int64_t n = D.n_cand;
   e.resize((size_t)n);
   for (int64_t i = 0; i < n; ++i) e[(size_t)i] = Entry{scores[i], i};
   std::sort(e.begin(), e.end(), [](const Entry& a, const Entry& b) { return a.score > b.score; });
-  if (argmax_flat) *argmax_flat = e[0].idx;
-
-  const double f = P.search_space_resolution / G.mres;
-  const int64_t ns = D.n_space, nss = ns * ns;
-  auto cand_x = [&](int64_t idx) { return W.x0 + (int)((idx / ns) % ns) * f; };
-  auto cand_y = [&](int64_t idx) { return W.y0 + (int)(idx % ns) * f; };
-  auto cand_a = [&](int64_t idx) { return angles[idx / nss].angle; };
-
+  const double best = e[0].score;
   // FindBestCandidate (:670-710)
-  double best_x = cand_x(e[0].idx), best_y = cand_y(e[0].idx), best_a = cand_a(e[0].idx);
-  const double best_score = e[0].score;
-  {
-    double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;
-    int count = 0;
-    for (size_t i = 0; i < e.size(); ++i) {
-      const double sc = e[i].score;
-      if (!double_equal(sc, best_score, kResponseFilterTolerance)) break;
-      const double cx = cand_x(e[i].idx), cy = cand_y(e[i].idx), ca = cand_a(e[i].idx);
-      ax += cx * sc;
-      ay += cy * sc;
-      thx += std::cos(ca) * sc;
-      thy += std::sin(ca) * sc;
-      ssum += sc;
-      count++;
-    }
-    if (count > 1) {
-      ax /= ssum;
-      ay /= ssum;
-      thx /= ssum;
-      thy /= ssum;
-      best_x = ax;
-      best_y = ay;
-      best_a = std::atan2(thy, thx);
+  double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;
+  int count = 0;
+  for (size_t i = 0; i < e.size(); ++i) {
+    const double sc = e[i].score;
+    if (!double_equal(sc, best, kResponseFilterTolerance)) break;
+    ax += C.x(e[i].idx) * sc;
+    ay += C.y(e[i].idx) * sc;
+    thx += C.a(e[i].idx).cosine * sc;  // cos(candidate.angle()), host libm
+    thy += C.a(e[i].idx).sine * sc;
+    ssum += sc;
+    count++;
+  }
+  o.front_idx = (int32_t)e[0].idx;
+  o.count = count;
+  o.best_score = best;
+  o.thx = thx;
+  o.thy = thy;
+  o.ssum = ssum;
+  o.best_x = count > 1 ? ax / ssum : C.x(e[0].idx);
+  o.best_y = count > 1 ? ay / ssum : C.y(e[0].idx);
+  const double bound = std::min(best - 0.1, 0.5);
+  // ComputePositionalCovariance's candidates (:915-928)
+  o.n_pos = 0;
+  for (size_t i = 0; i < e.size() && o.n_pos < csm::kCovPoints; ++i) {
+    if (!(e[i].score > bound)) break;
+    o.pos_idx[o.n_pos] = (int32_t)e[i].idx;
+    o.pos_score[o.n_pos] = e[i].score;
+    o.n_pos++;
+  }
+  // ComputeAngularCovariance's candidates (:990-1003)
+  const double lin_tol = P.search_space_resolution / G.mres;
+  o.n_ang = 0;
+  for (size_t i = 0; i < e.size() && o.n_ang < csm::kCovPoints; ++i) {
+    if (!(e[i].score >= bound)) break;  // sorted: nothing later qualifies
+    const int64_t idx = e[i].idx;
+    if (double_equal(C.x(idx), o.best_x, lin_tol) && double_equal(C.y(idx), o.best_y, lin_tol)) {
+      o.ang_idx[o.n_ang] = (int32_t)idx;
+      o.ang_score[o.n_ang] = e[i].score;
+      o.n_ang++;
     }
   }
+}
+
+// Everything BasedCorrelationScanMatch::ScanMatch does once the sorted
+// candidates are summarised in `o` (correlate_scan_matcher.h:700-707,
+// 835-869, covariance :887-1019). Returns the response.
+double complete_window(const csm::FinishOut& o, const CandGeom& C, const csm_param& P,
+                       const Geometry& G, double pose[3], double cov[9]) {
+  const double best_score = o.best_score;
+  const double best_x = o.best_x, best_y = o.best_y;
+  double best_a = C.a(o.front_idx).angle;
+  if (o.count > 1) best_a = std::atan2(o.thy / o.ssum, o.thx / o.ssum);  // :702-706
 
   const double sres = P.search_space_resolution;
   const double max_ang_var = 4 * (P.search_angle_resolution * P.search_angle_resolution);  // :801
@@ -225,17 +253,13 @@ double finish_window(const double* scores, const Dims& D, const WindowPlan& W,
       return;
     }
     double vxx = 0.0, vxy = 0.0, vyy = 0.0, norm = 0.0;
-    const double bound = std::min(best_score - 0.1, 0.5);
-    int counter = 0;
-    for (size_t i = 0; i < e.size(); ++i) {
-      const double sc = e[i].score;
-      if (!(sc > bound && counter < kMaxVarianceUsePointSize)) break;
-      const double dx = cand_x(e[i].idx) - best_x, dy = cand_y(e[i].idx) - best_y;
+    for (int i = 0; i < o.n_pos; ++i) {
+      const double sc = o.pos_score[i];
+      const double dx = C.x(o.pos_idx[i]) - best_x, dy = C.y(o.pos_idx[i]) - best_y;
       norm += sc;
       vxx += (dx * dx * sc);
       vxy += (dx * dy * sc);
       vyy += (dy * dy * sc);
-      counter++;
     }
     if (norm > kDoubleTolerance) {
       double xx = vxx / norm, xy = vxy / norm, yy = vyy / norm;
@@ -258,21 +282,12 @@ double finish_window(const double* scores, const Dims& D, const WindowPlan& W,
       cov[8] = max_ang_var;
       return;
     }
-    const double lin_tol = sres / G.mres;
     double norm = 0.0, acc = 0.0;
-    const double bound = std::min(best_score - 0.1, 0.5);
-    int counter = 0;
-    for (size_t i = 0; i < e.size(); ++i) {
-      const double sc = e[i].score;
-      if (sc >= bound && counter < kMaxVarianceUsePointSize) {
-        const int64_t idx = e[i].idx;
-        if (double_equal(cand_x(idx), best_x, lin_tol) && double_equal(cand_y(idx), best_y, lin_tol)) {
-          const double d = cand_a(idx) - best_a;
-          norm += sc;
-          acc += (d * d * sc);
-          counter++;
-        }
-      }
+    for (int i = 0; i < o.n_ang; ++i) {
+      const double sc = o.ang_score[i];
+      const double d = C.a(o.ang_idx[i]).angle - best_a;
+      norm += sc;
+      acc += (d * d * sc);
     }
     cov[8] = (norm > kDoubleTolerance) ? acc / norm : 200 * max_ang_var;
   };
@@ -344,8 +359,9 @@ struct csm_ctx {
   int64_t key_stride = 0, key_version = -1;
   int32_t key_sx = -1, key_sy = -1;
 
-  DevBuf pts, scans, angles, scores, partials, best;
-  HostBuf h_scores;
+  DevBuf pts, scans, angles, scores, partials, best, fin;
+  HostBuf h_scores, h_fin;
+  bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
   std::vector<float> h_pack;
 
   // scans made resident by csm_load_scans (offsets relative to pts)
@@ -354,7 +370,7 @@ struct csm_ctx {
 
   // per-kernel HIP-event timing (csm_set_profiling / csm_kernel_stats)
   bool profiling = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   std::vector<csm_kernel_stat> stats;
   void account(const char* name, float ms, double bytes, double scorings) {
     for (auto& s : stats)
@@ -389,10 +405,13 @@ namespace {
 // Scores windows_n windows of one level on the device. plans[i] describes
 // window i, pts_dev is the batch's points already resident. When best_out is
 // null, every score is copied back into ctx->h_scores (window-major).
+enum class Finish { kScoresToHost, kDevice, kBest };
+
 int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
                 const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
                 const std::vector<AngleEntry>& angles, const std::vector<int32_t>& grid_index,
-                BestPartial* best_out) {
+                BestPartial* best_out, Finish mode = Finish::kScoresToHost) {
+  if (best_out) mode = Finish::kBest;
   const int nw = (int)plans.size();
   if (nw == 0) return CSM_OK;
   const int cpl = pick_cpl(D.n_cand);
@@ -452,17 +471,35 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   std::snprintf(kname, sizeof(kname), "%s<%d>", best_out ? "score_best_kernel" : "score_all_kernel", cpl);
   if (c->profiling && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
 
-  if (best_out == nullptr) {
+  if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
-    if ((e = c->h_scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scores)");
     if ((e = csm::launch_score_all(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                    (const AngleEntry*)c->angles.p, (double*)c->scores.p, cpl,
                                    c->stream)) != hipSuccess)
       return c->hip_fail(e, "score_all_kernel");
     if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
-    if ((e = hipMemcpyAsync(c->h_scores.p, c->scores.p, bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
-      return c->hip_fail(e, "hipMemcpyAsync(scores)");
+    if (mode == Finish::kScoresToHost) {
+      if ((e = c->h_scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scores)");
+      if ((e = hipMemcpyAsync(c->h_scores.p, c->scores.p, bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+        return c->hip_fail(e, "hipMemcpyAsync(scores)");
+    } else {
+      csm::FinishArgs A{};
+      A.n_cand = D.n_cand;
+      A.n_space = D.n_space;
+      A.step_cells = L.step_cells;
+      A.lin_tol = P.search_space_resolution / G.mres;
+      const size_t fbytes = (size_t)nw * sizeof(csm::FinishOut);
+      if ((e = c->fin.ensure(fbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(finish)");
+      if ((e = c->h_fin.ensure(fbytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(finish)");
+      if ((e = csm::launch_finish(A, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
+                                  (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw,
+                                  c->stream)) != hipSuccess)
+        return c->hip_fail(e, "finish_kernel");
+      if (c->profiling && (e = hipEventRecord(c->ev2, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+      if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, fbytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+        return c->hip_fail(e, "hipMemcpyAsync(finish)");
+    }
   } else {
     const size_t pbytes = (size_t)nw * (size_t)bps * sizeof(BestPartial);
     if ((e = c->partials.ensure(pbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(partials)");
@@ -483,6 +520,10 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     float ms = 0.f;
     if ((e = hipEventElapsedTime(&ms, c->ev0, c->ev1)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
     c->account(kname, ms, alg_bytes, scorings);
+    if (mode == Finish::kDevice) {
+      if ((e = hipEventElapsedTime(&ms, c->ev1, c->ev2)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
+      c->account("finish_kernel", ms, (double)nw * (double)D.n_cand * 8.0, 0.0);
+    }
   }
   return CSM_OK;
 }
@@ -534,36 +575,55 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
   if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
   if (P.type == CSM_FAST) return c->fail(CSM_ERR_UNSUPPORTED, "FAST (branch-and-bound) type not supported by this entry point");
   const Geometry G(c->info);
-  std::vector<WindowPlan> plans;
-  std::vector<int64_t> pt_off;
   std::vector<int> scan_of;
-  std::vector<AngleEntry> angles;
-  plans.reserve((size_t)n_scans);
+  scan_of.reserve((size_t)n_scans);
   for (int s = 0; s < n_scans; ++s) {
-    const int n = (int)(offsets[s + 1] - offsets[s]);
     responses[s] = 0.0;  // kMinResponse (:1034)
     if (argmax_flat) argmax_flat[s] = -1;
+    const int n = (int)(offsets[s + 1] - offsets[s]);
     if (!map_ready(c) || n == 0) continue;  // :792-795
-    double center[3];
-    G.to_map(poses + 3 * s, center);
-    WindowPlan W;
-    if (!plan_window(P, D, G, n, center, angles, W))
+    int step, use, n_used;
+    if (!beam_rule(n, P.use_point_size, step, use, n_used))
       return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
-    plans.push_back(W);
-    pt_off.push_back(offsets[s]);
     scan_of.push_back(s);
   }
-  st = run_windows(c, P, D, G, plans, pt_off, angles, {}, nullptr);
+  const int nw = (int)scan_of.size();
+  if (nw == 0) return CSM_OK;
+  std::vector<WindowPlan> plans((size_t)nw);
+  std::vector<int64_t> pt_off((size_t)nw);
+  std::vector<AngleEntry> angles((size_t)nw * (size_t)D.n_angles);
+  const int threads = (nw >= 64) ? c->host_threads : 1;
+  parallel_for(nw, threads, [&](int i) {  // host libm cos/sin per window angle
+    const int s = scan_of[(size_t)i];
+    double center[3];
+    G.to_map(poses + 3 * s, center);
+    std::vector<AngleEntry> row;
+    row.reserve((size_t)D.n_angles);
+    plan_window(P, D, G, (int)(offsets[s + 1] - offsets[s]), center, row, plans[(size_t)i]);
+    plans[(size_t)i].angle_off = (int64_t)i * D.n_angles;
+    std::copy(row.begin(), row.end(), angles.begin() + (size_t)i * (size_t)D.n_angles);
+    pt_off[(size_t)i] = offsets[s];
+  });
+  const bool dev = c->device_finish && D.n_cand <= csm::kFinishMaxCand;
+  st = run_windows(c, P, D, G, plans, pt_off, angles, {}, nullptr,
+                   dev ? Finish::kDevice : Finish::kScoresToHost);
   if (st != CSM_OK) return st;
-  const double* h = (const double*)c->h_scores.p;
-  const int nw = (int)plans.size();
-  const int threads = (nw >= 4) ? c->host_threads : 1;
+  const double f = P.search_space_resolution / G.mres;
   parallel_for(nw, threads, [&](int i) {
     thread_local std::vector<Entry> scratch;
     const int s = scan_of[(size_t)i];
-    responses[s] = finish_window(h + (size_t)i * (size_t)D.n_cand, D, plans[(size_t)i],
-                                 angles.data() + plans[(size_t)i].angle_off, P, G, poses + 3 * s,
-                                 covs + 9 * s, scratch, argmax_flat ? argmax_flat + s : nullptr);
+    const CandGeom C{plans[(size_t)i], angles.data() + plans[(size_t)i].angle_off, f, D.n_space,
+                     (int64_t)D.n_space * D.n_space};
+    csm::FinishOut local;
+    const csm::FinishOut* o = nullptr;
+    if (dev) {
+      o = (const csm::FinishOut*)c->h_fin.p + i;
+    } else {
+      host_sort_finish((const double*)c->h_scores.p + (size_t)i * (size_t)D.n_cand, D, C, P, G, scratch, local);
+      o = &local;
+    }
+    if (argmax_flat) argmax_flat[s] = o->front_idx;
+    responses[s] = complete_window(*o, C, P, G, poses + 3 * s, covs + 9 * s);
   });
   return CSM_OK;
 }
@@ -612,6 +672,7 @@ int csm_create(int device, csm_ctx** out) {
     if (v > 0) threads = v;
   }
   c->host_threads = threads;
+  if (const char* env = std::getenv("CSM_FINISH")) c->device_finish = std::strcmp(env, "host") != 0;
   *out = c;
   return CSM_OK;
 }
@@ -629,9 +690,12 @@ int csm_destroy(csm_ctx* c) {
     c->scores.release();
     c->partials.release();
     c->best.release();
+    c->fin.release();
     c->h_scores.release();
+    c->h_fin.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev2) (void)hipEventDestroy(c->ev2);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -794,6 +858,7 @@ int csm_set_profiling(csm_ctx* c, int32_t on) {
   if (on && !c->ev0) {
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
+    if ((e = hipEventCreate(&c->ev2)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
   }
   c->profiling = on != 0;
   c->stats.clear();

@@ -60,6 +60,65 @@ struct BestPartial {
 constexpr int kBlock = 256;      // 4 waves
 constexpr int kChunk = 1024;     // beams staged in LDS per pass (16 KB)
 
+// ---- device finish (csm_finish.hip) -------------------------------------
+constexpr int kCovPoints = 20;          // kMaxVarianceUsePointSize (:1033)
+constexpr int64_t kFinishMaxCand = 12288;  // windows above this finish on the host
+
+struct FinishArgs {
+  int64_t n_cand;
+  int32_t n_space;
+  int32_t pad;
+  double step_cells;   // res / map_resolution
+  double lin_tol;      // search_space_resolution / map_resolution (:840,:852)
+};
+
+// What the host needs to complete BasedCorrelationScanMatch::ScanMatch for
+// one window after the device sorted its candidates.
+struct FinishOut {
+  int32_t front_idx;   // flat index std::sort put first (the argmax)
+  int32_t count;       // FindBestCandidate tied-prefix length
+  int32_t n_pos, n_ang;
+  double best_score;
+  double best_x, best_y;   // averaged (count > 1) or front (map cells)
+  double thx, thy, ssum;   // sums for atan2(thy/ssum, thx/ssum) (host libm)
+  int32_t pos_idx[kCovPoints];
+  int32_t ang_idx[kCovPoints];
+  double pos_score[kCovPoints];
+  double ang_score[kCovPoints];
+};
+
+struct FinishLayout {
+  int cap, nwords;
+  size_t keys, vals, lpos, rpos, bounds, stack, total;
+};
+
+// LDS carve of the finish kernel for n candidates (16-byte aligned pieces).
+constexpr FinishLayout finish_layout(int64_t n) {
+  FinishLayout L{};
+  L.cap = (int)(n / 2 + 2);
+  L.nwords = (int)((n + 32) / 32);
+  size_t o = 64;  // misc: stack pointer + best (x, y)
+  L.keys = o;
+  o += (size_t)n * 8;
+  L.vals = o;
+  o += ((size_t)n * 2 + 15) & ~(size_t)15;
+  L.lpos = o;
+  o += ((size_t)(L.cap + 1) * 2 + 15) & ~(size_t)15;
+  L.rpos = o;
+  o += ((size_t)(L.cap + 1) * 2 + 15) & ~(size_t)15;
+  L.bounds = o;
+  o += ((size_t)L.nwords * 4 + 15) & ~(size_t)15;
+  L.stack = o;
+  o += 64 * 12;  // segment stack: depth <= 2*floor(log2 n) + 2 entries
+  L.total = o;
+  return L;
+}
+constexpr size_t finish_lds_bytes(int64_t n) { return finish_layout(n).total; }
+
+hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const AngleEntry* d_angles,
+                         const double* d_scores, FinishOut* d_out, int32_t n_windows,
+                         hipStream_t stream);
+
 // Launchers (csm_kernels.hip). All enqueue on `stream` and return hipError_t.
 hipError_t launch_score_all(const LevelWork& L, const ScanWork* d_scans,
                             const double* d_pts, const AngleEntry* d_angles,

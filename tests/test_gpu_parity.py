@@ -261,3 +261,51 @@ def test_best_window_large_matches_oracle(ctx, world2000):
         got = ctx.best_window(pts, p, c)
         s, flat = O.best_window(m, pts, p, c)
         assert got.score == s and got.flat_index == flat
+
+
+def test_device_finish_equals_host_sort(world2000):
+    """CSM_FINISH=host (std::sort on the host) and the device finish kernel
+    give identical poses, covariances, scores and argmax indices."""
+    import roborts_csm
+    from roborts_csm.params import SIM_YAML_LEVELS
+    w, b = world2000
+    os.environ["CSM_FINISH"] = "host"
+    try:
+        hctx = roborts_csm.Context(0)
+    finally:
+        del os.environ["CSM_FINISH"]
+    dctx = roborts_csm.Context(0)
+    out = []
+    for c in (hctx, dctx):
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+        for lv in SIM_YAML_LEVELS:
+            poses = np.ascontiguousarray(b.init_poses.copy())
+            covs = np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1))
+            r, am = c.scan_match_batch(b.points_cells, b.offsets, lv, poses, covs)
+            out.append((r, am, poses, covs))
+    hctx.close()
+    dctx.close()
+    for a, d in zip(out[:3], out[3:]):
+        for x, y in zip(a, d):
+            assert np.array_equal(x, y)
+
+
+def test_device_finish_ties_random_windows(ctx):
+    """Tie-heavy windows (coarse grid values on a sub-cell window step) through
+    the device sort, against the oracle's std::sort."""
+    from roborts_csm.params import SIM_YAML_LEVELS
+    rng = np.random.default_rng(17)
+    g = rng.choice(np.array([0.3, 0.5, 0.7, 1.0], dtype=np.float32), size=(300, 300))
+    ctx.set_grid(_map(g, 0.05, (7.5, 7.5)), force=True)
+    m = O.Map(g, 0.05, (7.5, 7.5))
+    for t in range(12):
+        pts = rng.uniform(-80, 80, size=(int(rng.integers(20, 400)), 2))
+        init = rng.uniform(-1, 1, size=3)
+        for lv in SIM_YAML_LEVELS:
+            lv = lv.with_(use_center_penalty=bool(t % 2))
+            pose = init.copy()
+            cov = np.eye(3).reshape(9).copy()
+            r, am = ctx.scan_match(pts, lv, pose, cov, return_argmax=True)
+            r2, pose2, cov2, am2, _ = O.scan_match(m, pts, lv, init, np.eye(3))
+            assert (r, am) == (r2, am2), (t, lv)
+            assert np.array_equal(pose, pose2) and np.array_equal(cov, cov2)
