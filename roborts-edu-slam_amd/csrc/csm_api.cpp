@@ -362,7 +362,17 @@ struct csm_ctx {
   DevBuf pts, scans, angles, scores, partials, best, fin;
   HostBuf h_scores, h_fin;
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
+  bool column_kernel = true;  // CSM_KERNEL=v1 selects the lane-per-candidate kernels
   std::vector<float> h_pack;
+
+  // exact fixed-point copy of the grid (ensure_int_grid)
+  DevBuf gridi, gstats;
+  bool int_checked = false, int_ok = false;
+  int int_exp = 0;
+  double int_max_abs = 0.0;  // max |cell| (and |outside|) for the per-launch exactness bound
+  int32_t outside_i = 0;
+  double pts_maxabs = 0.0;   // max |x|+|y| of the resident points (NaN: unbounded)
+
 
   // scans made resident by csm_load_scans (offsets relative to pts)
   int32_t loaded_n = -1;
@@ -402,6 +412,58 @@ struct csm_ctx {
 
 namespace {
 
+// Smallest power of two a float is an integer multiple of (0 for 0).
+int float_granularity(float v, bool* zero) {
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  u &= 0x7FFFFFFFu;
+  *zero = (u == 0);
+  if (*zero) return INT32_MAX;
+  const uint32_t e = u >> 23, m = u & 0x7FFFFFu;
+  const uint32_t mm = (e == 0) ? m : (m | 0x800000u);
+  return ((e == 0) ? -149 : (int)e - 150) + __builtin_ctz(mm);
+}
+
+// Decide whether the grid (+ outside value) can be summed exactly in fixed
+// point and build the shifted copy (value - outside) * 2^E on the device.
+// Exact when every value is a multiple of 2^-E and the chunk sums fit:
+// (max|v| + |outside|) * 2^E <= 2^26. Real scan-match grids (fp32 values in
+// [0.3, 1]) give E = 25. A sum of B such values is exact in the reference's
+// fp64 as long as B * max|v| * 2^E <= 2^53 (checked per launch).
+int ensure_int_grid(csm_ctx* c) {
+  if (c->int_checked) return CSM_OK;
+  c->int_checked = true;
+  c->int_ok = false;
+  const int64_t n = (int64_t)c->info.size_x * c->info.size_y;
+  hipError_t e;
+  if ((e = c->gstats.ensure(sizeof(csm::GridStats))) != hipSuccess) return c->hip_fail(e, "hipMalloc(stats)");
+  if ((e = csm::launch_analyze_grid(c->d_grid, n, (csm::GridStats*)c->gstats.p, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "analyze_grid_kernel");
+  csm::GridStats st{};
+  if ((e = hipMemcpyAsync(&st, c->gstats.p, sizeof(st), hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(stats)");
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(stats)");
+  if (st.nonfinite || !std::isfinite(c->outside)) return CSM_OK;
+  bool ozero = false;
+  const int og = float_granularity(c->outside, &ozero);
+  const int min_g = std::min(st.min_gexp, og);
+  float maxv;
+  std::memcpy(&maxv, &st.max_abs_bits, 4);
+  const double vmax = std::max((double)maxv, (double)std::fabs(c->outside));
+  const int E = (min_g == INT32_MAX) ? 0 : std::max(0, -min_g);
+  if (E > 60) return CSM_OK;
+  const double scale = std::ldexp(1.0, E);
+  if (((double)maxv + std::fabs((double)c->outside)) * scale > std::ldexp(1.0, 26)) return CSM_OK;
+  if ((e = c->gridi.ensure((size_t)n * sizeof(int32_t))) != hipSuccess) return c->hip_fail(e, "hipMalloc(gridi)");
+  if ((e = csm::launch_fixed_point(c->d_grid, n, c->outside, E, (int32_t*)c->gridi.p, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "fixed_point_kernel");
+  c->int_exp = E;
+  c->int_max_abs = vmax;
+  c->outside_i = (int32_t)((double)c->outside * scale);
+  c->int_ok = true;
+  return CSM_OK;
+}
+
 // Scores windows_n windows of one level on the device. plans[i] describes
 // window i, pts_dev is the batch's points already resident. When best_out is
 // null, every score is copied back into ctx->h_scores (window-major).
@@ -414,9 +476,29 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   if (best_out) mode = Finish::kBest;
   const int nw = (int)plans.size();
   if (nw == 0) return CSM_OK;
+  int st;
+  if ((st = ensure_int_grid(c)) != CSM_OK) return st;
+  // v2 column kernel: KT rows per lane, tiles balanced so at most a few rows idle
+  const int ktiles = (D.n_space + 15) / 16;
+  const int kt = (D.n_space + ktiles - 1) / ktiles;
+  const int64_t n_cols = (int64_t)D.n_angles * D.n_space;
+  const int64_t col_blocks = (n_cols + 63) / 64;
+  const bool v2 = c->column_kernel && n_cols < INT32_MAX;
+  // exact fixed-point accumulation: grid eligible, beams bounded, no offset wrap
+  bool use_int = v2 && c->int_ok;
+  const double f = P.search_space_resolution / G.mres;
+  for (const WindowPlan& W : plans) {
+    if (!use_int) break;
+    const double far = (double)(D.n_space - 1) * f;
+    const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
+                                 std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
+    const double R = c->pts_maxabs * (1.0 + 1e-9) + span + 2.0;
+    if (!(R * 4.0 * (double)c->info.size_x < std::ldexp(1.0, 30))) use_int = false;
+    if ((double)W.n_used * c->int_max_abs * std::ldexp(1.0, c->int_exp) > std::ldexp(1.0, 53)) use_int = false;
+  }
   const int cpl = pick_cpl(D.n_cand);
   const int64_t per_block = (int64_t)csm::kBlock * cpl;
-  const int64_t bps = (D.n_cand + per_block - 1) / per_block;
+  const int64_t bps = v2 ? col_blocks * ktiles : (D.n_cand + per_block - 1) / per_block;
   if (bps * nw > INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
 
   std::vector<ScanWork> sw((size_t)nw);
@@ -453,6 +535,13 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   L.size_x = c->info.size_x;
   L.size_y = c->info.size_y;
   L.outside = c->outside;
+  L.int_mode = use_int ? 1 : 0;
+  L.gridi = (const int32_t*)c->gridi.p;
+  L.int_scale = std::ldexp(1.0, -c->int_exp);
+  L.outside_i = c->outside_i;
+  L.n_cols = (int32_t)n_cols;
+  L.ktiles = ktiles;
+  L.col_blocks = (int32_t)col_blocks;
 
   hipError_t e;
   if ((e = c->scans.ensure(sw.size() * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
@@ -468,16 +557,24 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const double alg_bytes = beams * (double)D.n_cand * 4.0;
   const double scorings = (double)nw * (double)D.n_cand;
   char kname[48];
-  std::snprintf(kname, sizeof(kname), "%s<%d>", best_out ? "score_best_kernel" : "score_all_kernel", cpl);
+  if (v2)
+    std::snprintf(kname, sizeof(kname), "score_cols_kernel<%d,%s,%s>", kt, use_int ? "int" : "f64",
+                  best_out ? "best" : "all");
+  else
+    std::snprintf(kname, sizeof(kname), "%s<%d>", best_out ? "score_best_kernel" : "score_all_kernel", cpl);
   if (c->profiling && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
 
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
-    if ((e = csm::launch_score_all(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                   (const AngleEntry*)c->angles.p, (double*)c->scores.p, cpl,
-                                   c->stream)) != hipSuccess)
-      return c->hip_fail(e, "score_all_kernel");
+    if (v2)
+      e = csm::launch_score_cols(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                 (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, kt,
+                                 c->stream);
+    else
+      e = csm::launch_score_all(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                (const AngleEntry*)c->angles.p, (double*)c->scores.p, cpl, c->stream);
+    if (e != hipSuccess) return c->hip_fail(e, "score kernel");
     if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
     if (mode == Finish::kScoresToHost) {
       if ((e = c->h_scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scores)");
@@ -504,10 +601,15 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     const size_t pbytes = (size_t)nw * (size_t)bps * sizeof(BestPartial);
     if ((e = c->partials.ensure(pbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(partials)");
     if ((e = c->best.ensure((size_t)nw * sizeof(BestPartial))) != hipSuccess) return c->hip_fail(e, "hipMalloc(best)");
-    if ((e = csm::launch_score_best(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                    (const AngleEntry*)c->angles.p, (BestPartial*)c->partials.p, cpl,
-                                    c->stream)) != hipSuccess)
-      return c->hip_fail(e, "score_best_kernel");
+    if (v2)
+      e = csm::launch_score_cols(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                 (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
+                                 kt, c->stream);
+    else
+      e = csm::launch_score_best(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                 (const AngleEntry*)c->angles.p, (BestPartial*)c->partials.p, cpl,
+                                 c->stream);
+    if (e != hipSuccess) return c->hip_fail(e, "score kernel (best)");
     if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
     if ((e = csm::launch_reduce_best((const BestPartial*)c->partials.p, (int32_t)bps, nw,
                                      (BestPartial*)c->best.p, c->stream)) != hipSuccess)
@@ -555,6 +657,12 @@ bool plan_window(const csm_param& P, const Dims& D, const Geometry& G, int n_poi
 
 int upload_points(csm_ctx* c, const double* pts, int64_t n_total) {
   c->loaded_n = -1;  // the point buffer is shared with csm_load_scans
+  double m = 0.0;    // max |x| + |y| over the points: bounds every rotated endpoint
+  for (int64_t i = 0; i < n_total; ++i) {
+    const double a = std::fabs(pts[2 * i]) + std::fabs(pts[2 * i + 1]);
+    m = (a > m || a != a) ? a : m;
+  }
+  c->pts_maxabs = m;
   const size_t bytes = (size_t)std::max<int64_t>(n_total, 1) * 2 * sizeof(double);
   hipError_t e;
   if ((e = c->pts.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(points)");
@@ -673,6 +781,7 @@ int csm_create(int device, csm_ctx** out) {
   }
   c->host_threads = threads;
   if (const char* env = std::getenv("CSM_FINISH")) c->device_finish = std::strcmp(env, "host") != 0;
+  if (const char* env = std::getenv("CSM_KERNEL")) c->column_kernel = std::strcmp(env, "v1") != 0;
   *out = c;
   return CSM_OK;
 }
@@ -684,6 +793,8 @@ int csm_destroy(csm_ctx* c) {
     DeviceGuard g(c->device);
     (void)hipStreamSynchronize(c->stream);
     c->grid_buf.release();
+    c->gridi.release();
+    c->gstats.release();
     c->pts.release();
     c->scans.release();
     c->angles.release();
@@ -707,6 +818,7 @@ const char* csm_last_error(const csm_ctx* c) { return c ? c->err.c_str() : "null
 int csm_set_outside_value(csm_ctx* c, float value) {
   if (!c) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
+  if (value != c->outside) c->int_checked = false;  // the fixed-point copy is shifted by it
   c->outside = value;
   return CSM_OK;
 }
@@ -751,6 +863,7 @@ int csm_set_grid(csm_ctx* c, const void* cells, int64_t stride, const csm_map_in
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(grid)");
   c->d_grid = (const float*)c->grid_buf.p;
   c->has_grid = true;
+  c->int_checked = false;
   c->key_cells = cells;
   c->key_stride = stride;
   c->key_version = version;
@@ -769,6 +882,7 @@ int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) 
   c->info = *info;
   c->d_grid = dev;
   c->has_grid = true;
+  c->int_checked = false;
   c->key_cells = nullptr;
   c->key_version = -1;
   return CSM_OK;

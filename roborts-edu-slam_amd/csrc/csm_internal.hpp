@@ -48,7 +48,13 @@ struct LevelWork {
   int64_t grid_stride;     // floats between consecutive grids (submaps)
   int32_t size_x, size_y;
   float outside;
-  int32_t pad1;
+  int32_t int_mode;        // 1: accumulate the fixed-point copy gridi exactly
+  const int32_t* gridi;    // value * 2^int_exp, exact (see csm_set_grid)
+  double int_scale;        // 2^-int_exp
+  int32_t outside_i;
+  int32_t n_cols;          // n_angles * n_space (column kernel)
+  int32_t ktiles;          // ceil(n_space / KT)
+  int32_t col_blocks;      // ceil(n_cols / 64)
 };
 
 // Argmax partial: best score of a block and its flat candidate index.
@@ -126,6 +132,21 @@ hipError_t launch_score_all(const LevelWork& L, const ScanWork* d_scans,
 hipError_t launch_score_best(const LevelWork& L, const ScanWork* d_scans,
                              const double* d_pts, const AngleEntry* d_angles,
                              BestPartial* d_partials, int cpl, hipStream_t stream);
+// Column kernel (v2): lane = one (theta, x) column of a window, KT rows (y)
+// per lane; L.blocks_per_scan = col_blocks * ktiles. kt = 4, 8 or 16.
+hipError_t launch_score_cols(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
+                             const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
+                             int kt, hipStream_t stream);
+// Grid statistics for the exact integer path (csm_set_grid).
+struct GridStats {
+  int32_t min_gexp;       // every nonzero |v| is a multiple of 2^min_gexp
+  uint32_t max_abs_bits;  // bits of max |v| (positive floats order as integers)
+  int32_t nonfinite;
+  int32_t pad;
+};
+hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hipStream_t stream);
+hipError_t launch_fixed_point(const float* g, int64_t n, float outside, int int_exp, int32_t* gi,
+                              hipStream_t stream);
 // Reduce per-window partials (blocks_per_scan each) to one BestPartial per window.
 hipError_t launch_reduce_best(const BestPartial* d_partials, int32_t blocks_per_scan,
                               int32_t n_windows, BestPartial* d_out, hipStream_t stream);

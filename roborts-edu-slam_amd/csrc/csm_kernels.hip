@@ -105,19 +105,19 @@ __device__ __forceinline__ void accumulate(const LevelWork& L, const ScanWork& S
 }
 
 // Divisor (:659) and centre penalty (:718-745) of one candidate.
-__device__ __forceinline__ double finish_score(const LevelWork& L, const ScanWork& S,
-                                              const Lane& ln) {
-  double score = ln.acc / S.divisor;
+__device__ __forceinline__ double penalized(const LevelWork& L, const ScanWork& S, double acc,
+                                           double x, double y, double angle) {
+  double score = acc / S.divisor;
   if (L.use_penalty) {
     // util::DoubleEqual(score, 0.0) with kDoubleTolerance = 1e-6.
     const bool is_zero = (score < 0.0) ? (score >= -1e-06) : (score <= 1e-06);
     if (!is_zero) {
-      const double dx = ln.x - S.cx, dy = ln.y - S.cy;
+      const double dx = x - S.cx, dy = y - S.cy;
       double d2 = dx * dx + dy * dy;
       d2 *= (L.mres * L.mres);
       double dp = 1.0 - (L.dist_gain * d2 / (L.size / 2));
       dp = dp < 0.5 ? 0.5 : dp;  // std::max(dp, 0.5)
-      double da = ln.angle - S.ct;
+      double da = angle - S.ct;
       da = da * da;
       double ap = 1.0 - (0.25 * da / 0.349);
       ap = ap < 0.9 ? 0.9 : ap;
@@ -125,6 +125,11 @@ __device__ __forceinline__ double finish_score(const LevelWork& L, const ScanWor
     }
   }
   return score;
+}
+
+__device__ __forceinline__ double finish_score(const LevelWork& L, const ScanWork& S,
+                                              const Lane& ln) {
+  return penalized(L, S, ln.acc, ln.x, ln.y, ln.angle);
 }
 
 template <int CPL>
@@ -147,6 +152,173 @@ __global__ __launch_bounds__(kBlock) void score_all_kernel(
 
 __device__ __forceinline__ bool better(double s, int64_t f, double bs, int64_t bf) {
   return (s > bs) || (s == bs && f < bf);
+}
+
+// ---- v2: column kernel ------------------------------------------------------
+// One wave per block; lane = one (theta, x) column of the window, KT rows of
+// y per lane (KT == n_space for the front-end windows, so no row is wasted).
+// Per beam a lane rotates the point once (LUT entry :179-180) and truncates
+// the x index once (:647); only the y index (:648) is per candidate. The beam
+// is wave-uniform (scalar load). The loop body has no branches: all KT loads
+// of a beam are in flight together.
+//
+// INT mode: cells are read from an exact fixed-point copy holding
+// (value - outside) * 2^E through a buffer descriptor; an out-of-grid offset
+// fails the hardware range check and reads 0, i.e. exactly `outside`, which is
+// added back as n_used * outside * 2^E at the end. Sums run in 32-bit chunks
+// folded into 64-bit; csm_set_grid enables the mode only when that integer
+// sum equals the reference's sequential fp64 sum bit for bit.
+template <int KT, bool INT, bool BEST>
+__global__ __launch_bounds__(64) void score_cols_kernel(
+    LevelWork L, const ScanWork* __restrict__ scans, const double2* __restrict__ pts,
+    const AngleEntry* __restrict__ angles, double* __restrict__ out,
+    BestPartial* __restrict__ partials) {
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int win = bid / L.blocks_per_scan;
+  const int r = bid - win * L.blocks_per_scan;
+  const int cb = r / L.ktiles;
+  const int kt = r - cb * L.ktiles;
+  const ScanWork S = scans[win];
+  const int lane = threadIdx.x;
+  const int col = cb * 64 + lane;
+  const bool valid = col < L.n_cols;
+  const int colc = valid ? col : 0;
+  const int a = colc / L.n_space;
+  const int j = colc - a * L.n_space;
+  const AngleEntry ae = angles[S.angle_off + a];
+  const double x = S.x0 + j * L.step_cells;  // :569
+  const int k0 = kt * KT;
+  double y[KT];
+#pragma unroll
+  for (int kk = 0; kk < KT; ++kk) y[kk] = S.y0 + (k0 + kk) * L.step_cells;  // :572
+  const int sx = L.size_x, sy = L.size_y;
+  const int64_t cells = (int64_t)sx * sy;
+  const int64_t gofs = (int64_t)S.grid_index * L.grid_stride;
+  const double2* __restrict__ P = pts + S.pts_off;
+  const int step = S.step;
+  const int n_used = S.n_used;
+  double accd[KT];
+  int64_t acci[KT];
+#pragma unroll
+  for (int kk = 0; kk < KT; ++kk) {
+    accd[kk] = 0.0;
+    acci[kk] = 0;
+  }
+  if (INT) {
+    const int32_t* gi = L.gridi + gofs;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
+    const int32_t* gbase = (const int32_t*)(((uint64_t)hi << 32) | lo);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)gbase, (short)0, (int)(cells * 4), 0x00020000);
+    const int sx4 = sx * 4;
+    // Cells of beam b for every row of this lane (KT buffer loads in flight).
+    // The host guarantees |gy| * 4 * size_x < 2^30 for every candidate of the
+    // window (run_windows), so gy * sx4 never wraps: a row outside [0, sy)
+    // gives an offset < 0 or >= 4*cells, and an x outside [0, sx) adds -2^30;
+    // both fail the descriptor's range check and read 0 (= `outside`).
+    auto load_beam = [&](int b, int32_t (&v)[KT]) {
+      const double2 p = P[(int64_t)b * step];
+      const double lx = ae.cosine * p.x - ae.sine * p.y;
+      const double ly = ae.sine * p.x + ae.cosine * p.y;
+      const int gx = (int)((lx + x) + 0.5);
+      const int gx4 = ((unsigned)gx < (unsigned)sx) ? gx * 4 : -(1 << 30);
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) {
+        const int gy = (int)((ly + y[kk]) + 0.5);
+        v[kk] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, __mul24(gy, sx4) + gx4, 0, 0);
+      }
+    };
+    constexpr int kFold = 32;  // 32 * 2^26 <= 2^31: int32 chunk sums cannot overflow
+    // two register sets, beams alternate between them: beam b+1's loads are
+    // in flight while beam b is summed, with no register copies in between
+    int32_t va[KT], vb[KT];
+    load_beam(0, va);
+    for (int base = 0; base < n_used; base += kFold) {
+      const int nb = min(kFold, n_used - base);
+      int32_t part[KT];
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) part[kk] = 0;
+      for (int b = 0; b < nb; b += 2) {
+        load_beam(min(base + b + 1, n_used - 1), vb);
+        // keep the sums below the next beam's loads: the waits then leave
+        // those KT loads in flight (vmcnt(KT)) instead of draining them
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < KT; ++kk) part[kk] += va[kk];
+        load_beam(min(base + b + 2, n_used - 1), va);
+        __builtin_amdgcn_sched_barrier(0);
+        if (b + 1 < nb) {
+#pragma unroll
+          for (int kk = 0; kk < KT; ++kk) part[kk] += vb[kk];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) acci[kk] += part[kk];
+      // kFold is even, so every chunk but the last ends with va holding beam
+      // base + kFold, the next chunk's first; only the last chunk can be odd.
+    }
+  } else {
+    const float* __restrict__ gf = L.grid + gofs;
+    const float outside = L.outside;
+    auto load_beam = [&](int b, float (&v)[KT]) {
+      const double2 p = P[(int64_t)b * step];
+      const double lx = ae.cosine * p.x - ae.sine * p.y;
+      const double ly = ae.sine * p.x + ae.cosine * p.y;
+      const int gx = (int)((lx + x) + 0.5);
+      const bool inx = (unsigned)gx < (unsigned)sx;
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) {
+        const int gy = (int)((ly + y[kk]) + 0.5);
+        const bool inb = inx & ((unsigned)gy < (unsigned)sy);
+        const float g = gf[inb ? gy * sx + gx : 0];
+        v[kk] = inb ? g : outside;  // :651
+      }
+    };
+    float v[KT];
+    load_beam(0, v);
+    for (int b = 0; b < n_used; ++b) {
+      float vn[KT];
+      load_beam(min(b + 1, n_used - 1), vn);
+#pragma unroll
+      for (int kk = 0; kk < KT; ++kk) {
+        accd[kk] += (double)v[kk];  // :652, beam order
+        v[kk] = vn[kk];
+      }
+    }
+  }
+  const int krem = min(KT, L.n_space - k0);
+  double bs = -1.0e300;
+  int64_t bf = INT64_MAX;
+#pragma unroll
+  for (int kk = 0; kk < KT; ++kk) {
+    if (kk < krem && valid) {
+      const double acc =
+          INT ? (double)(acci[kk] + (int64_t)n_used * L.outside_i) * L.int_scale : accd[kk];
+      const double score = penalized(L, S, acc, x, y[kk], ae.angle);
+      const int64_t flat = ((int64_t)a * L.n_space + j) * L.n_space + (k0 + kk);
+      if (BEST) {
+        if (better(score, flat, bs, bf)) {
+          bs = score;
+          bf = flat;
+        }
+      } else {
+        out[S.out_off + flat] = score;
+      }
+    }
+  }
+  if (BEST) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double os = __shfl_down(bs, off, 64);
+      const int64_t of = __shfl_down(bf, off, 64);
+      if (better(os, of, bs, bf)) {
+        bs = os;
+        bf = of;
+      }
+    }
+    if (lane == 0) partials[(int64_t)win * L.blocks_per_scan + r] = BestPartial{bs, bf};
+  }
 }
 
 template <int CPL>
@@ -274,11 +446,114 @@ hipError_t launch_score_best(const LevelWork& L, const ScanWork* d_scans, const 
   return hipGetLastError();
 }
 
+template <int KT>
+static hipError_t launch_cols_kt(const LevelWork& L, const ScanWork* d_scans, const double2* d_pts,
+                                 const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
+                                 hipStream_t stream) {
+  const int64_t nblk = (int64_t)L.blocks_per_scan * L.n_scans;
+  if (nblk <= 0 || nblk > INT32_MAX) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)nblk), block(64);
+  if (d_partials) {
+    if (L.int_mode)
+      hipLaunchKernelGGL((score_cols_kernel<KT, true, true>), grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_out, d_partials);
+    else
+      hipLaunchKernelGGL((score_cols_kernel<KT, false, true>), grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_out, d_partials);
+  } else {
+    if (L.int_mode)
+      hipLaunchKernelGGL((score_cols_kernel<KT, true, false>), grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_out, d_partials);
+    else
+      hipLaunchKernelGGL((score_cols_kernel<KT, false, false>), grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_out, d_partials);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_score_cols(const LevelWork& L, const ScanWork* d_scans, const double* d_pts_raw,
+                             const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
+                             int kt, hipStream_t stream) {
+  const double2* d_pts = reinterpret_cast<const double2*>(d_pts_raw);
+#define CSM_KT_CASE(K) \
+  case K: return launch_cols_kt<K>(L, d_scans, d_pts, d_angles, d_out, d_partials, stream);
+  switch (kt) {
+    CSM_KT_CASE(1) CSM_KT_CASE(2) CSM_KT_CASE(3) CSM_KT_CASE(4) CSM_KT_CASE(5) CSM_KT_CASE(6)
+    CSM_KT_CASE(7) CSM_KT_CASE(8) CSM_KT_CASE(9) CSM_KT_CASE(10) CSM_KT_CASE(11)
+    CSM_KT_CASE(12) CSM_KT_CASE(13) CSM_KT_CASE(14) CSM_KT_CASE(15) CSM_KT_CASE(16)
+    default: return hipErrorInvalidValue;
+  }
+#undef CSM_KT_CASE
+}
+
 hipError_t launch_reduce_best(const BestPartial* d_partials, int32_t blocks_per_scan,
                               int32_t n_windows, BestPartial* d_out, hipStream_t stream) {
   if (n_windows <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(reduce_best_kernel, dim3(n_windows), dim3(kBlock), 0, stream, d_partials,
                      blocks_per_scan, d_out);
+  return hipGetLastError();
+}
+
+}  // namespace csm
+
+// ---- grid analysis / fixed-point copy (csm_set_grid) -----------------------
+namespace csm {
+namespace {
+
+// Per cell: finite? smallest power of two the value is a multiple of, and |v|.
+__global__ __launch_bounds__(256) void analyze_grid_kernel(const float* __restrict__ g, int64_t n,
+                                                           GridStats* __restrict__ st) {
+  int min_g = INT32_MAX;
+  uint32_t max_bits = 0;
+  int bad = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t u = __float_as_uint(g[i]) & 0x7FFFFFFFu;
+    const uint32_t e = u >> 23, m = u & 0x7FFFFFu;
+    if (e == 0xFF) {
+      bad = 1;
+      continue;
+    }
+    if (u == 0) continue;
+    const uint32_t mm = (e == 0) ? m : (m | 0x800000u);
+    const int gexp = ((e == 0) ? -149 : (int)e - 150) + __builtin_ctz(mm);
+    min_g = min(min_g, gexp);
+    max_bits = max(max_bits, u);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    min_g = min(min_g, __shfl_down(min_g, off, 64));
+    max_bits = max(max_bits, (uint32_t)__shfl_down((int)max_bits, off, 64));
+    bad |= __shfl_down(bad, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&st->min_gexp, min_g);
+    atomicMax(&st->max_abs_bits, max_bits);
+    atomicOr(&st->nonfinite, bad);
+  }
+}
+
+// gi = (g - outside) * 2^E, exact when the host accepted E.
+__global__ __launch_bounds__(256) void fixed_point_kernel(const float* __restrict__ g, int64_t n,
+                                                          float outside, double scale,
+                                                          int32_t* __restrict__ gi) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    gi[i] = (int32_t)(((double)g[i] - (double)outside) * scale);
+}
+
+}  // namespace
+
+hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hipStream_t stream) {
+  const GridStats init{INT32_MAX, 0u, 0, 0};
+  hipError_t e = hipMemcpyAsync(d_stats, &init, sizeof(GridStats), hipMemcpyHostToDevice, stream);
+  if (e != hipSuccess) return e;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(analyze_grid_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0,
+                     stream, g, n, d_stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed_point(const float* g, int64_t n, float outside, int int_exp, int32_t* gi,
+                              hipStream_t stream) {
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(fixed_point_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0,
+                     stream, g, n, outside, ldexp(1.0, int_exp), gi);
   return hipGetLastError();
 }
 

@@ -309,3 +309,54 @@ def test_device_finish_ties_random_windows(ctx):
             r2, pose2, cov2, am2, _ = O.scan_match(m, pts, lv, init, np.eye(3))
             assert (r, am) == (r2, am2), (t, lv)
             assert np.array_equal(pose, pose2) and np.array_equal(cov, cov2)
+
+
+@pytest.mark.parametrize("grid_kind", ["blur", "hostile", "coarse_values"])
+def test_kernel_variants_agree(f1, grid_kind):
+    """v1 (lane per candidate, fp64), v2 fp64 and v2 fixed-point column
+    kernels all reproduce the oracle bit for bit (which one runs depends on
+    the grid: the fixed-point path needs exactly summable cell values)."""
+    import roborts_csm
+    from roborts_csm import worlds
+    from roborts_csm.params import SIM_YAML_LEVELS
+    rng = np.random.default_rng(23)
+    if grid_kind == "blur":
+        g = f1["grid"]
+    elif grid_kind == "hostile":
+        g = worlds.hostile_grid(400, 400)
+    else:
+        g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
+    m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
+    os.environ["CSM_KERNEL"] = "v1"
+    try:
+        c1 = roborts_csm.Context(0)
+    finally:
+        del os.environ["CSM_KERNEL"]
+    c2 = roborts_csm.Context(0)
+    params = [_param(f1["param"])] + list(SIM_YAML_LEVELS) + [l.with_(use_point_size=1081) for l in SIM_YAML_LEVELS]
+    for c in (c1, c2):
+        c.set_grid(_map(g, f1["resolution"], f1["offset"]), force=True)
+        for p in params:
+            sc = c.score_window(f1["points"], p, f1["center"])
+            assert np.array_equal(sc, O.score_window(m, f1["points"], p, f1["center"], sc.size)), (grid_kind, p)
+    c1.close()
+    c2.close()
+
+
+def test_fixed_point_path_out_of_grid(ctx):
+    """Exactly-summable grid (the fixed-point kernel) with endpoints far
+    outside it: the hardware range check must read the outside value."""
+    rng = np.random.default_rng(29)
+    g = rng.choice(np.array([0.3, 0.5, 0.7, 1.0], dtype=np.float32), size=(50, 70))
+    pts = rng.uniform(-400, 400, size=(700, 2))
+    from roborts_csm.params import SIM_YAML_LEVELS
+    ctx.set_grid(_map(g, 0.05, (0.0, 0.0)), force=True)
+    for outside in (0.3, 0.0, 0.5):
+        ctx.set_outside_value(outside)
+        m = O.Map(g, 0.05, (0.0, 0.0), outside=outside)
+        for lv in SIM_YAML_LEVELS:
+            for center in ([25.0, 35.0, 0.3], [-30.0, 90.0, 2.0], [69.6, 0.2, -1.0]):
+                p = lv.with_(use_point_size=700)
+                sc = ctx.score_window(pts, p, np.array(center))
+                assert np.array_equal(sc, O.score_window(m, pts, p, np.array(center), sc.size))
+    ctx.set_outside_value(0.3)
