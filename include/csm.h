@@ -190,6 +190,11 @@ int csm_set_profiling(csm_ctx* ctx, int32_t on);
 /* Copy up to capacity stats; *count = number of distinct kernels seen. */
 int csm_kernel_stats(csm_ctx* ctx, csm_kernel_stat* out, int32_t capacity, int32_t* count);
 
+/* Test hook: the permutation the device finish applies to n keys — its
+ * emulation of libstdc++'s std::sort(greater) (correlate_scan_matcher.h:607).
+ * n <= 10240. order receives n indices. */
+int csm_sort_order(csm_ctx* ctx, const double* keys, int64_t n, int64_t* order);
+
 /* --- raw scoring --------------------------------------------------------- */
 /* Every candidate score of one window (after the centre penalty when
  * param->use_center_penalty), in reference enumeration order. center_map is

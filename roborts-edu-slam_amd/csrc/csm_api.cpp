@@ -18,6 +18,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <memory>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -313,26 +317,93 @@ double complete_window(const csm::FinishOut& o, const CandGeom& C, const csm_par
   return response;
 }
 
-template <class F>
-void parallel_for(int n, int threads, F&& fn) {
-  if (threads <= 1 || n <= 1) {
-    for (int i = 0; i < n; ++i) fn(i);
-    return;
-  }
-  threads = std::min(threads, n);
-  std::atomic<int> next{0};
-  std::vector<std::thread> pool;
-  pool.reserve(threads - 1);
-  auto worker = [&]() {
-    for (;;) {
-      const int i = next.fetch_add(1);
-      if (i >= n) break;
-      fn(i);
+// Persistent worker pool for the per-window host work (angle tables before a
+// launch, completion after it). Workers sleep on a condition variable between
+// jobs; the calling thread works too.
+class ThreadPool {
+ public:
+  explicit ThreadPool(int threads) : n_threads_(std::max(1, threads)) {}
+  ~ThreadPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
     }
-  };
-  for (int t = 0; t < threads - 1; ++t) pool.emplace_back(worker);
-  worker();
-  for (auto& t : pool) t.join();
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+  template <class F>
+  void run(int n, int max_threads, F&& fn) {
+    const int threads = std::min(std::min(n_threads_, max_threads), n);
+    if (threads <= 1) {
+      for (int i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    start(threads - 1);
+    std::function<void(int)> job = std::forward<F>(fn);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &job;
+      n_items_ = n;
+      next_.store(0);
+      active_ = threads - 1;
+      ++epoch_;
+    }
+    cv_.notify_all();
+    drain(job, n);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return active_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void drain(const std::function<void(int)>& job, int n) {
+    for (;;) {
+      const int i = next_.fetch_add(1);
+      if (i >= n) break;
+      job(i);
+    }
+  }
+  void start(int want) {
+    std::lock_guard<std::mutex> lk(mu_);
+    while ((int)workers_.size() < want) {
+      const int id = (int)workers_.size();
+      workers_.emplace_back([this, id] { loop(id); });
+    }
+    wanted_ = want;
+  }
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* job = nullptr;
+      int n = 0;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || (epoch_ != seen && id < wanted_); });
+        if (stop_) return;
+        seen = epoch_;
+        job = job_;
+        n = n_items_;
+      }
+      drain(*job, n);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (--active_ == 0) done_cv_.notify_one();
+      }
+    }
+  }
+  int n_threads_;
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* job_ = nullptr;
+  int n_items_ = 0, active_ = 0, wanted_ = 0;
+  uint64_t epoch_ = 0;
+  std::atomic<int> next_{0};
+  bool stop_ = false;
+};
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 int pick_cpl(int64_t n_cand) {
@@ -350,6 +421,12 @@ struct csm_ctx {
   std::string err;
   float outside = 0.3f;  // kMapUnknownCellProb (slam/slam_processor.h:264)
   int host_threads = 1;
+  std::unique_ptr<ThreadPool> pool;
+  template <class F>
+  void parallel_for(int n, int threads, F&& fn) {
+    if (!pool) pool.reset(new ThreadPool(host_threads));
+    pool->run(n, threads, std::forward<F>(fn));
+  }
 
   csm_map_info info{};
   bool has_grid = false;
@@ -360,8 +437,9 @@ struct csm_ctx {
   int32_t key_sx = -1, key_sy = -1;
 
   DevBuf pts, scans, angles, scores, partials, best, fin;
-  HostBuf h_scores, h_fin;
+  HostBuf h_scores, h_fin, h_angles, h_sw;
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
+  int device_finish_min = 1;  // fewest windows per launch that finish on the device
   bool column_kernel = true;  // CSM_KERNEL=v1 selects the lane-per-candidate kernels
   std::vector<float> h_pack;
 
@@ -471,8 +549,9 @@ enum class Finish { kScoresToHost, kDevice, kBest };
 
 int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
                 const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
-                const std::vector<AngleEntry>& angles, const std::vector<int32_t>& grid_index,
-                BestPartial* best_out, Finish mode = Finish::kScoresToHost) {
+                const AngleEntry* angles, size_t n_angle_entries,
+                const std::vector<int32_t>& grid_index, BestPartial* best_out,
+                Finish mode = Finish::kScoresToHost) {
   if (best_out) mode = Finish::kBest;
   const int nw = (int)plans.size();
   if (nw == 0) return CSM_OK;
@@ -501,10 +580,12 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const int64_t bps = v2 ? col_blocks * ktiles : (D.n_cand + per_block - 1) / per_block;
   if (bps * nw > INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
 
-  std::vector<ScanWork> sw((size_t)nw);
+  hipError_t e;
+  if ((e = c->h_sw.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scans)");
+  ScanWork* sw = (ScanWork*)c->h_sw.p;  // pinned staging
   for (int i = 0; i < nw; ++i) {
     const WindowPlan& W = plans[(size_t)i];
-    ScanWork& s = sw[(size_t)i];
+    ScanWork& s = sw[i];
     s.pts_off = pt_offsets[(size_t)i];
     s.angle_off = W.angle_off;
     s.out_off = (int64_t)i * D.n_cand;
@@ -543,12 +624,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   L.ktiles = ktiles;
   L.col_blocks = (int32_t)col_blocks;
 
-  hipError_t e;
-  if ((e = c->scans.ensure(sw.size() * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
-  if ((e = c->angles.ensure(angles.size() * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
-  if ((e = hipMemcpyAsync(c->scans.p, sw.data(), sw.size() * sizeof(ScanWork), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+  if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
+  if ((e = c->angles.ensure(n_angle_entries * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
+  if ((e = hipMemcpyAsync(c->scans.p, sw, (size_t)nw * sizeof(ScanWork), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
     return c->hip_fail(e, "hipMemcpyAsync(scans)");
-  if ((e = hipMemcpyAsync(c->angles.p, angles.data(), angles.size() * sizeof(AngleEntry), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(c->angles.p, angles, n_angle_entries * sizeof(AngleEntry), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
     return c->hip_fail(e, "hipMemcpyAsync(angles)");
 
   // algorithmic traffic: one fp32 grid read per summed beam per candidate
@@ -632,8 +712,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
 
 // Fill a WindowPlan + its AngleEntry rows (AngleSearchLookUpTable::UpdateLookUpTable
 // :154-172 and ScanMatch :538-548) for a window centred at `center` (map coords).
-bool plan_window(const csm_param& P, const Dims& D, const Geometry& G, int n_points,
-                 const double center[3], std::vector<AngleEntry>& angles, WindowPlan& W) {
+// Writes D.n_angles rows at `out`; the caller sets W.angle_off.
+bool plan_window_into(const csm_param& P, const Dims& D, const Geometry& G, int n_points,
+                      const double center[3], AngleEntry* out, WindowPlan& W) {
   W.center[0] = center[0];
   W.center[1] = center[1];
   W.center[2] = center[2];
@@ -644,15 +725,21 @@ bool plan_window(const csm_param& P, const Dims& D, const Geometry& G, int n_poi
   W.y0 = center[1] - (ssize / G.mres) * 0.5;
   const double offset = (P.search_angle_offset * 2) / 2;
   const double start = center[2] - offset;
-  W.angle_off = (int64_t)angles.size();
   for (int a = 0; a < D.n_angles; ++a) {
-    AngleEntry ae;
+    AngleEntry& ae = out[a];
     ae.angle = start + a * P.search_angle_resolution;
     ae.cosine = std::cos(ae.angle);
     ae.sine = std::sin(ae.angle);
-    angles.push_back(ae);
   }
   return true;
+}
+
+bool plan_window(const csm_param& P, const Dims& D, const Geometry& G, int n_points,
+                 const double center[3], std::vector<AngleEntry>& angles, WindowPlan& W) {
+  const size_t base = angles.size();
+  angles.resize(base + (size_t)D.n_angles);
+  W.angle_off = (int64_t)base;
+  return plan_window_into(P, D, G, n_points, center, angles.data() + base, W);
 }
 
 int upload_points(csm_ctx* c, const double* pts, int64_t n_total) {
@@ -697,30 +784,42 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
   }
   const int nw = (int)scan_of.size();
   if (nw == 0) return CSM_OK;
+  const double t0 = now_ms();
   std::vector<WindowPlan> plans((size_t)nw);
   std::vector<int64_t> pt_off((size_t)nw);
-  std::vector<AngleEntry> angles((size_t)nw * (size_t)D.n_angles);
+  hipError_t he;
+  const size_t n_ang_total = (size_t)nw * (size_t)D.n_angles;
+  if ((he = c->h_angles.ensure(n_ang_total * sizeof(AngleEntry))) != hipSuccess)
+    return c->hip_fail(he, "hipHostMalloc(angles)");
+  AngleEntry* angles = (AngleEntry*)c->h_angles.p;  // pinned: uploaded by DMA
   const int threads = (nw >= 64) ? c->host_threads : 1;
-  parallel_for(nw, threads, [&](int i) {  // host libm cos/sin per window angle
+  c->parallel_for(nw, threads, [&](int i) {  // host libm cos/sin per window angle
     const int s = scan_of[(size_t)i];
     double center[3];
     G.to_map(poses + 3 * s, center);
-    std::vector<AngleEntry> row;
-    row.reserve((size_t)D.n_angles);
-    plan_window(P, D, G, (int)(offsets[s + 1] - offsets[s]), center, row, plans[(size_t)i]);
+    plan_window_into(P, D, G, (int)(offsets[s + 1] - offsets[s]), center,
+                     angles + (size_t)i * (size_t)D.n_angles, plans[(size_t)i]);
     plans[(size_t)i].angle_off = (int64_t)i * D.n_angles;
-    std::copy(row.begin(), row.end(), angles.begin() + (size_t)i * (size_t)D.n_angles);
     pt_off[(size_t)i] = offsets[s];
   });
-  const bool dev = c->device_finish && D.n_cand <= csm::kFinishMaxCand;
-  st = run_windows(c, P, D, G, plans, pt_off, angles, {}, nullptr,
+  // device finish for the front-end windows (and enough of them to fill the
+  // chip); a handful of windows finish faster on the host's std::sort
+  const bool dev = c->device_finish && D.n_cand <= csm::kFinishMaxCand &&
+                   csm::finish_lds_bytes(D.n_cand) <= 160 * 1024 && nw >= c->device_finish_min;
+  const double t1 = now_ms();
+  st = run_windows(c, P, D, G, plans, pt_off, angles, n_ang_total, {}, nullptr,
                    dev ? Finish::kDevice : Finish::kScoresToHost);
   if (st != CSM_OK) return st;
+  const double t2 = now_ms();
+  if (dev)
+    for (int i = 0; i < nw; ++i)
+      if (((const csm::FinishOut*)c->h_fin.p)[i].count < 0)
+        return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
   const double f = P.search_space_resolution / G.mres;
-  parallel_for(nw, threads, [&](int i) {
+  c->parallel_for(nw, threads, [&](int i) {
     thread_local std::vector<Entry> scratch;
     const int s = scan_of[(size_t)i];
-    const CandGeom C{plans[(size_t)i], angles.data() + plans[(size_t)i].angle_off, f, D.n_space,
+    const CandGeom C{plans[(size_t)i], angles + plans[(size_t)i].angle_off, f, D.n_space,
                      (int64_t)D.n_space * D.n_space};
     csm::FinishOut local;
     const csm::FinishOut* o = nullptr;
@@ -733,6 +832,12 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
     if (argmax_flat) argmax_flat[s] = o->front_idx;
     responses[s] = complete_window(*o, C, P, G, poses + 3 * s, covs + 9 * s);
   });
+  if (c->profiling) {
+    const double t3 = now_ms();
+    c->account("host:plan", (float)(t1 - t0), 0.0, 0.0);
+    c->account("host:launch+wait", (float)(t2 - t1), 0.0, 0.0);
+    c->account("host:complete", (float)(t3 - t2), 0.0, 0.0);
+  }
   return CSM_OK;
 }
 
@@ -780,7 +885,11 @@ int csm_create(int device, csm_ctx** out) {
     if (v > 0) threads = v;
   }
   c->host_threads = threads;
-  if (const char* env = std::getenv("CSM_FINISH")) c->device_finish = std::strcmp(env, "host") != 0;
+  if (const char* env = std::getenv("CSM_FINISH")) {
+    c->device_finish = std::strcmp(env, "host") != 0;
+    if (std::strcmp(env, "device") == 0) c->device_finish_min = 1;
+  }
+  if (const char* env = std::getenv("CSM_FINISH_MIN_WINDOWS")) c->device_finish_min = std::max(1, std::atoi(env));
   if (const char* env = std::getenv("CSM_KERNEL")) c->column_kernel = std::strcmp(env, "v1") != 0;
   *out = c;
   return CSM_OK;
@@ -804,6 +913,8 @@ int csm_destroy(csm_ctx* c) {
     c->fin.release();
     c->h_scores.release();
     c->h_fin.release();
+    c->h_angles.release();
+    c->h_sw.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -1013,7 +1124,8 @@ int csm_score_window(csm_ctx* c, const double* pts, int32_t n_points, const csm_
   if (!plan_window(*param, D, G, n_points, center_map, angles, plans[0]))
     return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
   if ((st = upload_points(c, pts, n_points)) != CSM_OK) return st;
-  if ((st = run_windows(c, *param, D, G, plans, {0}, angles, {}, nullptr)) != CSM_OK) return st;
+  if ((st = run_windows(c, *param, D, G, plans, {0}, angles.data(), angles.size(), {}, nullptr)) != CSM_OK)
+    return st;
   std::memcpy(scores_out, c->h_scores.p, (size_t)n_out * sizeof(double));
   return CSM_OK;
 }
@@ -1036,7 +1148,8 @@ int csm_best_window(csm_ctx* c, const double* pts, int32_t n_points, const csm_p
     return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
   if ((st = upload_points(c, pts, n_points)) != CSM_OK) return st;
   BestPartial bp{};
-  if ((st = run_windows(c, *param, D, G, plans, {0}, angles, {}, &bp)) != CSM_OK) return st;
+  if ((st = run_windows(c, *param, D, G, plans, {0}, angles.data(), angles.size(), {}, &bp)) != CSM_OK)
+    return st;
   const WindowPlan& W = plans[0];
   const int64_t ns = D.n_space, nss = ns * ns;
   best->score = bp.score;
@@ -1044,6 +1157,43 @@ int csm_best_window(csm_ctx* c, const double* pts, int32_t n_points, const csm_p
   best->x = W.x0 + (int)((bp.flat / ns) % ns) * (param->search_space_resolution / G.mres);
   best->y = W.y0 + (int)(bp.flat % ns) * (param->search_space_resolution / G.mres);
   best->angle = angles[(size_t)(bp.flat / nss)].angle;
+  return CSM_OK;
+}
+
+int csm_sort_order(csm_ctx* c, const double* keys, int64_t n, int64_t* order) {
+  if (!c || !keys || !order) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (n <= 0 || n > csm::kFinishMaxCand) return c->fail(CSM_ERR_INVALID_ARG, "n must be in [1, 10240]");
+  // one dummy window whose "scores" are the keys: n_space = n keeps every
+  // candidate on angle 0 for the scans that follow the sort
+  ScanWork sw{};
+  AngleEntry ae{0.0, 1.0, 0.0};
+  hipError_t e;
+  if ((e = c->scores.ensure((size_t)n * sizeof(double))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
+  if ((e = c->scans.ensure(sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
+  if ((e = c->angles.ensure(sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
+  if ((e = c->fin.ensure(sizeof(csm::FinishOut) + (size_t)n * sizeof(int32_t))) != hipSuccess)
+    return c->hip_fail(e, "hipMalloc(finish)");
+  if ((e = hipMemcpyAsync(c->scores.p, keys, (size_t)n * sizeof(double), hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(c->scans.p, &sw, sizeof(sw), hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(c->angles.p, &ae, sizeof(ae), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(sort inputs)");
+  csm::FinishArgs A{};
+  A.n_cand = n;
+  A.n_space = (int32_t)n;
+  A.step_cells = 1.0;
+  A.lin_tol = 1.0;
+  int32_t* d_order = (int32_t*)((char*)c->fin.p + sizeof(csm::FinishOut));
+  A.order_out = d_order;
+  if ((e = csm::launch_finish(A, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
+                              (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, 1, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "finish_kernel");
+  std::vector<int32_t> o((size_t)n);
+  if ((e = hipMemcpyAsync(o.data(), d_order, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(order)");
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize");
+  for (int64_t i = 0; i < n; ++i) order[i] = o[(size_t)i];
   return CSM_OK;
 }
 

@@ -68,7 +68,7 @@ constexpr int kChunk = 1024;     // beams staged in LDS per pass (16 KB)
 
 // ---- device finish (csm_finish.hip) -------------------------------------
 constexpr int kCovPoints = 20;          // kMaxVarianceUsePointSize (:1033)
-constexpr int64_t kFinishMaxCand = 12288;  // windows above this finish on the host
+constexpr int64_t kFinishMaxCand = 10240;  // windows above this finish on the host (LDS: 160 KB)
 
 struct FinishArgs {
   int64_t n_cand;
@@ -76,6 +76,7 @@ struct FinishArgs {
   int32_t pad;
   double step_cells;   // res / map_resolution
   double lin_tol;      // search_space_resolution / map_resolution (:840,:852)
+  int32_t* order_out;  // optional: the sorted permutation, n_cand per window
 };
 
 // What the host needs to complete BasedCorrelationScanMatch::ScanMatch for
@@ -93,29 +94,30 @@ struct FinishOut {
   double ang_score[kCovPoints];
 };
 
+constexpr int kFinishWaveScratch = 640;  // bytes of per-wave scratch (4 waves)
+
 struct FinishLayout {
-  int cap, nwords;
-  size_t keys, vals, lpos, rpos, bounds, stack, total;
+  size_t wave_scratch, keys, vals, lpos, rpos, stack, total;
 };
 
-// LDS carve of the finish kernel for n candidates (16-byte aligned pieces).
+// LDS carve of the finish kernel for n candidates (16-byte aligned pieces):
+// misc | 4 wave scratches | keys f64[n] | vals u16[n] | lpos u16[n] | rpos u16[n]
+// | shared segment stack.
 constexpr FinishLayout finish_layout(int64_t n) {
   FinishLayout L{};
-  L.cap = (int)(n / 2 + 2);
-  L.nwords = (int)((n + 32) / 32);
-  size_t o = 64;  // misc: stack pointer + best (x, y)
+  size_t o = 64;  // misc: lock, stack top, pending count, best (x, y)
+  L.wave_scratch = o;
+  o += 4 * (size_t)kFinishWaveScratch;
   L.keys = o;
   o += (size_t)n * 8;
   L.vals = o;
   o += ((size_t)n * 2 + 15) & ~(size_t)15;
   L.lpos = o;
-  o += ((size_t)(L.cap + 1) * 2 + 15) & ~(size_t)15;
+  o += ((size_t)n * 2 + 15) & ~(size_t)15;
   L.rpos = o;
-  o += ((size_t)(L.cap + 1) * 2 + 15) & ~(size_t)15;
-  L.bounds = o;
-  o += ((size_t)L.nwords * 4 + 15) & ~(size_t)15;
+  o += ((size_t)n * 2 + 15) & ~(size_t)15;
   L.stack = o;
-  o += 64 * 12;  // segment stack: depth <= 2*floor(log2 n) + 2 entries
+  o += ((size_t)(n / 16 + 64) * 12 + 15) & ~(size_t)15;  // live segments
   L.total = o;
   return L;
 }

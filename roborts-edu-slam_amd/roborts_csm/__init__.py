@@ -253,6 +253,13 @@ class Context:
                                                   _dptr(covs), _dptr(scores)))
         return scores
 
+    def sort_order(self, keys) -> np.ndarray:
+        """Device emulation of std::sort(greater) on keys (test hook)."""
+        k = np.ascontiguousarray(keys, dtype=np.float64)
+        out = np.empty(k.size, dtype=np.int64)
+        self._check(_lib.csm_sort_order(self._h, _dptr(k), k.size, _i64ptr(out)))
+        return out
+
     def set_profiling(self, on: bool = True):
         self._check(_lib.csm_set_profiling(self._h, 1 if on else 0))
 

@@ -27,7 +27,7 @@ EXPORTED = (
     "csm_window_dims", "csm_scan_match", "csm_scan_matchers",
     "csm_scan_match_batch", "csm_scan_matchers_batch", "csm_score_window",
     "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded",
-    "csm_set_profiling", "csm_kernel_stats",
+    "csm_set_profiling", "csm_kernel_stats", "csm_sort_order",
 )
 
 
@@ -105,6 +105,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_scan_matchers_loaded": (C.c_int, [_ctx, C.POINTER(CsmParam), C.c_int32, _dp, _dp, _dp]),
         "csm_set_profiling": (C.c_int, [_ctx, C.c_int32]),
         "csm_kernel_stats": (C.c_int, [_ctx, C.POINTER(CsmKernelStat), C.c_int32, _i32p]),
+        "csm_sort_order": (C.c_int, [_ctx, _dp, C.c_int64, _i64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -360,3 +360,32 @@ def test_fixed_point_path_out_of_grid(ctx):
                 sc = ctx.score_window(pts, p, np.array(center))
                 assert np.array_equal(sc, O.score_window(m, pts, p, np.array(center), sc.size))
     ctx.set_outside_value(0.3)
+
+
+def _killer(n):
+    """Median-of-3 killer-ish sequences that drive introsort to its depth limit."""
+    k = np.zeros(n)
+    half = n // 2
+    for i in range(half):
+        k[2 * i] = i + 1
+        k[2 * i + 1] = half + i + 1
+    return k[::-1].copy()
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_device_sort_matches_libstdcxx(ctx, seed):
+    """The finish kernel's sort == libstdc++ std::sort(greater), ties and
+    depth-limit heap sort included."""
+    rng = np.random.default_rng(seed)
+    cases = [np.zeros(5070), np.ones(17), (np.arange(5070) % 2).astype(float), _killer(4096),
+             _killer(5070), np.arange(10240, dtype=float), np.arange(10240, dtype=float)[::-1].copy()]
+    for t in range(40):
+        n = int(rng.integers(1, 10241))
+        k = rng.integers(0, int(rng.integers(1, 80)), size=n).astype(float)
+        if t % 3 == 0:
+            k = rng.random(n)
+        if t % 5 == 0:
+            k = np.sort(k)
+        cases.append(k)
+    for k in cases:
+        assert np.array_equal(ctx.sort_order(k), O.std_sort_order(k)), k.size
