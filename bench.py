@@ -181,7 +181,8 @@ def main():
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            tj = json.load(f)  # tools/pmc_traffic.py output, keyed by kernel
+        traffic = tj.get(dom["name"], {}).get("hbm_bytes_per_launch")
     kernel_total_ms = sum(s["total_ms"] for s in kstats)
     kernel_scorings = sum(s["scorings"] for s in kstats)
 

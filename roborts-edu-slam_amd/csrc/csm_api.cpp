@@ -441,12 +441,14 @@ struct csm_ctx {
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
   int device_finish_min = 1;  // fewest windows per launch that finish on the device
   bool column_kernel = true;  // CSM_KERNEL=v1 selects the lane-per-candidate kernels
+  bool row_kernel = true;     // CSM_KERNEL=v2 (or v1) turns the row-segment kernel off
   std::vector<float> h_pack;
 
   // exact fixed-point copy of the grid (ensure_int_grid)
   DevBuf gridi, gstats;
   bool int_checked = false, int_ok = false;
   int int_exp = 0;
+  int32_t pitch = 0;  // gridi row pitch (cells)
   double int_max_abs = 0.0;  // max |cell| (and |outside|) for the per-launch exactness bound
   int32_t outside_i = 0;
   double pts_maxabs = 0.0;   // max |x|+|y| of the resident points (NaN: unbounded)
@@ -531,10 +533,16 @@ int ensure_int_grid(csm_ctx* c) {
   const int E = (min_g == INT32_MAX) ? 0 : std::max(0, -min_g);
   if (E > 60) return CSM_OK;
   const double scale = std::ldexp(1.0, E);
-  if (((double)maxv + std::fabs((double)c->outside)) * scale > std::ldexp(1.0, 26)) return CSM_OK;
-  if ((e = c->gridi.ensure((size_t)n * sizeof(int32_t))) != hipSuccess) return c->hip_fail(e, "hipMalloc(gridi)");
-  if ((e = csm::launch_fixed_point(c->d_grid, n, c->outside, E, (int32_t*)c->gridi.p, c->stream)) != hipSuccess)
+  // strict: |v - outside| * 2^E <= 2^26 - 1, so 32 of them fit an int32 chunk
+  if (((double)maxv + std::fabs((double)c->outside)) * scale >= std::ldexp(1.0, 26)) return CSM_OK;
+  const int32_t pitch = (c->info.size_x + 3) & ~3;  // 16-byte aligned rows
+  const int64_t ni = (int64_t)pitch * c->info.size_y;
+  if (ni * 4 > 0x7F000000LL) return CSM_OK;  // buffer byte offsets (+ the kernels' bad offset) < 2^31
+  if ((e = c->gridi.ensure((size_t)ni * sizeof(int32_t))) != hipSuccess) return c->hip_fail(e, "hipMalloc(gridi)");
+  if ((e = csm::launch_fixed_point(c->d_grid, c->info.size_x, c->info.size_y, pitch, c->outside, E,
+                                   (int32_t*)c->gridi.p, c->stream)) != hipSuccess)
     return c->hip_fail(e, "fixed_point_kernel");
+  c->pitch = pitch;
   c->int_exp = E;
   c->int_max_abs = vmax;
   c->outside_i = (int32_t)((double)c->outside * scale);
@@ -572,12 +580,25 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
                                  std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
     const double R = c->pts_maxabs * (1.0 + 1e-9) + span + 2.0;
-    if (!(R * 4.0 * (double)c->info.size_x < std::ldexp(1.0, 30))) use_int = false;
+    if (!(R * 4.0 * (double)c->pitch < std::ldexp(1.0, 30))) use_int = false;
     if ((double)W.n_used * c->int_max_abs * std::ldexp(1.0, c->int_exp) > std::ldexp(1.0, 53)) use_int = false;
+  }
+  // v3 row-segment kernel: fixed-point grid and an instantiation whose row
+  // segment covers the x-span of a group, (n_space-1)*f cells (+2 for the
+  // truncations); the kernel re-checks and recomputes exactly if exceeded
+  int rows_sq = 0;
+  if (use_int && c->row_kernel && D.n_space <= 64) {
+    const double span = (double)(D.n_space - 1) * f;
+    // distinct columns of a group <= floor(span) + 2
+    rows_sq = csm::rows_pick_sq(D.n_space, (int)std::floor(span * (1.0 + 1e-9) + 1e-9) + 2);
+    if (c->info.size_x < 4 * rows_sq) rows_sq = 0;
   }
   const int cpl = pick_cpl(D.n_cand);
   const int64_t per_block = (int64_t)csm::kBlock * cpl;
-  const int64_t bps = v2 ? col_blocks * ktiles : (D.n_cand + per_block - 1) / per_block;
+  const int64_t rows_groups = rows_sq ? 64 / D.n_space : 1;
+  const int64_t bps = rows_sq ? (D.n_angles + rows_groups - 1) / rows_groups
+                      : v2    ? col_blocks * ktiles
+                              : (D.n_cand + per_block - 1) / per_block;
   if (bps * nw > INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
 
   hipError_t e;
@@ -623,6 +644,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   L.n_cols = (int32_t)n_cols;
   L.ktiles = ktiles;
   L.col_blocks = (int32_t)col_blocks;
+  L.pitch = c->pitch;
+  L.gridi_stride = (int64_t)c->pitch * c->info.size_y;
 
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
   if ((e = c->angles.ensure(n_angle_entries * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
@@ -637,7 +660,10 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const double alg_bytes = beams * (double)D.n_cand * 4.0;
   const double scorings = (double)nw * (double)D.n_cand;
   char kname[48];
-  if (v2)
+  if (rows_sq)
+    std::snprintf(kname, sizeof(kname), "score_rows_kernel<%d,%d,%s>", D.n_space, rows_sq,
+                  best_out ? "best" : "all");
+  else if (v2)
     std::snprintf(kname, sizeof(kname), "score_cols_kernel<%d,%s,%s>", kt, use_int ? "int" : "f64",
                   best_out ? "best" : "all");
   else
@@ -647,7 +673,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
-    if (v2)
+    if (rows_sq)
+      e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                 (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr,
+                                 D.n_space, rows_sq, c->stream);
+    else if (v2)
       e = csm::launch_score_cols(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, kt,
                                  c->stream);
@@ -681,7 +711,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     const size_t pbytes = (size_t)nw * (size_t)bps * sizeof(BestPartial);
     if ((e = c->partials.ensure(pbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(partials)");
     if ((e = c->best.ensure((size_t)nw * sizeof(BestPartial))) != hipSuccess) return c->hip_fail(e, "hipMalloc(best)");
-    if (v2)
+    if (rows_sq)
+      e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                 (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
+                                 D.n_space, rows_sq, c->stream);
+    else if (v2)
       e = csm::launch_score_cols(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
                                  kt, c->stream);
@@ -890,7 +924,10 @@ int csm_create(int device, csm_ctx** out) {
     if (std::strcmp(env, "device") == 0) c->device_finish_min = 1;
   }
   if (const char* env = std::getenv("CSM_FINISH_MIN_WINDOWS")) c->device_finish_min = std::max(1, std::atoi(env));
-  if (const char* env = std::getenv("CSM_KERNEL")) c->column_kernel = std::strcmp(env, "v1") != 0;
+  if (const char* env = std::getenv("CSM_KERNEL")) {
+    c->column_kernel = std::strcmp(env, "v1") != 0;
+    c->row_kernel = std::strcmp(env, "v1") != 0 && std::strcmp(env, "v2") != 0;
+  }
   *out = c;
   return CSM_OK;
 }

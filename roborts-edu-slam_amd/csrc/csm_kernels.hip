@@ -192,7 +192,6 @@ __global__ __launch_bounds__(64) void score_cols_kernel(
 #pragma unroll
   for (int kk = 0; kk < KT; ++kk) y[kk] = S.y0 + (k0 + kk) * L.step_cells;  // :572
   const int sx = L.size_x, sy = L.size_y;
-  const int64_t cells = (int64_t)sx * sy;
   const int64_t gofs = (int64_t)S.grid_index * L.grid_stride;
   const double2* __restrict__ P = pts + S.pts_off;
   const int step = S.step;
@@ -205,17 +204,17 @@ __global__ __launch_bounds__(64) void score_cols_kernel(
     acci[kk] = 0;
   }
   if (INT) {
-    const int32_t* gi = L.gridi + gofs;
+    const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
     const int32_t* gbase = (const int32_t*)(((uint64_t)hi << 32) | lo);
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)gbase, (short)0, (int)(cells * 4), 0x00020000);
-    const int sx4 = sx * 4;
+        __builtin_amdgcn_make_buffer_rsrc((void*)gbase, (short)0, (int)(L.gridi_stride * 4), 0x00020000);
+    const int sx4 = L.pitch * 4;  // row stride of gridi (bytes)
     // Cells of beam b for every row of this lane (KT buffer loads in flight).
-    // The host guarantees |gy| * 4 * size_x < 2^30 for every candidate of the
+    // The host guarantees |gy| * 4 * pitch < 2^30 for every candidate of the
     // window (run_windows), so gy * sx4 never wraps: a row outside [0, sy)
-    // gives an offset < 0 or >= 4*cells, and an x outside [0, sx) adds -2^30;
+    // gives an offset < 0 or >= 4*pitch*sy, and an x outside [0, sx) adds -2^30;
     // both fail the descriptor's range check and read 0 (= `outside`).
     auto load_beam = [&](int b, int32_t (&v)[KT]) {
       const double2 p = P[(int64_t)b * step];
@@ -318,6 +317,192 @@ __global__ __launch_bounds__(64) void score_cols_kernel(
       }
     }
     if (lane == 0) partials[(int64_t)win * L.blocks_per_scan + r] = BestPartial{bs, bf};
+  }
+}
+
+// ---- v3: row-segment kernel (INT mode) -------------------------------------
+// For one beam and one angle the endpoint cells of a window's candidates form
+// a separable set: ix depends only on the x step j, iy only on the y step k
+// (:647-648). With lane (theta, r) of an angle group of NS lanes:
+//   * the group's NS grid rows iy_r are each needed over the same short x-span
+//     [xs, xs + SEG) (SEG = 4*SQ cells > (n_space-1)*f + 1, chosen by the host),
+//     so a wave fetches its R = G*NS row segments as R*SQ 16-byte pieces; the
+//     pieces are dealt to lanes row-major (lane l of load instruction i takes
+//     piece 64*i + l), so one instruction covers ~64/SQ whole row segments and
+//     touches few cache lines (a lane-per-row deal made every lane hit its own
+//     line: 64 lines per instruction, measured slower than v2). Each piece's
+//     row address comes from its owner lane by ds_bpermute, and the pieces are
+//     parked in an LDS tile, one row per segment;
+//   * lane (theta, j = r) computes its exact ix_r (reference arithmetic) and
+//     reads column ix_r - xs of each of its group's NS tile rows: NS LDS reads
+//     at immediate offsets.
+// Per beam a wave issues ceil(R*SQ/64) gathers for R*NS candidates (v2: NS
+// gathers for 64 candidates; TA-busy ~85% there, profiles/r01). A cell outside
+// the grid reads 0 (= `outside`, pre-subtracted): rows through the buffer range
+// check, x through a zero pad column of the tile. A lane whose x-span ever
+// exceeds SEG (impossible for the host's SEG; kept as a guard) is recomputed
+// exactly after the loop.
+template <int NS, int SQ, bool BEST>
+__global__ __launch_bounds__(64) void score_rows_kernel(
+    LevelWork L, const ScanWork* __restrict__ scans, const double2* __restrict__ pts,
+    const AngleEntry* __restrict__ angles, double* __restrict__ out,
+    BestPartial* __restrict__ partials) {
+  constexpr int G = 64 / NS;           // angle groups per wave
+  constexpr int R = G * NS;            // row segments per beam
+  constexpr int SEG = 4 * SQ;          // cells per row segment
+  constexpr int RS = SEG + 4;          // tile row stride: segment + zero pad (16-byte multiple)
+  constexpr int NP = R * SQ;           // 16-byte pieces per beam
+  constexpr int NI = (NP + 63) / 64;   // gathers per beam
+  typedef int32_t v4i __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) int32_t tile[(R + 1) * RS];  // + a sink row
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int win = bid / L.blocks_per_scan;
+  const int blk = bid - win * L.blocks_per_scan;
+  const ScanWork S = scans[win];
+  const int lane = threadIdx.x;
+  const int g = lane / NS;
+  const int r = lane - g * NS;
+  const int a_raw = blk * G + g;
+  const bool valid = (g < G) && (a_raw < L.n_angles);
+  const int a = valid ? a_raw : 0;
+  const int row0 = (g < G) ? g * NS : 0;  // tile row of this group's k = 0
+  const AngleEntry ae = angles[S.angle_off + a];
+  const double f = L.step_cells;
+  const double x_0 = S.x0 + 0 * f;  // :569 at j = 0
+  const double x_r = S.x0 + r * f;  // :569 at j = r
+  const double y_r = S.y0 + r * f;  // :572 at k = r
+  const int sx = L.size_x, sy = L.size_y;
+  const int pitch4 = L.pitch * 4;  // gridi row stride in bytes
+  const int xs_max = sx - SEG;     // host: sx >= SEG
+  const double2* __restrict__ P = pts + S.pts_off;
+  const int step = S.step;
+  const int n_used = S.n_used;
+  const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
+  const int32_t* gbase = (const int32_t*)(((uint64_t)hi << 32) | lo);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)gbase, (short)0, (int)(L.gridi_stride * 4), 0x00020000);
+  constexpr int kBadOff = 0x7F800000;  // >= 4*pitch*sy (host), + 16*SQ still < 2^31: reads 0
+
+  // This lane's piece of gather i: owner row (bpermute source), byte offset
+  // inside the segment, and its tile slot (idle pieces go to the sink row).
+  int src4[NI], qoff[NI], dst[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int p = i * 64 + lane;
+    const bool act = p < NP;
+    const int rho = act ? p / SQ : 0;
+    const int q = act ? p - rho * SQ : 0;
+    src4[i] = rho * 4;
+    qoff[i] = act ? 16 * q : -1;
+    dst[i] = act ? (rho * RS + 4 * q) * 4 : R * RS * 4;
+  }
+  if (lane < R) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tile[lane * RS + SEG + q] = 0;  // zero pad column
+  }
+
+  // Beam b: gather this lane's pieces, and the LDS byte address of its own
+  // column (the pad column when x is off the grid).
+  auto prep = [&](int b, v4i (&v)[NI], int& rd, bool& bad) {
+    const double2 p = P[(int64_t)b * step];
+    const double lx = ae.cosine * p.x - ae.sine * p.y;  // :179
+    const double ly = ae.sine * p.x + ae.cosine * p.y;  // :180
+    const int ix0 = (int)((lx + x_0) + 0.5);
+    const int ixr = (int)((lx + x_r) + 0.5);
+    const int iyr = (int)((ly + y_r) + 0.5);
+    const int xs = min(max(ix0, 0), xs_max);
+    const int rowoff = ((unsigned)iyr < (unsigned)sy) ? __mul24(iyr, pitch4) + xs * 4 : kBadOff;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int o = __builtin_amdgcn_ds_bpermute(src4[i], rowoff);
+      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, qoff[i] < 0 ? kBadOff : o + qoff[i], 0, 0);
+    }
+    const int pos = ixr - xs;
+    const bool inx = (unsigned)ixr < (unsigned)sx;
+    bad |= inx & ((unsigned)pos >= (unsigned)SEG);
+    rd = (row0 * RS + (inx ? pos : SEG)) * 4;
+  };
+  auto consume = [&](const v4i (&v)[NI], int rd, int32_t (&part)[NS]) {
+    char* tb = reinterpret_cast<char*>(tile);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) *reinterpret_cast<v4i*>(tb + dst[i]) = v[i];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) part[k] += *reinterpret_cast<const int32_t*>(tb + rd + k * RS * 4);
+  };
+
+  int64_t acci[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) acci[k] = 0;
+  bool bad = false;
+  constexpr int kFold = 32;  // 32 * (2^26 - 1) < 2^31 (ensure_int_grid)
+  v4i va[NI], vb[NI];
+  int ra = 0, rb = 0;
+  prep(0, va, ra, bad);
+  for (int base = 0; base < n_used; base += kFold) {
+    const int nb = min(kFold, n_used - base);
+    int32_t part[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) part[k] = 0;
+    for (int b = 0; b < nb; b += 2) {
+      prep(min(base + b + 1, n_used - 1), vb, rb, bad);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(va, ra, part);
+      prep(min(base + b + 2, n_used - 1), va, ra, bad);
+      __builtin_amdgcn_sched_barrier(0);
+      if (b + 1 < nb) consume(vb, rb, part);
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k) acci[k] += part[k];
+  }
+  if (bad) {  // guard (never taken for the host's SEG): exact per-cell recompute
+#pragma unroll
+    for (int k = 0; k < NS; ++k) acci[k] = 0;
+    for (int b = 0; b < n_used; ++b) {
+      const double2 p = P[(int64_t)b * step];
+      const double lx = ae.cosine * p.x - ae.sine * p.y;
+      const double ly = ae.sine * p.x + ae.cosine * p.y;
+      const int gx = (int)((lx + x_r) + 0.5);
+      const int gx4 = ((unsigned)gx < (unsigned)sx) ? gx * 4 : -(1 << 30);
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        const int gy = (int)((ly + (S.y0 + k * f)) + 0.5);
+        const int o = ((unsigned)gy < (unsigned)sy && gx4 >= 0) ? __mul24(gy, pitch4) + gx4 : kBadOff;
+        acci[k] += __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
+      }
+    }
+  }
+  double bs = -1.0e300;
+  int64_t bf = INT64_MAX;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    if (valid) {
+      const double acc = (double)(acci[k] + (int64_t)n_used * L.outside_i) * L.int_scale;
+      const double yk = S.y0 + k * f;  // :572
+      const double score = penalized(L, S, acc, x_r, yk, ae.angle);
+      const int64_t flat = ((int64_t)a * NS + r) * NS + k;
+      if (BEST) {
+        if (better(score, flat, bs, bf)) {
+          bs = score;
+          bf = flat;
+        }
+      } else {
+        out[S.out_off + flat] = score;
+      }
+    }
+  }
+  if (BEST) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double os = __shfl_down(bs, o, 64);
+      const int64_t of = __shfl_down(bf, o, 64);
+      if (better(os, of, bs, bf)) {
+        bs = os;
+        bf = of;
+      }
+    }
+    if (lane == 0) partials[(int64_t)win * L.blocks_per_scan + blk] = BestPartial{bs, bf};
   }
 }
 
@@ -482,6 +667,40 @@ hipError_t launch_score_cols(const LevelWork& L, const ScanWork* d_scans, const 
 #undef CSM_KT_CASE
 }
 
+// Row-segment instantiations (n_space, SQ): the sim-YAML levels (13,4) (11,2)
+// (3,1), param_config.h's coarse (9,5) and config 1's window (21,6) at 5 cm.
+#define CSM_ROWS_LIST(X) X(13, 4) X(11, 2) X(3, 1) X(9, 5) X(21, 6)
+
+int rows_pick_sq(int ns, int need_seg) {
+#define CSM_ROWS_PICK(N, Q) \
+  if (ns == N && 4 * Q >= need_seg) return Q;
+  CSM_ROWS_LIST(CSM_ROWS_PICK)
+#undef CSM_ROWS_PICK
+  return 0;
+}
+
+hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const double* d_pts_raw,
+                             const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
+                             int ns, int sq, hipStream_t stream) {
+  const double2* d_pts = reinterpret_cast<const double2*>(d_pts_raw);
+  const int64_t nblk = (int64_t)L.blocks_per_scan * L.n_scans;
+  if (nblk <= 0 || nblk > INT32_MAX || !L.int_mode || L.size_x < 4 * sq) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)nblk), block(64);
+#define CSM_ROWS_CASE(N, Q)                                                                       \
+  if (ns == N && sq == Q) {                                                                       \
+    if (d_partials)                                                                               \
+      hipLaunchKernelGGL((score_rows_kernel<N, Q, true>), grid, block, 0, stream, L, d_scans,    \
+                         d_pts, d_angles, d_out, d_partials);                                     \
+    else                                                                                          \
+      hipLaunchKernelGGL((score_rows_kernel<N, Q, false>), grid, block, 0, stream, L, d_scans,   \
+                         d_pts, d_angles, d_out, d_partials);                                     \
+    return hipGetLastError();                                                                     \
+  }
+  CSM_ROWS_LIST(CSM_ROWS_CASE)
+#undef CSM_ROWS_CASE
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_reduce_best(const BestPartial* d_partials, int32_t blocks_per_scan,
                               int32_t n_windows, BestPartial* d_out, hipStream_t stream) {
   if (n_windows <= 0) return hipErrorInvalidValue;
@@ -529,12 +748,17 @@ __global__ __launch_bounds__(256) void analyze_grid_kernel(const float* __restri
 }
 
 // gi = (g - outside) * 2^E, exact when the host accepted E.
-__global__ __launch_bounds__(256) void fixed_point_kernel(const float* __restrict__ g, int64_t n,
-                                                          float outside, double scale,
-                                                          int32_t* __restrict__ gi) {
+// gi[y * pitch + x] = (g[y * sx + x] - outside) * 2^E; pad cells (x >= sx) = 0.
+__global__ __launch_bounds__(256) void fixed_point_kernel(const float* __restrict__ g, int32_t sx,
+                                                          int32_t sy, int32_t pitch, float outside,
+                                                          double scale, int32_t* __restrict__ gi) {
+  const int64_t n = (int64_t)pitch * sy;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    gi[i] = (int32_t)(((double)g[i] - (double)outside) * scale);
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t y = i / pitch;
+    const int x = (int)(i - y * pitch);
+    gi[i] = (x < sx) ? (int32_t)(((double)g[y * sx + x] - (double)outside) * scale) : 0;
+  }
 }
 
 }  // namespace
@@ -549,11 +773,12 @@ hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hi
   return hipGetLastError();
 }
 
-hipError_t launch_fixed_point(const float* g, int64_t n, float outside, int int_exp, int32_t* gi,
-                              hipStream_t stream) {
+hipError_t launch_fixed_point(const float* g, int32_t sx, int32_t sy, int32_t pitch, float outside,
+                              int int_exp, int32_t* gi, hipStream_t stream) {
+  const int64_t n = (int64_t)pitch * sy;
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(fixed_point_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0,
-                     stream, g, n, outside, ldexp(1.0, int_exp), gi);
+                     stream, g, sx, sy, pitch, outside, ldexp(1.0, int_exp), gi);
   return hipGetLastError();
 }
 

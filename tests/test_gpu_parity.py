@@ -231,6 +231,28 @@ def test_batch_three_level_bit_exact(ctx, world2000, which):
     assert np.median(err) < 0.05
 
 
+def test_headline_runs_row_segment_kernels(ctx, world2000):
+    """The config-2 levels run on the v3 row-segment kernels (not a fallback),
+    and the device finish, and the result is the oracle's bit for bit."""
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+    n = 24
+    poses = np.ascontiguousarray(b.init_poses[:n].copy())
+    covs = np.tile(np.eye(3).reshape(1, 9), (n, 1))
+    ctx.set_profiling(True)
+    s = ctx.scan_matchers_batch(b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(), poses, covs)
+    names = {k["name"] for k in ctx.kernel_stats()}
+    ctx.set_profiling(False)
+    for want in ("score_rows_kernel<13,4,all>", "score_rows_kernel<11,2,all>",
+                 "score_rows_kernel<3,1,all>", "finish_kernel"):
+        assert want in names, names
+    m = O.Map(w.grid, w.resolution, w.offset)
+    s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(),
+                                       b.init_poses[:n], np.tile(np.eye(3).reshape(1, 9), (n, 1)))
+    assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2)
+
+
 def test_batch_single_level_matches_single_calls(ctx, world2000):
     from roborts_csm.params import SIM_YAML_LEVELS
     w, b = world2000
@@ -318,7 +340,7 @@ def test_kernel_variants_agree(f1, grid_kind):
     the grid: the fixed-point path needs exactly summable cell values)."""
     import roborts_csm
     from roborts_csm import worlds
-    from roborts_csm.params import SIM_YAML_LEVELS
+    from roborts_csm.params import PARAM_CONFIG_LEVELS, SIM_YAML_LEVELS
     rng = np.random.default_rng(23)
     if grid_kind == "blur":
         g = f1["grid"]
@@ -327,20 +349,23 @@ def test_kernel_variants_agree(f1, grid_kind):
     else:
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
-    os.environ["CSM_KERNEL"] = "v1"
-    try:
-        c1 = roborts_csm.Context(0)
-    finally:
-        del os.environ["CSM_KERNEL"]
-    c2 = roborts_csm.Context(0)
+    ctxs = []
+    for kern in ("v1", "v2", None):  # None: default (v3 row-segment where eligible)
+        if kern:
+            os.environ["CSM_KERNEL"] = kern
+        try:
+            ctxs.append(roborts_csm.Context(0))
+        finally:
+            os.environ.pop("CSM_KERNEL", None)
     params = [_param(f1["param"])] + list(SIM_YAML_LEVELS) + [l.with_(use_point_size=1081) for l in SIM_YAML_LEVELS]
-    for c in (c1, c2):
+    params += [l.with_(use_point_size=1081) for l in PARAM_CONFIG_LEVELS]
+    for c in ctxs:
         c.set_grid(_map(g, f1["resolution"], f1["offset"]), force=True)
         for p in params:
             sc = c.score_window(f1["points"], p, f1["center"])
             assert np.array_equal(sc, O.score_window(m, f1["points"], p, f1["center"], sc.size)), (grid_kind, p)
-    c1.close()
-    c2.close()
+    for c in ctxs:
+        c.close()
 
 
 def test_fixed_point_path_out_of_grid(ctx):

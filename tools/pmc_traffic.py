@@ -1,0 +1,74 @@
+"""Turn rocprofv3 --pmc CSV output into per-kernel HBM bytes per launch.
+
+Usage: python tools/pmc_traffic.py OUT.json FETCH_DIR [WRITE_DIR]
+
+Each DIR is a rocprofv3 -d output directory of one `--pmc` pass
+(FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950: TCC slots,
+MI355X_MICROARCH.md "rocprofv3 PMC slots"). Counters are in KiB per dispatch.
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE tallies 128-B
+fabric read requests at 64 B, so the read side is doubled; WRITE_SIZE is
+taken as is. Both raw and corrected figures are written.
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def _short(name: str) -> str:
+    """rocprof's demangled name -> the name csm_kernel_stats reports."""
+    key = "score_cols_kernel<"
+    if key in name:  # template <int KT, bool INT, bool BEST>
+        i = name.index(key) + len(key)
+        kt, integer, best = [a.strip() for a in name[i:name.index(">", i)].split(",")]
+        return (f"score_cols_kernel<{kt},{'int' if integer == 'true' else 'f64'},"
+                f"{'best' if best == 'true' else 'all'}>")
+    for key in ("score_all_kernel<", "score_best_kernel<"):
+        if key in name:
+            i = name.index(key)
+            return name[i:name.index(">", i) + 1]
+    for key in ("finish_kernel", "analyze_grid_kernel", "fixed_point_kernel", "reduce_best_kernel"):
+        if key in name:
+            return key
+    return name[:64]
+
+
+def read_pass(d: str):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    per = defaultdict(lambda: defaultdict(list))
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            per[_short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    out, fetch_dir = sys.argv[1], sys.argv[2]
+    write_dir = sys.argv[3] if len(sys.argv) > 3 else None
+    fp = read_pass(fetch_dir)
+    wp = read_pass(write_dir) if write_dir else {}
+    res = {}
+    for k, ctr in fp.items():
+        f = ctr.get("FETCH_SIZE", [])
+        w = wp.get(k, {}).get("WRITE_SIZE", []) if wp else []
+        fkb = sum(f) / len(f) if f else 0.0
+        wkb = sum(w) / len(w) if w else 0.0
+        res[k] = {
+            "dispatches": len(f),
+            "fetch_kib_raw": fkb,
+            "write_kib_raw": wkb,
+            "hbm_bytes_per_launch": (2.0 * fkb + wkb) * 1024.0,
+            "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B), WRITE_SIZE x1",
+        }
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    for k, v in res.items():
+        print(f"{k:40s} {v['dispatches']:5d} {v['hbm_bytes_per_launch'] / 1e6:12.2f} MB/launch")
+
+
+if __name__ == "__main__":
+    main()
