@@ -441,7 +441,8 @@ struct csm_ctx {
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
   int device_finish_min = 1;  // fewest windows per launch that finish on the device
   bool column_kernel = true;  // CSM_KERNEL=v1 selects the lane-per-candidate kernels
-  bool row_kernel = true;     // CSM_KERNEL=v2 (or v1) turns the row-segment kernel off
+  bool row_kernel = true;     // CSM_KERNEL=v2 (or v1) turns the row-segment kernels off
+  bool row_dma = true;        // CSM_KERNEL=v3: register-staged row segments instead of LDS-DMA
   std::vector<float> h_pack;
 
   // exact fixed-point copy of the grid (ensure_int_grid)
@@ -536,7 +537,7 @@ int ensure_int_grid(csm_ctx* c) {
   // strict: |v - outside| * 2^E <= 2^26 - 1, so 32 of them fit an int32 chunk
   if (((double)maxv + std::fabs((double)c->outside)) * scale >= std::ldexp(1.0, 26)) return CSM_OK;
   const int32_t pitch = (c->info.size_x + 3) & ~3;  // 16-byte aligned rows
-  const int64_t ni = (int64_t)pitch * c->info.size_y;
+  const int64_t ni = (int64_t)pitch * (c->info.size_y + 1);  // + the zero row
   if (ni * 4 > 0x7F000000LL) return CSM_OK;  // buffer byte offsets (+ the kernels' bad offset) < 2^31
   if ((e = c->gridi.ensure((size_t)ni * sizeof(int32_t))) != hipSuccess) return c->hip_fail(e, "hipMalloc(gridi)");
   if ((e = csm::launch_fixed_point(c->d_grid, c->info.size_x, c->info.size_y, pitch, c->outside, E,
@@ -645,7 +646,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   L.ktiles = ktiles;
   L.col_blocks = (int32_t)col_blocks;
   L.pitch = c->pitch;
-  L.gridi_stride = (int64_t)c->pitch * c->info.size_y;
+  L.gridi_stride = (int64_t)c->pitch * (c->info.size_y + 1);
 
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
   if ((e = c->angles.ensure(n_angle_entries * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
@@ -661,8 +662,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const double scorings = (double)nw * (double)D.n_cand;
   char kname[48];
   if (rows_sq)
-    std::snprintf(kname, sizeof(kname), "score_rows_kernel<%d,%d,%s>", D.n_space, rows_sq,
-                  best_out ? "best" : "all");
+    std::snprintf(kname, sizeof(kname), "%s<%d,%d,%s>", c->row_dma ? "score_rowsd_kernel" : "score_rows_kernel",
+                  D.n_space, rows_sq, best_out ? "best" : "all");
   else if (v2)
     std::snprintf(kname, sizeof(kname), "score_cols_kernel<%d,%s,%s>", kt, use_int ? "int" : "f64",
                   best_out ? "best" : "all");
@@ -676,7 +677,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if (rows_sq)
       e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr,
-                                 D.n_space, rows_sq, c->stream);
+                                 D.n_space, rows_sq, c->row_dma, c->stream);
     else if (v2)
       e = csm::launch_score_cols(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, kt,
@@ -714,7 +715,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if (rows_sq)
       e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
-                                 D.n_space, rows_sq, c->stream);
+                                 D.n_space, rows_sq, c->row_dma, c->stream);
     else if (v2)
       e = csm::launch_score_cols(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
@@ -927,6 +928,7 @@ int csm_create(int device, csm_ctx** out) {
   if (const char* env = std::getenv("CSM_KERNEL")) {
     c->column_kernel = std::strcmp(env, "v1") != 0;
     c->row_kernel = std::strcmp(env, "v1") != 0 && std::strcmp(env, "v2") != 0;
+    c->row_dma = std::strcmp(env, "v3") != 0;
   }
   *out = c;
   return CSM_OK;

@@ -56,7 +56,8 @@ struct LevelWork {
   int32_t ktiles;          // ceil(n_space / KT)
   int32_t col_blocks;      // ceil(n_cols / 64)
   int32_t pitch;           // gridi row pitch in cells (size_x rounded up to 4)
-  int64_t gridi_stride;    // int32 cells between consecutive gridi grids (pitch * size_y)
+  int64_t gridi_stride;    // int32 cells between consecutive gridi grids (pitch * (size_y + 1):
+                           // each grid ends with a zero row)
 };
 
 // Argmax partial: best score of a block and its flat candidate index.
@@ -146,9 +147,10 @@ hipError_t launch_score_cols(const LevelWork& L, const ScanWork* d_scans, const 
 // ceil(n_angles / (64/ns)). sq 16-byte loads per row segment (4*sq cells).
 // rows_pick_sq returns the sq of an instantiation with 4*sq >= need_seg, or 0.
 int rows_pick_sq(int ns, int need_seg);
+// dma: v4 (LDS-DMA staging, score_rowsd_kernel) instead of v3 (register staging).
 hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
-                             int ns, int sq, hipStream_t stream);
+                             int ns, int sq, bool dma, hipStream_t stream);
 // Grid statistics for the exact integer path (csm_set_grid).
 struct GridStats {
   int32_t min_gexp;       // every nonzero |v| is a multiple of 2^min_gexp
@@ -157,7 +159,8 @@ struct GridStats {
   int32_t pad;
 };
 hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hipStream_t stream);
-// Row pitch of gridi is a multiple of 4 cells, so 16-byte row segments are aligned.
+// Row pitch of gridi is a multiple of 4 cells, so 16-byte row segments are
+// aligned; size_y + 1 rows are written, the last one zero.
 hipError_t launch_fixed_point(const float* g, int32_t sx, int32_t sy, int32_t pitch, float outside,
                               int int_exp, int32_t* gi, hipStream_t stream);
 // Reduce per-window partials (blocks_per_scan each) to one BestPartial per window.

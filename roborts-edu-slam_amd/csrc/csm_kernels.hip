@@ -354,7 +354,13 @@ __global__ __launch_bounds__(64) void score_rows_kernel(
   constexpr int NP = R * SQ;           // 16-byte pieces per beam
   constexpr int NI = (NP + 63) / 64;   // gathers per beam
   typedef int32_t v4i __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) int32_t tile[(R + 1) * RS];  // + a sink row
+  // Groups are spaced GS floats apart with GS = GT (mod 64): a consumer read
+  // instruction (one k) then puts group g on banks [g*GT, g*GT + NS), disjoint
+  // for the groups of a wave (without the spacing 4 groups shared banks:
+  // SQ_LDS_BANK_CONFLICT was 43% of the kernel's cycles).
+  constexpr int GT = (64 / G) / 4 * 4 < 4 ? 4 : (64 / G) / 4 * 4;
+  constexpr int GS = NS * RS + (((GT - (NS * RS) % 64) % 64) + 64) % 64;
+  __shared__ __attribute__((aligned(16))) int32_t tile[G * GS + RS];  // + a sink row
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int win = bid / L.blocks_per_scan;
   const int blk = bid - win * L.blocks_per_scan;
@@ -365,7 +371,7 @@ __global__ __launch_bounds__(64) void score_rows_kernel(
   const int a_raw = blk * G + g;
   const bool valid = (g < G) && (a_raw < L.n_angles);
   const int a = valid ? a_raw : 0;
-  const int row0 = (g < G) ? g * NS : 0;  // tile row of this group's k = 0
+  const int gbase_f = (g < G) ? g * GS : 0;  // tile float offset of this group's k = 0 row
   const AngleEntry ae = angles[S.angle_off + a];
   const double f = L.step_cells;
   const double x_0 = S.x0 + 0 * f;  // :569 at j = 0
@@ -396,11 +402,12 @@ __global__ __launch_bounds__(64) void score_rows_kernel(
     const int q = act ? p - rho * SQ : 0;
     src4[i] = rho * 4;
     qoff[i] = act ? 16 * q : -1;
-    dst[i] = act ? (rho * RS + 4 * q) * 4 : R * RS * 4;
+    const int rg = rho / NS;
+    dst[i] = act ? (rg * GS + (rho - rg * NS) * RS + 4 * q) * 4 : G * GS * 4;
   }
   if (lane < R) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) tile[lane * RS + SEG + q] = 0;  // zero pad column
+    for (int q = 0; q < 4; ++q) tile[gbase_f + r * RS + SEG + q] = 0;  // zero pad column
   }
 
   // Beam b: gather this lane's pieces, and the LDS byte address of its own
@@ -422,7 +429,7 @@ __global__ __launch_bounds__(64) void score_rows_kernel(
     const int pos = ixr - xs;
     const bool inx = (unsigned)ixr < (unsigned)sx;
     bad |= inx & ((unsigned)pos >= (unsigned)SEG);
-    rd = (row0 * RS + (inx ? pos : SEG)) * 4;
+    rd = (gbase_f + (inx ? pos : SEG)) * 4;
   };
   auto consume = [&](const v4i (&v)[NI], int rd, int32_t (&part)[NS]) {
     char* tb = reinterpret_cast<char*>(tile);
@@ -470,6 +477,192 @@ __global__ __launch_bounds__(64) void score_rows_kernel(
         const int gy = (int)((ly + (S.y0 + k * f)) + 0.5);
         const int o = ((unsigned)gy < (unsigned)sy && gx4 >= 0) ? __mul24(gy, pitch4) + gx4 : kBadOff;
         acci[k] += __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
+      }
+    }
+  }
+  double bs = -1.0e300;
+  int64_t bf = INT64_MAX;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    if (valid) {
+      const double acc = (double)(acci[k] + (int64_t)n_used * L.outside_i) * L.int_scale;
+      const double yk = S.y0 + k * f;  // :572
+      const double score = penalized(L, S, acc, x_r, yk, ae.angle);
+      const int64_t flat = ((int64_t)a * NS + r) * NS + k;
+      if (BEST) {
+        if (better(score, flat, bs, bf)) {
+          bs = score;
+          bf = flat;
+        }
+      } else {
+        out[S.out_off + flat] = score;
+      }
+    }
+  }
+  if (BEST) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double os = __shfl_down(bs, o, 64);
+      const int64_t of = __shfl_down(bf, o, 64);
+      if (better(os, of, bs, bf)) {
+        bs = os;
+        bf = of;
+      }
+    }
+    if (lane == 0) partials[(int64_t)win * L.blocks_per_scan + blk] = BestPartial{bs, bf};
+  }
+}
+
+// ---- v4: row-segment kernel, LDS-DMA staging (INT mode) --------------------
+// v3's data flow with the 16-byte pieces written straight into LDS by
+// global_load_lds_dwordx4 (dest = wave-uniform base + 16 * lane): no VGPR
+// staging and no ds_write_b128 (13 LDS cycles each, the largest LDS cost of
+// v3). Pieces are dealt row-major, so the LDS image is [row][SEG] with rows
+// contiguous; beams alternate between two images (DMA of beam b+1 in flight
+// while beam b is summed, counted vmcnt). DMA has no range check: rows outside
+// the grid point at the zero row the host appends to gridi, columns outside
+// the grid read a zero block.
+template <int NS, int SQ, bool BEST>
+__global__ __launch_bounds__(64) void score_rowsd_kernel(
+    LevelWork L, const ScanWork* __restrict__ scans, const double2* __restrict__ pts,
+    const AngleEntry* __restrict__ angles, double* __restrict__ out,
+    BestPartial* __restrict__ partials) {
+  constexpr int G = 64 / NS;           // angle groups per wave
+  constexpr int R = G * NS;            // row segments per beam
+  constexpr int SEG = 4 * SQ;          // cells per row segment
+  constexpr int NP = R * SQ;           // 16-byte pieces per beam
+  constexpr int NI = (NP + 63) / 64;   // DMA instructions per beam
+  constexpr int IMG = NI * 256;        // ints per image
+  typedef __attribute__((address_space(3))) int32_t lds_i32;
+  // two images as distinct objects, so the compiler's LDS-DMA wait tracking
+  // can tell a read of one from the DMA still writing the other
+  __shared__ __attribute__((aligned(16))) int32_t img0[IMG];
+  __shared__ __attribute__((aligned(16))) int32_t img1[IMG];
+  __shared__ __attribute__((aligned(16))) int32_t zblk[NS * SEG];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int win = bid / L.blocks_per_scan;
+  const int blk = bid - win * L.blocks_per_scan;
+  const ScanWork S = scans[win];
+  const int lane = threadIdx.x;
+  const int g = lane / NS;
+  // idle lanes (g >= G) shadow lane (G-1, NS-1): identical LDS addresses
+  // broadcast instead of adding bank conflicts
+  const int ge = g < G ? g : G - 1;
+  const int r = g < G ? lane - g * NS : NS - 1;
+  const int a_raw = blk * G + ge;
+  const bool valid = (g < G) && (a_raw < L.n_angles);
+  const int a = a_raw < L.n_angles ? a_raw : 0;
+  const AngleEntry ae = angles[S.angle_off + a];
+  const double f = L.step_cells;
+  const double x_0 = S.x0 + 0 * f;  // :569 at j = 0
+  const double x_r = S.x0 + r * f;  // :569 at j = r
+  const double y_r = S.y0 + r * f;  // :572 at k = r
+  const int sx = L.size_x, sy = L.size_y;
+  const int pitch = L.pitch;
+  const int xs_max = sx - SEG;  // host: sx >= SEG
+  const double2* __restrict__ P = pts + S.pts_off;
+  const int step = S.step;
+  const int n_used = S.n_used;
+  const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
+  const int zero_row = sy * pitch;  // first cell of the appended zero row
+
+  int src4[NI], qofs[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int p = i * 64 + lane;
+    const bool act = p < NP;
+    const int rho = act ? p / SQ : 0;
+    src4[i] = rho * 4;
+    qofs[i] = act ? 4 * (p - rho * SQ) : -1;  // cells into the segment; -1: idle piece
+  }
+  for (int t = lane; t < NS * SEG; t += 64) zblk[t] = 0;
+  __syncthreads();
+
+  // Beam b into image buf: issue this lane's DMA pieces; return the LDS byte
+  // address of this lane's column in its group's k = 0 row.
+  auto prep = [&](int b, int buf, lds_i32*& rd, bool& bad) {
+    const double2 p = P[(int64_t)b * step];
+    const double lx = ae.cosine * p.x - ae.sine * p.y;  // :179
+    const double ly = ae.sine * p.x + ae.cosine * p.y;  // :180
+    const int ix0 = (int)((lx + x_0) + 0.5);
+    const int ixr = (int)((lx + x_r) + 0.5);
+    const int iyr = (int)((ly + y_r) + 0.5);
+    const int xs = min(max(ix0, 0), xs_max);
+    const int rowcell = ((unsigned)iyr < (unsigned)sy) ? __mul24(iyr, pitch) + xs : zero_row;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int o = __builtin_amdgcn_ds_bpermute(src4[i], rowcell);
+      const int32_t* src = gi + (qofs[i] < 0 ? zero_row : o + qofs[i]);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_i32*)((buf ? img1 : img0) + i * 256), 16, 0, 0);
+    }
+    const int pos = ixr - xs;
+    const bool inx = (unsigned)ixr < (unsigned)sx;
+    bad |= inx & ((unsigned)pos >= (unsigned)SEG);
+    lds_i32* row0 = (lds_i32*)((buf ? img1 : img0) + ge * NS * SEG);
+    rd = inx ? row0 + pos : (lds_i32*)&zblk[0];
+  };
+  // The reads are inline asm: hipcc's wait insertion treats every LDS read as
+  // aliasing any LDS-DMA in flight and drains vmcnt(0), serialising the
+  // pipeline; the explicit vmcnt(NI) before these reads is the real fence.
+  auto consume = [&](const lds_i32* rd, int32_t (&part)[NS]) {
+    int32_t v[NS];
+    const uint32_t a = (uint32_t)(uintptr_t)rd;
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v[k]) : "v"(a), "i"(k * SEG * 4));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      asm volatile("" : "+v"(v[k]));
+      part[k] += v[k];
+    }
+  };
+
+  int64_t acci[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) acci[k] = 0;
+  bool bad = false;
+  constexpr int kFold = 32;  // 32 * (2^26 - 1) < 2^31 (ensure_int_grid)
+  constexpr short kWaitNI = (short)(0xF70 | NI);  // vmcnt(NI): the newer beam stays in flight
+  lds_i32 *ra = nullptr, *rb = nullptr;
+  prep(0, 0, ra, bad);
+  for (int base = 0; base < n_used; base += kFold) {
+    const int nb = min(kFold, n_used - base);
+    int32_t part[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) part[k] = 0;
+    for (int b = 0; b < nb; b += 2) {
+      prep(min(base + b + 1, n_used - 1), 1, rb, bad);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(kWaitNI);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(ra, part);
+      __builtin_amdgcn_sched_barrier(0);
+      prep(min(base + b + 2, n_used - 1), 0, ra, bad);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(kWaitNI);
+      __builtin_amdgcn_sched_barrier(0);
+      if (b + 1 < nb) consume(rb, part);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k) acci[k] += part[k];
+  }
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): no DMA outlives the workgroup
+  if (bad) {  // guard (never taken for the host's SEG): exact per-cell recompute
+#pragma unroll
+    for (int k = 0; k < NS; ++k) acci[k] = 0;
+    for (int b = 0; b < n_used; ++b) {
+      const double2 p = P[(int64_t)b * step];
+      const double lx = ae.cosine * p.x - ae.sine * p.y;
+      const double ly = ae.sine * p.x + ae.cosine * p.y;
+      const int gx = (int)((lx + x_r) + 0.5);
+      const bool inx = (unsigned)gx < (unsigned)sx;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        const int gy = (int)((ly + (S.y0 + k * f)) + 0.5);
+        const bool in = inx && (unsigned)gy < (unsigned)sy;
+        acci[k] += gi[in ? (int64_t)gy * pitch + gx : zero_row];
       }
     }
   }
@@ -681,23 +874,31 @@ int rows_pick_sq(int ns, int need_seg) {
 
 hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const double* d_pts_raw,
                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
-                             int ns, int sq, hipStream_t stream) {
+                             int ns, int sq, bool dma, hipStream_t stream) {
   const double2* d_pts = reinterpret_cast<const double2*>(d_pts_raw);
   const int64_t nblk = (int64_t)L.blocks_per_scan * L.n_scans;
   if (nblk <= 0 || nblk > INT32_MAX || !L.int_mode || L.size_x < 4 * sq) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblk), block(64);
-#define CSM_ROWS_CASE(N, Q)                                                                       \
-  if (ns == N && sq == Q) {                                                                       \
+#define CSM_ROWS_LAUNCH(KERN, N, Q)                                                               \
+  do {                                                                                            \
     if (d_partials)                                                                               \
-      hipLaunchKernelGGL((score_rows_kernel<N, Q, true>), grid, block, 0, stream, L, d_scans,    \
-                         d_pts, d_angles, d_out, d_partials);                                     \
+      hipLaunchKernelGGL((KERN<N, Q, true>), grid, block, 0, stream, L, d_scans, d_pts, d_angles, \
+                         d_out, d_partials);                                                      \
     else                                                                                          \
-      hipLaunchKernelGGL((score_rows_kernel<N, Q, false>), grid, block, 0, stream, L, d_scans,   \
-                         d_pts, d_angles, d_out, d_partials);                                     \
-    return hipGetLastError();                                                                     \
+      hipLaunchKernelGGL((KERN<N, Q, false>), grid, block, 0, stream, L, d_scans, d_pts,         \
+                         d_angles, d_out, d_partials);                                            \
+  } while (0)
+#define CSM_ROWS_CASE(N, Q)                                \
+  if (ns == N && sq == Q) {                                \
+    if (dma)                                               \
+      CSM_ROWS_LAUNCH(score_rowsd_kernel, N, Q);           \
+    else                                                   \
+      CSM_ROWS_LAUNCH(score_rows_kernel, N, Q);            \
+    return hipGetLastError();                              \
   }
   CSM_ROWS_LIST(CSM_ROWS_CASE)
 #undef CSM_ROWS_CASE
+#undef CSM_ROWS_LAUNCH
   return hipErrorInvalidValue;
 }
 
@@ -748,16 +949,17 @@ __global__ __launch_bounds__(256) void analyze_grid_kernel(const float* __restri
 }
 
 // gi = (g - outside) * 2^E, exact when the host accepted E.
-// gi[y * pitch + x] = (g[y * sx + x] - outside) * 2^E; pad cells (x >= sx) = 0.
+// gi[y * pitch + x] = (g[y * sx + x] - outside) * 2^E; pad cells (x >= sx)
+// and the appended zero row y = sy (what DMA reads for rows off the grid) = 0.
 __global__ __launch_bounds__(256) void fixed_point_kernel(const float* __restrict__ g, int32_t sx,
                                                           int32_t sy, int32_t pitch, float outside,
                                                           double scale, int32_t* __restrict__ gi) {
-  const int64_t n = (int64_t)pitch * sy;
+  const int64_t n = (int64_t)pitch * (sy + 1);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t y = i / pitch;
     const int x = (int)(i - y * pitch);
-    gi[i] = (x < sx) ? (int32_t)(((double)g[y * sx + x] - (double)outside) * scale) : 0;
+    gi[i] = (x < sx && y < sy) ? (int32_t)(((double)g[y * sx + x] - (double)outside) * scale) : 0;
   }
 }
 
@@ -775,7 +977,7 @@ hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hi
 
 hipError_t launch_fixed_point(const float* g, int32_t sx, int32_t sy, int32_t pitch, float outside,
                               int int_exp, int32_t* gi, hipStream_t stream) {
-  const int64_t n = (int64_t)pitch * sy;
+  const int64_t n = (int64_t)pitch * (sy + 1);
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(fixed_point_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0,
                      stream, g, sx, sy, pitch, outside, ldexp(1.0, int_exp), gi);

@@ -244,8 +244,8 @@ def test_headline_runs_row_segment_kernels(ctx, world2000):
     s = ctx.scan_matchers_batch(b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(), poses, covs)
     names = {k["name"] for k in ctx.kernel_stats()}
     ctx.set_profiling(False)
-    for want in ("score_rows_kernel<13,4,all>", "score_rows_kernel<11,2,all>",
-                 "score_rows_kernel<3,1,all>", "finish_kernel"):
+    for want in ("score_rowsd_kernel<13,4,all>", "score_rowsd_kernel<11,2,all>",
+                 "score_rowsd_kernel<3,1,all>", "finish_kernel"):
         assert want in names, names
     m = O.Map(w.grid, w.resolution, w.offset)
     s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(),
@@ -350,7 +350,7 @@ def test_kernel_variants_agree(f1, grid_kind):
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
     ctxs = []
-    for kern in ("v1", "v2", None):  # None: default (v3 row-segment where eligible)
+    for kern in ("v1", "v2", "v3", None):  # None: default (v4 LDS-DMA row segments where eligible)
         if kern:
             os.environ["CSM_KERNEL"] = kern
         try:
