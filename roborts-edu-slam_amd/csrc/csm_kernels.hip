@@ -513,6 +513,17 @@ __global__ __launch_bounds__(64) void score_rows_kernel(
   }
 }
 
+// 16-byte buffer load written straight into LDS at lds + 16 * lane. The
+// builtin has no host-side form; the guard only keeps hipcc's host pass (which
+// must still emit the kernel's launch stub) from seeing it.
+__device__ __forceinline__ void buffer_load_lds16(__amdgpu_buffer_rsrc_t rsrc,
+                                                  __attribute__((address_space(3))) int32_t* lds,
+                                                  int voffset) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, lds, 16, voffset, 0, 0, 0);
+#endif
+}
+
 // ---- v4: row-segment kernel, LDS-DMA staging (INT mode) --------------------
 // v3's data flow with the 16-byte pieces written straight into LDS by
 // global_load_lds_dwordx4 (dest = wave-uniform base + 16 * lane): no VGPR
@@ -538,6 +549,7 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
   // can tell a read of one from the DMA still writing the other
   __shared__ __attribute__((aligned(16))) int32_t img0[IMG];
   __shared__ __attribute__((aligned(16))) int32_t img1[IMG];
+  __shared__ __attribute__((aligned(16))) int32_t img2[IMG];
   __shared__ __attribute__((aligned(16))) int32_t zblk[NS * SEG];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int win = bid / L.blocks_per_scan;
@@ -564,7 +576,12 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
   const int step = S.step;
   const int n_used = S.n_used;
   const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
-  const int zero_row = sy * pitch;  // first cell of the appended zero row
+  const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
+  const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)ghi << 32) | glo), (short)0, (int)(L.gridi_stride * 4), 0x00020000);
+  const int pitch4 = pitch * 4;
+  const int zero_off = sy * pitch4;  // byte offset of the appended zero row
 
   int src4[NI], qofs[NI];
 #pragma unroll
@@ -573,48 +590,79 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
     const bool act = p < NP;
     const int rho = act ? p / SQ : 0;
     src4[i] = rho * 4;
-    qofs[i] = act ? 4 * (p - rho * SQ) : -1;  // cells into the segment; -1: idle piece
+    qofs[i] = act ? 16 * (p - rho * SQ) : -1;  // bytes into the segment; -1: idle piece
   }
   for (int t = lane; t < NS * SEG; t += 64) zblk[t] = 0;
   __syncthreads();
 
+  // Beam points, 64 at a time in registers (lane l holds beam pbase + l) and
+  // broadcast by readlane: no scalar load (and its lgkmcnt(0) drain of the
+  // LDS queue) per beam.
+  double2 pw = P[(int64_t)min(lane, n_used - 1) * step];
+  int pbase = 0;
+  auto bcast = [](double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+  };
+  auto point = [&](int b) {
+    const int l = b - pbase;
+    double2 p;
+    p.x = bcast(pw.x, l);
+    p.y = bcast(pw.y, l);
+    return p;
+  };
+
+  auto image = [&](int buf) -> int32_t* { return buf == 0 ? img0 : (buf == 1 ? img1 : img2); };
   // Beam b into image buf: issue this lane's DMA pieces; return the LDS byte
   // address of this lane's column in its group's k = 0 row.
   auto prep = [&](int b, int buf, lds_i32*& rd, bool& bad) {
-    const double2 p = P[(int64_t)b * step];
+    const double2 p = point(b);
     const double lx = ae.cosine * p.x - ae.sine * p.y;  // :179
     const double ly = ae.sine * p.x + ae.cosine * p.y;  // :180
     const int ix0 = (int)((lx + x_0) + 0.5);
     const int ixr = (int)((lx + x_r) + 0.5);
     const int iyr = (int)((ly + y_r) + 0.5);
     const int xs = min(max(ix0, 0), xs_max);
-    const int rowcell = ((unsigned)iyr < (unsigned)sy) ? __mul24(iyr, pitch) + xs : zero_row;
+    const int rowoff = ((unsigned)iyr < (unsigned)sy) ? __mul24(iyr, pitch4) + xs * 4 : zero_off;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int o = __builtin_amdgcn_ds_bpermute(src4[i], rowcell);
-      const int32_t* src = gi + (qofs[i] < 0 ? zero_row : o + qofs[i]);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_i32*)((buf ? img1 : img0) + i * 256), 16, 0, 0);
+      const int o = __builtin_amdgcn_ds_bpermute(src4[i], rowoff);
+      buffer_load_lds16(rsrc, (lds_i32*)(image(buf) + i * 256), qofs[i] < 0 ? zero_off : o + qofs[i]);
     }
     const int pos = ixr - xs;
     const bool inx = (unsigned)ixr < (unsigned)sx;
     bad |= inx & ((unsigned)pos >= (unsigned)SEG);
-    lds_i32* row0 = (lds_i32*)((buf ? img1 : img0) + ge * NS * SEG);
+    lds_i32* row0 = (lds_i32*)(image(buf) + ge * NS * SEG);
     rd = inx ? row0 + pos : (lds_i32*)&zblk[0];
   };
   // The reads are inline asm: hipcc's wait insertion treats every LDS read as
   // aliasing any LDS-DMA in flight and drains vmcnt(0), serialising the
   // pipeline; the explicit vmcnt(NI) before these reads is the real fence.
   auto consume = [&](const lds_i32* rd, int32_t (&part)[NS]) {
-    int32_t v[NS];
+    typedef int32_t v2i __attribute__((ext_vector_type(2)));
+    v2i w[(NS + 1) / 2];  // rows 2h, 2h+1; untouched until the lgkmcnt(0) below
     const uint32_t a = (uint32_t)(uintptr_t)rd;
 #pragma unroll
-    for (int k = 0; k < NS; ++k)
-      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v[k]) : "v"(a), "i"(k * SEG * 4));
+    for (int h = 0; h < (NS + 1) / 2; ++h) {
+      const int k = 2 * h;
+      if (k + 1 < NS && (k + 1) * SEG <= 255) {  // two rows per instruction (dword offsets)
+        asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3"
+                     : "=v"(w[h]) : "v"(a), "i"(k * SEG), "i"((k + 1) * SEG));
+      } else if (k + 1 < NS) {
+        asm volatile("ds_read_b32 %0, %2 offset:%3\n\tds_read_b32 %1, %2 offset:%4"
+                     : "=&v"(w[h].x), "=&v"(w[h].y) : "v"(a), "i"(k * SEG * 4), "i"((k + 1) * SEG * 4));
+      } else {
+        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(w[h].x) : "v"(a), "i"(k * SEG * 4));
+      }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int k = 0; k < NS; ++k) {
-      asm volatile("" : "+v"(v[k]));
-      part[k] += v[k];
+    for (int h = 0; h < (NS + 1) / 2; ++h) {
+      asm volatile("" : "+v"(w[h]));
+      part[2 * h] += w[h].x;
+      if (2 * h + 1 < NS) part[2 * h + 1] += w[h].y;
     }
   };
 
@@ -622,27 +670,42 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
 #pragma unroll
   for (int k = 0; k < NS; ++k) acci[k] = 0;
   bool bad = false;
-  constexpr int kFold = 32;  // 32 * (2^26 - 1) < 2^31 (ensure_int_grid)
-  constexpr short kWaitNI = (short)(0xF70 | NI);  // vmcnt(NI): the newer beam stays in flight
-  lds_i32 *ra = nullptr, *rb = nullptr;
-  prep(0, 0, ra, bad);
+  // Three images: beam b is summed while the DMAs of b+1 and b+2 are in
+  // flight (vmcnt(2*NI)). Chunks of 30 beams keep beam -> image static
+  // (30 * (2^26 - 1) < 2^31, ensure_int_grid).
+  constexpr int kFold = 30;
+  constexpr short kWait2 = (short)(0xF70 | (2 * NI));  // needs 2*NI < 16
+  static_assert(2 * NI < 16, "vmcnt field");
+  lds_i32 *r0 = nullptr, *r1 = nullptr, *r2 = nullptr;
+  prep(0, 0, r0, bad);
+  prep(min(1, n_used - 1), 1, r1, bad);
   for (int base = 0; base < n_used; base += kFold) {
     const int nb = min(kFold, n_used - base);
+    if (base != pbase) {  // this chunk preps beams base+2 .. base+kFold+1
+      pbase = base;
+      pw = P[(int64_t)min(base + lane, n_used - 1) * step];
+    }
     int32_t part[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) part[k] = 0;
-    for (int b = 0; b < nb; b += 2) {
-      prep(min(base + b + 1, n_used - 1), 1, rb, bad);
+    for (int b = 0; b < nb; b += 3) {
+      prep(min(base + b + 2, n_used - 1), 2, r2, bad);
       __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(kWaitNI);
+      __builtin_amdgcn_s_waitcnt(kWait2);
       __builtin_amdgcn_sched_barrier(0);
-      consume(ra, part);
+      consume(r0, part);
       __builtin_amdgcn_sched_barrier(0);
-      prep(min(base + b + 2, n_used - 1), 0, ra, bad);
+      prep(min(base + b + 3, n_used - 1), 0, r0, bad);
       __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(kWaitNI);
+      __builtin_amdgcn_s_waitcnt(kWait2);
       __builtin_amdgcn_sched_barrier(0);
-      if (b + 1 < nb) consume(rb, part);
+      if (b + 1 < nb) consume(r1, part);
+      __builtin_amdgcn_sched_barrier(0);
+      prep(min(base + b + 4, n_used - 1), 1, r1, bad);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(kWait2);
+      __builtin_amdgcn_sched_barrier(0);
+      if (b + 2 < nb) consume(r2, part);
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
@@ -662,7 +725,7 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
       for (int k = 0; k < NS; ++k) {
         const int gy = (int)((ly + (S.y0 + k * f)) + 0.5);
         const bool in = inx && (unsigned)gy < (unsigned)sy;
-        acci[k] += gi[in ? (int64_t)gy * pitch + gx : zero_row];
+        acci[k] += gi[in ? (int64_t)gy * pitch + gx : (int64_t)sy * pitch];
       }
     }
   }
