@@ -25,8 +25,9 @@
  *   csm_best_window           same scoring, reduced on device to (max score, lowest flat index)
  *                             (large windows / loop-closure shards; no reference counterpart,
  *                             SURVEY.md 8e)
- *   csm_bnb_match             BranchAndBoundCorrelateScanMatcher::ScanMatch (FAST type)
- *                                                        correlate_scan_matcher.h:274-331
+ *   csm_scan_match with       BranchAndBoundCorrelateScanMatcher::ScanMatch (FAST type,
+ *   type == CSM_FAST          dispatched from BasedCorrelationScanMatch::ScanMatch :815-821)
+ *                                                        correlate_scan_matcher.h:274-502
  *
  * Threading: every entry point locks the context; a context may be shared by
  * the front-end (ROS callback) thread and the back-end thread exactly like the

@@ -796,6 +796,132 @@ int upload_points(csm_ctx* c, const double* pts, int64_t n_total) {
 
 bool map_ready(const csm_ctx* c) { return c->has_grid && c->info.update_index >= 0; }
 
+// ---- FAST (branch-and-bound) -------------------------------------------------
+// BranchAndBoundCorrelateScanMatcher (correlate_scan_matcher.h:271-502). The
+// device scores every node of the search tree (csm_bnb.hip); bnb_search then
+// replays the reference's depth-first search over that table.
+
+struct BCand {  // Candidate2D as the search uses it
+  double score, x, y, angle;
+  int a, i, j;  // angle index, node indices at its level
+};
+inline bool bcand_greater(const BCand& p, const BCand& q) { return p.score > q.score; }
+
+struct TreeView {
+  const double* s;  // one window's node scores
+  int64_t per_angle;
+  int64_t off[csm::kTreeMaxDepth + 1], m[csm::kTreeMaxDepth + 1];
+  double score(int a, int level, int i, int j) const {
+    return s[(int64_t)a * per_angle + off[level] + (int64_t)i * m[level] + j];
+  }
+};
+
+// BranchAndBound (:434-476), recursion and all: the loop breaks on the
+// caller's min_score, children are generated x-offset-major (:456-462), sorted
+// by std::sort (:430; four elements: insertion sort) and searched with the
+// best score so far; std::max keeps `best` unless best < sub.
+BCand bnb_search(const TreeView& V, const std::vector<BCand>& list, int depth, double min_score,
+                 const double* hw, const AngleEntry* ang) {
+  if (depth == 0) return list.front();
+  BCand best{min_score, 0.0, 0.0, 0.0, 0, 0, 0};  // Candidate2D(0, 0.0, 0.0, 0.0)
+  std::vector<BCand> kids;
+  for (const BCand& c : list) {
+    if (c.score <= min_score) break;
+    kids.clear();
+    const double half_width = hw[depth];
+    for (int ox = 0; ox < 2; ++ox) {
+      for (int oy = 0; oy < 2; ++oy) {
+        BCand k;
+        k.x = c.x + (ox ? half_width : 0.0);
+        k.y = c.y + (oy ? half_width : 0.0);
+        k.angle = ang[c.a].angle;
+        k.a = c.a;
+        k.i = 2 * c.i + ox;
+        k.j = 2 * c.j + oy;
+        k.score = V.score(c.a, depth - 1, k.i, k.j);
+        kids.push_back(k);
+      }
+    }
+    std::sort(kids.begin(), kids.end(), bcand_greater);
+    const BCand sub = bnb_search(V, std::vector<BCand>(kids), depth - 1, best.score, hw, ang);
+    if (best.score < sub.score) best = sub;
+  }
+  return best;
+}
+
+// Positional + angular covariance over the sorted lowest-resolution list
+// (:835-839 for FAST; :887-1019), pose write-back (:861-869).
+double complete_fast(const std::vector<BCand>& cands, const BCand& best, const csm_param& P,
+                     const Geometry& G, double pose[3], double cov[9]) {
+  const double sres = P.search_space_resolution;
+  const double max_ang_var = 4 * (P.search_angle_resolution * P.search_angle_resolution);
+  const double bs = best.score;
+  for (int i = 0; i < 9; ++i) cov[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  if (bs < kDoubleTolerance) {
+    cov[0] = kMaxVariance;
+    cov[4] = kMaxVariance;
+    cov[8] = max_ang_var;
+  } else {
+    double vxx = 0.0, vxy = 0.0, vyy = 0.0, norm = 0.0;
+    const double bound = std::min(bs - 0.1, 0.5);
+    int counter = 0;
+    for (const BCand& c : cands) {
+      const double sc = c.score;
+      if (!(sc > bound && counter < kMaxVarianceUsePointSize)) break;
+      norm += sc;
+      const double dx = c.x - best.x, dy = c.y - best.y;
+      vxx += (dx * dx * sc);
+      vxy += (dx * dy * sc);
+      vyy += (dy * dy * sc);
+      counter++;
+    }
+    if (norm > kDoubleTolerance) {
+      double xx = vxx / norm, xy = vxy / norm, yy = vyy / norm;
+      const double r = sres / G.mres;
+      const double minv = 0.1 * (r * r);
+      xx = std::max<double>(xx, minv);
+      yy = std::max<double>(yy, minv);
+      const double m2 = G.mres * G.mres;
+      cov[0] = (xx * m2) / bs;
+      cov[1] = (xy * m2) / bs;
+      cov[3] = (xy * m2) / bs;
+      cov[4] = (yy * m2) / bs;
+      cov[8] = max_ang_var;
+    }
+    if (double_equal(cov[0], 0.0)) cov[0] = kMaxVariance;
+    if (double_equal(cov[4], 0.0)) cov[4] = kMaxVariance;
+  }
+  if (bs < kDoubleTolerance) {
+    cov[8] = max_ang_var;
+  } else {
+    const double lin_tol = sres / G.mres;
+    const double bound = std::min(bs - 0.1, 0.5);
+    double norm = 0.0, acc = 0.0;
+    int counter = 0;
+    for (const BCand& c : cands) {
+      const double sc = c.score;
+      if (sc >= bound && counter < kMaxVarianceUsePointSize) {
+        if (double_equal(c.x, best.x, lin_tol) && double_equal(c.y, best.y, lin_tol)) {
+          const double d = c.angle - best.angle;
+          norm += sc;
+          acc += (d * d * sc);
+          counter++;
+        }
+      }
+    }
+    cov[8] = (norm > kDoubleTolerance) ? acc / norm : 200 * max_ang_var;
+  }
+  const double response = bs > 1.0 ? 1.0 : bs;
+  if (response > P.response_threshold) {
+    const double bp[3] = {best.x, best.y, best.angle};
+    G.to_world(bp, pose);
+  }
+  return response;
+}
+
+int match_level_fast(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
+                     double* poses, double* covs, double* responses, int64_t* argmax_flat);
+
 // One level (BasedCorrelationScanMatch::ScanMatch) over a batch of scans.
 // Points must already be uploaded; offsets index them.
 int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
@@ -803,7 +929,7 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
   Dims D;
   int st = window_dims(P, D);
   if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
-  if (P.type == CSM_FAST) return c->fail(CSM_ERR_UNSUPPORTED, "FAST (branch-and-bound) type not supported by this entry point");
+  if (P.type == CSM_FAST) return match_level_fast(c, n_scans, offsets, P, poses, covs, responses, argmax_flat);
   const Geometry G(c->info);
   std::vector<int> scan_of;
   scan_of.reserve((size_t)n_scans);
@@ -872,6 +998,132 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
     c->account("host:plan", (float)(t1 - t0), 0.0, 0.0);
     c->account("host:launch+wait", (float)(t2 - t1), 0.0, 0.0);
     c->account("host:complete", (float)(t3 - t2), 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+// FAST windows: tree scores on the device, the search and covariance on the
+// host (BranchAndBoundCorrelateScanMatcher::ScanMatch :274-331, then
+// BasedCorrelationScanMatch :815-869). Windows go in chunks bounded by the
+// score table size.
+int match_level_fast(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
+                     double* poses, double* covs, double* responses, int64_t* argmax_flat) {
+  Dims D;  // the angle LUT is the multi-resolution matcher's (:297-300)
+  if (window_dims(P, D) != CSM_OK) return c->fail(CSM_ERR_INVALID_ARG, "invalid search window parameters");
+  const int depth = P.max_depth;
+  if (depth < 0 || depth > csm::kTreeMaxDepth)
+    return c->fail(CSM_ERR_UNSUPPORTED, "FAST: max_depth outside [0, 12]");
+  const Geometry G(c->info);
+  const double sres = P.search_space_resolution;
+  const double lowest = (1 << depth) * sres;                                    // :308
+  const double nl = round_half_away(P.search_space_size / lowest) + 1;          // :337
+  if (!(nl >= 1.0 && nl < 4096.0)) return c->fail(CSM_ERR_INVALID_ARG, "FAST: bad lowest-resolution grid");
+  csm::TreeWork T{};
+  T.n_angles = D.n_angles;
+  T.n_low = (int32_t)nl;
+  T.depth = depth;
+  T.f_low = lowest / G.mres;  // :347
+  for (int d = 1; d <= depth; ++d) T.hw[d] = ((1 << (d - 1)) * sres) / G.mres;  // :454-455
+  TreeView V{};
+  V.per_angle = 0;
+  for (int l = depth; l >= 0; --l) {
+    V.m[l] = (int64_t)T.n_low << (depth - l);
+    V.off[l] = V.per_angle;
+    V.per_angle += V.m[l] * V.m[l];
+  }
+  T.nodes_per_angle = V.per_angle;
+  T.grid = c->d_grid;
+  T.size_x = c->info.size_x;
+  T.size_y = c->info.size_y;
+  T.outside = c->outside;
+  const int64_t per_window = (int64_t)D.n_angles * V.per_angle;
+  if (per_window > ((int64_t)1 << 31)) return c->fail(CSM_ERR_UNSUPPORTED, "FAST: search tree too large");
+
+  std::vector<int> scan_of;
+  for (int s = 0; s < n_scans; ++s) {
+    responses[s] = 0.0;  // kMinResponse (:1034)
+    if (argmax_flat) argmax_flat[s] = -1;  // no enumeration index for a tree node
+    const int n = (int)(offsets[s + 1] - offsets[s]);
+    if (!map_ready(c) || n == 0) continue;  // :792-795
+    int step, use, n_used;
+    if (!beam_rule(n, P.use_point_size, step, use, n_used))
+      return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+    scan_of.push_back(s);
+  }
+  const int nw_all = (int)scan_of.size();
+  const int chunk = (int)std::max<int64_t>(1, ((int64_t)256 << 20) / (per_window * 8));
+  std::vector<WindowPlan> plans;
+  std::vector<AngleEntry> angles;
+  for (int w0 = 0; w0 < nw_all; w0 += chunk) {
+    const int nw = std::min(chunk, nw_all - w0);
+    plans.assign((size_t)nw, WindowPlan{});
+    angles.clear();
+    std::vector<ScanWork> sw((size_t)nw);
+    for (int i = 0; i < nw; ++i) {
+      const int s = scan_of[(size_t)(w0 + i)];
+      double center[3];
+      G.to_map(poses + 3 * s, center);  // :293
+      plan_window(P, D, G, (int)(offsets[s + 1] - offsets[s]), center, angles, plans[(size_t)i]);
+      const WindowPlan& W = plans[(size_t)i];
+      ScanWork& q = sw[(size_t)i];
+      q = ScanWork{};
+      q.pts_off = offsets[s];
+      q.angle_off = W.angle_off;
+      q.out_off = (int64_t)i * per_window;
+      q.n_used = W.n_used;
+      q.step = W.step;
+      q.divisor = (double)W.use;
+      q.x0 = W.x0;  // search_space_start_x (:345-346)
+      q.y0 = W.y0;
+      q.cx = W.center[0];
+      q.cy = W.center[1];
+      q.ct = W.center[2];
+    }
+    T.n_windows = nw;
+    hipError_t e;
+    const size_t bytes = (size_t)nw * (size_t)per_window * sizeof(double);
+    if ((e = c->scans.ensure(sw.size() * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
+    if ((e = c->angles.ensure(angles.size() * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
+    if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(tree scores)");
+    if ((e = c->h_scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(tree scores)");
+    if ((e = hipMemcpyAsync(c->scans.p, sw.data(), sw.size() * sizeof(ScanWork), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(scans)");
+    if ((e = hipMemcpyAsync(c->angles.p, angles.data(), angles.size() * sizeof(AngleEntry), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(angles)");
+    if (c->profiling && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+    if ((e = csm::launch_score_tree(T, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                    (const AngleEntry*)c->angles.p, (double*)c->scores.p, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "score_tree_kernel");
+    if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+    if ((e = hipMemcpyAsync(c->h_scores.p, c->scores.p, bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(tree scores)");
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize");
+    if (c->profiling) {
+      float ms = 0.f;
+      if ((e = hipEventElapsedTime(&ms, c->ev0, c->ev1)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
+      double beams = 0.0;
+      for (const WindowPlan& W : plans) beams += (double)W.n_used;
+      c->account("score_tree_kernel", ms, beams * (double)per_window * 4.0, (double)nw * (double)per_window);
+    }
+    const int threads = (nw >= 8) ? c->host_threads : 1;
+    c->parallel_for(nw, threads, [&](int i) {
+      const int s = scan_of[(size_t)(w0 + i)];
+      const WindowPlan& W = plans[(size_t)i];
+      const AngleEntry* ang = angles.data() + W.angle_off;
+      TreeView v = V;
+      v.s = (const double*)c->h_scores.p + (size_t)i * (size_t)per_window;
+      // ComputeLowestResolutionCandidates (:333-393): enumeration order, std::sort
+      std::vector<BCand> low;
+      low.reserve((size_t)D.n_angles * T.n_low * T.n_low);
+      for (int a = 0; a < D.n_angles; ++a)
+        for (int xi = 0; xi < T.n_low; ++xi)
+          for (int yi = 0; yi < T.n_low; ++yi)
+            low.push_back(BCand{v.score(a, depth, xi, yi), W.x0 + xi * T.f_low, W.y0 + yi * T.f_low,
+                                ang[a].angle, a, xi, yi});
+      std::sort(low.begin(), low.end(), bcand_greater);
+      const BCand best = bnb_search(v, low, depth, low.front().score - 0.1, T.hw, ang);  // :316-318
+      responses[s] = complete_fast(low, best, P, G, poses + 3 * s, covs + 9 * s);
+    });
   }
   return CSM_OK;
 }

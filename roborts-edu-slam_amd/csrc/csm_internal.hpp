@@ -151,6 +151,22 @@ int rows_pick_sq(int ns, int need_seg);
 hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
                              int ns, int sq, bool dma, hipStream_t stream);
+// FAST (branch-and-bound) tree scoring (csm_bnb.hip): every node of every
+// level, per window and angle, laid out level max_depth first.
+constexpr int kTreeMaxDepth = 12;
+struct TreeWork {
+  int32_t n_angles, n_low, depth, n_windows;
+  int64_t nodes_per_angle;     // sum over levels of (n_low << (depth - l))^2
+  double f_low;                // lowest-resolution step in cells (:347)
+  double hw[kTreeMaxDepth + 1];  // hw[d]: half_width applied below depth d (:454-455)
+  const float* grid;           // packed fp32 grid
+  int32_t size_x, size_y;
+  float outside;
+  int32_t pad;
+};
+hipError_t launch_score_tree(const TreeWork& T, const ScanWork* d_scans, const double* d_pts,
+                             const AngleEntry* d_angles, double* d_out, hipStream_t stream);
+
 // Grid statistics for the exact integer path (csm_set_grid).
 struct GridStats {
   int32_t min_gexp;       // every nonzero |v| is a multiple of 2^min_gexp

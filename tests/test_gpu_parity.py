@@ -414,3 +414,59 @@ def test_device_sort_matches_libstdcxx(ctx, seed):
         cases.append(k)
     for k in cases:
         assert np.array_equal(ctx.sort_order(k), O.std_sort_order(k)), k.size
+
+
+def test_f4_bnb_fixture(ctx, golden_dir, f1):
+    """FAST (branch-and-bound, correlate_scan_matcher.h:271-502) on the F1
+    inputs: device-scored tree + host replay of the search, bit-exact."""
+    f4 = np.load(os.path.join(golden_dir, "f4_bnb.npz"))
+    ctx.set_grid(_map(f1["grid"], f1["resolution"], f1["offset"]), force=True)
+    pose = np.array(f1["init_pose"], dtype=np.float64)
+    cov = np.eye(3).reshape(9).copy()
+    r = ctx.scan_match(f1["points"], _param(f4["param"]), pose, cov)
+    assert r == f4["response"]
+    assert np.array_equal(pose, f4["pose"]) and np.array_equal(cov, f4["cov"])
+
+
+@pytest.mark.parametrize("grid_kind,depth,U", [("blur", 4, 100), ("blur", 2, 1081), ("values", 3, 50),
+                                               ("hostile", 4, 100), ("flat", 4, 100), ("blur", 0, 100)])
+def test_bnb_matches_oracle(ctx, f1, grid_kind, depth, U):
+    """FAST on several grids / depths, incl. a flat grid (every node ties:
+    the search order and std::sort decide) and depth 0 (no search)."""
+    from roborts_csm import worlds
+    from roborts_csm.params import FAST_PARAM
+    rng = np.random.default_rng(depth * 31 + U)
+    if grid_kind == "blur":
+        g = f1["grid"]
+    elif grid_kind == "hostile":
+        g = worlds.hostile_grid(400, 400)
+    elif grid_kind == "flat":
+        g = np.full((400, 400), 0.3, dtype=np.float32)
+    else:
+        g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
+    p = FAST_PARAM.with_(max_depth=depth, use_point_size=U)
+    ctx.set_grid(_map(g, f1["resolution"], f1["offset"]), force=True)
+    m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
+    for k in range(3):
+        init = np.array(f1["init_pose"], dtype=np.float64) + np.array([0.03 * k, -0.02 * k, 0.01 * k])
+        pose, cov = init.copy(), np.eye(3).reshape(9).copy()
+        r = ctx.scan_match(f1["points"], p, pose, cov)
+        r2, pose2, cov2, _, _ = O.scan_match(m, f1["points"], p, init, np.eye(3))
+        assert r == r2, (grid_kind, depth, k)
+        assert np.array_equal(pose, pose2) and np.array_equal(cov, cov2), (grid_kind, depth, k)
+
+
+def test_bnb_batch_matches_single(ctx, world2000):
+    """csm_scan_match_batch with FAST params: each scan as if alone."""
+    from roborts_csm.params import FAST_PARAM
+    w, b = world2000
+    ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+    n = 6
+    poses = np.ascontiguousarray(b.init_poses[:n].copy())
+    covs = np.tile(np.eye(3).reshape(1, 9), (n, 1))
+    r, _ = ctx.scan_match_batch(b.points_cells[:b.offsets[n]], b.offsets[:n + 1], FAST_PARAM, poses, covs)
+    m = O.Map(w.grid, w.resolution, w.offset)
+    for k in range(n):
+        pts = b.points_cells[b.offsets[k]:b.offsets[k + 1]]
+        r2, pose2, cov2, _, _ = O.scan_match(m, pts, FAST_PARAM, b.init_poses[k], np.eye(3))
+        assert r[k] == r2 and np.array_equal(poses[k], pose2) and np.array_equal(covs[k], cov2)
