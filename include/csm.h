@@ -211,6 +211,21 @@ int csm_best_window(csm_ctx* ctx, const double* points_xy, int32_t n_points,
                     const csm_param* param, const double center_map[3],
                     csm_best* best);
 
+/* --- loop-closure shards ----------------------------------- */
+/* Make n_grids same-size packed fp32 grids resident back to back (submaps of
+ * one shard: n_grids * size_y * size_x floats). info gives their common size
+ * and resolution; every window names its grid and carries its own centre, so
+ * per-submap offsets stay with the caller. Replaces the single grid of
+ * csm_set_grid. */
+int csm_set_grid_stack(csm_ctx* ctx, const float* cells, int32_t n_grids,
+                       const csm_map_info* info, int64_t version);
+/* Argmax-only scoring of one scan in n_windows windows, window i on grid
+ * grid_index[i] (null: grid 0) centred at centers_map[3i..3i+2] (map cells /
+ * rad). best[i] as csm_best_window. One launch for all windows. */
+int csm_best_windows(csm_ctx* ctx, const double* points_xy, int32_t n_points,
+                     const csm_param* param, int32_t n_windows, const int32_t* grid_index,
+                     const double* centers_map, csm_best* best);
+
 #ifdef __cplusplus
 }
 #endif

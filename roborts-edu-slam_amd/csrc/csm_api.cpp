@@ -450,6 +450,7 @@ struct csm_ctx {
   bool int_checked = false, int_ok = false;
   int int_exp = 0;
   int32_t pitch = 0;  // gridi row pitch (cells)
+  int32_t n_grids = 1;  // grids resident back to back (csm_set_grid_stack)
   double int_max_abs = 0.0;  // max |cell| (and |outside|) for the per-launch exactness bound
   int32_t outside_i = 0;
   double pts_maxabs = 0.0;   // max |x|+|y| of the resident points (NaN: unbounded)
@@ -515,7 +516,7 @@ int ensure_int_grid(csm_ctx* c) {
   if (c->int_checked) return CSM_OK;
   c->int_checked = true;
   c->int_ok = false;
-  const int64_t n = (int64_t)c->info.size_x * c->info.size_y;
+  const int64_t n = (int64_t)c->info.size_x * c->info.size_y * c->n_grids;
   hipError_t e;
   if ((e = c->gstats.ensure(sizeof(csm::GridStats))) != hipSuccess) return c->hip_fail(e, "hipMalloc(stats)");
   if ((e = csm::launch_analyze_grid(c->d_grid, n, (csm::GridStats*)c->gstats.p, c->stream)) != hipSuccess)
@@ -539,10 +540,13 @@ int ensure_int_grid(csm_ctx* c) {
   const int32_t pitch = (c->info.size_x + 3) & ~3;  // 16-byte aligned rows
   const int64_t ni = (int64_t)pitch * (c->info.size_y + 1);  // + the zero row
   if (ni * 4 > 0x7F000000LL) return CSM_OK;  // buffer byte offsets (+ the kernels' bad offset) < 2^31
-  if ((e = c->gridi.ensure((size_t)ni * sizeof(int32_t))) != hipSuccess) return c->hip_fail(e, "hipMalloc(gridi)");
-  if ((e = csm::launch_fixed_point(c->d_grid, c->info.size_x, c->info.size_y, pitch, c->outside, E,
-                                   (int32_t*)c->gridi.p, c->stream)) != hipSuccess)
-    return c->hip_fail(e, "fixed_point_kernel");
+  if ((e = c->gridi.ensure((size_t)ni * (size_t)c->n_grids * sizeof(int32_t))) != hipSuccess)
+    return c->hip_fail(e, "hipMalloc(gridi)");
+  const int64_t cells1 = (int64_t)c->info.size_x * c->info.size_y;
+  for (int gi = 0; gi < c->n_grids; ++gi)
+    if ((e = csm::launch_fixed_point(c->d_grid + gi * cells1, c->info.size_x, c->info.size_y, pitch, c->outside, E,
+                                     (int32_t*)c->gridi.p + gi * ni, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "fixed_point_kernel");
   c->pitch = pitch;
   c->int_exp = E;
   c->int_max_abs = vmax;
@@ -1264,6 +1268,7 @@ int csm_set_grid(csm_ctx* c, const void* cells, int64_t stride, const csm_map_in
     return c->hip_fail(e, "hipMemcpyAsync(grid)");
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(grid)");
   c->d_grid = (const float*)c->grid_buf.p;
+  c->n_grids = 1;
   c->has_grid = true;
   c->int_checked = false;
   c->key_cells = cells;
@@ -1283,6 +1288,7 @@ int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) 
     return c->fail(CSM_ERR_INVALID_ARG, "grid larger than 2^31 cells");
   c->info = *info;
   c->d_grid = dev;
+  c->n_grids = 1;
   c->has_grid = true;
   c->int_checked = false;
   c->key_cells = nullptr;
@@ -1448,6 +1454,81 @@ int csm_best_window(csm_ctx* c, const double* pts, int32_t n_points, const csm_p
   best->x = W.x0 + (int)((bp.flat / ns) % ns) * (param->search_space_resolution / G.mres);
   best->y = W.y0 + (int)(bp.flat % ns) * (param->search_space_resolution / G.mres);
   best->angle = angles[(size_t)(bp.flat / nss)].angle;
+  return CSM_OK;
+}
+
+int csm_best_windows(csm_ctx* c, const double* pts, int32_t n_points, const csm_param* param,
+                     int32_t n_windows, const int32_t* grid_index, const double* centers_map,
+                     csm_best* best) {
+  if (!c || !param || !centers_map || !best || n_windows < 0) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (n_windows == 0) return CSM_OK;
+  Dims D;
+  int st = window_dims(*param, D);
+  if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
+  if (n_points <= 0) return c->fail(CSM_ERR_INVALID_ARG, "no points");
+  if ((st = check_points(c, pts, n_points)) != CSM_OK) return st;
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  std::vector<int32_t> gidx((size_t)n_windows, 0);
+  for (int i = 0; i < n_windows; ++i) {
+    gidx[(size_t)i] = grid_index ? grid_index[i] : 0;
+    if (gidx[(size_t)i] < 0 || gidx[(size_t)i] >= c->n_grids)
+      return c->fail(CSM_ERR_INVALID_ARG, "grid_index outside the resident grid stack");
+  }
+  const Geometry G(c->info);
+  std::vector<WindowPlan> plans((size_t)n_windows);
+  std::vector<AngleEntry> angles;
+  for (int i = 0; i < n_windows; ++i)
+    if (!plan_window(*param, D, G, n_points, centers_map + 3 * i, angles, plans[(size_t)i]))
+      return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+  if ((st = upload_points(c, pts, n_points)) != CSM_OK) return st;
+  std::vector<BestPartial> bp((size_t)n_windows);
+  std::vector<int64_t> pt_off((size_t)n_windows, 0);
+  if ((st = run_windows(c, *param, D, G, plans, pt_off, angles.data(), angles.size(), gidx, bp.data())) != CSM_OK)
+    return st;
+  const int64_t ns = D.n_space, nss = ns * ns;
+  const double f = param->search_space_resolution / G.mres;
+  for (int i = 0; i < n_windows; ++i) {
+    const WindowPlan& W = plans[(size_t)i];
+    best[i].score = bp[(size_t)i].score;
+    best[i].flat_index = bp[(size_t)i].flat;
+    best[i].x = W.x0 + (int)((bp[(size_t)i].flat / ns) % ns) * f;
+    best[i].y = W.y0 + (int)(bp[(size_t)i].flat % ns) * f;
+    best[i].angle = angles[(size_t)(W.angle_off + bp[(size_t)i].flat / nss)].angle;
+  }
+  return CSM_OK;
+}
+
+int csm_set_grid_stack(csm_ctx* c, const float* cells, int32_t n_grids, const csm_map_info* info,
+                       int64_t version) {
+  if (!c || !info || !cells || n_grids <= 0) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (info->size_x <= 0 || info->size_y <= 0 || !(info->resolution > 0.0))
+    return c->fail(CSM_ERR_INVALID_ARG, "grid size and resolution must be positive");
+  const int64_t ncell = (int64_t)info->size_x * info->size_y;
+  if (ncell >= ((int64_t)1 << 31)) return c->fail(CSM_ERR_INVALID_ARG, "grid larger than 2^31 cells");
+  const bool same = c->has_grid && c->d_grid == c->grid_buf.p && version >= 0 && (const void*)cells == c->key_cells &&
+                    c->key_stride == -n_grids && version == c->key_version && info->size_x == c->key_sx &&
+                    info->size_y == c->key_sy;
+  c->info = *info;
+  if (same) return CSM_OK;
+  const size_t bytes = (size_t)ncell * (size_t)n_grids * sizeof(float);
+  hipError_t e;
+  if ((e = c->grid_buf.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(grid stack)");
+  if ((e = hipMemcpyAsync(c->grid_buf.p, cells, bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(grid stack)");
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(grid stack)");
+  c->d_grid = (const float*)c->grid_buf.p;
+  c->n_grids = n_grids;
+  c->has_grid = true;
+  c->int_checked = false;
+  c->key_cells = cells;
+  c->key_stride = -n_grids;  // never equal to a csm_set_grid stride
+  c->key_version = version;
+  c->key_sx = info->size_x;
+  c->key_sy = info->size_y;
   return CSM_OK;
 }
 

@@ -290,6 +290,30 @@ class Context:
                                          C.byref(b)))
         return b
 
+    def set_grid_stack(self, grids: np.ndarray, resolution: float, version: int = -1) -> None:
+        """Resident stack of same-size fp32 grids (loop-closure submaps)."""
+        g = np.ascontiguousarray(grids, dtype=np.float32)
+        assert g.ndim == 3
+        self._stack = g  # the cache key is the host pointer: keep it alive
+        info = CsmMapInfo(float(resolution), 0.0, 0.0, g.shape[2], g.shape[1], 0, 0)
+        self._check(_lib.csm_set_grid_stack(self._h, g.ctypes.data_as(C.c_void_p), g.shape[0], C.byref(info),
+                                            int(version)))
+
+    def best_windows(self, points_cells, param, grid_index, centers_map):
+        """Argmax of one scan over many windows -> (scores, flat, x, y, angle) arrays."""
+        pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
+        p = _as_param(param)
+        gi = np.ascontiguousarray(grid_index, dtype=np.int32)
+        ctr = np.ascontiguousarray(centers_map, dtype=np.float64).reshape(-1, 3)
+        assert gi.size == ctr.shape[0]
+        out = (CsmBest * max(1, gi.size))()
+        self._check(_lib.csm_best_windows(self._h, _dptr(pts), pts.shape[0], C.byref(p), gi.size,
+                                          gi.ctypes.data_as(C.POINTER(C.c_int32)), _dptr(ctr), out))
+        n = gi.size
+        return (np.array([out[i].score for i in range(n)]), np.array([out[i].flat_index for i in range(n)]),
+                np.array([out[i].x for i in range(n)]), np.array([out[i].y for i in range(n)]),
+                np.array([out[i].angle for i in range(n)]))
+
 
 def window_dims(param) -> tuple[int, int]:
     p = _as_param(param)

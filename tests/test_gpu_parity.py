@@ -470,3 +470,38 @@ def test_bnb_batch_matches_single(ctx, world2000):
         pts = b.points_cells[b.offsets[k]:b.offsets[k + 1]]
         r2, pose2, cov2, _, _ = O.scan_match(m, pts, FAST_PARAM, b.init_poses[k], np.eye(3))
         assert r[k] == r2 and np.array_equal(poses[k], pose2) and np.array_equal(covs[k], cov2)
+
+
+def test_grid_stack_best_windows(f1):
+    """Loop-closure shard: submaps resident as a stack, one launch scores a
+    scan in a large window on every submap (csm_best_windows), each argmax
+    equal to the oracle's; the rank-local reduction of ShardedLoopClosure
+    then picks the lowest global index among equal scores."""
+    import roborts_csm
+    from roborts_csm.loop_closure import ShardedLoopClosure, world_to_map
+    from roborts_csm.params import CorrelationScanMatchParam
+    rng = np.random.default_rng(41)
+    base = np.stack([f1["grid"], np.roll(f1["grid"], 37, axis=0), np.roll(f1["grid"], -53, axis=1),
+                     rng.choice(np.array([0.3, 0.5, 1.0], dtype=np.float32), size=f1["grid"].shape)])
+    grids = np.concatenate([base, base[2:3]])  # submap 4 == submap 2: cross-submap ties
+    res = float(f1["resolution"])
+    offsets = np.tile(np.asarray(f1["offset"], dtype=np.float64), (grids.shape[0], 1))
+    p = CorrelationScanMatchParam(2.0, 0.05, math.pi / 2, 0.0349, 0.5, 100, 0, False, 0)
+    c = roborts_csm.Context(0)
+    try:
+        c.set_grid_stack(grids, res, version=3)
+        centers = np.stack([world_to_map(f1["init_pose"], res, o) for o in offsets])
+        sc, flat, x, y, a = c.best_windows(f1["points"], p, np.arange(grids.shape[0]), centers)
+        for g in range(grids.shape[0]):
+            m = O.Map(grids[g], res, tuple(offsets[g]))
+            s2, fl2 = O.best_window(m, f1["points"], p, centers[g])
+            assert sc[g] == s2 and flat[g] == fl2, g
+        assert sc[4] == sc[2] and flat[4] == flat[2]
+        lc = ShardedLoopClosure(c, grids.shape[0], res, offsets)
+        r = lc.match(f1["points"], p, f1["init_pose"])
+        na, ns = roborts_csm.window_dims(p)
+        gidx = np.arange(grids.shape[0]) * (na * ns * ns) + flat
+        k = int(np.argmin(np.where(sc == sc.max(), gidx, np.iinfo(np.int64).max)))
+        assert r.score == sc.max() and r.global_index == gidx[k] and r.submap == k
+    finally:
+        c.close()
