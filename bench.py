@@ -140,6 +140,72 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
     }
 
 
+def willow_bench(args, rank, world_size, dist, torch):
+    """Config 4: the reference's willow map (1165x945, padded
+    by 200 cells to 1565x1345), one argmax-only window per query scan,
+    +-pi at 0.0349 (181 angles), every beam summed (U = 1081). The window
+    edge is --window-m (the whole-map window of the survey is ~78 m: 181 x
+    1566^2 candidates, minutes per query; scale it here). Queries are
+    independent: weak scaling, one replica per GPU."""
+    import roborts_csm
+    from roborts_csm import worlds
+    from roborts_csm.params import CorrelationScanMatchParam
+    w = worlds.willow_world()
+    batch = worlds.make_scan_batch(w, max(1, args.steps + args.warmup), seed=31 + rank)
+    param = CorrelationScanMatchParam(args.window_m, 0.05, math.pi, 0.0349, 0.5, 1081, 0, False, 0)
+    na, ns = roborts_csm.window_dims(param)
+    ctx = roborts_csm.Context(int(os.environ.get("LOCAL_RANK", "0")))
+    ctx.set_grid(roborts_csm.ScanMatchMap(w.grid, w.resolution, w.offset, 0, 1))
+    from roborts_csm.loop_closure import world_to_map
+
+    def query(k):
+        pts = batch.points_cells[batch.offsets[k]:batch.offsets[k + 1]]
+        return ctx.best_window(pts, param, world_to_map(batch.init_poses[k], w.resolution, w.offset))
+
+    for k in range(args.warmup):
+        query(args.steps + k)
+    ctx.set_profiling(True)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    beams = 0
+    for k in range(args.steps):
+        query(k)
+        beams += int(batch.offsets[k + 1] - batch.offsets[k])
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stats = ctx.kernel_stats()
+    local = float(na * ns * ns * args.steps)
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    if dist is not None:
+        t = torch.tensor([elapsed, local], dtype=torch.float64, device=dev)
+        e, s = t[:1].clone(), t[1:].clone()
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        elapsed, total = float(e.item()), float(s.item())
+    else:
+        total = local
+    kst = [s for s in stats if not s["name"].startswith("host:")]
+    dom = max(kst, key=lambda s: s["total_ms"])
+    avg_ms = dom["total_ms"] / dom["launches"]
+    achieved = dom["algorithmic_bytes"] / dom["launches"] / (avg_ms * 1e-3) / 1e9
+    return {
+        "metric": METRIC, "value": total / elapsed, "unit": "scorings/s", "n_gpus": world_size,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "willow-full-0.05 occupancy (tests/golden/willow_walls.npz) with the blur splat; "
+                "ray-cast scans at free poses",
+        "config": {"workload": f"config4: willow 1565x1345 @5cm, {args.window_m} m / +-pi window "
+                               f"({na}x{ns}^2 candidates), all beams",
+                   "mean_beams": beams / args.steps, "parallelism": f"replicas x{world_size}"},
+        "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "avg_launch_ms": avg_ms},
+        "kernels": stats, "cpu_baseline": None,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,8 +214,9 @@ def main():
     ap.add_argument("--scans", type=int, default=4096, help="scans per GPU per step")
     ap.add_argument("--levels", choices=["headline", "sim"], default="headline",
                     help="headline: every beam summed (B=1081); sim: reference YAML U=100 (B=109)")
-    ap.add_argument("--workload", choices=["config2", "loop_closure"], default="config2",
-                    help="config2: the headline front-end batch; loop_closure: config 3")
+    ap.add_argument("--workload", choices=["config2", "loop_closure", "willow"], default="config2",
+                    help="config2: the headline front-end batch; loop_closure: config 3; willow: config 4")
+    ap.add_argument("--window-m", type=float, default=20.0, help="willow: window edge (m)")
     ap.add_argument("--submaps", type=int, default=512, help="loop_closure: submaps in total")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -171,8 +238,9 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
 
-    if args.workload == "loop_closure":
-        out = loop_closure_bench(args, rank, world_size, dist, torch)
+    if args.workload in ("loop_closure", "willow"):
+        fn = loop_closure_bench if args.workload == "loop_closure" else willow_bench
+        out = fn(args, rank, world_size, dist, torch)
         if rank == 0:
             print(json.dumps(out))
         if dist is not None:

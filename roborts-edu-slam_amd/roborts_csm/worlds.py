@@ -18,6 +18,7 @@ All generation is numpy, seeded; nothing here runs in the timed path.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -322,3 +323,24 @@ def read_pgm(path: str) -> np.ndarray:
     w, h, maxv = int(tokens[1]), int(tokens[2]), int(tokens[3])
     assert maxv < 256
     return np.frombuffer(data, dtype=np.uint8, count=w * h, offset=pos).reshape(h, w)
+
+
+WILLOW_FIXTURE = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..",
+                                               "tests", "golden", "willow_walls.npz"))
+
+
+def willow_world(pad: int = 200, path: str = WILLOW_FIXTURE) -> World:
+    """Config 4: the reference's willow-full-0.05 map
+    (tests/golden/make_willow.py) padded by `pad` cells of unknown (0.3) on
+    every side, walls splatted like the synthetic worlds. World offset: the
+    map_offset_ that puts the yaml origin at cell (pad, pad)
+    (world_to_map = Scaling(1/res) * Translation(offset), grid_map_base.h:68-69)."""
+    f = np.load(path)
+    h, w = (int(v) for v in f["shape"])
+    wall = np.unpackbits(f["wall_bits"])[: h * w].reshape(h, w).astype(bool)
+    res = float(f["resolution"])
+    wall = np.pad(wall, pad, constant_values=False)
+    grid = splat_walls(wall, res)
+    origin = f["origin"]
+    off = (-float(origin[0]) + pad * res, -float(origin[1]) + pad * res)
+    return World(grid, wall, res, off)

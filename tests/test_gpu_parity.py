@@ -505,3 +505,43 @@ def test_grid_stack_best_windows(f1):
         assert r.score == sc.max() and r.global_index == gidx[k] and r.submap == k
     finally:
         c.close()
+
+
+@pytest.fixture(scope="module")
+def willow():
+    from roborts_csm import worlds
+    w = worlds.willow_world()
+    b = worlds.make_scan_batch(w, 24, seed=5)
+    return w, b
+
+
+@pytest.mark.parametrize("which", ["sim", "headline"])
+def test_willow_three_level_bit_exact(ctx, willow, which):
+    """Config 4 map (the reference's willow-full-0.05, padded): batched
+    3-level matching, bit-exact against the oracle."""
+    from roborts_csm.params import SIM_YAML_LEVELS, headline_levels
+    w, b = willow
+    levels = SIM_YAML_LEVELS if which == "sim" else headline_levels()
+    ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=11))
+    poses = np.ascontiguousarray(b.init_poses.copy())
+    covs = np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1))
+    s = ctx.scan_matchers_batch(b.points_cells, b.offsets, levels, poses, covs)
+    m = O.Map(w.grid, w.resolution, w.offset)
+    s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells, b.offsets, levels, b.init_poses,
+                                       np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1)))
+    assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2)
+
+
+def test_willow_best_window(ctx, willow):
+    """Config 4 shape at test size: a 3 m / +-45 deg window, B = all beams."""
+    from roborts_csm.params import CorrelationScanMatchParam
+    w, b = willow
+    ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=11))
+    m = O.Map(w.grid, w.resolution, w.offset)
+    p = CorrelationScanMatchParam(3.0, 0.05, math.pi / 4, 0.0349, 0.5, 1081, 0, False, 0)
+    for k in range(2):
+        pts = b.points_cells[b.offsets[k]:b.offsets[k + 1]]
+        c = O.world_to_map(m, b.init_poses[k])
+        got = ctx.best_window(pts, p, c)
+        s, flat = O.best_window(m, pts, p, c)
+        assert got.score == s and got.flat_index == flat
