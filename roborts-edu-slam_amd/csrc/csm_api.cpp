@@ -463,6 +463,33 @@ struct csm_ctx {
   // per-kernel HIP-event timing (csm_set_profiling / csm_kernel_stats)
   bool profiling = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  hipEvent_t ev_done = nullptr;  // end of a launch's work (async runs)
+
+  // Second set of per-launch buffers: the 3-level driver keeps two halves of
+  // a batch in flight (match_levels_pipelined); swap_slot() exchanges the
+  // sets so run_windows works on whichever half is current.
+  struct Slot {
+    DevBuf scans, angles, scores, partials, best, fin;
+    HostBuf h_scores, h_fin, h_angles, h_sw;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr;
+  } alt;
+  int pipeline_min = 512;  // fewest scans the 3-level driver splits into two halves (CSM_PIPELINE)
+  void swap_slot() {
+    std::swap(scans, alt.scans);
+    std::swap(angles, alt.angles);
+    std::swap(scores, alt.scores);
+    std::swap(partials, alt.partials);
+    std::swap(best, alt.best);
+    std::swap(fin, alt.fin);
+    std::swap(h_scores, alt.h_scores);
+    std::swap(h_fin, alt.h_fin);
+    std::swap(h_angles, alt.h_angles);
+    std::swap(h_sw, alt.h_sw);
+    std::swap(ev0, alt.ev0);
+    std::swap(ev1, alt.ev1);
+    std::swap(ev2, alt.ev2);
+    std::swap(ev_done, alt.ev_done);
+  }
   std::vector<csm_kernel_stat> stats;
   void account(const char* name, float ms, double bytes, double scorings) {
     for (auto& s : stats)
@@ -560,11 +587,38 @@ int ensure_int_grid(csm_ctx* c) {
 // null, every score is copied back into ctx->h_scores (window-major).
 enum class Finish { kScoresToHost, kDevice, kBest };
 
+// A launch left in flight by run_windows(..., pend): what wait_run needs to
+// join it and account its kernels.
+struct PendingRun {
+  char kname[48] = {0};
+  char fname[48] = {0};
+  double alg_bytes = 0.0, scorings = 0.0, finish_bytes = 0.0;
+  bool device_finish = false, timed = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, done = nullptr;
+};
+
+int wait_run(csm_ctx* c, const PendingRun& p) {
+  hipError_t e;
+  if ((e = hipEventSynchronize(p.done)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize");
+  if (p.timed) {
+    float ms = 0.f;
+    if ((e = hipEventElapsedTime(&ms, p.ev0, p.ev1)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
+    c->account(p.kname, ms, p.alg_bytes, p.scorings);
+    if (p.device_finish) {
+      if ((e = hipEventElapsedTime(&ms, p.ev1, p.ev2)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
+      c->account(p.fname, ms, p.finish_bytes, 0.0);
+    }
+  }
+  return CSM_OK;
+}
+
+// With pend == nullptr the call returns once results are on the host; with
+// pend it returns as soon as the work is enqueued (join with wait_run).
 int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
                 const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
                 const AngleEntry* angles, size_t n_angle_entries,
                 const std::vector<int32_t>& grid_index, BestPartial* best_out,
-                Finish mode = Finish::kScoresToHost) {
+                Finish mode = Finish::kScoresToHost, PendingRun* pend = nullptr) {
   if (best_out) mode = Finish::kBest;
   const int nw = (int)plans.size();
   if (nw == 0) return CSM_OK;
@@ -736,17 +790,22 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if ((e = hipMemcpyAsync(best_out, c->best.p, (size_t)nw * sizeof(BestPartial), hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
       return c->hip_fail(e, "hipMemcpyAsync(best)");
   }
-  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize");
-  if (c->profiling) {
-    float ms = 0.f;
-    if ((e = hipEventElapsedTime(&ms, c->ev0, c->ev1)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
-    c->account(kname, ms, alg_bytes, scorings);
-    if (mode == Finish::kDevice) {
-      if ((e = hipEventElapsedTime(&ms, c->ev1, c->ev2)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
-      c->account("finish_kernel", ms, (double)nw * (double)D.n_cand * 8.0, 0.0);
-    }
-  }
-  return CSM_OK;
+  PendingRun local;
+  PendingRun& p = pend ? *pend : local;
+  std::snprintf(p.kname, sizeof(p.kname), "%s", kname);
+  std::snprintf(p.fname, sizeof(p.fname), "finish_kernel<%lld>", (long long)D.n_cand);
+  p.alg_bytes = alg_bytes;
+  p.scorings = scorings;
+  p.finish_bytes = (double)nw * (double)D.n_cand * 8.0;
+  p.device_finish = mode == Finish::kDevice;
+  p.timed = c->profiling;
+  p.ev0 = c->ev0;
+  p.ev1 = c->ev1;
+  p.ev2 = c->ev2;
+  p.done = c->ev_done;
+  if ((e = hipEventRecord(c->ev_done, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+  if (pend) return CSM_OK;
+  return wait_run(c, p);
 }
 
 // Fill a WindowPlan + its AngleEntry rows (AngleSearchLookUpTable::UpdateLookUpTable
@@ -926,17 +985,33 @@ double complete_fast(const std::vector<BCand>& cands, const BCand& best, const c
 int match_level_fast(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
                      double* poses, double* covs, double* responses, int64_t* argmax_flat);
 
-// One level (BasedCorrelationScanMatch::ScanMatch) over a batch of scans.
+// One level (BasedCorrelationScanMatch::ScanMatch) over a batch of scans,
+// split in two so a pipelined caller can overlap the host work of one half
+// with the device work of the other: level_begin plans the windows and
+// enqueues them (nothing waits), level_end joins and completes them.
 // Points must already be uploaded; offsets index them.
-int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
-                double* poses, double* covs, double* responses, int64_t* argmax_flat) {
+struct LevelRun {
+  csm_param P{};
   Dims D;
-  int st = window_dims(P, D);
-  if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
-  if (P.type == CSM_FAST) return match_level_fast(c, n_scans, offsets, P, poses, covs, responses, argmax_flat);
-  const Geometry G(c->info);
   std::vector<int> scan_of;
-  scan_of.reserve((size_t)n_scans);
+  std::vector<WindowPlan> plans;
+  std::vector<int64_t> pt_off;
+  const AngleEntry* angles = nullptr;    // pinned buffer of the slot that ran it
+  const csm::FinishOut* fin = nullptr;   // ditto (device finish)
+  const double* scores = nullptr;        // ditto (host finish)
+  bool dev = false;
+  PendingRun pend;
+};
+
+int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
+                const double* poses, double* responses, int64_t* argmax_flat, LevelRun& R) {
+  R.P = P;
+  R.scan_of.clear();
+  int st = window_dims(P, R.D);
+  if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
+  const Dims& D = R.D;
+  const Geometry G(c->info);
+  R.scan_of.reserve((size_t)n_scans);
   for (int s = 0; s < n_scans; ++s) {
     responses[s] = 0.0;  // kMinResponse (:1034)
     if (argmax_flat) argmax_flat[s] = -1;
@@ -945,63 +1020,122 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
     int step, use, n_used;
     if (!beam_rule(n, P.use_point_size, step, use, n_used))
       return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
-    scan_of.push_back(s);
+    R.scan_of.push_back(s);
   }
-  const int nw = (int)scan_of.size();
+  const int nw = (int)R.scan_of.size();
   if (nw == 0) return CSM_OK;
   const double t0 = now_ms();
-  std::vector<WindowPlan> plans((size_t)nw);
-  std::vector<int64_t> pt_off((size_t)nw);
+  R.plans.assign((size_t)nw, WindowPlan{});
+  R.pt_off.assign((size_t)nw, 0);
   hipError_t he;
   const size_t n_ang_total = (size_t)nw * (size_t)D.n_angles;
   if ((he = c->h_angles.ensure(n_ang_total * sizeof(AngleEntry))) != hipSuccess)
     return c->hip_fail(he, "hipHostMalloc(angles)");
   AngleEntry* angles = (AngleEntry*)c->h_angles.p;  // pinned: uploaded by DMA
+  R.angles = angles;
   const int threads = (nw >= 64) ? c->host_threads : 1;
   c->parallel_for(nw, threads, [&](int i) {  // host libm cos/sin per window angle
-    const int s = scan_of[(size_t)i];
+    const int s = R.scan_of[(size_t)i];
     double center[3];
     G.to_map(poses + 3 * s, center);
     plan_window_into(P, D, G, (int)(offsets[s + 1] - offsets[s]), center,
-                     angles + (size_t)i * (size_t)D.n_angles, plans[(size_t)i]);
-    plans[(size_t)i].angle_off = (int64_t)i * D.n_angles;
-    pt_off[(size_t)i] = offsets[s];
+                     angles + (size_t)i * (size_t)D.n_angles, R.plans[(size_t)i]);
+    R.plans[(size_t)i].angle_off = (int64_t)i * D.n_angles;
+    R.pt_off[(size_t)i] = offsets[s];
   });
   // device finish for the front-end windows (and enough of them to fill the
   // chip); a handful of windows finish faster on the host's std::sort
-  const bool dev = c->device_finish && D.n_cand <= csm::kFinishMaxCand &&
-                   csm::finish_lds_bytes(D.n_cand) <= 160 * 1024 && nw >= c->device_finish_min;
+  R.dev = c->device_finish && D.n_cand <= csm::kFinishMaxCand &&
+          csm::finish_lds_bytes(D.n_cand) <= 160 * 1024 && nw >= c->device_finish_min;
   const double t1 = now_ms();
-  st = run_windows(c, P, D, G, plans, pt_off, angles, n_ang_total, {}, nullptr,
-                   dev ? Finish::kDevice : Finish::kScoresToHost);
+  st = run_windows(c, P, D, G, R.plans, R.pt_off, angles, n_ang_total, {}, nullptr,
+                   R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend);
+  if (st != CSM_OK) return st;
+  R.fin = (const csm::FinishOut*)c->h_fin.p;
+  R.scores = (const double*)c->h_scores.p;
+  if (c->profiling) c->account("host:plan", (float)(t1 - t0), 0.0, 0.0);
+  return CSM_OK;
+}
+
+int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* responses,
+              int64_t* argmax_flat) {
+  const int nw = (int)R.scan_of.size();
+  if (nw == 0) return CSM_OK;
+  const double t1 = now_ms();
+  int st = wait_run(c, R.pend);
   if (st != CSM_OK) return st;
   const double t2 = now_ms();
-  if (dev)
+  const Dims& D = R.D;
+  const csm_param& P = R.P;
+  const Geometry G(c->info);
+  if (R.dev)
     for (int i = 0; i < nw; ++i)
-      if (((const csm::FinishOut*)c->h_fin.p)[i].count < 0)
-        return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
+      if (R.fin[i].count < 0) return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
   const double f = P.search_space_resolution / G.mres;
+  const int threads = (nw >= 64) ? c->host_threads : 1;
   c->parallel_for(nw, threads, [&](int i) {
     thread_local std::vector<Entry> scratch;
-    const int s = scan_of[(size_t)i];
-    const CandGeom C{plans[(size_t)i], angles + plans[(size_t)i].angle_off, f, D.n_space,
+    const int s = R.scan_of[(size_t)i];
+    const CandGeom C{R.plans[(size_t)i], R.angles + R.plans[(size_t)i].angle_off, f, D.n_space,
                      (int64_t)D.n_space * D.n_space};
     csm::FinishOut local;
     const csm::FinishOut* o = nullptr;
-    if (dev) {
-      o = (const csm::FinishOut*)c->h_fin.p + i;
+    if (R.dev) {
+      o = R.fin + i;
     } else {
-      host_sort_finish((const double*)c->h_scores.p + (size_t)i * (size_t)D.n_cand, D, C, P, G, scratch, local);
+      host_sort_finish(R.scores + (size_t)i * (size_t)D.n_cand, D, C, P, G, scratch, local);
       o = &local;
     }
     if (argmax_flat) argmax_flat[s] = o->front_idx;
     responses[s] = complete_window(*o, C, P, G, poses + 3 * s, covs + 9 * s);
   });
   if (c->profiling) {
-    const double t3 = now_ms();
-    c->account("host:plan", (float)(t1 - t0), 0.0, 0.0);
-    c->account("host:launch+wait", (float)(t2 - t1), 0.0, 0.0);
-    c->account("host:complete", (float)(t3 - t2), 0.0, 0.0);
+    c->account("host:wait", (float)(t2 - t1), 0.0, 0.0);
+    c->account("host:complete", (float)(now_ms() - t2), 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
+                double* poses, double* covs, double* responses, int64_t* argmax_flat) {
+  if (P.type == CSM_FAST) return match_level_fast(c, n_scans, offsets, P, poses, covs, responses, argmax_flat);
+  LevelRun R;
+  int st = level_begin(c, n_scans, offsets, P, poses, responses, argmax_flat, R);
+  if (st != CSM_OK) return st;
+  return level_end(c, R, poses, covs, responses, argmax_flat);
+}
+
+// ScanMatchers::ScanMatch over a resident batch (scan_matchers.h:179-289),
+// two halves in flight: while the device runs one half's level, the host
+// completes the other half's previous level and plans its next one. Scans
+// are independent, so the split changes no result.
+int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
+                           int n_levels, double* poses, double* covs, double* sum) {
+  const int32_t h0 = n_scans / 2;
+  const int32_t first[2] = {0, h0}, count[2] = {h0, n_scans - h0};
+  std::vector<double> resp((size_t)n_scans, 0.0);
+  LevelRun R[2];
+  auto begin = [&](int l, int h) {
+    if (h == 1) c->swap_slot();
+    const int32_t s0 = first[h];
+    const int st = level_begin(c, count[h], offsets + s0, levels[l], poses + 3 * (size_t)s0,
+                               resp.data() + s0, nullptr, R[h]);
+    if (h == 1) c->swap_slot();
+    return st;
+  };
+  auto end = [&](int h) {
+    const int32_t s0 = first[h];
+    const int st = level_end(c, R[h], poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, nullptr);
+    for (int s = s0; s < s0 + count[h]; ++s) sum[(size_t)s] += resp[(size_t)s];
+    return st;
+  };
+  int st;
+  if ((st = begin(0, 0)) != CSM_OK || (st = begin(0, 1)) != CSM_OK) return st;
+  for (int l = 0; l < n_levels; ++l) {
+    for (int h = 0; h < 2; ++h) {
+      if ((st = end(h)) != CSM_OK) return st;
+      if (l + 1 < n_levels && (st = begin(l + 1, h)) != CSM_OK) return st;
+    }
   }
   return CSM_OK;
 }
@@ -1186,6 +1320,16 @@ int csm_create(int device, csm_ctx** out) {
     c->row_kernel = std::strcmp(env, "v1") != 0 && std::strcmp(env, "v2") != 0;
     c->row_dma = std::strcmp(env, "v3") != 0;
   }
+  if (const char* env = std::getenv("CSM_PIPELINE")) {  // 0: never split the 3-level batch
+    const int v = std::atoi(env);
+    c->pipeline_min = v > 0 ? v : INT32_MAX;
+  }
+  if (hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->alt.ev_done, hipEventDisableTiming) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return CSM_ERR_HIP;
+  }
   *out = c;
   return CSM_OK;
 }
@@ -1210,9 +1354,18 @@ int csm_destroy(csm_ctx* c) {
     c->h_fin.release();
     c->h_angles.release();
     c->h_sw.release();
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->ev2) (void)hipEventDestroy(c->ev2);
+    c->alt.scans.release();
+    c->alt.angles.release();
+    c->alt.scores.release();
+    c->alt.partials.release();
+    c->alt.best.release();
+    c->alt.fin.release();
+    c->alt.h_scores.release();
+    c->alt.h_fin.release();
+    c->alt.h_angles.release();
+    c->alt.h_sw.release();
+    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->alt.ev0, c->alt.ev1, c->alt.ev2, c->alt.ev_done})
+      if (ev) (void)hipEventDestroy(ev);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;
@@ -1354,10 +1507,18 @@ int csm_scan_matchers_loaded(csm_ctx* c, const csm_param levels[3], int32_t use_
   std::vector<double> resp((size_t)n_scans, 0.0), sum((size_t)n_scans, 0.0);
   const int n_levels = use_fine ? 3 : 1;
   int st;
-  for (int l = 0; l < n_levels; ++l) {
-    if ((st = match_level(c, n_scans, c->loaded_off.data(), levels[l], poses, covs, resp.data(), nullptr)) != CSM_OK)
+  bool fast = false;
+  for (int l = 0; l < n_levels; ++l) fast |= levels[l].type == CSM_FAST;
+  if (n_scans >= c->pipeline_min && !fast) {
+    if ((st = match_levels_pipelined(c, n_scans, c->loaded_off.data(), levels, n_levels, poses, covs,
+                                     sum.data())) != CSM_OK)
       return st;
-    for (int s = 0; s < n_scans; ++s) sum[(size_t)s] += resp[(size_t)s];
+  } else {
+    for (int l = 0; l < n_levels; ++l) {
+      if ((st = match_level(c, n_scans, c->loaded_off.data(), levels[l], poses, covs, resp.data(), nullptr)) != CSM_OK)
+        return st;
+      for (int s = 0; s < n_scans; ++s) sum[(size_t)s] += resp[(size_t)s];
+    }
   }
   for (int s = 0; s < n_scans; ++s) scores[s] = sum[(size_t)s] / n_levels;  // :281
   return CSM_OK;
@@ -1378,9 +1539,8 @@ int csm_set_profiling(csm_ctx* c, int32_t on) {
   DeviceGuard g(c->device);
   hipError_t e;
   if (on && !c->ev0) {
-    if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
-    if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
-    if ((e = hipEventCreate(&c->ev2)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
+    for (hipEvent_t* ev : {&c->ev0, &c->ev1, &c->ev2, &c->alt.ev0, &c->alt.ev1, &c->alt.ev2})
+      if ((e = hipEventCreate(ev)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
   }
   c->profiling = on != 0;
   c->stats.clear();

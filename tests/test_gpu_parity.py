@@ -245,7 +245,7 @@ def test_headline_runs_row_segment_kernels(ctx, world2000):
     names = {k["name"] for k in ctx.kernel_stats()}
     ctx.set_profiling(False)
     for want in ("score_rowsd_kernel<13,4,all>", "score_rowsd_kernel<11,2,all>",
-                 "score_rowsd_kernel<3,1,all>", "finish_kernel"):
+                 "score_rowsd_kernel<3,1,all>", "finish_kernel<5070>"):
         assert want in names, names
     m = O.Map(w.grid, w.resolution, w.offset)
     s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(),
@@ -545,3 +545,34 @@ def test_willow_best_window(ctx, willow):
         got = ctx.best_window(pts, p, c)
         s, flat = O.best_window(m, pts, p, c)
         assert got.score == s and got.flat_index == flat
+
+
+@pytest.mark.parametrize("finish", ["device", "host"])
+def test_pipelined_three_level_driver(world2000, finish):
+    """Two halves of the batch in flight (CSM_PIPELINE threshold lowered so
+    96 scans split): results equal the oracle's bit for bit."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    os.environ["CSM_PIPELINE"] = "16"
+    os.environ["CSM_FINISH"] = finish
+    try:
+        c = roborts_csm.Context(0)
+    finally:
+        del os.environ["CSM_PIPELINE"]
+        del os.environ["CSM_FINISH"]
+    try:
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+        poses = np.ascontiguousarray(b.init_poses.copy())
+        covs = np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1))
+        c.set_profiling(True)
+        s = c.scan_matchers_batch(b.points_cells, b.offsets, headline_levels(), poses, covs)
+        st = {k["name"]: k["launches"] for k in c.kernel_stats()}
+        c.set_profiling(False)
+        m = O.Map(w.grid, w.resolution, w.offset)
+        s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells, b.offsets, headline_levels(), b.init_poses,
+                                           np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1)))
+        assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2)
+        assert st["host:wait"] == 6  # 3 levels x 2 halves
+    finally:
+        c.close()
