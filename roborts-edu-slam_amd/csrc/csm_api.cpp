@@ -439,6 +439,7 @@ struct csm_ctx {
   DevBuf pts, scans, angles, scores, partials, best, fin;
   HostBuf h_scores, h_fin, h_angles, h_sw;
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
+  bool fast_finish = true;    // CSM_FINISH=exact: always the full device std::sort emulation
   int device_finish_min = 1;  // fewest windows per launch that finish on the device
   bool column_kernel = true;  // CSM_KERNEL=v1 selects the lane-per-candidate kernels
   bool row_kernel = true;     // CSM_KERNEL=v2 (or v1) turns the row-segment kernels off
@@ -595,6 +596,8 @@ struct PendingRun {
   double alg_bytes = 0.0, scorings = 0.0, finish_bytes = 0.0;
   bool device_finish = false, timed = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, done = nullptr;
+  const int32_t* flags = nullptr;  // need-exact flags on the host (profiling)
+  int n_flags = 0;
 };
 
 int wait_run(csm_ctx* c, const PendingRun& p) {
@@ -607,6 +610,11 @@ int wait_run(csm_ctx* c, const PendingRun& p) {
     if (p.device_finish) {
       if ((e = hipEventElapsedTime(&ms, p.ev1, p.ev2)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
       c->account(p.fname, ms, p.finish_bytes, 0.0);
+      if (p.flags) {  // "scorings" of this entry = windows that took the exact sort
+        int exact = 0;
+        for (int i = 0; i < p.n_flags; ++i) exact += p.flags[i] != 0;
+        c->account("finish:exact_windows", 0.f, 0.0, (double)exact);
+      }
     }
   }
   return CSM_OK;
@@ -729,6 +737,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     std::snprintf(kname, sizeof(kname), "%s<%d>", best_out ? "score_best_kernel" : "score_all_kernel", cpl);
   if (c->profiling && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
 
+  const int32_t* flags_h = nullptr;
+  int n_flags = 0;
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
@@ -756,15 +766,24 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       A.step_cells = L.step_cells;
       A.lin_tol = P.search_space_resolution / G.mres;
       const size_t fbytes = (size_t)nw * sizeof(csm::FinishOut);
-      if ((e = c->fin.ensure(fbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(finish)");
-      if ((e = c->h_fin.ensure(fbytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(finish)");
+      // + one "needs the exact sort" flag per window (fast finish, csm_finish.hip)
+      if ((e = c->fin.ensure(fbytes + (size_t)nw * sizeof(int32_t))) != hipSuccess) return c->hip_fail(e, "hipMalloc(finish)");
+      A.need_exact = c->fast_finish ? (int32_t*)((char*)c->fin.p + fbytes) : nullptr;
+      if ((e = c->h_fin.ensure(fbytes + (size_t)nw * sizeof(int32_t))) != hipSuccess)
+        return c->hip_fail(e, "hipHostMalloc(finish)");
       if ((e = csm::launch_finish(A, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
                                   (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw,
                                   c->stream)) != hipSuccess)
         return c->hip_fail(e, "finish_kernel");
       if (c->profiling && (e = hipEventRecord(c->ev2, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
-      if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, fbytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+      // with profiling on, the flags come back too: how many windows needed the exact sort
+      const size_t cbytes = fbytes + ((c->profiling && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
+      if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, cbytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
         return c->hip_fail(e, "hipMemcpyAsync(finish)");
+      if (cbytes > fbytes) {
+        flags_h = (const int32_t*)((const char*)c->h_fin.p + fbytes);
+        n_flags = nw;
+      }
     }
   } else {
     const size_t pbytes = (size_t)nw * (size_t)bps * sizeof(BestPartial);
@@ -792,6 +811,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   }
   PendingRun local;
   PendingRun& p = pend ? *pend : local;
+  p.flags = flags_h;
+  p.n_flags = n_flags;
   std::snprintf(p.kname, sizeof(p.kname), "%s", kname);
   std::snprintf(p.fname, sizeof(p.fname), "finish_kernel<%lld>", (long long)D.n_cand);
   p.alg_bytes = alg_bytes;
@@ -1312,6 +1333,7 @@ int csm_create(int device, csm_ctx** out) {
   c->host_threads = threads;
   if (const char* env = std::getenv("CSM_FINISH")) {
     c->device_finish = std::strcmp(env, "host") != 0;
+    c->fast_finish = std::strcmp(env, "exact") != 0;
     if (std::strcmp(env, "device") == 0) c->device_finish_min = 1;
   }
   if (const char* env = std::getenv("CSM_FINISH_MIN_WINDOWS")) c->device_finish_min = std::max(1, std::atoi(env));

@@ -22,9 +22,8 @@
 // l_k < r_k and returns cut = min(l_{p+1}, r_p) for p such pairs.
 // The formulation is validated against libstdc++ in tests/wave_sort_model.py.
 //
-// Layout: one 256-thread workgroup (4 waves) per window. The waves pull
-// segments from a shared LDS stack (spin lock). A segment of more than 64
-// elements is partitioned by one wave in LDS; a segment of at most 64 is
+// Layout: one 4-wave workgroup per window, segments in per-level LDS lists. A
+// segment of more than 64 elements is partitioned by one wave in LDS; a segment of at most 64 is
 // loaded into registers (lane = element) and finished there: its whole
 // introsort recursion (ballot / bpermute partitions) and the stable sort of
 // its leaves, then written back once.
@@ -38,6 +37,9 @@ namespace csm {
 
 namespace {
 
+// Waves per window of the exact path. Segments are handed out level by level
+// with barriers in between (an earlier version pulled them from a spin-locked
+// LDS stack and, rarely, spun past its iteration bound).
 constexpr int kWaves = 4;
 
 struct Seg {
@@ -140,22 +142,6 @@ __device__ __forceinline__ double read_lane(double x, int l) {
   return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ int read_lane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
-
-// ---- shared work stack ------------------------------------------------------
-__device__ __forceinline__ void lock(Shared* sh) {
-  for (int spins = 0; atomicCAS(&sh->lock, 0, 1) != 0; ++spins) {
-    if (spins > (1 << 24)) {  // bounded: a stuck lock aborts the window
-      sh->pad = 1;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ __forceinline__ void unlock(Shared* sh) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  atomicExch(&sh->lock, 0);
-}
 
 // ---- large segments: one wave, LDS -------------------------------------------
 // Parallel std::__unguarded_partition(first+1, last, pivot=first). lpos/rpos
@@ -323,6 +309,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
                                                              FinishOut* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int w = blockIdx.x;
+  if (A.need_exact && A.need_exact[w] == 0) return;  // the fast finish settled this window
   const int n = (int)A.n_cand;
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
@@ -340,67 +327,62 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     keys[i] = sc[i];
     vals[i] = (uint16_t)i;
   }
+  // Level-synchronous introsort: every segment of a level is independent, so
+  // the waves take them round-robin, children go to the next level's list
+  // (LDS atomic add, no lock), a barrier separates levels. Depth decreases at
+  // every partition, so there are at most 2*floor(log2 n) + 2 levels.
+  const int half = (n / 16 + 64) / 2;  // finish_layout: the stack region holds two lists
+  Seg* cur = stack;
+  Seg* nxt = stack + half;
   if (threadIdx.x == 0) {
     int lg = 0;
     while ((2 << lg) <= n) ++lg;  // floor(log2 n)
-    stack[0] = Seg{0, n, 2 * lg};
-    sh->lock = 0;
-    sh->top = 1;
-    sh->pending = 1;
+    cur[0] = Seg{0, n, 2 * lg};
+    sh->top = 1;      // segments in cur
+    sh->pending = 0;  // segments appended to nxt
     sh->pad = 0;
   }
   __syncthreads();
-
-  // introsort loop, segments pulled by whichever wave is free (bounded: a
-  // window never needs more than ~n iterations per wave)
-  for (int iter = 0;; ++iter) {
-    if (iter > 4 * n + (1 << 16) || sh->pad) {
-      sh->pad = 1;  // reported as count = -1: the host fails the call loudly
+  for (int level = 0;; ++level) {
+    const int ncur = sh->top;
+    if (ncur == 0) break;
+    if (level > 64) {  // cannot happen (depth bound); reported as count = -1
+      if (threadIdx.x == 0) sh->pad = 1;
       break;
     }
-    int got = 0, pend = 0;
-    Seg s{0, 0, 0};
-    if (lane == 0) {
-      lock(sh);
-      if (sh->top > 0) {
-        s = stack[--sh->top];
-        got = 1;
+    for (int i = wave; i < ncur; i += kWaves) {
+      const Seg s = cur[i];
+      const int first = uni(s.first), last = uni(s.last), depth = uni(s.depth);
+      const int len = last - first;
+      if (len <= 64) {
+        if (len > 1) sort_small(keys, vals, first, len, depth, ws);
+      } else if (depth == 0) {
+        if (lane == 0) heap_sort(keys, vals, first, last);
+      } else {
+        if (lane == 0) move_median_to_first(keys, vals, first, first + 1, first + len / 2, last - 1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const int cut = partition_lds(keys, vals, lpos, rpos, first, last);
+        if (lane == 0) {
+          const int at = atomicAdd(&sh->pending, 2);
+          if (at + 2 <= half) {
+            nxt[at] = Seg{cut, last, depth - 1};
+            nxt[at + 1] = Seg{first, cut, depth - 1};
+          } else {
+            sh->pad = 1;  // list overflow: cannot happen for the layout's capacity
+          }
+        }
       }
-      pend = sh->pending;
-      unlock(sh);
-    }
-    got = uni(got);
-    if (!got) {
-      if (uni(pend) == 0) break;
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    const int first = uni(s.first), last = uni(s.last), depth = uni(s.depth);
-    const int len = last - first;
-    int delta = -1;  // change of `pending` when this segment is done
-    Seg c0{0, 0, 0}, c1{0, 0, 0};
-    if (len <= 64) {
-      if (len > 1) sort_small(keys, vals, first, len, depth, ws);
-    } else if (depth == 0) {
-      if (lane == 0) heap_sort(keys, vals, first, last);
-    } else {
-      if (lane == 0) move_median_to_first(keys, vals, first, first + 1, first + len / 2, last - 1);
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      const int cut = partition_lds(keys, vals, lpos, rpos, first, last);
-      c0 = Seg{cut, last, depth - 1};
-      c1 = Seg{first, cut, depth - 1};
-      delta = 1;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) {
-      lock(sh);
-      if (delta > 0) {
-        stack[sh->top++] = c0;
-        stack[sh->top++] = c1;
-      }
-      sh->pending += delta;
-      unlock(sh);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      sh->top = sh->pad ? 0 : sh->pending;
+      sh->pending = 0;
     }
+    Seg* t = cur;
+    cur = nxt;
+    nxt = t;
+    __syncthreads();
   }
   __syncthreads();
   if (A.order_out)
@@ -504,6 +486,257 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
   }
 }
 
+// ---- fast finish: no sort when no tie can matter ----------------------------
+// Everything the sorted candidates feed is decided by the elements with
+// score >= bound = min(best - 0.1, 0.5) (:912,:986; FindBestCandidate's
+// prefix, s >= best - 0.01, lies inside): the FindBest prefix (all of it, in
+// sorted order: its sums are order-dependent), the first 20 with score > bound
+// (:915-928) and the first 20 near the best with score >= bound (:990-1003).
+// std::sort leaves distinct scores in strictly decreasing order, so if the
+// prefix has no equal scores and neither list's 20 (nor the value at its
+// boundary) repeats, these are fixed by value alone: the prefix is ranked,
+// each list is extracted by 20 rounds of wave argmax below the previous
+// value, each round checking that its value occurs once. Any repeat (or a
+// NaN, or an oversized prefix/region) flags the window for finish_kernel's
+// exact std::sort emulation, which runs next and skips every other window.
+// One wave per window.
+constexpr int kFastRCap = 2048;  // region size kept (registers: kFastPer per thread)
+constexpr int kFastFBCap = 64;   // FindBest prefix
+constexpr int kFastThreads = 256;
+constexpr int kFastPer = kFastRCap / kFastThreads;
+
+__device__ __forceinline__ double wave_max_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const double t = __shfl_xor(v, o, 64);
+    v = (t > v) ? t : v;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A, const ScanWork* __restrict__ scans,
+                                                                   const AngleEntry* __restrict__ angles,
+                                                                   const double* __restrict__ scores,
+                                                                   FinishOut* __restrict__ out) {
+  __shared__ double rk[kFastRCap];
+  __shared__ uint16_t ri[kFastRCap];
+  __shared__ double fk[kFastFBCap], gk[kFastFBCap];
+  __shared__ int fi[kFastFBCap], gi[kFastFBCap];
+  __shared__ double red[4];
+  __shared__ int redc[4];
+  __shared__ int nR_s, nF_s, flag_s, gid_s;
+  __shared__ double sbx, sby;
+  const int w = blockIdx.x;
+  const int n = (int)A.n_cand;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const double* sc = scores + (int64_t)w * A.n_cand;
+  int32_t* need = A.need_exact + w;
+  if (tid == 0) {
+    nR_s = 0;
+    nF_s = 0;
+    flag_s = 0;
+    gid_s = INT32_MAX;
+  }
+
+  // best = the front of the sorted candidates (:607); NaN anywhere: exact path
+  double m = -INFINITY;
+  bool nan = false;
+  for (int i0 = tid; i0 < n; i0 += 4 * kFastThreads) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (i0 + u * kFastThreads < n) ? sc[i0 + u * kFastThreads] : -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      nan |= (v[u] != v[u]);
+      m = (v[u] > m) ? v[u] : m;
+    }
+  }
+  m = wave_max_d(m);
+  if (lane == 0) red[wave] = m;
+  if (__ballot(nan) != 0 && lane == 0) flag_s = 1;
+  __syncthreads();
+  const double best = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  if (flag_s || n <= 0) {
+    if (tid == 0) *need = 1;
+    return;
+  }
+  const double lo = best - 0.1;
+  const double bound = (0.5 < lo) ? 0.5 : lo;  // std::min(best - 0.1, 0.5) (:912,:986)
+
+  // the region s >= bound and FindBest's prefix, compacted (order irrelevant)
+  for (int i0 = wave * 64 + lane; i0 - lane < n; i0 += 4 * 64) {
+    const bool in = i0 < n;
+    const double s = in ? sc[i0] : -INFINITY;
+    const bool inR = in && s >= bound;
+    const double d = s - best;
+    const bool eq = in && (d < 0.0 ? d >= -1e-2 : d <= 1e-2);  // DoubleEqual(s, best, 1e-2)
+    const uint64_t mR = __ballot(inR), mF = __ballot(eq);
+    int baseR = 0, baseF = 0;
+    if (lane == 0) {
+      baseR = mR ? atomicAdd(&nR_s, popc(mR)) : 0;
+      baseF = mF ? atomicAdd(&nF_s, popc(mF)) : 0;
+    }
+    baseR = uni(baseR);
+    baseF = uni(baseF);
+    const int pr = baseR + popc(mR & below_mask(lane)), pf = baseF + popc(mF & below_mask(lane));
+    if (inR && pr < kFastRCap) {
+      rk[pr] = s;
+      ri[pr] = (uint16_t)i0;
+    }
+    if (eq && pf < kFastFBCap) {
+      fk[pf] = s;
+      fi[pf] = i0;
+    }
+  }
+  __syncthreads();
+  const int nR = nR_s, nF = nF_s;
+  if (nR > kFastRCap || nF > kFastFBCap) {
+    if (tid == 0) *need = 1;
+    return;
+  }
+
+  // FindBestCandidate's prefix, ranked by value (distinct or exact path)
+  if (wave == 0) {
+    const double mk = lane < nF ? fk[lane] : 0.0;
+    int rank = 0;
+    bool tie = false;
+    for (int j = 0; j < nF; ++j) {
+      const double kj = fk[j];
+      if (lane < nF && j != lane) {
+        rank += (kj > mk) ? 1 : 0;
+        tie |= (kj == mk);
+      }
+    }
+    if (__ballot(tie) != 0) {
+      if (lane == 0) flag_s = 1;
+    } else if (lane < nF) {
+      gk[rank] = mk;
+      gi[rank] = fi[lane];
+    }
+  }
+  __syncthreads();
+  if (flag_s) {
+    if (tid == 0) *need = 1;
+    return;
+  }
+  const ScanWork S = scans[w];
+  const int ns = A.n_space;
+  const int nss = ns * ns;
+  const double f = A.step_cells;
+  auto cx = [&](int idx) { return S.x0 + ((idx / ns) % ns) * f; };
+  auto cy = [&](int idx) { return S.y0 + (idx % ns) * f; };
+  FinishOut* o = out + w;
+  if (tid == 0) {  // :676-707, the same sequential sums as finish_kernel
+    double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;
+    for (int r = 0; r < nF; ++r) {
+      const double s = gk[r];
+      const int idx = gi[r];
+      const AngleEntry ae = angles[S.angle_off + idx / nss];
+      ax += cx(idx) * s;
+      ay += cy(idx) * s;
+      thx += ae.cosine * s;
+      thy += ae.sine * s;
+      ssum += s;
+    }
+    const int fi0 = gi[0];
+    o->front_idx = fi0;
+    o->count = nF;
+    o->best_score = best;
+    o->thx = thx;
+    o->thy = thy;
+    o->ssum = ssum;
+    if (nF > 1) {
+      sbx = ax / ssum;
+      sby = ay / ssum;
+    } else {
+      sbx = cx(fi0);
+      sby = cy(fi0);
+    }
+    o->best_x = sbx;
+    o->best_y = sby;
+  }
+  __syncthreads();
+  // this thread's share of the region, in registers, with the near flag of
+  // the angular list (:994-995)
+  const double bx = sbx, by = sby, tol = A.lin_tol;
+  double my_s[kFastPer];
+  int my_i[kFastPer];  // candidate index; bit 15: near the best
+#pragma unroll
+  for (int t = 0; t < kFastPer; ++t) {
+    const int j = tid + t * kFastThreads;
+    my_s[t] = -INFINITY;
+    my_i[t] = 0;
+    if (j < nR) {
+      const int idx = ri[j];
+      const double dx = cx(idx) - bx, dy = cy(idx) - by;
+      const bool ex = dx < 0.0 ? dx >= -fabs(tol) : dx <= fabs(tol);
+      const bool ey = dy < 0.0 ? dy >= -fabs(tol) : dy <= fabs(tol);
+      my_s[t] = rk[j];
+      my_i[t] = idx | ((ex && ey) ? 0x8000 : 0);
+    }
+  }
+  // the two lists: 0 = positional (score > bound), 1 = angular (score >=
+  // bound, near); round r takes the largest value below round r-1's and
+  // checks that it occurs once among the list's candidates
+  for (int list = 0; list < 2; ++list) {
+    double prev = INFINITY;
+    int cnt = 0;
+    for (int r = 0; r < kCovPoints; ++r) {
+      double lm = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < kFastPer; ++t) {
+        const bool ok = my_s[t] < prev && (list == 0 ? my_s[t] > bound : (my_i[t] & 0x8000) != 0);
+        if (ok && my_s[t] > lm) lm = my_s[t];
+      }
+      lm = wave_max_d(lm);
+      if (lane == 0) red[wave] = lm;
+      __syncthreads();
+      const double g = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+      __syncthreads();
+      if (g == -INFINITY) break;
+      int c = 0, id = INT32_MAX;
+#pragma unroll
+      for (int t = 0; t < kFastPer; ++t) {
+        const bool ok = my_s[t] == g && (list == 0 || (my_i[t] & 0x8000) != 0);
+        if (ok) {
+          c++;
+          id = my_i[t] & 0x7FFF;
+        }
+      }
+      const uint64_t b1 = __ballot(c >= 1), b2 = __ballot(c >= 2);
+      if (lane == 0) redc[wave] = popc(b1) + (b2 ? 2 : 0);
+      if (c >= 1) atomicMin(&gid_s, id);
+      __syncthreads();
+      const int total = redc[0] + redc[1] + redc[2] + redc[3];
+      const int gid = gid_s;
+      __syncthreads();
+      if (tid == 0) gid_s = INT32_MAX;
+      if (total > 1) {  // equal scores where the order decides the list
+        if (tid == 0) *need = 1;
+        return;
+      }
+#ifdef CSM_DEBUG_FAST
+      if (tid == 0 && w == 0) printf("list %d r %d g %.17g gid %d total %d nR %d nF %d best %.17g bound %.17g\n", list, r, g, gid, total, nR, nF, best, bound);
+#endif
+      if (tid == 0) {
+        if (list == 0) {
+          o->pos_idx[r] = gid;
+          o->pos_score[r] = g;
+        } else {
+          o->ang_idx[r] = gid;
+          o->ang_score[r] = g;
+        }
+      }
+      prev = g;
+      cnt++;
+    }
+    if (tid == 0) {
+      if (list == 0) o->n_pos = cnt;
+      else o->n_ang = cnt;
+    }
+  }
+  if (tid == 0) *need = 0;
+}
+
 hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const AngleEntry* d_angles,
                          const double* d_scores, FinishOut* d_out, int32_t n_windows, hipStream_t stream) {
   const size_t lds = finish_lds_bytes(A.n_cand);
@@ -515,7 +748,15 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(finish_kernel, dim3(n_windows), dim3(64 * kWaves), lds, stream, A, d_scans,
+  if (A.need_exact && !A.order_out) {  // fast pass first; the exact pass only where it flagged
+    hipLaunchKernelGGL(finish_fast_kernel, dim3(n_windows), dim3(kFastThreads), 0, stream, A, d_scans,
+                       d_angles, d_scores, d_out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  FinishArgs B = A;
+  if (A.order_out) B.need_exact = nullptr;  // the permutation hook always sorts
+  hipLaunchKernelGGL(finish_kernel, dim3(n_windows), dim3(64 * kWaves), lds, stream, B, d_scans,
                      d_angles, d_scores, d_out);
   return hipGetLastError();
 }

@@ -80,6 +80,7 @@ struct FinishArgs {
   double step_cells;   // res / map_resolution
   double lin_tol;      // search_space_resolution / map_resolution (:840,:852)
   int32_t* order_out;  // optional: the sorted permutation, n_cand per window
+  int32_t* need_exact; // per window: 1 = the fast finish saw a tie that matters (device scratch)
 };
 
 // What the host needs to complete BasedCorrelationScanMatch::ScanMatch for

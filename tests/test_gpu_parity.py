@@ -285,31 +285,44 @@ def test_best_window_large_matches_oracle(ctx, world2000):
         assert got.score == s and got.flat_index == flat
 
 
-def test_device_finish_equals_host_sort(world2000):
-    """CSM_FINISH=host (std::sort on the host) and the device finish kernel
-    give identical poses, covariances, scores and argmax indices."""
+@pytest.mark.parametrize("levels", ["sim", "headline"])
+def test_device_finish_equals_host_sort(world2000, levels):
+    """CSM_FINISH=host (std::sort on the host), CSM_FINISH=exact (the device
+    std::sort emulation on every window) and the default device finish (the
+    fast no-sort path, exact emulation only where ties matter) give identical
+    poses, covariances, scores and argmax indices; the fast path is taken."""
     import roborts_csm
-    from roborts_csm.params import SIM_YAML_LEVELS
+    from roborts_csm.params import SIM_YAML_LEVELS, headline_levels
     w, b = world2000
-    os.environ["CSM_FINISH"] = "host"
-    try:
-        hctx = roborts_csm.Context(0)
-    finally:
-        del os.environ["CSM_FINISH"]
-    dctx = roborts_csm.Context(0)
+    ctxs = []
+    for mode in ("host", "exact", None):
+        if mode:
+            os.environ["CSM_FINISH"] = mode
+        try:
+            ctxs.append(roborts_csm.Context(0))
+        finally:
+            os.environ.pop("CSM_FINISH", None)
+    lvs = SIM_YAML_LEVELS if levels == "sim" else headline_levels()
     out = []
-    for c in (hctx, dctx):
+    for c in ctxs:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
-        for lv in SIM_YAML_LEVELS:
+        c.set_profiling(True)
+        res = []
+        for lv in lvs:
             poses = np.ascontiguousarray(b.init_poses.copy())
             covs = np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1))
             r, am = c.scan_match_batch(b.points_cells, b.offsets, lv, poses, covs)
-            out.append((r, am, poses, covs))
-    hctx.close()
-    dctx.close()
-    for a, d in zip(out[:3], out[3:]):
-        for x, y in zip(a, d):
-            assert np.array_equal(x, y)
+            res.append((r, am, poses, covs))
+        out.append(res)
+    st = {k["name"]: k for k in ctxs[2].kernel_stats()}
+    for c in ctxs:
+        c.close()
+    for other in out[1:]:
+        for a, d in zip(out[0], other):
+            for x, y in zip(a, d):
+                assert np.array_equal(x, y)
+    # most windows settled without the sort
+    assert st["finish:exact_windows"]["scorings"] < 0.5 * 3 * b.offsets.size
 
 
 def test_device_finish_ties_random_windows(ctx):
