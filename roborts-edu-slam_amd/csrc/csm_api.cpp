@@ -444,6 +444,9 @@ struct csm_ctx {
   bool column_kernel = true;  // CSM_KERNEL=v1 selects the lane-per-candidate kernels
   bool row_kernel = true;     // CSM_KERNEL=v2 (or v1) turns the row-segment kernels off
   bool row_dma = true;        // CSM_KERNEL=v3: register-staged row segments instead of LDS-DMA
+  bool tile_kernel = false;   // CSM_KERNEL=v5 opts into the beam-tile kernel (exact; measured
+                              // slower than v4 on config 2: 8.3 vs 7.0 ms, profiles/r01)
+  int tile_beams = 8;         // beams per box of the beam-tile kernel (CSM_TILE_BEAMS: 4 or 8)
   std::vector<float> h_pack;
 
   // exact fixed-point copy of the grid (ensure_int_grid)
@@ -660,10 +663,24 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     rows_sq = csm::rows_pick_sq(D.n_space, (int)std::floor(span * (1.0 + 1e-9) + 1e-9) + 2);
     if (c->info.size_x < 4 * rows_sq) rows_sq = 0;
   }
+  // v5 beam-tile kernel: whole-cell window step, supported n_space, every
+  // endpoint within 16000 cells of the map origin (its packed row/column base)
+  bool tiles = false;
+  if (use_int && c->tile_kernel && f == 1.0 && csm::tiles_supported(D.n_space) && c->pitch >= 32 &&
+      c->pitch < 65536 && c->info.size_y < 16000) {
+    tiles = true;
+    for (const WindowPlan& W : plans) {
+      const double far = (double)(D.n_space - 1) * f;
+      const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
+                                   std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
+      if (!(c->pts_maxabs * (1.0 + 1e-9) + span + 64.0 < 16000.0)) tiles = false;
+    }
+  }
+  if (tiles) rows_sq = 0;
   const int cpl = pick_cpl(D.n_cand);
   const int64_t per_block = (int64_t)csm::kBlock * cpl;
-  const int64_t rows_groups = rows_sq ? 64 / D.n_space : 1;
-  const int64_t bps = rows_sq ? (D.n_angles + rows_groups - 1) / rows_groups
+  const int64_t rows_groups = (rows_sq || tiles) ? 64 / D.n_space : 1;
+  const int64_t bps = (rows_sq || tiles) ? (D.n_angles + rows_groups - 1) / rows_groups
                       : v2    ? col_blocks * ktiles
                               : (D.n_cand + per_block - 1) / per_block;
   if (bps * nw > INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
@@ -727,7 +744,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const double alg_bytes = beams * (double)D.n_cand * 4.0;
   const double scorings = (double)nw * (double)D.n_cand;
   char kname[48];
-  if (rows_sq)
+  if (tiles)
+    std::snprintf(kname, sizeof(kname), "score_tiles_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
+  else if (rows_sq)
     std::snprintf(kname, sizeof(kname), "%s<%d,%d,%s>", c->row_dma ? "score_rowsd_kernel" : "score_rows_kernel",
                   D.n_space, rows_sq, best_out ? "best" : "all");
   else if (v2)
@@ -742,7 +761,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
-    if (rows_sq)
+    if (tiles)
+      e = csm::launch_score_tiles(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
+                                  c->tile_beams, c->stream);
+    else if (rows_sq)
       e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr,
                                  D.n_space, rows_sq, c->row_dma, c->stream);
@@ -789,7 +812,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     const size_t pbytes = (size_t)nw * (size_t)bps * sizeof(BestPartial);
     if ((e = c->partials.ensure(pbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(partials)");
     if ((e = c->best.ensure((size_t)nw * sizeof(BestPartial))) != hipSuccess) return c->hip_fail(e, "hipMalloc(best)");
-    if (rows_sq)
+    if (tiles)
+      e = csm::launch_score_tiles(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                  (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
+                                  D.n_space, c->tile_beams, c->stream);
+    else if (rows_sq)
       e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
                                  D.n_space, rows_sq, c->row_dma, c->stream);
@@ -1341,7 +1368,9 @@ int csm_create(int device, csm_ctx** out) {
     c->column_kernel = std::strcmp(env, "v1") != 0;
     c->row_kernel = std::strcmp(env, "v1") != 0 && std::strcmp(env, "v2") != 0;
     c->row_dma = std::strcmp(env, "v3") != 0;
+    c->tile_kernel = std::strcmp(env, "v5") == 0;
   }
+  if (const char* env = std::getenv("CSM_TILE_BEAMS")) c->tile_beams = std::atoi(env) == 4 ? 4 : 8;
   if (const char* env = std::getenv("CSM_PIPELINE")) {  // 0: never split the 3-level batch
     const int v = std::atoi(env);
     c->pipeline_min = v > 0 ? v : INT32_MAX;

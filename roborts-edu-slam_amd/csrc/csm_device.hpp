@@ -1,0 +1,66 @@
+// csm_device.hpp — device helpers shared by the scoring kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "csm_internal.hpp"
+
+namespace csm {
+namespace dev {
+
+// XCD-aware, bijective block remap (cdna_hip_programming.md T1): blocks that
+// share a logical neighbourhood (one window) land on one XCD's L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (orig >> 3);
+}
+
+// Divisor (:659) and centre penalty (:718-745) of one candidate.
+__device__ __forceinline__ double penalized(const LevelWork& L, const ScanWork& S, double acc, double x,
+                                           double y, double angle) {
+  double score = acc / S.divisor;
+  if (L.use_penalty) {
+    // util::DoubleEqual(score, 0.0) with kDoubleTolerance = 1e-6.
+    const bool is_zero = (score < 0.0) ? (score >= -1e-06) : (score <= 1e-06);
+    if (!is_zero) {
+      const double dx = x - S.cx, dy = y - S.cy;
+      double d2 = dx * dx + dy * dy;
+      d2 *= (L.mres * L.mres);
+      double dp = 1.0 - (L.dist_gain * d2 / (L.size / 2));
+      dp = dp < 0.5 ? 0.5 : dp;  // std::max(dp, 0.5)
+      double da = angle - S.ct;
+      da = da * da;
+      double ap = 1.0 - (0.25 * da / 0.349);
+      ap = ap < 0.9 ? 0.9 : ap;
+      score = score * (dp * ap);
+    }
+  }
+  return score;
+}
+
+__device__ __forceinline__ bool better(double s, int64_t f, double bs, int64_t bf) {
+  return (s > bs) || (s == bs && f < bf);
+}
+
+// 16-byte buffer load written straight into LDS at lds + 16 * lane. The
+// builtin has no host-side form; the guard only keeps hipcc's host pass (which
+// must still emit the kernel's launch stub) from seeing it.
+__device__ __forceinline__ void buffer_load_lds16(__amdgpu_buffer_rsrc_t rsrc,
+                                                  __attribute__((address_space(3))) int32_t* lds,
+                                                  int voffset) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, lds, 16, voffset, 0, 0, 0);
+#endif
+}
+
+__device__ __forceinline__ double bcast_lane(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+}  // namespace dev
+}  // namespace csm

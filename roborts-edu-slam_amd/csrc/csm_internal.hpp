@@ -168,6 +168,13 @@ struct TreeWork {
 hipError_t launch_score_tree(const TreeWork& T, const ScanWork* d_scans, const double* d_pts,
                              const AngleEntry* d_angles, double* d_out, hipStream_t stream);
 
+// Beam-tile kernel (v5, csm_tiles.hip): INT mode, window step exactly one
+// cell, n_space in {13, 21}; same block layout as the row-segment kernels.
+// The host also keeps every endpoint within |map coords| < 16000 cells.
+bool tiles_supported(int ns);
+hipError_t launch_score_tiles(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
+                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
+                              int tile_beams, hipStream_t stream);
 // Grid statistics for the exact integer path (csm_set_grid).
 struct GridStats {
   int32_t min_gexp;       // every nonzero |v| is a multiple of 2^min_gexp
