@@ -223,8 +223,9 @@ def main():
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-scan latency probe (profiling runs: keeps rocprof "
                          "per-kernel averages equal to the timed steps' launches)")
-    ap.add_argument("--traffic-json", default=None,
-                    help="PMC-derived HBM bytes per launch of the dominant kernel (profiles/)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch per kernel (tools/pmc_run.sh -> "
+                         "tools/pmc_traffic.py; FETCH_SIZE and WRITE_SIZE passes of the same command)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -361,6 +362,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": (os.path.relpath(args.traffic_json, ROOT) if traffic is not None else None),
             "avg_launch_ms": avg_ms,
             "algorithmic_bytes_per_launch": bytes_per_launch,
         },

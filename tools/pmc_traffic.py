@@ -27,11 +27,22 @@ def _short(name: str) -> str:
         kt, integer, best = [a.strip() for a in name[i:name.index(">", i)].split(",")]
         return (f"score_cols_kernel<{kt},{'int' if integer == 'true' else 'f64'},"
                 f"{'best' if best == 'true' else 'all'}>")
+    for key in ("score_rowsd_kernel<", "score_rows_kernel<"):  # <int NS, int SQ, bool BEST>
+        if key in name:
+            i = name.index(key) + len(key)
+            ns, sq, best = [a.strip() for a in name[i:name.index(">", i)].split(",")]
+            return f"{key[:-1]}<{ns},{sq},{'best' if best == 'true' else 'all'}>"
+    key = "score_tiles_kernel<"
+    if key in name:  # <int NS, int T, bool BEST>
+        i = name.index(key) + len(key)
+        ns, _, best = [a.strip() for a in name[i:name.index(">", i)].split(",")]
+        return f"score_tiles_kernel<{ns},{'best' if best == 'true' else 'all'}>"
     for key in ("score_all_kernel<", "score_best_kernel<"):
         if key in name:
             i = name.index(key)
             return name[i:name.index(">", i) + 1]
-    for key in ("finish_kernel", "analyze_grid_kernel", "fixed_point_kernel", "reduce_best_kernel"):
+    for key in ("finish_fast_kernel", "finish_kernel", "analyze_grid_kernel", "fixed_point_kernel",
+                "reduce_best_kernel", "score_tree_kernel"):
         if key in name:
             return key
     return name[:64]
