@@ -447,6 +447,8 @@ struct csm_ctx {
   bool tile_kernel = false;   // CSM_KERNEL=v5 opts into the beam-tile kernel (exact; measured
                               // slower than v4 on config 2: 8.3 vs 7.0 ms, profiles/r01)
   int tile_beams = 8;         // beams per box of the beam-tile kernel (CSM_TILE_BEAMS: 4 or 8)
+  bool box_kernel = true;     // v6 box kernel for one-cell window steps; any CSM_KERNEL other
+                              // than v6 turns it off (CSM_KERNEL=v4: the LDS-DMA row kernel)
   std::vector<float> h_pack;
 
   // exact fixed-point copy of the grid (ensure_int_grid)
@@ -568,8 +570,8 @@ int ensure_int_grid(csm_ctx* c) {
   const double scale = std::ldexp(1.0, E);
   // strict: |v - outside| * 2^E <= 2^26 - 1, so 32 of them fit an int32 chunk
   if (((double)maxv + std::fabs((double)c->outside)) * scale >= std::ldexp(1.0, 26)) return CSM_OK;
-  const int32_t pitch = (c->info.size_x + 3) & ~3;  // 16-byte aligned rows
-  const int64_t ni = (int64_t)pitch * (c->info.size_y + 1);  // + the zero row
+  const int32_t pitch = csm::gridi_pitch(c->info.size_x);  // 16-byte aligned rows, zero pad columns
+  const int64_t ni = (int64_t)pitch * (c->info.size_y + csm::kGridiPadRows);  // + zero rows
   if (ni * 4 > 0x7F000000LL) return CSM_OK;  // buffer byte offsets (+ the kernels' bad offset) < 2^31
   if ((e = c->gridi.ensure((size_t)ni * (size_t)c->n_grids * sizeof(int32_t))) != hipSuccess)
     return c->hip_fail(e, "hipMalloc(gridi)");
@@ -677,10 +679,16 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     }
   }
   if (tiles) rows_sq = 0;
+  // v6 box kernel: whole-cell window step (use_int bounds |t| < 2^24 cells,
+  // which its rounding margin needs)
+  const bool box = !tiles && use_int && c->box_kernel && f == 1.0 && csm::box_supported(D.n_space) &&
+                   c->pitch >= c->info.size_x + csm::kGridiPadCols;
+  if (box) rows_sq = 0;
   const int cpl = pick_cpl(D.n_cand);
   const int64_t per_block = (int64_t)csm::kBlock * cpl;
   const int64_t rows_groups = (rows_sq || tiles) ? 64 / D.n_space : 1;
-  const int64_t bps = (rows_sq || tiles) ? (D.n_angles + rows_groups - 1) / rows_groups
+  const int64_t bps = box ? D.n_angles
+                      : (rows_sq || tiles) ? (D.n_angles + rows_groups - 1) / rows_groups
                       : v2    ? col_blocks * ktiles
                               : (D.n_cand + per_block - 1) / per_block;
   if (bps * nw > INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
@@ -702,7 +710,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     s.cx = W.center[0];
     s.cy = W.center[1];
     s.ct = W.center[2];
-    s.grid_sel = 0.f;
+    s.reserved = 0;
     s.grid_index = grid_index.empty() ? 0 : grid_index[(size_t)i];
   }
   LevelWork L{};
@@ -729,7 +737,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   L.ktiles = ktiles;
   L.col_blocks = (int32_t)col_blocks;
   L.pitch = c->pitch;
-  L.gridi_stride = (int64_t)c->pitch * (c->info.size_y + 1);
+  L.gridi_stride = (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows);
 
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
   if ((e = c->angles.ensure(n_angle_entries * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
@@ -744,7 +752,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const double alg_bytes = beams * (double)D.n_cand * 4.0;
   const double scorings = (double)nw * (double)D.n_cand;
   char kname[48];
-  if (tiles)
+  if (box)
+    std::snprintf(kname, sizeof(kname), "score_box_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
+  else if (tiles)
     std::snprintf(kname, sizeof(kname), "score_tiles_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (rows_sq)
     std::snprintf(kname, sizeof(kname), "%s<%d,%d,%s>", c->row_dma ? "score_rowsd_kernel" : "score_rows_kernel",
@@ -761,7 +771,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
-    if (tiles)
+    if (box)
+      e = csm::launch_score_box(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
+                                c->stream);
+    else if (tiles)
       e = csm::launch_score_tiles(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                   (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
                                   c->tile_beams, c->stream);
@@ -812,7 +826,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     const size_t pbytes = (size_t)nw * (size_t)bps * sizeof(BestPartial);
     if ((e = c->partials.ensure(pbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(partials)");
     if ((e = c->best.ensure((size_t)nw * sizeof(BestPartial))) != hipSuccess) return c->hip_fail(e, "hipMalloc(best)");
-    if (tiles)
+    if (box)
+      e = csm::launch_score_box(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
+                                D.n_space, c->stream);
+    else if (tiles)
       e = csm::launch_score_tiles(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                   (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
                                   D.n_space, c->tile_beams, c->stream);
@@ -1369,6 +1387,7 @@ int csm_create(int device, csm_ctx** out) {
     c->row_kernel = std::strcmp(env, "v1") != 0 && std::strcmp(env, "v2") != 0;
     c->row_dma = std::strcmp(env, "v3") != 0;
     c->tile_kernel = std::strcmp(env, "v5") == 0;
+    c->box_kernel = std::strcmp(env, "v6") == 0;
   }
   if (const char* env = std::getenv("CSM_TILE_BEAMS")) c->tile_beams = std::atoi(env) == 4 ? 4 : 8;
   if (const char* env = std::getenv("CSM_PIPELINE")) {  // 0: never split the 3-level batch

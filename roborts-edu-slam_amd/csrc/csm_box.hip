@@ -1,0 +1,260 @@
+// csm_box.hip — v6 "box" scoring kernel: window levels whose step is exactly
+// one map cell (the coarse level of every shipped parameter set at its own map
+// resolution, e.g. simulatin_param.yaml's 0.05 m window on a 0.05 m map).
+//
+// With step 1, candidate (j, k) of angle a reads, for beam b, cell
+// (ix_j, iy_k) = (trunc((lx + x_j) + 0.5), trunc((ly + y_k) + 0.5))
+// (correlate_scan_matcher.h:637-662 with x_j = x0 + j, y_k = y0 + k, :569/:572).
+// Whenever t = (lx + x0) + 0.5 is non-negative with a fraction at least
+// kBoxMargin away from an integer, ix_j = trunc(t) + j for every j (see
+// kBoxMargin for the rounding argument): the beam's cells form one
+// n_space x n_space box of the grid. The fixed-point grid (gridi) is padded
+// with zero columns and rows, so the box is n_space row pieces of 16 bytes
+// that one buffer_load_dwordx4 per lane fetches: lane (k, q) loads row
+// iy0 + k, cells ix0 + 4q .. ix0 + 4q + 3, and adds them to its four
+// candidates (j = 4q .. 4q+3, k). The box corner is one scalar per beam
+// (soffset), so a beam costs one vector-memory instruction, one readlane and
+// four integer adds per wave: no LDS, no per-lane address arithmetic.
+// Beams that fail the test (off the grid on the low side, or a fraction
+// within the margin of a rounding boundary) read the zero
+// block and are summed afterwards cell by cell with the reference's own
+// expressions, so the scores are the reference's bit for bit in every case.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "csm_device.hpp"
+#include "csm_internal.hpp"
+
+namespace csm {
+namespace {
+
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+
+// Rounding argument. Host: every |x_j|, |lx + x_j|, |t_j| < 2^24 cells
+// (use_int's R * 4 * pitch < 2^30, pitch >= 16). With T = lx + x0 + 0.5 (real)
+// and x_j = fl(x0 + j) = x0 + j + d_j, |d_j| <= 2^-29, the computed
+// t_j = fl(fl(lx + x_j) + 0.5) = T + j + E_j with |E_j| <= 3 * 2^-29 < 2^-27.
+// If t_0 >= 0 and frac(t_0) is in [2^-20, 1 - 2^-20], T is more than
+// 2^-20 - 2^-27 > |E_j| from an integer, so trunc(t_j) = floor(T) + j =
+// trunc(t_0) + j for every j; the same for rows.
+constexpr double kBoxMargin = 0x1p-20;
+
+template <int NS, int D, bool BEST>
+__global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWork* __restrict__ scans,
+                                                       const double2* __restrict__ pts,
+                                                       const AngleEntry* __restrict__ angles,
+                                                       double* __restrict__ out,
+                                                       BestPartial* __restrict__ partials) {
+  constexpr int NQ = (NS + 3) / 4;  // 16-byte pieces per box row
+  static_assert(NS * NQ <= 64, "one box row piece per lane");
+  static_assert(64 % D == 0 && 32 % D == 0, "loads in flight divide the fold block");
+  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int win = bid / L.n_angles;
+  const int a = bid - win * L.n_angles;
+  const ScanWork S = scans[win];
+  const AngleEntry ae = angles[S.angle_off + a];
+  const int lane = threadIdx.x;
+  const bool act = lane < NS * NQ;
+  // idle lanes repeat row 0's addresses (no extra cache lines)
+  const int k = act ? lane / NQ : 0;
+  const int q = act ? lane - k * NQ : lane % NQ;
+  const double f = L.step_cells;     // 1.0 (host)
+  const double x_0 = S.x0 + 0 * f;   // :569 at j = 0
+  const double y_0 = S.y0 + 0 * f;   // :572 at k = 0
+  const int sx = L.size_x, sy = L.size_y;
+  const int pitch4 = L.pitch * 4;
+  const int zero_off = sy * pitch4;  // first of the zero rows
+  const double2* __restrict__ P = pts + S.pts_off;
+  const int step = S.step;
+  const int n_used = S.n_used;
+  const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
+  const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
+  const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)ghi << 32) | glo), (short)0, (int)(L.gridi_stride * 4), 0x00020000);
+  const int voff = k * pitch4 + 16 * q;
+
+  // The box test of one beam point; on success (ix0, iy0) is the box corner.
+  auto box_test = [&](const double2 p, double& lx, double& ly, int& ix0, int& iy0) -> bool {
+    lx = ae.cosine * p.x - ae.sine * p.y;  // :179
+    ly = ae.sine * p.x + ae.cosine * p.y;  // :180
+    const double tx = (lx + x_0) + 0.5;
+    const double ty = (ly + y_0) + 0.5;
+    const double fx = tx - floor(tx);
+    const double fy = ty - floor(ty);
+    const bool clean = tx >= 0.0 && ty >= 0.0 && fx >= kBoxMargin && fx <= 1.0 - kBoxMargin &&
+                       fy >= kBoxMargin && fy <= 1.0 - kBoxMargin;
+    ix0 = clean ? (int)tx : 0;
+    iy0 = clean ? (int)ty : 0;
+    return clean;
+  };
+  // Lane l: the box byte offset of beam cb + l (the zero block for beams past
+  // n_used, boxes wholly past the grid's high edges and rejected beams).
+  auto offsets = [&](const double2 p, int cb, bool& slow) -> int {
+    double lx, ly;
+    int ix0, iy0;
+    const bool clean = box_test(p, lx, ly, ix0, iy0);
+    const bool live = cb + lane < n_used;
+    slow |= live && !clean;
+    return (live && clean && ix0 < sx && iy0 < sy) ? iy0 * pitch4 + ix0 * 4 : zero_off;
+  };
+  auto point = [&](int cb) { return P[(int64_t)min(cb + lane, n_used - 1) * step]; };
+
+  bool slow = false;
+  int offA = offsets(point(0), 0, slow);    // beams of the current chunk
+  int offB = offsets(point(64), 64, slow);  // and of the next one
+  double2 pn = point(128);                  // points of the chunk after, in flight
+  // soffset of beam cb + r, 0 <= r < 128
+  auto off_of = [&](int r) -> int {
+    return r < 64 ? __builtin_amdgcn_readlane(offA, r) : __builtin_amdgcn_readlane(offB, r - 64);
+  };
+  auto load = [&](int soff) { return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0); };
+
+  int64_t acc[4] = {0, 0, 0, 0};
+  v4i buf[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) buf[j] = load(off_of(j));
+  const int nchunks = (n_used + 63) / 64;
+  for (int c = 0; c < nchunks; ++c) {
+#pragma unroll
+    for (int h = 0; h < 64; h += 32) {  // 32 * (2^26 - 1) < 2^31 (ensure_int_grid)
+      int32_t part[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < 32; i += D) {
+        // the D box corners this group issues (readlanes batched: a VALU
+        // SGPR write needs 5 wait states before a VMEM instruction reads it)
+        int so[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) so[j] = off_of(h + i + j + D);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          v4i v = buf[j];
+          asm volatile("" : "+v"(v));  // consume beam h+i+j here, in order
+          part[0] += v.x;
+          part[1] += v.y;
+          part[2] += v.z;
+          part[3] += v.w;
+          asm volatile("" : "+v"(part[0]), "+v"(part[1]), "+v"(part[2]), "+v"(part[3]));
+          buf[j] = load(so[j]);
+          // keep the issue order: D loads in flight, not the whole chunk
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] += part[t];
+    }
+    offA = offB;
+    offB = offsets(pn, (c + 2) * 64, slow);
+    pn = point((c + 3) * 64);
+  }
+
+  if (__builtin_amdgcn_ballot_w64(slow) != 0) {
+    // rejected beams, cell by cell with the reference's expressions
+    for (int b = 0; b < n_used; ++b) {
+      const double2 p = P[(int64_t)b * step];
+      double lx, ly;
+      int ix0, iy0;
+      if (box_test(p, lx, ly, ix0, iy0)) continue;  // uniform: one beam for the whole wave
+      const int gy = (int)((ly + (S.y0 + k * f)) + 0.5);
+      const bool iny = (unsigned)gy < (unsigned)sy;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = 4 * q + t;
+        if (j < NS) {
+          const int gx = (int)((lx + (S.x0 + j * f)) + 0.5);
+          const bool in = iny && (unsigned)gx < (unsigned)sx;
+          acc[t] += gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)sy * L.pitch];
+        }
+      }
+    }
+  }
+
+  double bs = -1.0e300;
+  int64_t bf = INT64_MAX;
+  const double yk = S.y0 + k * f;  // :572
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int j = 4 * q + t;
+    if (act && j < NS) {
+      const double accd = (double)(acc[t] + (int64_t)n_used * L.outside_i) * L.int_scale;
+      const double xj = S.x0 + j * f;  // :569
+      const double score = dev::penalized(L, S, accd, xj, yk, ae.angle);
+      const int64_t flat = ((int64_t)a * NS + j) * NS + k;
+      if (BEST) {
+        if (dev::better(score, flat, bs, bf)) {
+          bs = score;
+          bf = flat;
+        }
+      } else {
+        out[S.out_off + flat] = score;
+      }
+    }
+  }
+  if (BEST) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double os = __shfl_down(bs, o, 64);
+      const int64_t of = __shfl_down(bf, o, 64);
+      if (dev::better(os, of, bs, bf)) {
+        bs = os;
+        bf = of;
+      }
+    }
+    if (lane == 0) partials[(int64_t)win * L.blocks_per_scan + a] = BestPartial{bs, bf};
+  }
+}
+
+template <int NS, int D>
+hipError_t launch_ns(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
+                     BestPartial* part, unsigned nblk, hipStream_t stream) {
+  if (part)
+    hipLaunchKernelGGL((score_box_kernel<NS, D, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+  else
+    hipLaunchKernelGGL((score_box_kernel<NS, D, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool box_supported(int ns) { return ns >= 9 && ns <= 16; }
+
+int box_depth() {
+  static const int d = [] {
+    const char* env = std::getenv("CSM_BOX_DEPTH");
+    return (env && std::atoi(env) == 16) ? 16 : 8;
+  }();
+  return d;
+}
+
+hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
+                            const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
+                            hipStream_t stream) {
+  const int64_t nblk = (int64_t)L.n_scans * L.n_angles;
+  if (nblk <= 0 || nblk > INT32_MAX || !L.int_mode || L.step_cells != 1.0 || L.blocks_per_scan != L.n_angles ||
+      L.pitch < L.size_x + kGridiPadCols || L.pitch % 4 != 0)
+    return hipErrorInvalidValue;
+  const double2* p = reinterpret_cast<const double2*>(d_pts);
+  const unsigned n = (unsigned)nblk;
+  const bool deep = box_depth() == 16;
+#define CSM_BOX_CASE(N)                                                                           \
+  case N:                                                                                         \
+    return deep ? launch_ns<N, 16>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)         \
+                : launch_ns<N, 8>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+  switch (ns) {
+    CSM_BOX_CASE(9)
+    CSM_BOX_CASE(10)
+    CSM_BOX_CASE(11)
+    CSM_BOX_CASE(12)
+    CSM_BOX_CASE(13)
+    CSM_BOX_CASE(14)
+    CSM_BOX_CASE(15)
+    CSM_BOX_CASE(16)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef CSM_BOX_CASE
+}
+
+}  // namespace csm

@@ -21,7 +21,7 @@ struct ScanWork {
   double divisor;       // use_point_size after the :561 rule
   double x0, y0;        // search_space_start_x/y (:546-547), map cells
   double cx, cy, ct;    // window centre (map cells, rad)
-  float grid_sel;       // reserved
+  int32_t reserved;
   int32_t grid_index;   // which resident grid (submap) this window reads
 };
 
@@ -55,9 +55,9 @@ struct LevelWork {
   int32_t n_cols;          // n_angles * n_space (column kernel)
   int32_t ktiles;          // ceil(n_space / KT)
   int32_t col_blocks;      // ceil(n_cols / 64)
-  int32_t pitch;           // gridi row pitch in cells (size_x rounded up to 4)
-  int64_t gridi_stride;    // int32 cells between consecutive gridi grids (pitch * (size_y + 1):
-                           // each grid ends with a zero row)
+  int32_t pitch;           // gridi row pitch in cells (gridi_pitch(size_x))
+  int64_t gridi_stride;    // int32 cells between consecutive gridi grids (pitch * (size_y +
+                           // kGridiPadRows): each grid ends with zero rows)
 };
 
 // Argmax partial: best score of a block and its flat candidate index.
@@ -175,6 +175,19 @@ bool tiles_supported(int ns);
 hipError_t launch_score_tiles(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                               const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
                               int tile_beams, hipStream_t stream);
+// Box kernel (v6, csm_box.hip): INT mode, window step exactly one cell,
+// n_space <= 16; one wave per (window, angle), one 16-byte row piece per lane
+// per beam. blocks_per_scan = n_angles.
+bool box_supported(int ns);
+hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
+                            const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
+                            hipStream_t stream);
+// gridi layout: row pitch = round4(size_x + kGridiPadCols) cells, size_y +
+// kGridiPadRows rows; every cell outside [0,size_x) x [0,size_y) is zero, so a
+// 16 x 16 box whose corner lies on the grid never leaves the buffer.
+constexpr int kGridiPadCols = 15;
+constexpr int kGridiPadRows = 16;
+constexpr int32_t gridi_pitch(int32_t sx) { return (sx + kGridiPadCols + 3) & ~3; }
 // Grid statistics for the exact integer path (csm_set_grid).
 struct GridStats {
   int32_t min_gexp;       // every nonzero |v| is a multiple of 2^min_gexp
@@ -184,7 +197,7 @@ struct GridStats {
 };
 hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hipStream_t stream);
 // Row pitch of gridi is a multiple of 4 cells, so 16-byte row segments are
-// aligned; size_y + 1 rows are written, the last one zero.
+// aligned; size_y + kGridiPadRows rows are written, the pad zero.
 hipError_t launch_fixed_point(const float* g, int32_t sx, int32_t sy, int32_t pitch, float outside,
                               int int_exp, int32_t* gi, hipStream_t stream);
 // Reduce per-window partials (blocks_per_scan each) to one BestPartial per window.

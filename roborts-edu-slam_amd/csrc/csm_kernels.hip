@@ -1017,7 +1017,7 @@ __global__ __launch_bounds__(256) void analyze_grid_kernel(const float* __restri
 __global__ __launch_bounds__(256) void fixed_point_kernel(const float* __restrict__ g, int32_t sx,
                                                           int32_t sy, int32_t pitch, float outside,
                                                           double scale, int32_t* __restrict__ gi) {
-  const int64_t n = (int64_t)pitch * (sy + 1);
+  const int64_t n = (int64_t)pitch * (sy + kGridiPadRows);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t y = i / pitch;
@@ -1040,7 +1040,7 @@ hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hi
 
 hipError_t launch_fixed_point(const float* g, int32_t sx, int32_t sy, int32_t pitch, float outside,
                               int int_exp, int32_t* gi, hipStream_t stream) {
-  const int64_t n = (int64_t)pitch * (sy + 1);
+  const int64_t n = (int64_t)pitch * (sy + kGridiPadRows);
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(fixed_point_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0,
                      stream, g, sx, sy, pitch, outside, ldexp(1.0, int_exp), gi);

@@ -232,8 +232,9 @@ def test_batch_three_level_bit_exact(ctx, world2000, which):
 
 
 def test_headline_runs_row_segment_kernels(ctx, world2000):
-    """The config-2 levels run on the v3 row-segment kernels (not a fallback),
-    and the device finish, and the result is the oracle's bit for bit."""
+    """The config-2 levels run on the box kernel (coarse: one-cell step) and the
+    LDS-DMA row-segment kernels (fine, super-fine), not a fallback, and the
+    device finish, and the result is the oracle's bit for bit."""
     from roborts_csm.params import headline_levels
     w, b = world2000
     ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
@@ -244,7 +245,7 @@ def test_headline_runs_row_segment_kernels(ctx, world2000):
     s = ctx.scan_matchers_batch(b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(), poses, covs)
     names = {k["name"] for k in ctx.kernel_stats()}
     ctx.set_profiling(False)
-    for want in ("score_rowsd_kernel<13,4,all>", "score_rowsd_kernel<11,2,all>",
+    for want in ("score_box_kernel<13,all>", "score_rowsd_kernel<11,2,all>",
                  "score_rowsd_kernel<3,1,all>", "finish_kernel<5070>"):
         assert want in names, names
     m = O.Map(w.grid, w.resolution, w.offset)
@@ -363,7 +364,7 @@ def test_kernel_variants_agree(f1, grid_kind):
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
     ctxs = []
-    for kern in ("v1", "v2", "v3", "v5", None):  # None: default (v4 LDS-DMA row segments where eligible)
+    for kern in ("v1", "v2", "v3", "v4", "v5", None):  # None: default (v6 box kernel / v4 where eligible)
         if kern:
             os.environ["CSM_KERNEL"] = kern
         try:
@@ -377,6 +378,53 @@ def test_kernel_variants_agree(f1, grid_kind):
         for p in params:
             sc = c.score_window(f1["points"], p, f1["center"])
             assert np.array_equal(sc, O.score_window(m, f1["points"], p, f1["center"], sc.size)), (grid_kind, p)
+    for c in ctxs:
+        c.close()
+
+
+def test_box_kernel_edge_beams(world2000):
+    """v6 box kernel (one-cell window step) on its margin cases: beams whose
+    (lx + x0) + 0.5 is an exact integer (points at the origin, window with
+    x0 + 0.5 integral), beams off the grid's low edge (negative t, where the
+    reference's truncation is not a floor) and past its high edges, and windows
+    whose x0 + j crosses a power of two (inexact steps) -- all scores and the
+    argmax against the oracle and against the v4 row kernel."""
+    import roborts_csm
+    from roborts_csm.params import SIM_YAML_LEVELS
+    w, b = world2000
+    m = O.Map(w.grid, w.resolution, w.offset)
+    pts = b.points_cells[b.offsets[0]:b.offsets[1]]
+    extra = np.array([[0.0, 0.0], [0.0, 0.0], [1.0, -2.0], [-1500.0, 3.0], [2.0, -1500.0],
+                      [900.0, 900.0], [-3000.0, -3000.0], [0.25, 0.0]])
+    pts = np.ascontiguousarray(np.concatenate([pts, extra]))
+    lv = SIM_YAML_LEVELS[0].with_(use_point_size=pts.shape[0])
+    half = (lv.search_space_size / w.resolution) * 0.5
+    c0 = 100.5 + half
+    assert float(c0 - half) + 0.5 == 101.0  # origin points sit exactly on a rounding boundary
+    centers = [[c0, 200.5 + half, 0.0], [c0, 200.5 + half, 1.3],
+               [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
+               [6.2, 3.1, -2.5], [1995.0, 1990.0, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
+    ctxs = []
+    for kern in (None, "v4"):
+        if kern:
+            os.environ["CSM_KERNEL"] = kern
+        try:
+            ctxs.append(roborts_csm.Context(0))
+        finally:
+            os.environ.pop("CSM_KERNEL", None)
+    for c in ctxs:
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+    ctxs[0].set_profiling(True)
+    for cen in centers:
+        cen = np.array(cen)
+        want = O.score_window(m, pts, lv, cen, 30 * 13 * 13)
+        for c in ctxs:
+            assert np.array_equal(c.score_window(pts, lv, cen), want), cen
+            got = c.best_window(pts, lv, cen)
+            s, flat = O.best_window(m, pts, lv, cen)
+            assert got.score == s and got.flat_index == flat
+    names = {k["name"] for k in ctxs[0].kernel_stats()}
+    assert "score_box_kernel<13,all>" in names and "score_box_kernel<13,best>" in names, names
     for c in ctxs:
         c.close()
 
