@@ -23,6 +23,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 
 #include "csm_device.hpp"
 #include "csm_internal.hpp"
@@ -41,7 +42,10 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));
 // trunc(t_0) + j for every j; the same for rows.
 constexpr double kBoxMargin = 0x1p-20;
 
-template <int NS, int D, bool BEST>
+// Beams per run-list segment (RUNS): the list of one segment lives in LDS.
+constexpr int kRunSeg = 1152;
+
+template <int NS, int D, bool RUNS, bool BEST>
 __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWork* __restrict__ scans,
                                                        const double2* __restrict__ pts,
                                                        const AngleEntry* __restrict__ angles,
@@ -102,52 +106,125 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   };
   auto point = [&](int cb) { return P[(int64_t)min(cb + lane, n_used - 1) * step]; };
 
-  bool slow = false;
-  int offA = offsets(point(0), 0, slow);    // beams of the current chunk
-  int offB = offsets(point(64), 64, slow);  // and of the next one
-  double2 pn = point(128);                  // points of the chunk after, in flight
-  // soffset of beam cb + r, 0 <= r < 128
-  auto off_of = [&](int r) -> int {
-    return r < 64 ? __builtin_amdgcn_readlane(offA, r) : __builtin_amdgcn_readlane(offB, r - 64);
-  };
   auto load = [&](int soff) { return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0); };
-
   int64_t acc[4] = {0, 0, 0, 0};
+  bool slow = false;
   v4i buf[D];
+  if constexpr (!RUNS) {
+    int offA = offsets(point(0), 0, slow);    // beams of the current chunk
+    int offB = offsets(point(64), 64, slow);  // and of the next one
+    double2 pn = point(128);                  // points of the chunk after, in flight
+    // soffset of beam cb + r, 0 <= r < 128
+    auto off_of = [&](int r) -> int {
+      return r < 64 ? __builtin_amdgcn_readlane(offA, r) : __builtin_amdgcn_readlane(offB, r - 64);
+    };
 #pragma unroll
-  for (int j = 0; j < D; ++j) buf[j] = load(off_of(j));
-  const int nchunks = (n_used + 63) / 64;
-  for (int c = 0; c < nchunks; ++c) {
+    for (int j = 0; j < D; ++j) buf[j] = load(off_of(j));
+    const int nchunks = (n_used + 63) / 64;
+    for (int c = 0; c < nchunks; ++c) {
 #pragma unroll
-    for (int h = 0; h < 64; h += 32) {  // 32 * (2^26 - 1) < 2^31 (ensure_int_grid)
-      int32_t part[4] = {0, 0, 0, 0};
+      for (int h = 0; h < 64; h += 32) {  // 32 * (2^26 - 1) < 2^31 (ensure_int_grid)
+        int32_t part[4] = {0, 0, 0, 0};
 #pragma unroll
-      for (int i = 0; i < 32; i += D) {
-        // the D box corners this group issues (readlanes batched: a VALU
-        // SGPR write needs 5 wait states before a VMEM instruction reads it)
-        int so[D];
+        for (int i = 0; i < 32; i += D) {
+          // the D box corners this group issues (readlanes batched: a VALU
+          // SGPR write needs 5 wait states before a VMEM instruction reads it)
+          int so[D];
 #pragma unroll
-        for (int j = 0; j < D; ++j) so[j] = off_of(h + i + j + D);
+          for (int j = 0; j < D; ++j) so[j] = off_of(h + i + j + D);
+#pragma unroll
+          for (int j = 0; j < D; ++j) {
+            v4i v = buf[j];
+            asm volatile("" : "+v"(v));  // consume beam h+i+j here, in order
+            part[0] += v.x;
+            part[1] += v.y;
+            part[2] += v.z;
+            part[3] += v.w;
+            asm volatile("" : "+v"(part[0]), "+v"(part[1]), "+v"(part[2]), "+v"(part[3]));
+            buf[j] = load(so[j]);
+            // keep the issue order: D loads in flight, not the whole chunk
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] += part[t];
+      }
+      offA = offB;
+      offB = offsets(pn, (c + 2) * 64, slow);
+      pn = point((c + 3) * 64);
+    }
+  } else {
+    // Run list: consecutive beams with the same box corner (common: at a few
+    // metres, neighbouring beams of a 0.25 deg scanner land in the same cell)
+    // form one run; a run is one load whose values are added count times.
+    // Runs of boxes wholly off the grid and of rejected beams are dropped
+    // (they read zeros). Lists are built per segment of kRunSeg beams.
+    __shared__ int32_t run_off[kRunSeg + 64 + 2 * D];
+    __shared__ int32_t run_cnt[kRunSeg + 64 + 2 * D];
+    for (int s0 = 0; s0 < n_used; s0 += kRunSeg) {
+      const int s1 = min(n_used, s0 + kRunSeg);
+      int nruns = 0;
+      for (int cb = s0; cb < s1; cb += 64) {
+        int off = offsets(point(cb), cb, slow);
+        const bool live = cb + lane < s1;
+        const int prev = __shfl_up(off, 1, 64);
+        const bool edge = live && (lane == 0 || off != prev);  // a new corner starts here
+        const uint64_t E = __builtin_amdgcn_ballot_w64(edge);
+        const int nlive = min(64, s1 - cb);
+        const uint64_t above = lane == 63 ? 0ull : (E >> (lane + 1)) << (lane + 1);
+        const int next = above ? (int)__builtin_ctzll(above) : nlive;
+        const bool head = edge && off != zero_off;
+        const uint64_t Hm = __builtin_amdgcn_ballot_w64(head);
+        const int rank = __builtin_popcountll(Hm & ((1ull << lane) - 1));
+        if (head) {
+          run_off[nruns + rank] = off;
+          run_cnt[nruns + rank] = next - lane;
+        }
+        nruns += __builtin_popcountll(Hm);
+      }
+      // whole groups of D, then empty runs (zero block, count 0) far enough
+      // past the list for the issue-ahead window below
+      const int npad = (nruns + D - 1) / D * D;
+      for (int i = nruns + lane; i < npad + 64 + D; i += 64) {
+        run_off[i] = zero_off;
+        run_cnt[i] = 0;
+      }
+      __syncthreads();
+      if (npad == 0) continue;
+      // lane i of cA: count of run rb + i; of wI: corner of run rb + D + i
+      // (loads are issued exactly D runs ahead of their use)
+      int rb = 0;
+      int cA = run_cnt[lane];
+      int wI = run_off[D + lane];
+#pragma unroll
+      for (int j = 0; j < D; ++j) buf[j] = load(run_off[j]);
+      for (int r0 = 0; r0 < npad; r0 += D) {
+        int so[D], cn[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          cn[j] = __builtin_amdgcn_readlane(cA, r0 + j - rb);
+          so[j] = __builtin_amdgcn_readlane(wI, r0 + j - rb);
+        }
 #pragma unroll
         for (int j = 0; j < D; ++j) {
           v4i v = buf[j];
-          asm volatile("" : "+v"(v));  // consume beam h+i+j here, in order
-          part[0] += v.x;
-          part[1] += v.y;
-          part[2] += v.z;
-          part[3] += v.w;
-          asm volatile("" : "+v"(part[0]), "+v"(part[1]), "+v"(part[2]), "+v"(part[3]));
+          asm volatile("" : "+v"(v));  // consume run r0+j here, in order
+          acc[0] += (int64_t)cn[j] * v.x;
+          acc[1] += (int64_t)cn[j] * v.y;
+          acc[2] += (int64_t)cn[j] * v.z;
+          acc[3] += (int64_t)cn[j] * v.w;
+          asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
           buf[j] = load(so[j]);
-          // keep the issue order: D loads in flight, not the whole chunk
           __builtin_amdgcn_sched_barrier(0);
         }
+        if (((r0 + D) & 63) == 0) {  // slide the register windows by 64 runs
+          rb += 64;
+          cA = run_cnt[rb + lane];
+          wI = run_off[rb + D + lane];
+        }
       }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] += part[t];
+      __syncthreads();  // the next segment rewrites the list
     }
-    offA = offB;
-    offB = offsets(pn, (c + 2) * 64, slow);
-    pn = point((c + 3) * 64);
   }
 
   if (__builtin_amdgcn_ballot_w64(slow) != 0) {
@@ -206,13 +283,15 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   }
 }
 
-template <int NS, int D>
+template <int NS, int D, bool RUNS>
 hipError_t launch_ns(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
                      BestPartial* part, unsigned nblk, hipStream_t stream) {
   if (part)
-    hipLaunchKernelGGL((score_box_kernel<NS, D, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+    hipLaunchKernelGGL((score_box_kernel<NS, D, RUNS, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out,
+                       part);
   else
-    hipLaunchKernelGGL((score_box_kernel<NS, D, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+    hipLaunchKernelGGL((score_box_kernel<NS, D, RUNS, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out,
+                       part);
   return hipGetLastError();
 }
 
@@ -220,12 +299,15 @@ hipError_t launch_ns(const LevelWork& L, const ScanWork* s, const double2* p, co
 
 bool box_supported(int ns) { return ns >= 9 && ns <= 16; }
 
-int box_depth() {
-  static const int d = [] {
+// CSM_BOX=beams: one load per beam (no run list); CSM_BOX_DEPTH=16: 16 loads
+// in flight per wave instead of 8.
+int box_mode() {
+  static const int m = [] {
     const char* env = std::getenv("CSM_BOX_DEPTH");
-    return (env && std::atoi(env) == 16) ? 16 : 8;
+    const char* mode = std::getenv("CSM_BOX");
+    return ((env && std::atoi(env) == 16) ? 1 : 0) | ((mode && std::strcmp(mode, "beams") == 0) ? 2 : 0);
   }();
-  return d;
+  return m;
 }
 
 hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
@@ -237,11 +319,19 @@ hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const d
     return hipErrorInvalidValue;
   const double2* p = reinterpret_cast<const double2*>(d_pts);
   const unsigned n = (unsigned)nblk;
-  const bool deep = box_depth() == 16;
-#define CSM_BOX_CASE(N)                                                                           \
-  case N:                                                                                         \
-    return deep ? launch_ns<N, 16>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)         \
-                : launch_ns<N, 8>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+  const int mode = box_mode();
+#define CSM_BOX_CASE(N)                                                                        \
+  case N:                                                                                      \
+    switch (mode) {                                                                            \
+      case 0:                                                                                  \
+        return launch_ns<N, 8, true>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);   \
+      case 1:                                                                                  \
+        return launch_ns<N, 16, true>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);  \
+      case 2:                                                                                  \
+        return launch_ns<N, 8, false>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);  \
+      default:                                                                                 \
+        return launch_ns<N, 16, false>(L, d_scans, p, d_angles, d_out, d_partials, n, stream); \
+    }
   switch (ns) {
     CSM_BOX_CASE(9)
     CSM_BOX_CASE(10)
