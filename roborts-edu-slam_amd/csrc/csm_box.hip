@@ -43,7 +43,16 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));
 constexpr double kBoxMargin = 0x1p-20;
 
 // Beams per run-list segment (RUNS): the list of one segment lives in LDS.
-constexpr int kRunSeg = 1152;
+#ifndef CSM_RUN_SEG
+#define CSM_RUN_SEG 1152
+#endif
+constexpr int kRunSeg = CSM_RUN_SEG;
+#ifndef CSM_BOX_PF
+#define CSM_BOX_PF 6
+#endif
+constexpr int kPF = CSM_BOX_PF;  // chunks of beam points in flight while a run list is built
+static_assert(kRunSeg % 64 == 0, "segments of whole 64-beam chunks");
+
 
 template <int NS, int D, bool RUNS, bool BEST>
 __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWork* __restrict__ scans,
@@ -96,19 +105,21 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   };
   // Lane l: the box byte offset of beam cb + l (the zero block for beams past
   // n_used, boxes wholly past the grid's high edges and rejected beams).
-  auto offsets = [&](const double2 p, int cb, bool& slow) -> int {
+  // slow: bit c marks 64-beam chunk c as holding a rejected beam (bit 63:
+  // some chunk >= 63), for the cell-by-cell pass at the end.
+  auto offsets = [&](const double2 p, int cb, uint64_t& slow) -> int {
     double lx, ly;
     int ix0, iy0;
     const bool clean = box_test(p, lx, ly, ix0, iy0);
     const bool live = cb + lane < n_used;
-    slow |= live && !clean;
+    if (__builtin_amdgcn_ballot_w64(live && !clean) != 0) slow |= 1ull << min(cb >> 6, 63);
     return (live && clean && ix0 < sx && iy0 < sy) ? iy0 * pitch4 + ix0 * 4 : zero_off;
   };
   auto point = [&](int cb) { return P[(int64_t)min(cb + lane, n_used - 1) * step]; };
 
   auto load = [&](int soff) { return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0); };
   int64_t acc[4] = {0, 0, 0, 0};
-  bool slow = false;
+  uint64_t slow = 0;
   v4i buf[D];
   if constexpr (!RUNS) {
     int offA = offsets(point(0), 0, slow);    // beams of the current chunk
@@ -164,23 +175,36 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
     for (int s0 = 0; s0 < n_used; s0 += kRunSeg) {
       const int s1 = min(n_used, s0 + kRunSeg);
       int nruns = 0;
-      for (int cb = s0; cb < s1; cb += 64) {
-        int off = offsets(point(cb), cb, slow);
-        const bool live = cb + lane < s1;
-        const int prev = __shfl_up(off, 1, 64);
-        const bool edge = live && (lane == 0 || off != prev);  // a new corner starts here
-        const uint64_t E = __builtin_amdgcn_ballot_w64(edge);
-        const int nlive = min(64, s1 - cb);
-        const uint64_t above = lane == 63 ? 0ull : (E >> (lane + 1)) << (lane + 1);
-        const int next = above ? (int)__builtin_ctzll(above) : nlive;
-        const bool head = edge && off != zero_off;
-        const uint64_t Hm = __builtin_amdgcn_ballot_w64(head);
-        const int rank = __builtin_popcountll(Hm & ((1ull << lane) - 1));
-        if (head) {
-          run_off[nruns + rank] = off;
-          run_cnt[nruns + rank] = next - lane;
+      // points of kPF chunks in flight: the list build is latency-bound
+      // otherwise (one dependent load per 64 beams)
+      double2 pq[kPF];
+#pragma unroll
+      for (int u = 0; u < kPF; ++u) pq[u] = point(s0 + 64 * u);
+      for (int cb0 = s0; cb0 < s1; cb0 += 64 * kPF) {
+#pragma unroll
+        for (int u = 0; u < kPF; ++u) {
+          const int cb = cb0 + 64 * u;
+          if (cb >= s1) break;
+          const double2 pcur = pq[u];
+          pq[u] = point(cb + 64 * kPF);
+          const int off = offsets(pcur, cb, slow);
+          const bool live = cb + lane < s1;
+          // previous beam's corner (lane 0: none)
+          const int prev = __builtin_amdgcn_mov_dpp(off, 0x138, 0xF, 0xF, false);  // wave_shr:1
+          const bool edge = live && (lane == 0 || off != prev);  // a new corner starts here
+          const uint64_t E = __builtin_amdgcn_ballot_w64(edge);
+          const int nlive = min(64, s1 - cb);
+          const uint64_t above = lane == 63 ? 0ull : (E >> (lane + 1)) << (lane + 1);
+          const int next = above ? (int)__builtin_ctzll(above) : nlive;
+          const bool head = edge && off != zero_off;
+          const uint64_t Hm = __builtin_amdgcn_ballot_w64(head);
+          const int rank = __builtin_popcountll(Hm & ((1ull << lane) - 1));
+          if (head) {
+            run_off[nruns + rank] = off;
+            run_cnt[nruns + rank] = next - lane;
+          }
+          nruns += __builtin_popcountll(Hm);
         }
-        nruns += __builtin_popcountll(Hm);
       }
       // whole groups of D, then empty runs (zero block, count 0) far enough
       // past the list for the issue-ahead window below
@@ -194,6 +218,7 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
       // lane i of cA: count of run rb + i; of wI: corner of run rb + D + i
       // (loads are issued exactly D runs ahead of their use)
       int rb = 0;
+
       int cA = run_cnt[lane];
       int wI = run_off[D + lane];
 #pragma unroll
@@ -227,22 +252,30 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
     }
   }
 
-  if (__builtin_amdgcn_ballot_w64(slow) != 0) {
-    // rejected beams, cell by cell with the reference's expressions
-    for (int b = 0; b < n_used; ++b) {
-      const double2 p = P[(int64_t)b * step];
+  // Rejected beams, cell by cell with the reference's expressions: only the
+  // marked chunks are revisited, and only their rejected beams summed.
+  for (uint64_t m = slow; m != 0; m &= m - 1) {
+    const int c0 = (int)__builtin_ctzll(m);
+    const int c_end = c0 == 63 ? (n_used + 63) / 64 : c0 + 1;
+    for (int c = c0; c < c_end; ++c) {
+      const int cb = c * 64;
       double lx, ly;
       int ix0, iy0;
-      if (box_test(p, lx, ly, ix0, iy0)) continue;  // uniform: one beam for the whole wave
-      const int gy = (int)((ly + (S.y0 + k * f)) + 0.5);
-      const bool iny = (unsigned)gy < (unsigned)sy;
+      const bool clean = box_test(point(cb), lx, ly, ix0, iy0);
+      for (uint64_t rej = __builtin_amdgcn_ballot_w64(cb + lane < n_used && !clean); rej != 0; rej &= rej - 1) {
+        const int l = (int)__builtin_ctzll(rej);  // uniform: one beam for the whole wave
+        const double bx = dev::bcast_lane(lx, l);
+        const double by = dev::bcast_lane(ly, l);
+        const int gy = (int)((by + (S.y0 + k * f)) + 0.5);
+        const bool iny = (unsigned)gy < (unsigned)sy;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int j = 4 * q + t;
-        if (j < NS) {
-          const int gx = (int)((lx + (S.x0 + j * f)) + 0.5);
-          const bool in = iny && (unsigned)gx < (unsigned)sx;
-          acc[t] += gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)sy * L.pitch];
+        for (int t = 0; t < 4; ++t) {
+          const int j = 4 * q + t;
+          if (j < NS) {
+            const int gx = (int)((bx + (S.x0 + j * f)) + 0.5);
+            const bool in = iny && (unsigned)gx < (unsigned)sx;
+            acc[t] += gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)sy * L.pitch];
+          }
         }
       }
     }

@@ -120,7 +120,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
 
 def load_library(path: str | None = None) -> C.CDLL:
     """Load libroborts_csm.so; raises OSError when it has not been built."""
-    p = path or LIB_PATH
+    p = path or os.environ.get("CSM_LIB") or LIB_PATH  # CSM_LIB: A/B builds of the library
     if not os.path.exists(p):
         raise OSError(
             f"libroborts_csm.so not found at {p}; build it with "
