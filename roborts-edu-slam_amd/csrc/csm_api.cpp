@@ -478,23 +478,27 @@ struct csm_ctx {
     DevBuf scans, angles, scores, partials, best, fin;
     HostBuf h_scores, h_fin, h_angles, h_sw;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr;
-  } alt;
-  int pipeline_min = 512;  // fewest scans the 3-level driver splits into two halves (CSM_PIPELINE)
-  void swap_slot() {
-    std::swap(scans, alt.scans);
-    std::swap(angles, alt.angles);
-    std::swap(scores, alt.scores);
-    std::swap(partials, alt.partials);
-    std::swap(best, alt.best);
-    std::swap(fin, alt.fin);
-    std::swap(h_scores, alt.h_scores);
-    std::swap(h_fin, alt.h_fin);
-    std::swap(h_angles, alt.h_angles);
-    std::swap(h_sw, alt.h_sw);
-    std::swap(ev0, alt.ev0);
-    std::swap(ev1, alt.ev1);
-    std::swap(ev2, alt.ev2);
-    std::swap(ev_done, alt.ev_done);
+  };
+  static constexpr int kMaxParts = 4;
+  Slot alt[kMaxParts - 1];
+  int pipeline_min = 512;    // fewest scans the 3-level driver splits into parts (CSM_PIPELINE)
+  int pipeline_parts = 2;    // parts in flight (CSM_PIPELINE_PARTS: 2..kMaxParts; 2 measured fastest)
+  void swap_slot(int i) {    // i >= 1: exchange the current buffer set with alt[i - 1]
+    Slot& a = alt[i - 1];
+    std::swap(scans, a.scans);
+    std::swap(angles, a.angles);
+    std::swap(scores, a.scores);
+    std::swap(partials, a.partials);
+    std::swap(best, a.best);
+    std::swap(fin, a.fin);
+    std::swap(h_scores, a.h_scores);
+    std::swap(h_fin, a.h_fin);
+    std::swap(h_angles, a.h_angles);
+    std::swap(h_sw, a.h_sw);
+    std::swap(ev0, a.ev0);
+    std::swap(ev1, a.ev1);
+    std::swap(ev2, a.ev2);
+    std::swap(ev_done, a.ev_done);
   }
   std::vector<csm_kernel_stat> stats;
   void account(const char* name, float ms, double bytes, double scorings) {
@@ -1177,16 +1181,20 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
 // are independent, so the split changes no result.
 int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
                            int n_levels, double* poses, double* covs, double* sum) {
-  const int32_t h0 = n_scans / 2;
-  const int32_t first[2] = {0, h0}, count[2] = {h0, n_scans - h0};
+  const int K = std::max(2, std::min(c->pipeline_parts, csm_ctx::kMaxParts));
+  int32_t first[csm_ctx::kMaxParts], count[csm_ctx::kMaxParts];
+  for (int h = 0; h < K; ++h) {
+    first[h] = (int32_t)((int64_t)n_scans * h / K);
+    count[h] = (int32_t)((int64_t)n_scans * (h + 1) / K) - first[h];
+  }
   std::vector<double> resp((size_t)n_scans, 0.0);
-  LevelRun R[2];
+  LevelRun R[csm_ctx::kMaxParts];
   auto begin = [&](int l, int h) {
-    if (h == 1) c->swap_slot();
+    if (h > 0) c->swap_slot(h);
     const int32_t s0 = first[h];
     const int st = level_begin(c, count[h], offsets + s0, levels[l], poses + 3 * (size_t)s0,
                                resp.data() + s0, nullptr, R[h]);
-    if (h == 1) c->swap_slot();
+    if (h > 0) c->swap_slot(h);
     return st;
   };
   auto end = [&](int h) {
@@ -1196,9 +1204,10 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
     return st;
   };
   int st;
-  if ((st = begin(0, 0)) != CSM_OK || (st = begin(0, 1)) != CSM_OK) return st;
+  for (int h = 0; h < K; ++h)
+    if ((st = begin(0, h)) != CSM_OK) return st;
   for (int l = 0; l < n_levels; ++l) {
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < K; ++h) {
       if ((st = end(h)) != CSM_OK) return st;
       if (l + 1 < n_levels && (st = begin(l + 1, h)) != CSM_OK) return st;
     }
@@ -1394,8 +1403,11 @@ int csm_create(int device, csm_ctx** out) {
     const int v = std::atoi(env);
     c->pipeline_min = v > 0 ? v : INT32_MAX;
   }
-  if (hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->alt.ev_done, hipEventDisableTiming) != hipSuccess) {
+  if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
+    c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
+  bool ev_ok = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) == hipSuccess;
+  for (auto& a : c->alt) ev_ok = ev_ok && hipEventCreateWithFlags(&a.ev_done, hipEventDisableTiming) == hipSuccess;
+  if (!ev_ok) {
     (void)hipStreamDestroy(c->stream);
     delete c;
     return CSM_ERR_HIP;
@@ -1424,17 +1436,21 @@ int csm_destroy(csm_ctx* c) {
     c->h_fin.release();
     c->h_angles.release();
     c->h_sw.release();
-    c->alt.scans.release();
-    c->alt.angles.release();
-    c->alt.scores.release();
-    c->alt.partials.release();
-    c->alt.best.release();
-    c->alt.fin.release();
-    c->alt.h_scores.release();
-    c->alt.h_fin.release();
-    c->alt.h_angles.release();
-    c->alt.h_sw.release();
-    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->alt.ev0, c->alt.ev1, c->alt.ev2, c->alt.ev_done})
+    for (auto& a : c->alt) {
+      a.scans.release();
+      a.angles.release();
+      a.scores.release();
+      a.partials.release();
+      a.best.release();
+      a.fin.release();
+      a.h_scores.release();
+      a.h_fin.release();
+      a.h_angles.release();
+      a.h_sw.release();
+      for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done})
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done})
       if (ev) (void)hipEventDestroy(ev);
     (void)hipStreamDestroy(c->stream);
   }
@@ -1609,8 +1625,11 @@ int csm_set_profiling(csm_ctx* c, int32_t on) {
   DeviceGuard g(c->device);
   hipError_t e;
   if (on && !c->ev0) {
-    for (hipEvent_t* ev : {&c->ev0, &c->ev1, &c->ev2, &c->alt.ev0, &c->alt.ev1, &c->alt.ev2})
+    for (hipEvent_t* ev : {&c->ev0, &c->ev1, &c->ev2})
       if ((e = hipEventCreate(ev)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
+    for (auto& a : c->alt)
+      for (hipEvent_t* ev : {&a.ev0, &a.ev1, &a.ev2})
+        if ((e = hipEventCreate(ev)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
   }
   c->profiling = on != 0;
   c->stats.clear();

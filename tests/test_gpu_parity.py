@@ -608,19 +608,21 @@ def test_willow_best_window(ctx, willow):
         assert got.score == s and got.flat_index == flat
 
 
-@pytest.mark.parametrize("finish", ["device", "host"])
-def test_pipelined_three_level_driver(world2000, finish):
-    """Two halves of the batch in flight (CSM_PIPELINE threshold lowered so
-    96 scans split): results equal the oracle's bit for bit."""
+@pytest.mark.parametrize("finish,parts", [("device", 2), ("host", 2), ("device", 3), ("device", 4)])
+def test_pipelined_three_level_driver(world2000, finish, parts):
+    """The batch split into 2-4 parts in flight (CSM_PIPELINE threshold
+    lowered so 96 scans split): results equal the oracle's bit for bit."""
     import roborts_csm
     from roborts_csm.params import headline_levels
     w, b = world2000
     os.environ["CSM_PIPELINE"] = "16"
+    os.environ["CSM_PIPELINE_PARTS"] = str(parts)
     os.environ["CSM_FINISH"] = finish
     try:
         c = roborts_csm.Context(0)
     finally:
         del os.environ["CSM_PIPELINE"]
+        del os.environ["CSM_PIPELINE_PARTS"]
         del os.environ["CSM_FINISH"]
     try:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
@@ -634,6 +636,6 @@ def test_pipelined_three_level_driver(world2000, finish):
         s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells, b.offsets, headline_levels(), b.init_poses,
                                            np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1)))
         assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2)
-        assert st["host:wait"] == 6  # 3 levels x 2 halves
+        assert st["host:wait"] == 3 * parts  # 3 levels x parts
     finally:
         c.close()
