@@ -41,6 +41,18 @@ namespace {
 // with barriers in between (an earlier version pulled them from a spin-locked
 // LDS stack and, rarely, spun past its iteration bound).
 constexpr int kWaves = 4;
+// Partial sort (positions past what the ordered scans read stay unsorted) for
+// windows of at least this many candidates; kNearRounds: tighten the second
+// stage's limit to the 20th near-best score (20 block-wide rounds) instead of
+// every element >= bound.
+#ifndef CSM_PARTIAL_MIN
+#define CSM_PARTIAL_MIN 2048
+#endif
+#ifndef CSM_NEAR_ROUNDS
+#define CSM_NEAR_ROUNDS 0
+#endif
+constexpr int kPartialMinCand = CSM_PARTIAL_MIN;
+constexpr bool kNearRounds = CSM_NEAR_ROUNDS != 0;
 
 struct Seg {
   int32_t first, last, depth;
@@ -54,9 +66,35 @@ struct WaveScratch {      // per-wave LDS scratch of the register sort
 static_assert(sizeof(WaveScratch) <= kFinishWaveScratch, "finish_layout wave scratch");
 
 struct Shared {           // misc block of the LDS carve (finish_layout: 64 B + waves)
-  int lock, top, pending, pad;
+  int plim, top, pending, pad;
   double bx, by;
+  int ndef, cnt_a, cnt_b, nan;
+  double red[kWaves];
 };
+static_assert(sizeof(Shared) <= 128, "finish_layout misc block");
+
+// Block-wide reductions (all threads of the 4-wave block must call them).
+__device__ double block_max(double v, Shared* sh, int wave) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const double t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  __syncthreads();  // sh->red is free
+  if ((threadIdx.x & 63) == 0) sh->red[wave] = v;
+  __syncthreads();
+  double r = sh->red[0];
+  for (int i = 1; i < kWaves; ++i) r = sh->red[i] > r ? sh->red[i] : r;
+  return r;
+}
+__device__ int block_sum_i(int v, Shared* sh, int wave) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh->red[wave] = (double)v;
+  __syncthreads();
+  double r = 0.0;
+  for (int i = 0; i < kWaves; ++i) r += sh->red[i];
+  return (int)r;
+}
 
 __device__ __forceinline__ bool gt(double a, double b) { return a > b; }  // comp = greater
 
@@ -142,6 +180,10 @@ __device__ __forceinline__ double read_lane(double x, int l) {
   return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ int read_lane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ int wave_sum_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 
 // ---- large segments: one wave, LDS -------------------------------------------
 // Parallel std::__unguarded_partition(first+1, last, pivot=first). lpos/rpos
@@ -323,17 +365,48 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
   Seg* stack = reinterpret_cast<Seg*>(smem + Lo.stack);
 
   const double* sc = scores + (int64_t)w * A.n_cand;
+  // Load, and the limits of the partial sort: max, NaN, and the FindBest
+  // prefix size (every element with DoubleEqual(s, max, 1e-2): the prefix is
+  // exactly that set, in sorted order).
+  double lmax = -INFINITY;
+  bool lnan = false;
   for (int i = threadIdx.x; i < n; i += 64 * kWaves) {
-    keys[i] = sc[i];
+    const double x = sc[i];
+    keys[i] = x;
     vals[i] = (uint16_t)i;
+    lnan |= x != x;
+    lmax = x > lmax ? x : lmax;
+  }
+  lmax = block_max(lmax, sh, wave);
+  if (threadIdx.x == 0) {
+    sh->nan = 0;
+    sh->cnt_a = 0;
+    sh->cnt_b = 0;
+    sh->ndef = 0;
+  }
+  __syncthreads();
+  if (__ballot(lnan) != 0 && lane == 0) atomicOr(&sh->nan, 1);
+  {
+    int c = 0;
+    for (int i = threadIdx.x; i < n; i += 64 * kWaves) {
+      const double d = keys[i] - lmax;
+      c += (d < 0.0 ? d >= -1e-2 : d <= 1e-2) ? 1 : 0;
+    }
+    c = wave_sum_i(c);
+    if (lane == 0) atomicAdd(&sh->cnt_a, c);
   }
   // Level-synchronous introsort: every segment of a level is independent, so
   // the waves take them round-robin, children go to the next level's list
   // (LDS atomic add, no lock), a barrier separates levels. Depth decreases at
   // every partition, so there are at most 2*floor(log2 n) + 2 levels.
+  // Partial: a segment starting at or past sh->plim is set aside (positions
+  // past the limit are never read, and no element crosses a segment boundary
+  // afterwards), kept for the second stage in the deferred list.
   const int half = (n / 16 + 64) / 2;  // finish_layout: the stack region holds two lists
   Seg* cur = stack;
   Seg* nxt = stack + half;
+  Seg* deferred = reinterpret_cast<Seg*>(smem + Lo.defer);
+  __syncthreads();
   if (threadIdx.x == 0) {
     int lg = 0;
     while ((2 << lg) <= n) ++lg;  // floor(log2 n)
@@ -341,55 +414,66 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     sh->top = 1;      // segments in cur
     sh->pending = 0;  // segments appended to nxt
     sh->pad = 0;
+    // stage 1: FindBest's prefix and the positional list's 20
+    // (small windows sort whole: the limits' extra passes cost more there)
+    const bool full = sh->nan || A.order_out != nullptr || n < kPartialMinCand;
+    sh->plim = full ? n : min(n, max(sh->cnt_a, kCovPoints));
   }
   __syncthreads();
-  for (int level = 0;; ++level) {
-    const int ncur = sh->top;
-    if (ncur == 0) break;
-    if (level > 64) {  // cannot happen (depth bound); reported as count = -1
-      if (threadIdx.x == 0) sh->pad = 1;
-      break;
-    }
-    for (int i = wave; i < ncur; i += kWaves) {
-      const Seg s = cur[i];
-      const int first = uni(s.first), last = uni(s.last), depth = uni(s.depth);
-      const int len = last - first;
-      if (len <= 64) {
-        if (len > 1) sort_small(keys, vals, first, len, depth, ws);
-      } else if (depth == 0) {
-        if (lane == 0) heap_sort(keys, vals, first, last);
-      } else {
-        if (lane == 0) move_median_to_first(keys, vals, first, first + 1, first + len / 2, last - 1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        const int cut = partition_lds(keys, vals, lpos, rpos, first, last);
-        if (lane == 0) {
-          const int at = atomicAdd(&sh->pending, 2);
-          if (at + 2 <= half) {
-            nxt[at] = Seg{cut, last, depth - 1};
-            nxt[at + 1] = Seg{first, cut, depth - 1};
-          } else {
-            sh->pad = 1;  // list overflow: cannot happen for the layout's capacity
+  auto run_levels = [&]() {
+    const int plim = sh->plim;
+    for (int level = 0;; ++level) {
+      const int ncur = sh->top;
+      if (ncur == 0) break;
+      if (level > 64) {  // cannot happen (depth bound); reported as count = -1
+        if (threadIdx.x == 0) sh->pad = 1;
+        break;
+      }
+      for (int i = wave; i < ncur; i += kWaves) {
+        const Seg s = cur[i];
+        const int first = uni(s.first), last = uni(s.last), depth = uni(s.depth);
+        const int len = last - first;
+        if (first >= plim) {  // set aside for the second stage
+          if (lane == 0) {
+            const int at = atomicAdd(&sh->ndef, 1);
+            if (at < kFinishDefer) deferred[at] = s;
+            else sh->pad = 1;  // cannot happen: at most one straddling segment per level
+          }
+        } else if (len <= 64) {
+          if (len > 1) sort_small(keys, vals, first, len, depth, ws);
+        } else if (depth == 0) {
+          if (lane == 0) heap_sort(keys, vals, first, last);
+        } else {
+          if (lane == 0) move_median_to_first(keys, vals, first, first + 1, first + len / 2, last - 1);
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+          const int cut = partition_lds(keys, vals, lpos, rpos, first, last);
+          if (lane == 0) {
+            const int at = atomicAdd(&sh->pending, 2);
+            if (at + 2 <= half) {
+              nxt[at] = Seg{cut, last, depth - 1};
+              nxt[at + 1] = Seg{first, cut, depth - 1};
+            } else {
+              sh->pad = 1;  // list overflow: cannot happen for the layout's capacity
+            }
           }
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        sh->top = sh->pad ? 0 : sh->pending;
+        sh->pending = 0;
+      }
+      Seg* t = cur;
+      cur = nxt;
+      nxt = t;
+      __syncthreads();
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      sh->top = sh->pad ? 0 : sh->pending;
-      sh->pending = 0;
-    }
-    Seg* t = cur;
-    cur = nxt;
-    nxt = t;
-    __syncthreads();
-  }
+  };
+  run_levels();
   __syncthreads();
-  if (A.order_out)
-    for (int i = threadIdx.x; i < n; i += 64 * kWaves) A.order_out[(int64_t)w * n + i] = vals[i];
-  if (wave != 0) return;
 
-  // ---- ordered scans over the sorted candidates (wave 0) ---------------------
+  // ---- ordered scans over the sorted candidates -----------------------------
   const ScanWork S = scans[w];
   const int ns = A.n_space;
   const int nss = ns * ns;
@@ -398,7 +482,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
   auto cy = [&](int idx) { return S.y0 + (idx % ns) * f; };
   const double best = keys[0];
   FinishOut* o = out + w;
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     // FindBestCandidate (:670-710): sequential sums over the tied prefix.
     double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;
     int count = 0;
@@ -418,7 +502,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     }
     const int fi = vals[0];
     o->front_idx = fi;
-    o->count = sh->pad ? -1 : count;
+    o->count = count;
     o->best_score = best;
     o->thx = thx;
     o->thy = thy;
@@ -433,10 +517,79 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     o->best_x = sh->bx;
     o->best_y = sh->by;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __syncthreads();
   const double bx = sh->bx, by = sh->by;
   const double lo = best - 0.1;
   const double bound = (0.5 < lo) ? 0.5 : lo;  // std::min(best - 0.1, 0.5) (:912,:986)
+  const double tol = A.lin_tol;
+  auto near_best = [&](int idx) {
+    const double dx = cx(idx) - bx, dy = cy(idx) - by;
+    const bool ex = dx < 0.0 ? dx >= -fabs(tol) : dx <= fabs(tol);
+    const bool ey = dy < 0.0 ? dy >= -fabs(tol) : dy <= fabs(tol);
+    return ex && ey;
+  };
+  // Stage 2: the angular list reads the sorted order of every element with
+  // score >= bound while it still needs near-best ones: all of them when at
+  // most 20 are near the best, else up to the 20th near one in sorted order,
+  // i.e. every element scoring at least the 20th largest near-best score.
+  {
+    int cm = 0, cr = 0;
+    for (int i = threadIdx.x; i < n; i += 64 * kWaves) {
+      const double x = keys[i];
+      const bool above = x >= bound;
+      cr += above ? 1 : 0;
+      cm += (above && near_best(vals[i])) ? 1 : 0;
+    }
+    cm = wave_sum_i(cm);
+    cr = wave_sum_i(cr);
+    if (lane == 0) atomicAdd(&sh->cnt_b, cr);
+    if (threadIdx.x == 0) sh->top = 0;
+    __syncthreads();
+    if (lane == 0) atomicAdd(&sh->top, cm);  // reuse: |M|
+    __syncthreads();
+    int p2 = sh->cnt_b;  // every element >= bound
+    if (kNearRounds && sh->top > kCovPoints && sh->plim < n) {
+      // 20th largest near-best score: rounds of "largest below the previous"
+      double v = INFINITY;
+      int got = 0;
+      while (got < kCovPoints) {
+        double m = -INFINITY;
+        for (int i = threadIdx.x; i < n; i += 64 * kWaves) {
+          const double x = keys[i];
+          if (x >= bound && x < v && x > m && near_best(vals[i])) m = x;
+        }
+        m = block_max(m, sh, wave);
+        int c = 0;
+        for (int i = threadIdx.x; i < n; i += 64 * kWaves) c += (keys[i] == m && near_best(vals[i])) ? 1 : 0;
+        c = block_sum_i(c, sh, wave);
+        got += c;
+        v = m;
+      }
+      int c = 0;
+      for (int i = threadIdx.x; i < n; i += 64 * kWaves) c += keys[i] >= v ? 1 : 0;
+      p2 = block_sum_i(c, sh, wave);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int old = sh->plim;
+      sh->plim = max(old, min(n, p2));
+      int nd = 0;
+      const int ndef = min(sh->ndef, kFinishDefer);
+      for (int i = 0; i < ndef; ++i)
+        if (deferred[i].first < sh->plim) cur[nd++] = deferred[i];
+      sh->ndef = 0;
+      sh->top = sh->pad ? 0 : nd;
+      sh->pending = 0;
+    }
+    __syncthreads();
+    run_levels();
+    __syncthreads();
+  }
+  if (A.order_out)
+    for (int i = threadIdx.x; i < n; i += 64 * kWaves) A.order_out[(int64_t)w * n + i] = vals[i];
+  if (threadIdx.x == 0 && sh->pad) o->count = -1;
+  if (wave != 0) return;
+
   // positional list (:915-928): the sorted prefix with score > bound, <= 20
   {
     int npos = 0;
@@ -456,7 +609,6 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
   }
   // angular list (:990-1003): score >= bound and (x, y) within lin_tol of the best
   {
-    const double tol = A.lin_tol;
     int nang = 0;
     for (int base = 0; base < n && nang < kCovPoints; base += 64) {
       const int p = base + lane;
@@ -465,13 +617,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
       if (p < n) {
         const double s = keys[p];
         above = s >= bound;
-        if (above) {
-          const int idx = vals[p];
-          const double dx = cx(idx) - bx, dy = cy(idx) - by;
-          const bool ex = dx < 0.0 ? dx >= -fabs(tol) : dx <= fabs(tol);
-          const bool ey = dy < 0.0 ? dy >= -fabs(tol) : dy <= fabs(tol);
-          ok = ex && ey;
-        }
+        if (above) ok = near_best(vals[p]);
       }
       const uint64_t m = __ballot(ok);
       const int r = nang + popc(m & below_mask(lane));

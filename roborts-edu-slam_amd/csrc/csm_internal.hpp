@@ -101,17 +101,20 @@ struct FinishOut {
 constexpr int kFinishWaveScratch = 640;  // bytes of per-wave scratch (4 waves)
 
 struct FinishLayout {
-  size_t wave_scratch, keys, vals, lpos, rpos, stack, total;
+  size_t wave_scratch, defer, keys, vals, lpos, rpos, stack, total;
 };
+constexpr int kFinishDefer = 64;  // segments the partial sort may set aside (12 B each)
 
 // LDS carve of the finish kernel for n candidates (16-byte aligned pieces):
-// misc | 4 wave scratches | keys f64[n] | vals u16[n] | lpos u16[n] | rpos u16[n]
-// | shared segment stack.
+// misc | 4 wave scratches | deferred segments | keys f64[n] | vals u16[n] |
+// lpos u16[n] | rpos u16[n] | shared segment stack.
 constexpr FinishLayout finish_layout(int64_t n) {
   FinishLayout L{};
-  size_t o = 64;  // misc: lock, stack top, pending count, best (x, y)
+  size_t o = 128;  // misc (csm_finish.hip Shared): list counts, limits, best (x, y), reductions
   L.wave_scratch = o;
   o += 4 * (size_t)kFinishWaveScratch;
+  L.defer = o;
+  o += (size_t)kFinishDefer * 12;
   L.keys = o;
   o += (size_t)n * 8;
   L.vals = o;
