@@ -635,21 +635,25 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
 // ---- fast finish: no sort when no tie can matter ----------------------------
 // Everything the sorted candidates feed is decided by the elements with
 // score >= bound = min(best - 0.1, 0.5) (:912,:986; FindBestCandidate's
-// prefix, s >= best - 0.01, lies inside): the FindBest prefix (all of it, in
+// prefix, s >= best - 0.01, lies above it): the FindBest prefix (all of it, in
 // sorted order: its sums are order-dependent), the first 20 with score > bound
 // (:915-928) and the first 20 near the best with score >= bound (:990-1003).
-// std::sort leaves distinct scores in strictly decreasing order, so if the
-// prefix has no equal scores and neither list's 20 (nor the value at its
-// boundary) repeats, these are fixed by value alone: the prefix is ranked,
-// each list is extracted by 20 rounds of wave argmax below the previous
-// value, each round checking that its value occurs once. Any repeat (or a
-// NaN, or an oversized prefix/region) flags the window for finish_kernel's
-// exact std::sort emulation, which runs next and skips every other window.
-// One wave per window.
-constexpr int kFastRCap = 2048;  // region size kept (registers: kFastPer per thread)
-constexpr int kFastFBCap = 64;   // FindBest prefix
+// std::sort leaves distinct scores in strictly decreasing order, so if none of
+// the scores these read repeats (nor the value just past a list's 20th), they
+// are fixed by value alone:
+//   1. max, NaN check; counts above eight thresholds best - delta;
+//   2. the smallest threshold holding 20 elements > bound (or all of them):
+//      compacted (<= kFastCap), ranked by value in LDS (rank = elements
+//      greater), which gives the prefix and the positional list;
+//   3. FindBest's sums -> (bx, by); the near-best elements >= bound compacted
+//      (<= kFastNearCap) and ranked the same way for the angular list.
+// A repeat where order decides, a NaN or an oversized set flags the window
+// for finish_kernel's exact std::sort emulation, which runs next and skips
+// every other window. One 256-thread block per window, ~8 barriers.
 constexpr int kFastThreads = 256;
-constexpr int kFastPer = kFastRCap / kFastThreads;
+constexpr int kFastCap = 512;      // compacted candidates of step 2
+constexpr int kFastNearCap = 512;  // compacted near-best candidates of step 3
+constexpr int kFastLevels = 8;     // thresholds best - {0.01, 0.02, ..., 0.64}, then everything > bound
 
 __device__ __forceinline__ double wave_max_d(double v) {
   for (int o = 32; o > 0; o >>= 1) {
@@ -663,38 +667,35 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
                                                                    const AngleEntry* __restrict__ angles,
                                                                    const double* __restrict__ scores,
                                                                    FinishOut* __restrict__ out) {
-  __shared__ double rk[kFastRCap];
-  __shared__ uint16_t ri[kFastRCap];
-  __shared__ double fk[kFastFBCap], gk[kFastFBCap];
-  __shared__ int fi[kFastFBCap], gi[kFastFBCap];
+  __shared__ double ck[kFastCap];   // step 2 candidates (value, index), then ...
+  __shared__ int ci[kFastCap];
+  __shared__ double sk[kFastCap];   // ... sorted by value (rank order)
+  __shared__ int si[kFastCap];
+  __shared__ double nk[kFastNearCap];
+  __shared__ int ni[kFastNearCap];
   __shared__ double red[4];
-  __shared__ int redc[4];
-  __shared__ int nR_s, nF_s, flag_s, gid_s;
+  __shared__ int cnt_s[kFastLevels];
+  __shared__ int nC_s, nN_s, flag_s;
   __shared__ double sbx, sby;
   const int w = blockIdx.x;
   const int n = (int)A.n_cand;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double* sc = scores + (int64_t)w * A.n_cand;
   int32_t* need = A.need_exact + w;
+  if (tid < kFastLevels) cnt_s[tid] = 0;
   if (tid == 0) {
-    nR_s = 0;
-    nF_s = 0;
+    nC_s = 0;
+    nN_s = 0;
     flag_s = 0;
-    gid_s = INT32_MAX;
   }
 
-  // best = the front of the sorted candidates (:607); NaN anywhere: exact path
+  // 1. best = the front of the sorted candidates (:607); NaN anywhere: exact path
   double m = -INFINITY;
   bool nan = false;
-  for (int i0 = tid; i0 < n; i0 += 4 * kFastThreads) {
-    double v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = (i0 + u * kFastThreads < n) ? sc[i0 + u * kFastThreads] : -INFINITY;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      nan |= (v[u] != v[u]);
-      m = (v[u] > m) ? v[u] : m;
-    }
+  for (int i = tid; i < n; i += kFastThreads) {
+    const double v = sc[i];
+    nan |= (v != v);
+    m = (v > m) ? v : m;
   }
   m = wave_max_d(m);
   if (lane == 0) red[wave] = m;
@@ -707,57 +708,76 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   }
   const double lo = best - 0.1;
   const double bound = (0.5 < lo) ? 0.5 : lo;  // std::min(best - 0.1, 0.5) (:912,:986)
-
-  // the region s >= bound and FindBest's prefix, compacted (order irrelevant)
-  for (int i0 = wave * 64 + lane; i0 - lane < n; i0 += 4 * 64) {
-    const bool in = i0 < n;
-    const double s = in ? sc[i0] : -INFINITY;
-    const bool inR = in && s >= bound;
+  // level k < 7: s > bound and s - best >= -0.01 * 2^k; level 7: s > bound
+  auto level_of = [&](double s) {  // smallest level holding s (kFastLevels: none)
+    if (!(s > bound)) return kFastLevels;
     const double d = s - best;
-    const bool eq = in && (d < 0.0 ? d >= -1e-2 : d <= 1e-2);  // DoubleEqual(s, best, 1e-2)
-    const uint64_t mR = __ballot(inR), mF = __ballot(eq);
-    int baseR = 0, baseF = 0;
-    if (lane == 0) {
-      baseR = mR ? atomicAdd(&nR_s, popc(mR)) : 0;
-      baseF = mF ? atomicAdd(&nF_s, popc(mF)) : 0;
+    double dl = 0.01;
+    for (int k = 0; k < kFastLevels - 1; ++k, dl *= 2.0)
+      if (d >= -dl) return k;
+    return kFastLevels - 1;
+  };
+  {
+    int c[kFastLevels];
+#pragma unroll
+    for (int k = 0; k < kFastLevels; ++k) c[k] = 0;
+    for (int i = tid; i < n; i += kFastThreads) {
+      const int lv = level_of(sc[i]);
+#pragma unroll
+      for (int k = 0; k < kFastLevels; ++k) c[k] += (lv == k) ? 1 : 0;
     }
-    baseR = uni(baseR);
-    baseF = uni(baseF);
-    const int pr = baseR + popc(mR & below_mask(lane)), pf = baseF + popc(mF & below_mask(lane));
-    if (inR && pr < kFastRCap) {
-      rk[pr] = s;
-      ri[pr] = (uint16_t)i0;
-    }
-    if (eq && pf < kFastFBCap) {
-      fk[pf] = s;
-      fi[pf] = i0;
+#pragma unroll
+    for (int k = 0; k < kFastLevels; ++k) {
+      const int t = wave_sum_i(c[k]);
+      if (lane == 0 && t) atomicAdd(&cnt_s[k], t);
     }
   }
   __syncthreads();
-  const int nR = nR_s, nF = nF_s;
-  if (nR > kFastRCap || nF > kFastFBCap) {
+  // 2. the smallest level whose cumulative count reaches 20 (or all > bound)
+  int L = kFastLevels - 1, cum = 0;
+  for (int k = 0; k < kFastLevels; ++k) {
+    cum += cnt_s[k];
+    if (cum >= kCovPoints) {
+      L = k;
+      break;
+    }
+  }
+  int nC = 0;
+  for (int k = 0; k <= L; ++k) nC += cnt_s[k];
+  if (nC > kFastCap) {
     if (tid == 0) *need = 1;
     return;
   }
-
-  // FindBestCandidate's prefix, ranked by value (distinct or exact path)
-  if (wave == 0) {
-    const double mk = lane < nF ? fk[lane] : 0.0;
-    int rank = 0;
-    bool tie = false;
-    for (int j = 0; j < nF; ++j) {
-      const double kj = fk[j];
-      if (lane < nF && j != lane) {
-        rank += (kj > mk) ? 1 : 0;
-        tie |= (kj == mk);
-      }
+  for (int i0 = tid - lane; i0 < n; i0 += kFastThreads) {
+    const int i = i0 + lane;
+    const double s = i < n ? sc[i] : -INFINITY;
+    const bool in = i < n && level_of(s) <= L;
+    const uint64_t mm = __ballot(in);
+    int base = 0;
+    if (lane == 0 && mm) base = atomicAdd(&nC_s, popc(mm));
+    base = uni(base);
+    if (in) {
+      const int p = base + popc(mm & below_mask(lane));
+      ck[p] = s;
+      ci[p] = i;
     }
-    if (__ballot(tie) != 0) {
-      if (lane == 0) flag_s = 1;
-    } else if (lane < nF) {
-      gk[rank] = mk;
-      gi[rank] = fi[lane];
+  }
+  __syncthreads();
+  // rank = elements greater; any equal value where the order decides: exact
+  // path (the prefix, the positional 20 and the value just past them)
+  for (int t = tid; t < nC; t += kFastThreads) {
+    const double v = ck[t];
+    int r = 0, eq = 0;
+    for (int j = 0; j < nC; ++j) {
+      const double u = ck[j];
+      r += (u > v) ? 1 : 0;
+      eq += (u == v) ? 1 : 0;
     }
+    const double d = v - best;
+    const bool inF = d < 0.0 ? d >= -1e-2 : d <= 1e-2;  // DoubleEqual(s, best, 1e-2)
+    if (eq > 1 && (inF || r <= kCovPoints)) flag_s = 1;
+    sk[r] = v;  // distinct ranks whenever nothing is flagged
+    si[r] = ci[t];
   }
   __syncthreads();
   if (flag_s) {
@@ -773,24 +793,28 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   FinishOut* o = out + w;
   if (tid == 0) {  // :676-707, the same sequential sums as finish_kernel
     double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;
-    for (int r = 0; r < nF; ++r) {
-      const double s = gk[r];
-      const int idx = gi[r];
+    int count = 0;
+    for (int r = 0; r < nC; ++r) {
+      const double s = sk[r];
+      const double d = s - best;
+      if (!(d < 0.0 ? d >= -1e-2 : d <= 1e-2)) break;
+      const int idx = si[r];
       const AngleEntry ae = angles[S.angle_off + idx / nss];
       ax += cx(idx) * s;
       ay += cy(idx) * s;
       thx += ae.cosine * s;
       thy += ae.sine * s;
       ssum += s;
+      count++;
     }
-    const int fi0 = gi[0];
+    const int fi0 = si[0];
     o->front_idx = fi0;
-    o->count = nF;
+    o->count = count;
     o->best_score = best;
     o->thx = thx;
     o->thy = thy;
     o->ssum = ssum;
-    if (nF > 1) {
+    if (count > 1) {
       sbx = ax / ssum;
       sby = ay / ssum;
     } else {
@@ -799,88 +823,67 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     }
     o->best_x = sbx;
     o->best_y = sby;
+    // positional list (:915-928): the sorted prefix with score > bound, <= 20
+    const int np = min(nC, kCovPoints);
+    for (int r = 0; r < np; ++r) {
+      o->pos_idx[r] = si[r];
+      o->pos_score[r] = sk[r];
+    }
+    o->n_pos = np;
   }
   __syncthreads();
-  // this thread's share of the region, in registers, with the near flag of
-  // the angular list (:994-995)
+  // 3. angular list (:990-1003): near the best, score >= bound
   const double bx = sbx, by = sby, tol = A.lin_tol;
-  double my_s[kFastPer];
-  int my_i[kFastPer];  // candidate index; bit 15: near the best
-#pragma unroll
-  for (int t = 0; t < kFastPer; ++t) {
-    const int j = tid + t * kFastThreads;
-    my_s[t] = -INFINITY;
-    my_i[t] = 0;
-    if (j < nR) {
-      const int idx = ri[j];
-      const double dx = cx(idx) - bx, dy = cy(idx) - by;
-      const bool ex = dx < 0.0 ? dx >= -fabs(tol) : dx <= fabs(tol);
-      const bool ey = dy < 0.0 ? dy >= -fabs(tol) : dy <= fabs(tol);
-      my_s[t] = rk[j];
-      my_i[t] = idx | ((ex && ey) ? 0x8000 : 0);
+  for (int i0 = tid - lane; i0 < n; i0 += kFastThreads) {
+    const int i = i0 + lane;
+    bool in = false;
+    double s = 0.0;
+    if (i < n) {
+      s = sc[i];
+      if (s >= bound) {
+        const double dx = cx(i) - bx, dy = cy(i) - by;
+        const bool ex = dx < 0.0 ? dx >= -fabs(tol) : dx <= fabs(tol);
+        const bool ey = dy < 0.0 ? dy >= -fabs(tol) : dy <= fabs(tol);
+        in = ex && ey;
+      }
+    }
+    const uint64_t mm = __ballot(in);
+    int base = 0;
+    if (lane == 0 && mm) base = atomicAdd(&nN_s, popc(mm));
+    base = uni(base);
+    if (in) {
+      const int p = base + popc(mm & below_mask(lane));
+      if (p < kFastNearCap) {
+        nk[p] = s;
+        ni[p] = i;
+      }
     }
   }
-  // the two lists: 0 = positional (score > bound), 1 = angular (score >=
-  // bound, near); round r takes the largest value below round r-1's and
-  // checks that it occurs once among the list's candidates
-  for (int list = 0; list < 2; ++list) {
-    double prev = INFINITY;
-    int cnt = 0;
-    for (int r = 0; r < kCovPoints; ++r) {
-      double lm = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < kFastPer; ++t) {
-        const bool ok = my_s[t] < prev && (list == 0 ? my_s[t] > bound : (my_i[t] & 0x8000) != 0);
-        if (ok && my_s[t] > lm) lm = my_s[t];
-      }
-      lm = wave_max_d(lm);
-      if (lane == 0) red[wave] = lm;
-      __syncthreads();
-      const double g = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-      __syncthreads();
-      if (g == -INFINITY) break;
-      int c = 0, id = INT32_MAX;
-#pragma unroll
-      for (int t = 0; t < kFastPer; ++t) {
-        const bool ok = my_s[t] == g && (list == 0 || (my_i[t] & 0x8000) != 0);
-        if (ok) {
-          c++;
-          id = my_i[t] & 0x7FFF;
-        }
-      }
-      const uint64_t b1 = __ballot(c >= 1), b2 = __ballot(c >= 2);
-      if (lane == 0) redc[wave] = popc(b1) + (b2 ? 2 : 0);
-      if (c >= 1) atomicMin(&gid_s, id);
-      __syncthreads();
-      const int total = redc[0] + redc[1] + redc[2] + redc[3];
-      const int gid = gid_s;
-      __syncthreads();
-      if (tid == 0) gid_s = INT32_MAX;
-      if (total > 1) {  // equal scores where the order decides the list
-        if (tid == 0) *need = 1;
-        return;
-      }
-#ifdef CSM_DEBUG_FAST
-      if (tid == 0 && w == 0) printf("list %d r %d g %.17g gid %d total %d nR %d nF %d best %.17g bound %.17g\n", list, r, g, gid, total, nR, nF, best, bound);
-#endif
-      if (tid == 0) {
-        if (list == 0) {
-          o->pos_idx[r] = gid;
-          o->pos_score[r] = g;
-        } else {
-          o->ang_idx[r] = gid;
-          o->ang_score[r] = g;
-        }
-      }
-      prev = g;
-      cnt++;
+  __syncthreads();
+  const int nN = nN_s;
+  if (nN > kFastNearCap) {
+    if (tid == 0) *need = 1;
+    return;
+  }
+  for (int t = tid; t < nN; t += kFastThreads) {
+    const double v = nk[t];
+    int r = 0, eq = 0;
+    for (int j = 0; j < nN; ++j) {
+      const double u = nk[j];
+      r += (u > v) ? 1 : 0;
+      eq += (u == v) ? 1 : 0;
     }
-    if (tid == 0) {
-      if (list == 0) o->n_pos = cnt;
-      else o->n_ang = cnt;
+    if (eq > 1 && r <= kCovPoints) flag_s = 1;
+    if (r < kCovPoints) {
+      o->ang_idx[r] = ni[t];
+      o->ang_score[r] = v;
     }
   }
-  if (tid == 0) *need = 0;
+  __syncthreads();
+  if (tid == 0) {
+    o->n_ang = min(nN, kCovPoints);
+    *need = flag_s ? 1 : 0;
+  }
 }
 
 hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const AngleEntry* d_angles,
