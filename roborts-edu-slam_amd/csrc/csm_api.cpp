@@ -416,7 +416,11 @@ int pick_cpl(int64_t n_cand) {
 
 struct csm_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // kernels
+  // Per-launch copies run on their own streams (DMA engines), ordered against
+  // the kernels by events: a part's inputs go up while the other part's
+  // kernels run, its results come down while the next kernels run.
+  hipStream_t h2d = nullptr, d2h = nullptr;
   std::mutex mu;
   std::string err;
   float outside = 0.3f;  // kMapUnknownCellProb (slam/slam_processor.h:264)
@@ -470,6 +474,8 @@ struct csm_ctx {
   bool profiling = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   hipEvent_t ev_done = nullptr;  // end of a launch's work (async runs)
+  hipEvent_t ev_in = nullptr;    // a launch's inputs are on the device
+  hipEvent_t ev_k = nullptr;     // a launch's kernels are done
 
   // Second set of per-launch buffers: the 3-level driver keeps two halves of
   // a batch in flight (match_levels_pipelined); swap_slot() exchanges the
@@ -477,7 +483,7 @@ struct csm_ctx {
   struct Slot {
     DevBuf scans, angles, scores, partials, best, fin;
     HostBuf h_scores, h_fin, h_angles, h_sw;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr, ev_in = nullptr, ev_k = nullptr;
   };
   static constexpr int kMaxParts = 4;
   Slot alt[kMaxParts - 1];
@@ -499,6 +505,8 @@ struct csm_ctx {
     std::swap(ev1, a.ev1);
     std::swap(ev2, a.ev2);
     std::swap(ev_done, a.ev_done);
+    std::swap(ev_in, a.ev_in);
+    std::swap(ev_k, a.ev_k);
   }
   std::vector<csm_kernel_stat> stats;
   void account(const char* name, float ms, double bytes, double scorings) {
@@ -745,10 +753,12 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
 
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
   if ((e = c->angles.ensure(n_angle_entries * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
-  if ((e = hipMemcpyAsync(c->scans.p, sw, (size_t)nw * sizeof(ScanWork), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(c->scans.p, sw, (size_t)nw * sizeof(ScanWork), hipMemcpyHostToDevice, c->h2d)) != hipSuccess)
     return c->hip_fail(e, "hipMemcpyAsync(scans)");
-  if ((e = hipMemcpyAsync(c->angles.p, angles, n_angle_entries * sizeof(AngleEntry), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(c->angles.p, angles, n_angle_entries * sizeof(AngleEntry), hipMemcpyHostToDevice, c->h2d)) != hipSuccess)
     return c->hip_fail(e, "hipMemcpyAsync(angles)");
+  if ((e = hipEventRecord(c->ev_in, c->h2d)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->ev_in, 0)) != hipSuccess)
+    return c->hip_fail(e, "inputs event");
 
   // algorithmic traffic: one fp32 grid read per summed beam per candidate
   double beams = 0.0;
@@ -798,7 +808,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
     if (mode == Finish::kScoresToHost) {
       if ((e = c->h_scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scores)");
-      if ((e = hipMemcpyAsync(c->h_scores.p, c->scores.p, bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+      if ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
+        return c->hip_fail(e, "kernels event");
+      if ((e = hipMemcpyAsync(c->h_scores.p, c->scores.p, bytes, hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
         return c->hip_fail(e, "hipMemcpyAsync(scores)");
     } else {
       csm::FinishArgs A{};
@@ -819,7 +831,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       if (c->profiling && (e = hipEventRecord(c->ev2, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
       // with profiling on, the flags come back too: how many windows needed the exact sort
       const size_t cbytes = fbytes + ((c->profiling && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
-      if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, cbytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+      if ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
+        return c->hip_fail(e, "kernels event");
+      if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, cbytes, hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
         return c->hip_fail(e, "hipMemcpyAsync(finish)");
       if (cbytes > fbytes) {
         flags_h = (const int32_t*)((const char*)c->h_fin.p + fbytes);
@@ -855,7 +869,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if ((e = csm::launch_reduce_best((const BestPartial*)c->partials.p, (int32_t)bps, nw,
                                      (BestPartial*)c->best.p, c->stream)) != hipSuccess)
       return c->hip_fail(e, "reduce_best_kernel");
-    if ((e = hipMemcpyAsync(best_out, c->best.p, (size_t)nw * sizeof(BestPartial), hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+    if ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
+      return c->hip_fail(e, "kernels event");
+    if ((e = hipMemcpyAsync(best_out, c->best.p, (size_t)nw * sizeof(BestPartial), hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
       return c->hip_fail(e, "hipMemcpyAsync(best)");
   }
   PendingRun local;
@@ -873,7 +889,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   p.ev1 = c->ev1;
   p.ev2 = c->ev2;
   p.done = c->ev_done;
-  if ((e = hipEventRecord(c->ev_done, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+  if ((e = hipEventRecord(c->ev_done, c->d2h)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
   if (pend) return CSM_OK;
   return wait_run(c, p);
 }
@@ -1378,6 +1394,13 @@ int csm_create(int device, csm_ctx** out) {
     delete c;
     return CSM_ERR_HIP;
   }
+  if (hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    if (c->h2d) (void)hipStreamDestroy(c->h2d);
+    delete c;
+    return CSM_ERR_HIP;
+  }
   unsigned hw = std::thread::hardware_concurrency();
   int threads = (int)std::min<unsigned>(hw ? hw : 1, 16);
   if (const char* env = std::getenv("CSM_HOST_THREADS")) {
@@ -1405,8 +1428,12 @@ int csm_create(int device, csm_ctx** out) {
   }
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
-  bool ev_ok = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) == hipSuccess;
-  for (auto& a : c->alt) ev_ok = ev_ok && hipEventCreateWithFlags(&a.ev_done, hipEventDisableTiming) == hipSuccess;
+  bool ev_ok = true;
+  for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k})
+    ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
+  for (auto& a : c->alt)
+    for (hipEvent_t* ev : {&a.ev_done, &a.ev_in, &a.ev_k})
+      ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
   if (!ev_ok) {
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1422,6 +1449,8 @@ int csm_destroy(csm_ctx* c) {
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->h2d);
+    (void)hipStreamSynchronize(c->d2h);
     c->grid_buf.release();
     c->gridi.release();
     c->gstats.release();
@@ -1447,11 +1476,13 @@ int csm_destroy(csm_ctx* c) {
       a.h_fin.release();
       a.h_angles.release();
       a.h_sw.release();
-      for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done})
+      for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k})
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done})
+    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k})
       if (ev) (void)hipEventDestroy(ev);
+    (void)hipStreamDestroy(c->h2d);
+    (void)hipStreamDestroy(c->d2h);
     (void)hipStreamDestroy(c->stream);
   }
   delete c;

@@ -533,8 +533,11 @@ __device__ __forceinline__ void buffer_load_lds16(__amdgpu_buffer_rsrc_t rsrc,
 // while beam b is summed, counted vmcnt). DMA has no range check: rows outside
 // the grid point at the zero row the host appends to gridi, columns outside
 // the grid read a zero block.
-template <int NS, int SQ, bool BEST>
-__global__ __launch_bounds__(64) void score_rowsd_kernel(
+// BS waves per block split a window's beams into BS contiguous ranges (low
+// wave counts per launch otherwise: the super-fine level is one wave per
+// window); their integer sums meet in LDS, exact in any order.
+template <int NS, int SQ, bool BEST, int BS>
+__global__ __launch_bounds__(64 * BS) void score_rowsd_kernel(
     LevelWork L, const ScanWork* __restrict__ scans, const double2* __restrict__ pts,
     const AngleEntry* __restrict__ angles, double* __restrict__ out,
     BestPartial* __restrict__ partials) {
@@ -547,15 +550,20 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
   typedef __attribute__((address_space(3))) int32_t lds_i32;
   // two images as distinct objects, so the compiler's LDS-DMA wait tracking
   // can tell a read of one from the DMA still writing the other
-  __shared__ __attribute__((aligned(16))) int32_t img0[IMG];
-  __shared__ __attribute__((aligned(16))) int32_t img1[IMG];
-  __shared__ __attribute__((aligned(16))) int32_t img2[IMG];
+  __shared__ __attribute__((aligned(16))) int32_t img0_s[BS * IMG];
+  __shared__ __attribute__((aligned(16))) int32_t img1_s[BS * IMG];
+  __shared__ __attribute__((aligned(16))) int32_t img2_s[BS * IMG];
   __shared__ __attribute__((aligned(16))) int32_t zblk[NS * SEG];
+  __shared__ int64_t xsum[(BS - 1) * 64 * NS + 1];  // waves 1.. -> wave 0
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int win = bid / L.blocks_per_scan;
   const int blk = bid - win * L.blocks_per_scan;
   const ScanWork S = scans[win];
-  const int lane = threadIdx.x;
+  const int lane = BS > 1 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  const int wv = BS > 1 ? (int)(threadIdx.x >> 6) : 0;  // BS == 1: images at fixed LDS addresses
+  int32_t* const img0 = img0_s + wv * IMG;
+  int32_t* const img1 = img1_s + wv * IMG;
+  int32_t* const img2 = img2_s + wv * IMG;
   const int g = lane / NS;
   // idle lanes (g >= G) shadow lane (G-1, NS-1): identical LDS addresses
   // broadcast instead of adding bank conflicts
@@ -575,6 +583,8 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
   const double2* __restrict__ P = pts + S.pts_off;
   const int step = S.step;
   const int n_used = S.n_used;
+  const int b_lo = (int)((int64_t)n_used * wv / BS);  // this wave's beams
+  const int b_hi = (int)((int64_t)n_used * (wv + 1) / BS);
   const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
   const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
   const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
@@ -598,8 +608,8 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
   // Beam points, 64 at a time in registers (lane l holds beam pbase + l) and
   // broadcast by readlane: no scalar load (and its lgkmcnt(0) drain of the
   // LDS queue) per beam.
-  double2 pw = P[(int64_t)min(lane, n_used - 1) * step];
-  int pbase = 0;
+  double2 pw = P[(int64_t)max(0, min(b_lo + lane, b_hi - 1)) * step];
+  int pbase = b_lo;
   auto bcast = [](double v, int l) {
     const uint64_t u = __builtin_bit_cast(uint64_t, v);
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
@@ -677,31 +687,33 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
   constexpr short kWait2 = (short)(0xF70 | (2 * NI));  // needs 2*NI < 16
   static_assert(2 * NI < 16, "vmcnt field");
   lds_i32 *r0 = nullptr, *r1 = nullptr, *r2 = nullptr;
-  prep(0, 0, r0, bad);
-  prep(min(1, n_used - 1), 1, r1, bad);
-  for (int base = 0; base < n_used; base += kFold) {
-    const int nb = min(kFold, n_used - base);
+  if (b_hi > b_lo) {
+    prep(b_lo, 0, r0, bad);
+    prep(min(b_lo + 1, b_hi - 1), 1, r1, bad);
+  }
+  for (int base = b_lo; base < b_hi; base += kFold) {
+    const int nb = min(kFold, b_hi - base);
     if (base != pbase) {  // this chunk preps beams base+2 .. base+kFold+1
       pbase = base;
-      pw = P[(int64_t)min(base + lane, n_used - 1) * step];
+      pw = P[(int64_t)min(base + lane, b_hi - 1) * step];
     }
     int32_t part[NS];
 #pragma unroll
     for (int k = 0; k < NS; ++k) part[k] = 0;
     for (int b = 0; b < nb; b += 3) {
-      prep(min(base + b + 2, n_used - 1), 2, r2, bad);
+      prep(min(base + b + 2, b_hi - 1), 2, r2, bad);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_waitcnt(kWait2);
       __builtin_amdgcn_sched_barrier(0);
       consume(r0, part);
       __builtin_amdgcn_sched_barrier(0);
-      prep(min(base + b + 3, n_used - 1), 0, r0, bad);
+      prep(min(base + b + 3, b_hi - 1), 0, r0, bad);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_waitcnt(kWait2);
       __builtin_amdgcn_sched_barrier(0);
       if (b + 1 < nb) consume(r1, part);
       __builtin_amdgcn_sched_barrier(0);
-      prep(min(base + b + 4, n_used - 1), 1, r1, bad);
+      prep(min(base + b + 4, b_hi - 1), 1, r1, bad);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_waitcnt(kWait2);
       __builtin_amdgcn_sched_barrier(0);
@@ -715,7 +727,7 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
   if (bad) {  // guard (never taken for the host's SEG): exact per-cell recompute
 #pragma unroll
     for (int k = 0; k < NS; ++k) acci[k] = 0;
-    for (int b = 0; b < n_used; ++b) {
+    for (int b = b_lo; b < b_hi; ++b) {
       const double2 p = P[(int64_t)b * step];
       const double lx = ae.cosine * p.x - ae.sine * p.y;
       const double ly = ae.sine * p.x + ae.cosine * p.y;
@@ -728,6 +740,18 @@ __global__ __launch_bounds__(64) void score_rowsd_kernel(
         acci[k] += gi[in ? (int64_t)gy * pitch + gx : (int64_t)sy * pitch];
       }
     }
+  }
+  if constexpr (BS > 1) {  // the other waves' sums into wave 0
+    if (wv > 0) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) xsum[((wv - 1) * NS + k) * 64 + lane] = acci[k];
+    }
+    __syncthreads();
+    if (wv > 0) return;
+#pragma unroll
+    for (int w2 = 1; w2 < BS; ++w2)
+#pragma unroll
+      for (int k = 0; k < NS; ++k) acci[k] += xsum[((w2 - 1) * NS + k) * 64 + lane];
   }
   double bs = -1.0e300;
   int64_t bf = INT64_MAX;
@@ -935,6 +959,43 @@ int rows_pick_sq(int ns, int need_seg) {
   return 0;
 }
 
+// Waves per block of the LDS-DMA row kernel: launches of fewer than 4096
+// blocks (the super-fine level: one block per window) split each window's
+// beams over up to 8 waves, towards 16 waves per SIMD; at most 64 KB of LDS
+// per block (three images and the cross-wave sums per wave). Measured on the
+// fine level (6144 blocks), a 4-way split was 7% slower than none.
+int rows_beam_split(int64_t blocks) {
+  int bs = 1;
+  if (blocks >= 4096) return 1;
+  while (bs < 8 && blocks * bs < 16384) bs *= 2;
+  return bs;
+}
+template <int NS, int SQ>
+constexpr int rows_bs_cap() {
+  constexpr int NP = (64 / NS) * NS * SQ;
+  constexpr int IMG = (NP + 63) / 64 * 256;
+  int bs = 8;
+  while (bs > 1 && bs * (3 * IMG * 4 + NS * 64 * 8) > 64 * 1024) bs /= 2;
+  return bs;
+}
+template <int NS, int SQ, int B>
+hipError_t launch_rowsd(const LevelWork& L, const ScanWork* d_scans, const double2* d_pts,
+                        const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, dim3 grid,
+                        hipStream_t stream) {
+  if constexpr (B > rows_bs_cap<NS, SQ>()) {
+    return launch_rowsd<NS, SQ, rows_bs_cap<NS, SQ>()>(L, d_scans, d_pts, d_angles, d_out, d_partials, grid,
+                                                        stream);
+  } else {
+    if (d_partials)
+      hipLaunchKernelGGL((score_rowsd_kernel<NS, SQ, true, B>), grid, dim3(64 * B), 0, stream, L, d_scans, d_pts,
+                         d_angles, d_out, d_partials);
+    else
+      hipLaunchKernelGGL((score_rowsd_kernel<NS, SQ, false, B>), grid, dim3(64 * B), 0, stream, L, d_scans, d_pts,
+                         d_angles, d_out, d_partials);
+    return hipGetLastError();
+  }
+}
+
 hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const double* d_pts_raw,
                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
                              int ns, int sq, bool dma, hipStream_t stream) {
@@ -942,6 +1003,7 @@ hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const 
   const int64_t nblk = (int64_t)L.blocks_per_scan * L.n_scans;
   if (nblk <= 0 || nblk > INT32_MAX || !L.int_mode || L.size_x < 4 * sq) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblk), block(64);
+  const int bs = dma ? rows_beam_split(nblk) : 1;
 #define CSM_ROWS_LAUNCH(KERN, N, Q)                                                               \
   do {                                                                                            \
     if (d_partials)                                                                               \
@@ -951,16 +1013,22 @@ hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const 
       hipLaunchKernelGGL((KERN<N, Q, false>), grid, block, 0, stream, L, d_scans, d_pts,         \
                          d_angles, d_out, d_partials);                                            \
   } while (0)
-#define CSM_ROWS_CASE(N, Q)                                \
-  if (ns == N && sq == Q) {                                \
-    if (dma)                                               \
-      CSM_ROWS_LAUNCH(score_rowsd_kernel, N, Q);           \
-    else                                                   \
-      CSM_ROWS_LAUNCH(score_rows_kernel, N, Q);            \
-    return hipGetLastError();                              \
+#define CSM_ROWSD_LAUNCH(N, Q, B) \
+  return launch_rowsd<N, Q, B>(L, d_scans, d_pts, d_angles, d_out, d_partials, grid, stream)
+#define CSM_ROWS_CASE(N, Q)                     \
+  if (ns == N && sq == Q) {                     \
+    if (!dma) {                                 \
+      CSM_ROWS_LAUNCH(score_rows_kernel, N, Q); \
+      return hipGetLastError();                 \
+    }                                           \
+    if (bs == 1) CSM_ROWSD_LAUNCH(N, Q, 1);     \
+    if (bs == 2) CSM_ROWSD_LAUNCH(N, Q, 2);     \
+    if (bs == 4) CSM_ROWSD_LAUNCH(N, Q, 4);     \
+    CSM_ROWSD_LAUNCH(N, Q, 8);                  \
   }
   CSM_ROWS_LIST(CSM_ROWS_CASE)
 #undef CSM_ROWS_CASE
+#undef CSM_ROWSD_LAUNCH
 #undef CSM_ROWS_LAUNCH
   return hipErrorInvalidValue;
 }

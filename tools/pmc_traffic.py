@@ -27,10 +27,10 @@ def _short(name: str) -> str:
         kt, integer, best = [a.strip() for a in name[i:name.index(">", i)].split(",")]
         return (f"score_cols_kernel<{kt},{'int' if integer == 'true' else 'f64'},"
                 f"{'best' if best == 'true' else 'all'}>")
-    for key in ("score_rowsd_kernel<", "score_rows_kernel<"):  # <int NS, int SQ, bool BEST>
+    for key in ("score_rowsd_kernel<", "score_rows_kernel<"):  # <int NS, int SQ, bool BEST[, int BS]>
         if key in name:
             i = name.index(key) + len(key)
-            ns, sq, best = [a.strip() for a in name[i:name.index(">", i)].split(",")]
+            ns, sq, best = [a.strip() for a in name[i:name.index(">", i)].split(",")][:3]
             return f"{key[:-1]}<{ns},{sq},{'best' if best == 'true' else 'all'}>"
     key = "score_box_kernel<"
     if key in name:  # <int NS, int D, bool RUNS, bool BEST>
