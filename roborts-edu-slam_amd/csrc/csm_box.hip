@@ -112,7 +112,7 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
     int ix0, iy0;
     const bool clean = box_test(p, lx, ly, ix0, iy0);
     const bool live = cb + lane < n_used;
-    if (__builtin_amdgcn_ballot_w64(live && !clean) != 0) slow |= 1ull << min(cb >> 6, 63);
+    slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean) != 0) << min(cb >> 6, 63);
     return (live && clean && ix0 < sx && iy0 < sy) ? iy0 * pitch4 + ix0 * 4 : zero_off;
   };
   auto point = [&](int cb) { return P[(int64_t)min(cb + lane, n_used - 1) * step]; };
@@ -170,8 +170,10 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
     // form one run; a run is one load whose values are added count times.
     // Runs of boxes wholly off the grid and of rejected beams are dropped
     // (they read zeros). Lists are built per segment of kRunSeg beams.
-    __shared__ int32_t run_off[kRunSeg + 64 + 2 * D];
-    __shared__ int32_t run_cnt[kRunSeg + 64 + 2 * D];
+    // list, padding, then one scratch slot per lane (branch-free list writes)
+    constexpr int kScratch = kRunSeg + 64 + 2 * D;
+    __shared__ int32_t run_off[kScratch + 64];
+    __shared__ int32_t run_cnt[kScratch + 64];
     for (int s0 = 0; s0 < n_used; s0 += kRunSeg) {
       const int s1 = min(n_used, s0 + kRunSeg);
       int nruns = 0;
@@ -199,10 +201,9 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
           const bool head = edge && off != zero_off;
           const uint64_t Hm = __builtin_amdgcn_ballot_w64(head);
           const int rank = __builtin_popcountll(Hm & ((1ull << lane) - 1));
-          if (head) {
-            run_off[nruns + rank] = off;
-            run_cnt[nruns + rank] = next - lane;
-          }
+          const int slot = head ? nruns + rank : kScratch + lane;
+          run_off[slot] = off;
+          run_cnt[slot] = next - lane;
           nruns += __builtin_popcountll(Hm);
         }
       }
