@@ -1,0 +1,618 @@
+// map_oracle.cpp — CPU restatement of RoboRTS-Edu-SLAM's occupancy-grid map
+// building and of the post-match map check (row f4).
+//
+// *** TEST INFRASTRUCTURE — NOT PART OF THE PRODUCT. ***
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+// load this library (oracle/build/liboracle.so), as the checker / CPU
+// baseline. The product (libroborts_csm.so) never links, loads or calls it.
+//
+// PARITY UNPINNED by the reference: it ships no tests for map building and
+// cannot be compiled here (Eigen3, glog, boost, ROS absent).
+// This file is a sequential, call-for-call restatement of
+//   map/occu_grid_map.h      GaussianBlur :38-115, LineVisitor (Bresenham) :119-192,
+//                            InitMapWithRangeVec :222-255, UpdateMapByRange :258-329,
+//                            MapFeedbackResponsePenalty :331-392, CellUpdate and the
+//                            Set* cell updates :474-576
+//   map/grid_map_cell.h      ProbabilityCell(+Functions) :301-388, CountCell(+Functions) :42-161
+//   map/grid_map_base.h      Reset/ResetValueSpeedup :95-112, AllocateGridCell :152-166,
+//                            ExtendSize :182-244, UpdateBound :247-264, UpdateBoundAdaptMap
+//                            :266-273, set_map_offset :275-279, PointInMap :336-352
+//   util/boundbox.h          BoundBox :35-143
+//   slam/sensor_data_manager.h  CreateFrom / TransformLocalToMap :99-175
+// with the reference's evaluation order (g++ -O2 -ffp-contract=off, no FMA),
+// and it is cross-checked against an independent Python restatement
+// (tests/map_pyref.py) in the CPU tests.
+//
+// Reference behaviour kept on purpose (it changes results):
+//  * `new CellType[n]{default_cell_prob_}` (grid_map_base.h:160,214) initialises
+//    only element 0 from default_cell_prob_; every other element is
+//    value-initialised by the default constructor, i.e. kDefaultCellProb = 0.5f
+//    (grid_map_cell.h:30). Maps that are never Reset() keep that pattern.
+//  * map_update_point_ holds linear indices; ExtendSize does not remap them, so a
+//    later ResetValueSpeedup resets the cells now at those indices.
+//  * UpdateMapByRange returns false (nothing drawn) when the scan forced a resize.
+// Definitions where the reference is undefined:
+//  * An empty scan with auto-resize on: the reference would grow the map to a
+//    FLT_MAX box (UB); here the bound step is skipped.
+//  * MapFeedbackResponsePenalty reading a line cell outside the grid (possible
+//    only when the start cell rounds onto the map's far edge): such a cell is
+//    not occupied.
+
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <utility>
+#include <vector>
+
+namespace {
+
+constexpr float kDefaultCellProb = 0.5f;  // grid_map_cell.h:30
+
+enum CellKind { kProbabilityCell = 0, kCountCell = 1 };
+enum UpdateType { kSetFree = 0, kSetOccupied = 1, kSetOccupiedBlur = 2 };  // occu_grid_map.h:32-36
+enum GridState { kUnknown = -1, kOccupied = 100, kFree = 0 };              // grid_map_cell.h:32-37
+
+// Superset of ProbabilityCell {prob, update_index} and CountCell
+// {pass, hit, prob, update_index}; ProbabilityCell leaves pass/hit at 0.
+struct Cell {
+  float prob = kDefaultCellProb;
+  float pass = 0.0f;
+  float hit = 0.0f;
+  int32_t uidx = -1;
+};
+
+// BoundBox<double> (util/boundbox.h:35-143). Default max is FLT_MIN (the
+// smallest positive normal float), as in the reference.
+struct Box {
+  double minx = (double)FLT_MAX, miny = (double)FLT_MAX;
+  double maxx = (double)FLT_MIN, maxy = (double)FLT_MIN;
+  void reset() { *this = Box(); }
+  void add(double x, double y) {  // AddPoint :100-106
+    if (x < minx) minx = x;
+    if (y < miny) miny = y;
+    if (x > maxx) maxx = x;
+    if (y > maxy) maxy = y;
+  }
+  void add_box(const Box& b) {  // AddBoundBox :120-124
+    add(b.minx, b.miny);
+    add(b.maxx, b.maxy);
+  }
+  void extend(double e) {  // ExtendBoundBox :126-129
+    minx -= e;
+    miny -= e;
+    maxx += e;
+    maxy += e;
+  }
+  bool in(double x, double y) const {  // IsInBounds :131-135
+    return x > minx && x < maxx && y > miny && y < maxy;
+  }
+  int size_x() const { return (int)(std::ceil(maxx) - std::floor(minx)); }  // GetBoxSize :78-83
+  int size_y() const { return (int)(std::ceil(maxy) - std::floor(miny)); }
+};
+
+struct OMap {
+  int kind = kProbabilityCell;
+  // GridMapBase
+  double scale_factor = 1.0;
+  int size_x = 0, size_y = 0;  // map_size_
+  int row = 0;                 // size_x_ (row length used by GetCell)
+  double off_x = 0.0, off_y = 0.0;
+  Box bound;
+  double extend_factor = 1.0;
+  float default_prob = kDefaultCellProb;
+  int map_update_index = -1;
+  std::vector<Cell> cells;
+  // GaussianBlur (occu_grid_map.h:38-115)
+  bool blur_states = false;
+  int half_kernel = 0, kernel_size = 0;
+  std::vector<double> kernel;
+  // OccuGridMap
+  bool use_blur = false;
+  bool auto_resize = true;
+  bool just_update_occu = false;
+  int cur_update_index = 0, cur_mark_occu = -1, cur_mark_free = -1;
+  double occu_offset = 0.72;  // cell_occu_prob_offset_ (:601)
+  std::vector<int> update_points;
+  double bound_tolerance = 0.0;
+  int cur_end_x = 0, cur_end_y = 0;
+  // cell functions (grid_map_cell.h:82-92, 207-214, 330-337)
+  float occu_factor = 0.5f, free_factor = 0.2f, occu_threshold = 0.5f, min_pass = 2.0f;
+};
+
+Cell fresh_cell(const OMap& m, int64_t i) {  // `new CellType[n]{default}` (grid_map_base.h:160,214)
+  Cell c;
+  c.prob = i == 0 ? m.default_prob : kDefaultCellProb;
+  return c;
+}
+
+void reset_cell(const OMap& m, Cell& c) {  // ResetGridCell (grid_map_cell.h:64-69, 318-322)
+  c.prob = m.default_prob;
+  c.pass = 0.0f;
+  c.hit = 0.0f;
+  c.uidx = -1;
+}
+
+// ---- cell functions ----------------------------------------------------------
+void set_occupied(const OMap& m, Cell& c) {
+  if (m.kind == kCountCell) {  // CountCellFunctions::UpdateSetOccupied :94-101
+    c.hit += (1.0f + m.occu_factor);
+    c.pass += (1.0f + m.free_factor);
+    c.prob = c.hit / c.pass;
+    if (c.prob > 1.0f) c.prob = 1.0f;
+  } else {  // ProbabilityCellFunctions::UpdateSetOccupied :339-343
+    float v = c.prob + m.occu_factor;
+    if (v > 1.0f) v = 1.0f;
+    c.prob = v;
+  }
+}
+void set_free(const OMap& m, Cell& c) {
+  if (m.kind == kCountCell) {  // :103-106
+    c.pass += (1.0f + m.free_factor);
+    c.prob = c.hit / c.pass;
+  } else {  // :345-349
+    float v = c.prob - m.free_factor;
+    if (v < 0.0f) v = 0.0f;
+    c.prob = v;
+  }
+}
+void unset_free(const OMap& m, Cell& c) {
+  if (m.kind == kCountCell) {  // :108-111
+    c.pass -= (1.0f + m.free_factor);
+    c.prob = c.hit / c.pass;
+  } else {  // :351-355
+    float v = c.prob + m.free_factor;
+    if (v > 1.0f) v = 1.0f;
+    c.prob = v;
+  }
+}
+void set_probability(const OMap& m, Cell& c, float p) {
+  if (m.kind == kCountCell) {  // :117-123
+    if (c.prob < p) {
+      c.prob = p;
+      c.hit = p * c.pass;
+    }
+  } else if (c.prob < p && p <= 1.0f) {  // :361-365
+    c.prob = p;
+  }
+}
+int grid_state(const OMap& m, const Cell& c) {
+  if (m.kind == kCountCell) {  // :125-136
+    if (c.pass >= m.min_pass) return c.prob < m.occu_threshold ? kFree : kOccupied;
+    return kUnknown;
+  }
+  if (c.prob < 0.5f) return kFree;  // :367-375
+  if (c.prob > 0.5f) return kOccupied;
+  return kUnknown;
+}
+
+// ---- GridMapBase -----------------------------------------------------------------
+Cell& cell_at(OMap& m, int x, int y) { return m.cells[(size_t)((int64_t)y * m.row + x)]; }
+int grid_index(const OMap& m, int x, int y) { return y * m.row + x; }
+
+bool point_in_map(const OMap& m, double x, double y, double tol = 0.0) {  // :344-352
+  return x > tol && x < m.size_x - tol && y > tol && y < m.size_y - tol;
+}
+
+void allocate(OMap& m, int sx, int sy) {  // AllocateGridCell :152-166
+  const int64_t n = (int64_t)sx * sy;
+  m.cells.resize(n > 0 ? (size_t)n : 0);
+  for (int64_t i = 0; i < n; ++i) m.cells[(size_t)i] = fresh_cell(m, i);
+  m.size_x = sx;
+  m.size_y = sy;
+}
+
+void extend_size(OMap& m) {  // ExtendSize(EXTEND_PARTLY) :182-244
+  Box t;
+  t.add_box(m.bound);
+  const double map_min_x = 0.0, map_min_y = 0.0;
+  const double map_max_x = (double)m.size_x, map_max_y = (double)m.size_y;
+  t.add(map_min_x, map_min_y);
+  t.add(map_max_x, map_max_y);
+  double min_x = t.minx, min_y = t.miny, max_x = t.maxx, max_y = t.maxy;
+  if (m.bound.minx <= map_min_x) min_x -= (double)t.size_x() * m.extend_factor;
+  if (m.bound.miny <= map_min_y) min_y -= (double)t.size_y() * m.extend_factor;
+  if (m.bound.maxx >= map_max_x) max_x += (double)t.size_x() * m.extend_factor;
+  if (m.bound.maxy >= map_max_y) max_y += (double)t.size_y() * m.extend_factor;
+  t.add(min_x, min_y);
+  t.add(max_x, max_y);
+  const double fx = std::floor(t.minx), fy = std::floor(t.miny);
+  m.off_x -= fx / m.scale_factor;
+  m.off_y -= fy / m.scale_factor;
+  const int gx = -(int)fx, gy = -(int)fy;
+  const int pre_row = m.row, pre_sy = m.size_y;
+  const int nsx = t.size_x(), nsy = t.size_y();
+  std::vector<Cell> old;
+  old.swap(m.cells);
+  m.row = nsx;
+  const int64_t n = (int64_t)nsx * nsy;
+  m.cells.resize((size_t)n);
+  for (int64_t i = 0; i < n; ++i) m.cells[(size_t)i] = fresh_cell(m, i);
+  for (int r = 0; r < pre_sy; ++r)
+    std::memcpy(&m.cells[(size_t)((int64_t)(gy + r) * nsx + gx)], &old[(size_t)((int64_t)r * pre_row)],
+                sizeof(Cell) * (size_t)pre_row);
+  m.size_x = nsx;
+  m.size_y = nsy;
+  Box nb;
+  nb.minx = m.bound.minx - t.minx;
+  nb.miny = m.bound.miny - t.miny;
+  nb.maxx = m.bound.maxx - t.minx;
+  nb.maxy = m.bound.maxy - t.miny;
+  m.bound = nb;
+}
+
+bool update_bound(OMap& m, const Box& b) {  // UpdateBound :247-264
+  if (m.bound.in(b.minx, b.miny) && m.bound.in(b.maxx, b.maxy)) return true;
+  m.bound.add_box(b);
+  if (!point_in_map(m, m.bound.minx, m.bound.miny) || !point_in_map(m, m.bound.maxx, m.bound.maxy)) {
+    extend_size(m);
+    return false;
+  }
+  return true;
+}
+
+// GetMapCoordsPose (grid_map_base.h:89-93): Scaling(s) * Translation(o).
+void world_to_map(const OMap& m, const double w[3], double out[3]) {
+  const double s = m.scale_factor;
+  out[0] = s * w[0] + s * m.off_x;
+  out[1] = s * w[1] + s * m.off_y;
+  out[2] = w[2];
+}
+
+// ---- OccuGridMap --------------------------------------------------------------------
+void init_kernel(OMap& m, double sigma, double res) {  // GaussianBlur :40-105
+  if (sigma > 0.5 * res && sigma < 10 * res && res > 0) {
+    m.blur_states = true;
+    m.half_kernel = (int)((sigma / res) * std::sqrt(std::log(2)));
+    m.kernel_size = m.half_kernel * 2 + 1;
+    m.kernel.assign((size_t)m.kernel_size * m.kernel_size, 0.0);
+    for (int i = -m.half_kernel; i <= m.half_kernel; ++i)
+      for (int j = -m.half_kernel; j <= m.half_kernel; ++j) {
+        const double d = std::hypot(i * res, j * res);
+        const double q = d / sigma;
+        m.kernel[(size_t)((i + m.half_kernel) + m.kernel_size * (j + m.half_kernel))] = std::exp(-0.5 * (q * q));
+      }
+  } else {
+    m.blur_states = false;
+    m.half_kernel = 0;
+    m.kernel_size = 0;
+  }
+}
+
+void set_cell_free(OMap& m, int x, int y) {  // :499-510
+  Cell& c = cell_at(m, x, y);
+  if (c.uidx < m.cur_mark_free) {
+    set_free(m, c);
+    c.uidx = m.cur_mark_free;
+  }
+  m.update_points.push_back(grid_index(m, x, y));
+}
+
+void set_cell_occu(OMap& m, int x, int y) {  // :512-529
+  Cell& c = cell_at(m, x, y);
+  if (c.uidx < m.cur_mark_occu) {
+    if (c.uidx == m.cur_mark_free) unset_free(m, c);
+    set_occupied(m, c);
+    c.uidx = m.cur_mark_occu;
+  }
+  m.update_points.push_back(grid_index(m, x, y));
+}
+
+void set_cell_occu_blur(OMap& m, int x, int y) {  // :531-576
+  Cell& center = cell_at(m, x, y);
+  if (center.uidx < m.cur_mark_occu) {
+    if (!m.just_update_occu) {
+      if (center.uidx == m.cur_mark_free) unset_free(m, center);
+      set_occupied(m, center);
+      center.uidx = m.cur_mark_occu;
+    } else {
+      set_probability(m, center, 1.0f);
+    }
+    const int hk = m.half_kernel, ks = m.kernel_size;
+    for (int j = -hk; j <= hk; ++j)
+      for (int i = -hk; i <= hk; ++i) {
+        const int k = (i + hk) + ks * (j + hk);
+        set_probability(m, cell_at(m, x + i, y + j), (float)(m.kernel[(size_t)k] * m.occu_offset));
+        m.update_points.push_back(grid_index(m, x + i, y + j));
+      }
+  }
+}
+
+void cell_update(OMap& m, int x, int y, int type) {  // CellUpdate :474-497
+  if (!point_in_map(m, x, y, m.half_kernel + 1)) return;
+  if (type == kSetFree)
+    set_cell_free(m, x, y);
+  else if (type == kSetOccupied)
+    set_cell_occu(m, x, y);
+  else
+    set_cell_occu_blur(m, x, y);
+}
+
+// LineVisitor::ErgodLineBresenhami (occu_grid_map.h:125-188): visit(x, y)
+// for each cell in the reference's order.
+template <class F>
+void bresenham(int x0, int y0, int x1, int y1, F&& visit) {
+  const bool steep = std::abs(y1 - y0) > std::abs(x1 - x0);
+  if (steep) {
+    std::swap(x0, y0);
+    std::swap(x1, y1);
+  }
+  if (x0 > x1) {
+    std::swap(x0, x1);
+    std::swap(y0, y1);
+  }
+  const int dx = x1 - x0, dy = std::abs(y1 - y0);
+  int err = 0, y = y0;
+  const int ystep = y0 < y1 ? 1 : -1;
+  for (int x = x0; x <= x1; ++x) {
+    if (steep)
+      visit(y, x);
+    else
+      visit(x, y);
+    err += dy;
+    if (2 * err >= dx) {
+      y += ystep;
+      err -= dx;
+    }
+  }
+}
+
+// Affine2d(Translation2d(t) * Rotation2Dd(th)) applied to p: linear * p + t with
+// linear = [c -s; s c] (Rotation2D::toRotationMatrix), Eigen's
+// translation-then-add-product order.
+inline void pose_apply(double c, double s, double tx, double ty, double px, double py, double& ox, double& oy) {
+  ox = (c * px + (-s) * py) + tx;
+  oy = (s * px + c * py) + ty;
+}
+
+bool update_by_range(OMap& m, const double* pts, int n, const double origin[2], const double pose[3],
+                     bool use_blur) {  // UpdateMapByRange :258-329
+  if (!m.blur_states) use_blur = false;
+  m.use_blur = use_blur;
+  m.cur_mark_free = m.cur_update_index + 1;
+  m.cur_mark_occu = m.cur_update_index + 2;
+  double pm[3];
+  world_to_map(m, pose, pm);
+  const double c = std::cos(pm[2]), s = std::sin(pm[2]);
+  std::vector<double> tp((size_t)2 * (n > 0 ? n : 0));
+  for (int i = 0; i < n; ++i) pose_apply(c, s, pm[0], pm[1], pts[2 * i], pts[2 * i + 1], tp[2 * i], tp[2 * i + 1]);
+  if (m.auto_resize && n > 0) {
+    Box b;
+    for (int i = 0; i < n; ++i) b.add(tp[2 * i], tp[2 * i + 1]);
+    if (use_blur) b.extend((double)m.half_kernel);
+    if (!update_bound(m, b)) {
+      m.cur_update_index += 3;
+      return false;
+    }
+  }
+  double sx, sy;
+  pose_apply(c, s, pm[0], pm[1], origin[0], origin[1], sx, sy);
+  const int x0 = (int)(sx + 0.5), y0 = (int)(sy + 0.5);
+  for (int i = 0; i < n; ++i) {
+    const int x1 = (int)(tp[2 * i] + 0.5), y1 = (int)(tp[2 * i + 1] + 0.5);
+    if (x0 != x1 || y0 != y1) {
+      if (!m.just_update_occu) bresenham(x0, y0, x1, y1, [&](int x, int y) { cell_update(m, x, y, kSetFree); });
+      cell_update(m, x1, y1, use_blur ? kSetOccupiedBlur : kSetOccupied);
+    }
+  }
+  m.map_update_index++;
+  m.cur_update_index += 3;
+  return true;
+}
+
+void reset_all(OMap& m) {  // Reset :95-103
+  for (auto& c : m.cells) reset_cell(m, c);
+}
+
+void init_with_range_vec(OMap& m, const double* pts, const int64_t* offsets, int n_scans, const double* origins,
+                         const double* poses, bool use_blur, bool speedup) {  // InitMapWithRangeVec :222-255
+  if (speedup) {
+    for (int idx : m.update_points) reset_cell(m, m.cells[(size_t)idx]);  // ResetValueSpeedup :112-117
+  } else {
+    reset_all(m);
+  }
+  m.cur_update_index = 0;
+  m.cur_mark_occu = -1;
+  m.cur_mark_free = -1;
+  m.update_points.clear();
+  for (int k = 0; k < n_scans; ++k) {
+    int tries = 5;
+    while (!update_by_range(m, pts + 2 * offsets[k], (int)(offsets[k + 1] - offsets[k]), origins + 2 * k,
+                            poses + 3 * k, use_blur) &&
+           tries)
+      tries--;
+  }
+  if (!m.auto_resize) {  // UpdateBoundAdaptMap :266-273
+    m.bound.minx = 0.0;
+    m.bound.miny = 0.0;
+    m.bound.maxx = (double)(m.size_x + 1);
+    m.bound.maxy = (double)(m.size_y + 1);
+  }
+}
+
+double feedback_penalty(OMap& m, const double* pts, int n, const double origin[2], const double best_pose[3],
+                        int check_point_num, double bound_tolerance, double penalty_gain,
+                        bool use_blur) {  // MapFeedbackResponsePenalty :331-392
+  if (bound_tolerance < 0 || check_point_num <= 0 || penalty_gain <= 0.0 || penalty_gain >= 1.0) return 1.0;
+  m.use_blur = use_blur;
+  m.bound_tolerance = bound_tolerance;
+  double pm[3];
+  world_to_map(m, best_pose, pm);
+  if (!point_in_map(m, pm[0], pm[1])) return 0.0;
+  const double c = std::cos(pm[2]), s = std::sin(pm[2]);
+  double sx, sy;
+  pose_apply(c, s, pm[0], pm[1], origin[0], origin[1], sx, sy);
+  const int x0 = (int)(sx + 0.5), y0 = (int)(sy + 0.5);
+  int step = 1;
+  if (n < 2 * check_point_num)
+    step = 1;
+  else
+    step = n / (check_point_num - 1);
+  double penalty = 0;
+  for (int i = 0; i < n; i += step) {
+    double ex, ey;
+    pose_apply(c, s, pm[0], pm[1], pts[2 * i], pts[2 * i + 1], ex, ey);
+    const int x1 = (int)(ex + 0.5), y1 = (int)(ey + 0.5);
+    if ((x0 == x1 && y0 == y1) || !point_in_map(m, x1, y1)) continue;
+    m.cur_end_x = x1;
+    m.cur_end_y = y1;
+    double res = 0.0;
+    bresenham(x0, y0, x1, y1, [&](int x, int y) {  // CheckOccuLineVisitorCallback :447-471
+      double sum = 0.0;
+      bool occ = false;
+      if (x >= 0 && y >= 0 && x < m.size_x && y < m.size_y) {
+        const Cell& cell = cell_at(m, x, y);
+        occ = m.use_blur ? ((double)cell.prob > m.occu_offset) : (grid_state(m, cell) == kOccupied);
+      }
+      if (occ) {
+        const double dx = (double)m.cur_end_x - (double)x, dy = (double)m.cur_end_y - (double)y;
+        if (std::sqrt(dx * dx + dy * dy) > m.bound_tolerance) sum += 1.0;
+      }
+      if (res < 1.0) res += sum;
+    });
+    penalty += res;
+  }
+  penalty *= penalty_gain;
+  return std::max((1.0 + 2 * penalty_gain - penalty), 0.1);
+}
+
+}  // namespace
+
+extern "C" {
+
+// OccuGridMap(resolution, size, offset, deviation, default_cell_prob)
+// (occu_grid_map.h:201-217) with the cell functions' constructor factors.
+void* oracle_gridmap_create(int kind, double resolution, int size_x, int size_y, double off_x, double off_y,
+                            double deviation, float default_prob) {
+  auto m = std::make_unique<OMap>();
+  m->kind = kind;
+  m->scale_factor = 1.0 / resolution;
+  m->off_x = off_x;
+  m->off_y = off_y;
+  m->default_prob = default_prob;
+  if (kind == kCountCell) {
+    m->free_factor = 0.0f;
+    m->occu_factor = 0.0f;
+    m->occu_threshold = 0.5f;
+    m->min_pass = 2.0f;
+  }
+  allocate(*m, size_x, size_y);
+  m->row = m->size_x;
+  init_kernel(*m, deviation, resolution);
+  return m.release();
+}
+
+void oracle_gridmap_destroy(void* h) { delete static_cast<OMap*>(h); }
+
+// set_use_auto_map_resize / set_just_update_occu / set_cell_occu_prob_offset /
+// set_extend_factor (occu_grid_map.h:429-439, grid_map_base.h:175-179).
+void oracle_gridmap_set_options(void* h, int auto_resize, int just_update_occu, double occu_offset,
+                                double extend_factor) {
+  OMap& m = *static_cast<OMap*>(h);
+  m.auto_resize = auto_resize != 0;
+  m.just_update_occu = just_update_occu != 0;
+  m.occu_offset = occu_offset;
+  if (extend_factor > 0) m.extend_factor = extend_factor;
+}
+
+// SetUpdateFreeFactor / SetUpdateOccupiedFactor / SetOccuThreshold / SetMinPassThrough
+void oracle_gridmap_set_cell_params(void* h, float free_factor, float occu_factor, float occu_threshold,
+                                    float min_pass) {
+  OMap& m = *static_cast<OMap*>(h);
+  m.free_factor = free_factor;
+  m.occu_factor = occu_factor;
+  if (m.kind == kCountCell) {
+    m.occu_threshold = occu_threshold;
+    m.min_pass = min_pass;
+  }
+}
+
+void oracle_gridmap_set_map_offset(void* h, double ox, double oy) {
+  OMap& m = *static_cast<OMap*>(h);
+  m.off_x = ox;
+  m.off_y = oy;
+}
+
+void oracle_gridmap_reset(void* h) { reset_all(*static_cast<OMap*>(h)); }
+
+int oracle_gridmap_update_by_range(void* h, const double* pts, int n, const double origin[2], const double pose[3],
+                                   int use_blur) {
+  return update_by_range(*static_cast<OMap*>(h), pts, n, origin, pose, use_blur != 0) ? 1 : 0;
+}
+
+void oracle_gridmap_init_with_range_vec(void* h, const double* pts, const int64_t* offsets, int n_scans,
+                                        const double* origins, const double* poses, int use_blur, int speedup) {
+  init_with_range_vec(*static_cast<OMap*>(h), pts, offsets, n_scans, origins, poses, use_blur != 0, speedup != 0);
+}
+
+double oracle_gridmap_feedback_penalty(void* h, const double* pts, int n, const double origin[2],
+                                       const double best_pose[3], int check_point_num, double bound_tolerance,
+                                       double penalty_gain, int use_blur) {
+  return feedback_penalty(*static_cast<OMap*>(h), pts, n, origin, best_pose, check_point_num, bound_tolerance,
+                          penalty_gain, use_blur != 0);
+}
+
+// Geometry and counters: ints[0..7] = size_x, size_y, map_update_index,
+// cur_update_index, half_kernel, n_update_points, blur_states, kind;
+// dbl[0..6] = resolution, off_x, off_y, bound min x/y, max x/y.
+void oracle_gridmap_info(void* h, int32_t* ints, double* dbl) {
+  const OMap& m = *static_cast<OMap*>(h);
+  ints[0] = m.size_x;
+  ints[1] = m.size_y;
+  ints[2] = m.map_update_index;
+  ints[3] = m.cur_update_index;
+  ints[4] = m.half_kernel;
+  ints[5] = (int32_t)m.update_points.size();
+  ints[6] = m.blur_states ? 1 : 0;
+  ints[7] = m.kind;
+  dbl[0] = 1 / m.scale_factor;
+  dbl[1] = m.off_x;
+  dbl[2] = m.off_y;
+  dbl[3] = m.bound.minx;
+  dbl[4] = m.bound.miny;
+  dbl[5] = m.bound.maxx;
+  dbl[6] = m.bound.maxy;
+}
+
+// Cells as separate arrays (size_y * size_x each; any pointer may be null).
+void oracle_gridmap_cells(void* h, float* prob, float* pass, float* hit, int32_t* uidx) {
+  const OMap& m = *static_cast<OMap*>(h);
+  for (size_t i = 0; i < m.cells.size(); ++i) {
+    if (prob) prob[i] = m.cells[i].prob;
+    if (pass) pass[i] = m.cells[i].pass;
+    if (hit) hit[i] = m.cells[i].hit;
+    if (uidx) uidx[i] = m.cells[i].uidx;
+  }
+}
+
+// map_update_point_ as a set: flags[i] = 1 if linear index i is in the list.
+void oracle_gridmap_touched(void* h, uint8_t* flags) {
+  const OMap& m = *static_cast<OMap*>(h);
+  std::memset(flags, 0, m.cells.size());
+  for (int idx : m.update_points) flags[idx] = 1;
+}
+
+// Blur kernel values (kernel_size^2, index (i+hk) + ks*(j+hk)).
+int oracle_gridmap_kernel(void* h, double* out, int cap) {
+  const OMap& m = *static_cast<OMap*>(h);
+  const int n = (int)m.kernel.size();
+  for (int i = 0; i < n && i < cap; ++i) out[i] = m.kernel[(size_t)i];
+  return n;
+}
+
+// The reference's Bresenham visit order (test hook): writes up to cap cells
+// as (x, y) pairs, returns the count.
+int oracle_bresenham(int x0, int y0, int x1, int y1, int32_t* out, int cap) {
+  int k = 0;
+  bresenham(x0, y0, x1, y1, [&](int x, int y) {
+    if (k < cap) {
+      out[2 * k] = x;
+      out[2 * k + 1] = y;
+    }
+    ++k;
+  });
+  return k;
+}
+
+}  // extern "C"

@@ -198,3 +198,127 @@ def std_sort_order(keys) -> np.ndarray:
     out = np.empty(k.size, dtype=np.int64)
     _lib.oracle_std_sort_order(k.ctypes.data_as(_dp), k.size, out.ctypes.data_as(_i64p))
     return out
+
+
+# ---- occupancy-grid map building (map_oracle.cpp) ----
+PROBABILITY_CELL, COUNT_CELL = 0, 1
+_fp = C.POINTER(C.c_float)
+_i32p = C.POINTER(C.c_int32)
+_u8p = C.POINTER(C.c_uint8)
+for _k, (_r, _a) in {
+    "oracle_gridmap_create": (C.c_void_p, [C.c_int, C.c_double, C.c_int, C.c_int, C.c_double, C.c_double,
+                                           C.c_double, C.c_float]),
+    "oracle_gridmap_destroy": (None, [C.c_void_p]),
+    "oracle_gridmap_set_options": (None, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double]),
+    "oracle_gridmap_set_cell_params": (None, [C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_float]),
+    "oracle_gridmap_set_map_offset": (None, [C.c_void_p, C.c_double, C.c_double]),
+    "oracle_gridmap_reset": (None, [C.c_void_p]),
+    "oracle_gridmap_update_by_range": (C.c_int, [C.c_void_p, _dp, C.c_int, _dp, _dp, C.c_int]),
+    "oracle_gridmap_init_with_range_vec": (None, [C.c_void_p, _dp, _i64p, C.c_int, _dp, _dp, C.c_int, C.c_int]),
+    "oracle_gridmap_feedback_penalty": (C.c_double, [C.c_void_p, _dp, C.c_int, _dp, _dp, C.c_int, C.c_double,
+                                                     C.c_double, C.c_int]),
+    "oracle_gridmap_info": (None, [C.c_void_p, _i32p, _dp]),
+    "oracle_gridmap_cells": (None, [C.c_void_p, _fp, _fp, _fp, _i32p]),
+    "oracle_gridmap_touched": (None, [C.c_void_p, _u8p]),
+    "oracle_gridmap_kernel": (C.c_int, [C.c_void_p, _dp, C.c_int]),
+    "oracle_bresenham": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _i32p, C.c_int]),
+}.items():
+    _f = getattr(_lib, _k)
+    _f.restype, _f.argtypes = _r, _a
+
+
+def _d(a, n=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a
+
+
+class GridMap:
+    """Oracle OccuGridMap<ProbabilityCell | CountCell> (map_oracle.cpp)."""
+
+    def __init__(self, kind: int, resolution: float, size, offset, deviation: float = 0.0,
+                 default_prob: float = 0.5):
+        self.h = _lib.oracle_gridmap_create(kind, resolution, int(size[0]), int(size[1]), float(offset[0]),
+                                            float(offset[1]), deviation, default_prob)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            _lib.oracle_gridmap_destroy(h)
+            self.h = None
+
+    def set_options(self, auto_resize=True, just_update_occu=False, occu_offset=0.72, extend_factor=1.0):
+        _lib.oracle_gridmap_set_options(self.h, int(auto_resize), int(just_update_occu), occu_offset, extend_factor)
+
+    def set_cell_params(self, free_factor, occu_factor, occu_threshold=0.5, min_pass=2.0):
+        _lib.oracle_gridmap_set_cell_params(self.h, free_factor, occu_factor, occu_threshold, min_pass)
+
+    def set_map_offset(self, ox, oy):
+        _lib.oracle_gridmap_set_map_offset(self.h, ox, oy)
+
+    def reset(self):
+        _lib.oracle_gridmap_reset(self.h)
+
+    def update_by_range(self, points, pose, origin=(0.0, 0.0), use_blur=False) -> bool:
+        p = _pts(points)
+        o, w = _d(origin), _d(pose)
+        return bool(_lib.oracle_gridmap_update_by_range(self.h, p.ctypes.data_as(_dp), p.shape[0],
+                                                        o.ctypes.data_as(_dp), w.ctypes.data_as(_dp),
+                                                        int(use_blur)))
+
+    def init_with_range_vec(self, scans, poses, origins=None, use_blur=False, speedup=False):
+        pts = np.concatenate([_pts(s) for s in scans]) if scans else np.zeros((0, 2))
+        pts = np.ascontiguousarray(pts)
+        off = np.zeros(len(scans) + 1, dtype=np.int64)
+        off[1:] = np.cumsum([_pts(s).shape[0] for s in scans])
+        ps = _d(np.asarray(poses, dtype=np.float64).reshape(-1, 3))
+        og = _d(np.zeros((len(scans), 2)) if origins is None else np.asarray(origins).reshape(-1, 2))
+        _lib.oracle_gridmap_init_with_range_vec(self.h, pts.ctypes.data_as(_dp), off.ctypes.data_as(_i64p),
+                                                len(scans), og.ctypes.data_as(_dp), ps.ctypes.data_as(_dp),
+                                                int(use_blur), int(speedup))
+
+    def feedback_penalty(self, points, best_pose, check_point_num, bound_tolerance, penalty_gain,
+                         origin=(0.0, 0.0), use_blur=False) -> float:
+        p = _pts(points)
+        o, w = _d(origin), _d(best_pose)
+        return _lib.oracle_gridmap_feedback_penalty(self.h, p.ctypes.data_as(_dp), p.shape[0],
+                                                    o.ctypes.data_as(_dp), w.ctypes.data_as(_dp),
+                                                    int(check_point_num), bound_tolerance, penalty_gain,
+                                                    int(use_blur))
+
+    def info(self) -> dict:
+        ints = np.zeros(8, dtype=np.int32)
+        dbl = np.zeros(7)
+        _lib.oracle_gridmap_info(self.h, ints.ctypes.data_as(_i32p), dbl.ctypes.data_as(_dp))
+        return {"size_x": int(ints[0]), "size_y": int(ints[1]), "map_update_index": int(ints[2]),
+                "cur_update_index": int(ints[3]), "half_kernel": int(ints[4]), "n_update_points": int(ints[5]),
+                "blur_states": bool(ints[6]), "kind": int(ints[7]), "resolution": dbl[0],
+                "offset": (dbl[1], dbl[2]), "bound": tuple(dbl[3:7])}
+
+    def cells(self):
+        """(prob, pass, hit, update_index) as [size_y, size_x] arrays."""
+        inf = self.info()
+        n = inf["size_x"] * inf["size_y"]
+        prob, ps, hit = (np.zeros(n, dtype=np.float32) for _ in range(3))
+        uidx = np.zeros(n, dtype=np.int32)
+        _lib.oracle_gridmap_cells(self.h, prob.ctypes.data_as(_fp), ps.ctypes.data_as(_fp), hit.ctypes.data_as(_fp),
+                                  uidx.ctypes.data_as(_i32p))
+        sh = (inf["size_y"], inf["size_x"])
+        return prob.reshape(sh), ps.reshape(sh), hit.reshape(sh), uidx.reshape(sh)
+
+    def touched(self) -> np.ndarray:
+        inf = self.info()
+        f = np.zeros(inf["size_x"] * inf["size_y"], dtype=np.uint8)
+        _lib.oracle_gridmap_touched(self.h, f.ctypes.data_as(_u8p))
+        return f
+
+    def kernel(self) -> np.ndarray:
+        out = np.zeros(441)
+        n = _lib.oracle_gridmap_kernel(self.h, out.ctypes.data_as(_dp), out.size)
+        return out[:n]
+
+
+def bresenham(x0, y0, x1, y1) -> np.ndarray:
+    cap = abs(x1 - x0) + abs(y1 - y0) + 2
+    out = np.zeros(2 * cap, dtype=np.int32)
+    n = _lib.oracle_bresenham(x0, y0, x1, y1, out.ctypes.data_as(_i32p), cap)
+    return out[:2 * n].reshape(n, 2)

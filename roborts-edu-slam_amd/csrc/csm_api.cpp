@@ -15,6 +15,8 @@
 
 #include "csm.h"
 #include "csm_internal.hpp"
+#include "csm_gridmap.h"
+#include "csm_gridmap_internal.hpp"
 
 #include <algorithm>
 #include <atomic>
@@ -1564,6 +1566,29 @@ int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) 
   c->key_cells = nullptr;
   c->key_version = -1;
   return CSM_OK;
+}
+
+int csm_set_grid_gridmap(csm_ctx* c, csm_gridmap* map) {
+  if (!c || !map) return CSM_ERR_INVALID_ARG;
+  csm::GridMapView v{};
+  int st = csm::gridmap_view(map, &v);
+  if (st != CSM_OK) return st;
+  if (v.device != c->device) return c->fail(CSM_ERR_INVALID_ARG, "map lives on another device");
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    // the matcher's kernels run after the map's last update
+    hipError_t e = hipStreamWaitEvent(c->stream, v.ready, 0);
+    if (e != hipSuccess) return c->fail(CSM_ERR_HIP, hipGetErrorString(e));
+  }
+  csm_map_info info{};
+  info.resolution = v.resolution;
+  info.offset_x = v.offset_x;
+  info.offset_y = v.offset_y;
+  info.size_x = v.size_x;
+  info.size_y = v.size_y;
+  info.update_index = v.map_update_index;
+  return csm_set_grid_device(c, v.prob, &info);
 }
 
 int csm_scan_match_batch(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,

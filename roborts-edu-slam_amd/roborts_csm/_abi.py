@@ -29,7 +29,15 @@ EXPORTED = (
     "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded",
     "csm_set_profiling", "csm_kernel_stats", "csm_sort_order",
     "csm_set_grid_stack", "csm_best_windows",
+    # include/csm_gridmap.h
+    "csm_gridmap_create", "csm_gridmap_destroy", "csm_gridmap_last_error",
+    "csm_gridmap_set_options", "csm_gridmap_set_cell_params", "csm_gridmap_set_map_offset",
+    "csm_gridmap_reset", "csm_gridmap_update_by_range", "csm_gridmap_init_with_range_vec",
+    "csm_gridmap_feedback_penalty", "csm_gridmap_get_state", "csm_gridmap_download",
+    "csm_gridmap_device_prob", "csm_set_grid_gridmap",
 )
+
+PROBABILITY_CELL, COUNT_CELL = 0, 1
 
 
 class CsmParam(C.Structure):
@@ -80,6 +88,28 @@ class CsmKernelStat(C.Structure):
     ]
 
 
+class CsmGridmapState(C.Structure):
+    """csm_gridmap_state (include/csm_gridmap.h)."""
+
+    _fields_ = [
+        ("resolution", C.c_double),
+        ("offset_x", C.c_double),
+        ("offset_y", C.c_double),
+        ("bound_min_x", C.c_double),
+        ("bound_min_y", C.c_double),
+        ("bound_max_x", C.c_double),
+        ("bound_max_y", C.c_double),
+        ("size_x", C.c_int32),
+        ("size_y", C.c_int32),
+        ("map_update_index", C.c_int32),
+        ("cur_update_index", C.c_int32),
+        ("half_kernel", C.c_int32),
+        ("blur_states", C.c_int32),
+        ("kind", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
 _dp = C.POINTER(C.c_double)
 _i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
@@ -110,6 +140,24 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_set_grid_stack": (C.c_int, [_ctx, C.c_void_p, C.c_int32, C.POINTER(CsmMapInfo), C.c_int64]),
         "csm_best_windows": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), C.c_int32, _i32p, _dp,
                                        C.POINTER(CsmBest)]),
+        "csm_gridmap_create": (C.c_int, [C.c_int, C.c_int32, C.c_double, C.c_int32, C.c_int32, C.c_double,
+                                         C.c_double, C.c_double, C.c_float, C.POINTER(C.c_void_p)]),
+        "csm_gridmap_destroy": (C.c_int, [C.c_void_p]),
+        "csm_gridmap_last_error": (C.c_char_p, [C.c_void_p]),
+        "csm_gridmap_set_options": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_double, C.c_double]),
+        "csm_gridmap_set_cell_params": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_float]),
+        "csm_gridmap_set_map_offset": (C.c_int, [C.c_void_p, C.c_double, C.c_double]),
+        "csm_gridmap_reset": (C.c_int, [C.c_void_p]),
+        "csm_gridmap_update_by_range": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, _dp, C.c_int32, _i32p]),
+        "csm_gridmap_init_with_range_vec": (C.c_int, [C.c_void_p, C.c_int32, _dp, _i64p, _dp, _dp, C.c_int32,
+                                                      C.c_int32]),
+        "csm_gridmap_feedback_penalty": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, _dp, C.c_int32, C.c_double,
+                                                   C.c_double, C.c_int32, _dp]),
+        "csm_gridmap_get_state": (C.c_int, [C.c_void_p, C.POINTER(CsmGridmapState)]),
+        "csm_gridmap_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_void_p]),
+        "csm_gridmap_device_prob": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+        "csm_set_grid_gridmap": (C.c_int, [_ctx, C.c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

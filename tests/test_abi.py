@@ -1,4 +1,5 @@
-"""CPU: the C-ABI library loads, exports every symbol include/csm.h declares,
+"""CPU: the C-ABI library loads, exports every symbol include/csm.h and
+include/csm_gridmap.h declare,
 and its host-only entry points behave (no compute calls without a GPU)."""
 import ctypes as C
 import os
@@ -15,9 +16,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _declared():
-    txt = open(os.path.join(ROOT, "include", "csm.h")).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(csm_[a-z_0-9]+)\s*\(", txt)))
+    names = set()
+    for h in ("csm.h", "csm_gridmap.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b(csm_[a-z_0-9]+)\s*\(", txt))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():

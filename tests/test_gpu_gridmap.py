@@ -1,0 +1,96 @@
+"""GPU parity of the device-resident occupancy maps (SURVEY.md 8f rows f1,
+f4; include/csm_gridmap.h) against the oracle (oracle/map_oracle.cpp), which
+the CPU tests pin to an independent restatement. Bar: bit-identical cells
+(prob / pass / hit / update_index), touched-cell set, geometry after growth,
+update counters and map-check penalties — tolerance 0."""
+import math
+
+import numpy as np
+import pytest
+
+import map_scenarios as S
+from map_engines import DeviceEngine, OracleEngine, same_state
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def scans():
+    return S.make_scans(4)
+
+
+@pytest.mark.parametrize("name", sorted(S.scenarios()))
+def test_device_map_matches_oracle(name, scans):
+    sc = S.scenarios()[name]
+    a, pa = S.run(OracleEngine, sc, *scans)
+    b, pb = S.run(DeviceEngine, sc, *scans)
+    same_state(a, b)
+    assert pa == pb
+
+
+def test_unsupported_modes_fail_loudly(scans):
+    from roborts_csm.gridmap import COUNT_CELL, GridMapError, OccuGridMap
+    pts, poses = scans
+    m = OccuGridMap(0.05, (200, 200), (5.0, 5.0), 0.15, 0.3)
+    m.set_options(True, False, 0.88, 0.2)  # full update + blur: order-dependent, unused by the reference
+    with pytest.raises(GridMapError):
+        m.UpdateMapByRange(pts[0], poses[0], use_blur=True)
+    c = OccuGridMap(0.05, (200, 200), (5.0, 5.0), 0.15, 0.5, kind=COUNT_CELL)
+    c.set_options(True, True, 0.88, 0.2)
+    with pytest.raises(GridMapError):
+        c.UpdateMapByRange(pts[0], poses[0], use_blur=True)
+
+
+def _fine_map_stream(n_scans, seed=11):
+    """1081-beam scans along a path, in 1 cm cells (fine_map_resolution 0.01)."""
+    from roborts_csm import worlds
+    w = worlds.make_world(400, 400, 0.05, seed=seed)
+    laser = worlds.LaserSpec()
+    rng = np.random.default_rng(seed)
+    p0 = worlds.sample_free_poses(w, 1, rng, clearance_m=1.0)[0]
+    poses = np.array([[p0[0] + 0.1 * k * math.cos(p0[2]), p0[1] + 0.1 * k * math.sin(p0[2]),
+                       p0[2] + 0.02 * k] for k in range(n_scans)])
+    rngs = worlds.raycast_ranges(w, poses, laser)
+    return [worlds.scan_points(rngs[k], laser) * (1 / 0.01) for k in range(n_scans)], poses
+
+
+def test_fine_scan_match_map_full_size():
+    """Front-end fine ScanMatchMap as CreateAllMap builds it (slam_processor.cpp:
+    466-510: 3*range_max at 0.01 m = 3000 x 3000 cells, sigma 0.03, offset 0.88,
+    auto-resize, just_update_occu) fed a scan stream, then the back-end reset
+    path (ResetScanMatchMapWithRangeVec :448-462)."""
+    scans, poses = _fine_map_stream(6)
+    sc = dict(kind=0, res=0.01, size=(3000, 3000), off=None, dev=0.03, default=0.3,
+              opts=(True, True, 0.88, 0.2), cell=None, ops=[("update", k, True) for k in range(4)]
+              + [("opts", (False, True, 0.88, 0.2)), ("offset", "shift"), ("init", [3, 4, 5], True, True)])
+    sc["off"] = "centre"
+    a, _ = S.run(OracleEngine, sc, scans, poses)
+    b, _ = S.run(DeviceEngine, sc, scans, poses)
+    same_state(a, b)
+
+
+def test_matcher_reads_device_map():
+    """csm_set_grid_gridmap: the 3-level match on the device map equals the
+    oracle's match on the same cells."""
+    import pyoracle as O
+    import roborts_csm
+    from roborts_csm.gridmap import OccuGridMap, set_matcher_grid
+    from roborts_csm.params import SIM_YAML_LEVELS
+    scans, poses = _fine_map_stream(4)
+    res = 0.01
+    off = (-(poses[0][0] - 0.5 * 1500 * res), -(poses[0][1] - 0.5 * 1500 * res))
+    m = OccuGridMap(res, (1500, 1500), off, 0.03, 0.3)
+    m.set_options(True, True, 0.88, 0.2)
+    drawn = [m.UpdateMapByRange(scans[k], poses[k], use_blur=True) for k in range(3)]
+    assert any(drawn)  # a scan that makes the map grow is not drawn (occu_grid_map.h:294-298)
+    st = m.state()
+    prob = m.cells()[0]
+    init = poses[3] + np.array([0.03, -0.02, 0.02])
+    with roborts_csm.Context(0) as ctx:
+        set_matcher_grid(ctx, m)
+        pose = init.copy()
+        cov = np.eye(3).reshape(9).copy()
+        s = ctx.scan_matchers(scans[3], SIM_YAML_LEVELS, pose, cov)
+    om = O.Map(prob, st.resolution, (st.offset_x, st.offset_y), st.map_update_index)
+    s2, pose2, cov2 = O.scan_matchers(om, scans[3], SIM_YAML_LEVELS, init, np.eye(3))
+    assert s == s2 and np.array_equal(pose, pose2) and np.array_equal(cov, cov2)
