@@ -206,6 +206,83 @@ def willow_bench(args, rank, world_size, dist, torch):
     }
 
 
+def online_bench(args, rank, world_size, dist, torch):
+    """Config 5: a 40 Hz-style 1081-beam scan stream through the
+    device-resident front-end (include/csm_frontend.h: SlamProcessor::process
+    with the 3-level match on the 1 cm fine map, the PubMap check and the
+    three map updates; config/simulatin_param.yaml settings). One step = one
+    scan; the maps grow as the drive leaves the initial 30 m square. Replicas
+    only (one independent robot per rank)."""
+    from roborts_csm import worlds
+    from roborts_csm.frontend import CsmFrontendResult, FrontEndParam, SlamFrontEnd
+    n = args.warmup + args.steps
+    world = worlds.make_world(2000, 2000, 0.05, seed=20261015)
+    stream = worlds.make_scan_stream(world, n, seed=77 + rank)
+    fe = SlamFrontEnd(FrontEndParam(), device=int(os.environ.get("LOCAL_RANK", "0")))
+    for k in range(args.warmup):
+        fe.process(stream.points_m[k], stream.odom_poses[k])
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    lat = []
+    err = []
+    t0 = time.perf_counter()
+    for k in range(args.warmup, n):
+        t = time.perf_counter()
+        r = fe.process(stream.points_m[k], stream.odom_poses[k])
+        lat.append(time.perf_counter() - t)
+        err.append(r.pose)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    lat_ms = np.array(lat) * 1e3
+    # pose error against the drive (the SLAM frame is the first scan's pose)
+    t0p = stream.true_poses[0]
+    c, s = math.cos(-t0p[2]), math.sin(-t0p[2])
+    d = stream.true_poses[args.warmup:n] - t0p
+    rel = np.stack([c * d[:, 0] - s * d[:, 1], s * d[:, 0] + c * d[:, 1]], 1)
+    perr = np.linalg.norm(np.array(err)[:, :2] - rel, axis=1)
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu:
+        import pyoracle as O
+        ofe = O.FrontEnd(FrontEndParam().to_c())
+        tc = time.perf_counter()
+        m = 0
+        while m < n and (m < args.warmup + 2 or time.perf_counter() - tc < args.cpu_seconds):
+            if m == args.warmup:
+                tc2 = time.perf_counter()
+            ofe.process(stream.points_m[m], stream.odom_poses[m], CsmFrontendResult())
+            m += 1
+        dtc = time.perf_counter() - tc2
+        cpu = {"value": (m - args.warmup) / dtc, "unit": "scans/s", "cores": 1, "kind": "port",
+               "sample": f"scans {args.warmup}..{m - 1} of the same stream through the oracle's restatement "
+                         f"of the front-end (oracle/map_oracle.cpp), single-threaded, {dtc:.1f} s on {_cpu_model()}"}
+    return {
+        "metric": "front-end scans/sec (config 5 online: 1081-beam stream, 3-level match + map check + 3 map "
+                  "updates)",
+        "value": world_size * args.steps / elapsed, "unit": "scans/s", "n_gpus": world_size,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic drive (roborts_csm.worlds.make_scan_stream) in the seeded 2000x2000 @5cm world; "
+                "ray-cast 1081-beam Hokuyo scans, noisy odometry",
+        "config": {"workload": "config5: online front-end, simulatin_param.yaml (fine map 1 cm, coarse 8 cm, "
+                               "PubMap 5 cm, U=100)", "parallelism": f"replicas x{world_size}",
+                   "latency_ms": {"mean": float(lat_ms.mean()), "p50": float(np.median(lat_ms)),
+                                  "p99": float(np.percentile(lat_ms, 99)), "max": float(lat_ms.max())},
+                   "rate_40hz_headroom": float(world_size * args.steps / elapsed / 40.0),
+                   "median_pose_error_m": float(np.median(perr)), "max_pose_error_m": float(perr.max())},
+        "roofline": None, "cpu_baseline": cpu,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,8 +291,9 @@ def main():
     ap.add_argument("--scans", type=int, default=4096, help="scans per GPU per step")
     ap.add_argument("--levels", choices=["headline", "sim"], default="headline",
                     help="headline: every beam summed (B=1081); sim: reference YAML U=100 (B=109)")
-    ap.add_argument("--workload", choices=["config2", "loop_closure", "willow"], default="config2",
-                    help="config2: the headline front-end batch; loop_closure: config 3; willow: config 4")
+    ap.add_argument("--workload", choices=["config2", "loop_closure", "willow", "online"], default="config2",
+                    help="config2: the headline front-end batch; loop_closure: config 3; willow: config 4; "
+                         "online: config 5 (steps = scans)")
     ap.add_argument("--window-m", type=float, default=20.0, help="willow: window edge (m)")
     ap.add_argument("--submaps", type=int, default=512, help="loop_closure: submaps in total")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -239,8 +317,8 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
 
-    if args.workload in ("loop_closure", "willow"):
-        fn = loop_closure_bench if args.workload == "loop_closure" else willow_bench
+    if args.workload in ("loop_closure", "willow", "online"):
+        fn = {"loop_closure": loop_closure_bench, "willow": willow_bench, "online": online_bench}[args.workload]
         out = fn(args, rank, world_size, dist, torch)
         if rank == 0:
             print(json.dumps(out))

@@ -1,0 +1,94 @@
+/*
+ * csm_frontend.h — C-ABI of the device-resident SLAM front-end: one call per
+ * laser scan runs the reference's SlamProcessor::process front-end
+ * (slam/slam_processor.cpp:66-258) with every map and the scan matcher on the
+ * GPU. It is what BASELINE config 5 ("online mode: scan stream against a
+ * growing map") measures; the pose-graph back-end is out of scope (SURVEY.md
+ * 8f), so loop closure and map correction are not run.
+ *
+ * Per scan (reference lines):
+ *   - first scan: CreateAllMap (slam_processor.cpp:466-524) makes the PubMap
+ *     (CountCell) and the coarse and fine ScanMatchMaps; the pose starts at 0;
+ *   - later scans: the odometry prediction (PredictPoseByOdom :606-621), the
+ *     3-level correlative match on the fine map with MapSizeCheck on both maps
+ *     (ScanMatchers::ScanMatch, scan_matchers.h:179-289, use_optimize_scan_match
+ *     = false as in both reference YAMLs), the map check on the PubMap
+ *     (MapCheckPenalize :569-593 -> MapFeedbackResponsePenalty) and the
+ *     score gate on the pose (:166-186);
+ *   - every scan: UpdateMap (:527-567) draws the scan into the three maps when
+ *     the score passes (always for the first scan).
+ * Results equal the reference's sequential code bit for bit (tested against
+ * the oracle's restatement of the same loop).
+ *
+ * Threading: one caller at a time per front-end (the reference serialises the
+ * front-end in its ROS callback).
+ */
+#ifndef ROBORTS_CSM_FRONTEND_H
+#define ROBORTS_CSM_FRONTEND_H
+
+#include <stdint.h>
+
+#include "csm.h"
+#include "csm_gridmap.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The ParamConfig fields the front-end reads (param_config.h:40-118); the
+ * default values of config/simulatin_param.yaml are in roborts_csm.frontend. */
+typedef struct csm_frontend_param {
+  double range_max;                /* laser range_max (m): map sizes, MapSizeCheck  */
+  double init_map_size;            /* x range_max (kMinMapSize = 3 floor)           */
+  double map_offset_x, map_offset_y;
+  double map_extend_factor;
+  double gaussian_blur_offset;
+  double map_resolution;           /* PubMap                                        */
+  double map_update_free_factor, map_update_occu_factor;
+  double map_occu_threshold, map_min_passthrough;
+  double coarse_map_resolution, coarse_map_deviation;
+  double fine_map_resolution, fine_map_deviation;
+  int32_t coarse_map_use_blur, fine_map_use_blur;
+  int32_t use_odometry;
+  int32_t use_map_check_feedback;
+  int32_t map_check_point_num;
+  int32_t use_map_update_move_check;
+  double map_check_bound_tolerance, map_check_penalty_gain;
+  double map_update_score_threshold, map_update_distance_threshold, map_update_angle_threshold;
+  csm_param levels[3];             /* coarse, fine, super-fine correlative windows  */
+} csm_frontend_param;
+
+/* What one processed scan produced. */
+typedef struct csm_frontend_result {
+  double pose[3];         /* current_sensor_pose_ after the scan (world)            */
+  double match_pose[3];   /* the matcher's pose (before the score gate)              */
+  double cov[9];          /* process_cov_matrix                                      */
+  double score;           /* scan_match_score_ after the map check                   */
+  double map_penalty;     /* MapCheckPenalize result (1 when not run)                */
+  int32_t data_index;     /* current_data_index_ of the scan                          */
+  int32_t matched;        /* 0 for the first scan                                     */
+  int32_t map_updated;    /* UpdateMap drew the scan (it is kept)                     */
+  int32_t pose_accepted;  /* the score gate took the matched pose                     */
+} csm_frontend_result;
+
+enum csm_frontend_map { CSM_PUB_MAP = 0, CSM_COARSE_MAP = 1, CSM_FINE_MAP = 2 };
+
+typedef struct csm_frontend csm_frontend;
+
+int csm_frontend_create(int device, const csm_frontend_param* param, csm_frontend** out);
+int csm_frontend_destroy(csm_frontend* fe);
+const char* csm_frontend_last_error(const csm_frontend* fe);
+/* One scan: points_xy are the sensor-frame endpoints in metres
+ * (RangeDataContainer before CreateFrom); odom_pose the odometry pose read
+ * with the scan (used when use_odometry). */
+int csm_frontend_process(csm_frontend* fe, const double* points_xy, int32_t n_points, const double odom_pose[3],
+                         csm_frontend_result* result);
+/* Borrow one of the front-end's maps (owned by the front-end; null before the
+ * first scan). */
+int csm_frontend_map(csm_frontend* fe, int32_t which, csm_gridmap** map);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ROBORTS_CSM_FRONTEND_H */

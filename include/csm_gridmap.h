@@ -23,6 +23,8 @@
  *                             SetOccuThreshold / SetMinPassThrough  occu_grid_map.h:413-427
  *   csm_gridmap_set_map_offset   GridMapBase::set_map_offset  grid_map_base.h:275-279
  *   csm_gridmap_reset         GridMapBase::Reset               grid_map_base.h:95-103
+ *   csm_gridmap_update_bound  GridMapBase::UpdateBound (may ExtendSize)  grid_map_base.h:247-264
+ *                             (called by ScanMatchers::MapSizeCheck, scan_matchers.h:365-390)
  *   csm_gridmap_update_by_range  OccuGridMap::UpdateMapByRange occu_grid_map.h:258-329
  *   csm_gridmap_init_with_range_vec  OccuGridMap::InitMapWithRangeVec  occu_grid_map.h:222-255
  *                             (with use_reset_speedup: ResetValueSpeedup grid_map_base.h:112-117)
@@ -79,6 +81,7 @@ typedef struct csm_gridmap_state {
   int32_t blur_states;
   int32_t kind;             /* enum csm_cell_kind                                */
   int32_t reserved;
+  double scale_factor;      /* scale_factor_ = 1/resolution as constructed         */
 } csm_gridmap_state;
 
 int csm_gridmap_create(int device, int32_t kind, double resolution, int32_t size_x, int32_t size_y,
@@ -94,6 +97,9 @@ int csm_gridmap_set_cell_params(csm_gridmap* map, float update_free_factor, floa
                                 float occu_threshold, float min_pass);
 int csm_gridmap_set_map_offset(csm_gridmap* map, double offset_x, double offset_y);
 int csm_gridmap_reset(csm_gridmap* map);
+/* *inside = UpdateBound's return value (0: the map grew to hold the box). */
+int csm_gridmap_update_bound(csm_gridmap* map, double min_x, double min_y, double max_x, double max_y,
+                             int32_t* inside);
 
 /* *updated = UpdateMapByRange's return value (0 when the scan made the map grow). */
 int csm_gridmap_update_by_range(csm_gridmap* map, const double* points_xy, int32_t n_points,

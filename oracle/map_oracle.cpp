@@ -616,3 +616,224 @@ int oracle_bresenham(int x0, int y0, int x1, int y1, int32_t* out, int cap) {
 }
 
 }  // extern "C"
+
+// ---- SlamProcessor::process front-end (slam/slam_processor.cpp:65-248) ---------
+// Test-infrastructure restatement of the loop include/csm_frontend.h runs on
+// the device; the matcher is this library's oracle_scan_matchers
+// (csm_oracle.cpp) reading the fine map's cells.
+
+extern "C" {
+struct oracle_map_c {
+  const float* cells;
+  int64_t stride_floats;
+  int32_t size_x, size_y;
+  double resolution;
+  double offset_x, offset_y;
+  int32_t update_index;
+  float outside_value;
+};
+double oracle_scan_matchers(const oracle_map_c* mc, const double* pts, int n, const void* levels3, int use_fine,
+                            double pose[3], double cov[9]);
+}
+
+namespace {
+
+struct FeParam {  // layout of csm_frontend_param (include/csm_frontend.h)
+  double range_max, init_map_size, map_offset_x, map_offset_y, map_extend_factor, gaussian_blur_offset;
+  double map_resolution, map_update_free_factor, map_update_occu_factor, map_occu_threshold, map_min_passthrough;
+  double coarse_map_resolution, coarse_map_deviation, fine_map_resolution, fine_map_deviation;
+  int32_t coarse_map_use_blur, fine_map_use_blur, use_odometry, use_map_check_feedback, map_check_point_num,
+      use_map_update_move_check;
+  double map_check_bound_tolerance, map_check_penalty_gain;
+  double map_update_score_threshold, map_update_distance_threshold, map_update_angle_threshold;
+  struct Level {
+    double size, res, aoff, ares, thr;
+    int32_t use_point_size, max_depth, use_center_penalty, type;
+  } levels[3];
+};
+
+struct FeResult {  // layout of csm_frontend_result
+  double pose[3], match_pose[3], cov[9], score, map_penalty;
+  int32_t data_index, matched, map_updated, pose_accepted;
+};
+
+struct OFrontEnd {
+  FeParam p;
+  std::unique_ptr<OMap> maps[3];
+  int data_index = 0;
+  double cur[3] = {0, 0, 0}, last_odom[3] = {0, 0, 0}, last_update[3] = {0, 0, 0};
+  double score = 0.0;
+  int penalize_times = 0;
+};
+
+double norm_angle(double a) {  // util::NormalizeAngle (util/slam_util.h:103-111)
+  double n = std::fmod(std::fmod(a, 2.0 * M_PI) + 2.0 * M_PI, 2.0 * M_PI);
+  if (n > M_PI) n -= 2.0 * M_PI;
+  return n;
+}
+
+std::unique_ptr<OMap> make_map(int kind, double res, int sz, double ox, double oy, double dev, float dflt) {
+  auto m = std::make_unique<OMap>();
+  m->kind = kind;
+  m->scale_factor = 1.0 / res;
+  m->off_x = ox;
+  m->off_y = oy;
+  m->default_prob = dflt;
+  if (kind == kCountCell) {
+    m->free_factor = 0.0f;
+    m->occu_factor = 0.0f;
+    m->occu_threshold = 0.5f;
+    m->min_pass = 2.0f;
+  }
+  allocate(*m, sz, sz);
+  m->row = m->size_x;
+  init_kernel(*m, dev, res);
+  return m;
+}
+
+}  // namespace
+
+extern "C" {
+
+void* oracle_frontend_create(const void* param) {
+  auto* f = new OFrontEnd();
+  std::memcpy(&f->p, param, sizeof(FeParam));
+  return f;
+}
+void oracle_frontend_destroy(void* h) { delete static_cast<OFrontEnd*>(h); }
+int oracle_frontend_param_size(void) { return (int)sizeof(FeParam); }
+int oracle_frontend_result_size(void) { return (int)sizeof(FeResult); }
+void* oracle_frontend_map(void* h, int which) { return static_cast<OFrontEnd*>(h)->maps[which].get(); }
+
+int oracle_frontend_process(void* h, const double* pts, int n, const double odom[3], void* result) {
+  OFrontEnd& f = *static_cast<OFrontEnd*>(h);
+  const FeParam& p = f.p;
+  FeResult r;
+  std::memset(&r, 0, sizeof(r));
+  const bool first = f.data_index == 0;
+  if (first) {  // CreateAllMap (:464-527)
+    const double rm = p.range_max;
+    const double ims = (p.init_map_size < 3.0) ? (3.0 * rm) : (p.init_map_size * rm);
+    const double ox = ims * p.map_offset_x, oy = ims * p.map_offset_y;
+    f.maps[0] = make_map(kCountCell, p.map_resolution, (int)(ims / p.map_resolution), ox, oy, 0.0, 0.5f);
+    f.maps[1] = make_map(kProbabilityCell, p.coarse_map_resolution, (int)(ims / p.coarse_map_resolution), ox, oy,
+                         p.coarse_map_deviation, 0.3f);
+    f.maps[2] = make_map(kProbabilityCell, p.fine_map_resolution, (int)(ims / p.fine_map_resolution), ox, oy,
+                         p.fine_map_deviation, 0.3f);
+    for (int k = 0; k < 3; ++k) {
+      if (p.map_extend_factor > 0) f.maps[k]->extend_factor = p.map_extend_factor;
+      f.maps[k]->auto_resize = true;
+      if (k > 0) {
+        f.maps[k]->occu_offset = p.gaussian_blur_offset;
+        f.maps[k]->just_update_occu = true;
+      }
+    }
+    f.cur[0] = f.cur[1] = f.cur[2] = 0.0;
+  }
+  double predict[3] = {f.cur[0], f.cur[1], f.cur[2]};
+  std::vector<double> pp((size_t)2 * n), cp((size_t)2 * n), fp((size_t)2 * n);
+  const double fpub = 1 / p.map_resolution, fco = 1 / p.coarse_map_resolution, ffi = 1 / p.fine_map_resolution;
+  for (int i = 0; i < 2 * n; ++i) {
+    pp[(size_t)i] = pts[i] * fpub;
+    cp[(size_t)i] = pts[i] * fco;
+    fp[(size_t)i] = pts[i] * ffi;
+  }
+  double cov[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  r.map_penalty = 1.0;
+  if (!first) {
+    if (p.use_odometry) {  // PredictPoseByOdom (:618-635)
+      const double a = f.cur[2] - f.last_odom[2];
+      const double c = std::cos(a), s = std::sin(a);
+      const double tx = f.cur[0] - (c * f.last_odom[0] + (-s) * f.last_odom[1]);
+      const double ty = f.cur[1] - (s * f.last_odom[0] + c * f.last_odom[1]);
+      predict[0] = (c * odom[0] + (-s) * odom[1]) + tx;
+      predict[1] = (s * odom[0] + c * odom[1]) + ty;
+      predict[2] = a + odom[2];
+    }
+    double pose[3] = {predict[0], predict[1], predict[2]};
+    for (int k = 1; k <= 2; ++k) {  // MapSizeCheck (scan_matchers.h:365-390)
+      OMap& m = *f.maps[k];
+      double pm[3];
+      world_to_map(m, pose, pm);
+      const double mres = 1 / m.scale_factor;
+      const double max_size = (p.range_max + p.levels[0].size) / mres;
+      Box b;
+      b.minx = pm[0] - max_size;
+      b.miny = pm[1] - max_size;
+      b.maxx = pm[0] + max_size;
+      b.maxy = pm[1] + max_size;
+      update_bound(m, b);
+    }
+    OMap& fm = *f.maps[2];
+    oracle_map_c mc;
+    mc.cells = &fm.cells[0].prob;
+    mc.stride_floats = (int64_t)(sizeof(Cell) / sizeof(float));
+    mc.size_x = fm.size_x;
+    mc.size_y = fm.size_y;
+    mc.resolution = 1 / fm.scale_factor;
+    mc.offset_x = fm.off_x;
+    mc.offset_y = fm.off_y;
+    mc.update_index = fm.map_update_index;
+    mc.outside_value = 0.3f;
+    double score = oracle_scan_matchers(&mc, fp.data(), n, p.levels, 1, pose, cov);
+    std::memcpy(r.match_pose, pose, sizeof(pose));
+    double penalty = 1.0;
+    if (p.use_map_check_feedback)  // MapCheckPenalize (:573-595)
+      penalty = feedback_penalty(*f.maps[0], pp.data(), n, (const double[2]){0.0, 0.0}, pose, p.map_check_point_num,
+                                 p.map_check_bound_tolerance, p.map_check_penalty_gain, false);
+    r.map_penalty = penalty;
+    if (f.penalize_times < 5) {
+      score *= penalty;
+      score = (score > 1.0) ? (1.0) : (score);
+      if (penalty < 0.7)
+        f.penalize_times++;
+      else
+        f.penalize_times = 0;
+    } else {
+      f.penalize_times = 0;
+    }
+    if (score > std::max(0.5, p.map_update_score_threshold)) {
+      std::memcpy(f.cur, pose, sizeof(pose));
+      r.pose_accepted = 1;
+    }
+    f.score = score;
+    r.matched = 1;
+  }
+  bool updated = false;
+  const double dx = f.cur[0] - f.last_update[0], dy = f.cur[1] - f.last_update[1];
+  const bool moved = std::sqrt(dx * dx + dy * dy) >= p.map_update_distance_threshold ||
+                     std::fabs(norm_angle(f.cur[2] - f.last_update[2])) >= p.map_update_angle_threshold;
+  if ((f.score > p.map_update_score_threshold && (moved || !p.use_map_update_move_check)) || f.data_index < 1) {
+    OMap& pub = *f.maps[0];  // UpdateMap (:529-571)
+    if (first) {
+      pub.occu_threshold = 0.5f;
+      pub.min_pass = 1.0f;
+      pub.free_factor = (float)p.map_min_passthrough;
+      pub.occu_factor = (float)(p.map_min_passthrough * 2);
+    } else {
+      pub.occu_threshold = (float)p.map_occu_threshold;
+      pub.min_pass = (float)p.map_min_passthrough;
+      pub.free_factor = (float)p.map_update_free_factor;
+      pub.occu_factor = (float)p.map_update_occu_factor;
+    }
+    const double org[2] = {0.0, 0.0};
+    update_by_range(pub, pp.data(), n, org, f.cur, false);
+    update_by_range(*f.maps[1], cp.data(), n, org, f.cur, p.coarse_map_use_blur != 0);
+    update_by_range(*f.maps[2], fp.data(), n, org, f.cur, p.fine_map_use_blur != 0);
+    std::memcpy(f.last_update, f.cur, sizeof(f.cur));
+    updated = true;
+  }
+  r.data_index = f.data_index;
+  if (updated) {
+    f.data_index++;
+    std::memcpy(f.last_odom, odom, sizeof(f.last_odom));
+  }
+  std::memcpy(r.pose, f.cur, sizeof(r.pose));
+  std::memcpy(r.cov, cov, sizeof(cov));
+  r.score = f.score;
+  r.map_updated = updated ? 1 : 0;
+  std::memcpy(result, &r, sizeof(r));
+  return 0;
+}
+
+}  // extern "C"

@@ -322,3 +322,52 @@ def bresenham(x0, y0, x1, y1) -> np.ndarray:
     out = np.zeros(2 * cap, dtype=np.int32)
     n = _lib.oracle_bresenham(x0, y0, x1, y1, out.ctypes.data_as(_i32p), cap)
     return out[:2 * n].reshape(n, 2)
+
+
+# ---- SlamProcessor front-end (map_oracle.cpp oracle_frontend_*) ----------------
+for _k, (_r, _a) in {
+    "oracle_frontend_create": (C.c_void_p, [C.c_void_p]),
+    "oracle_frontend_destroy": (None, [C.c_void_p]),
+    "oracle_frontend_param_size": (C.c_int, []),
+    "oracle_frontend_result_size": (C.c_int, []),
+    "oracle_frontend_map": (C.c_void_p, [C.c_void_p, C.c_int]),
+    "oracle_frontend_process": (C.c_int, [C.c_void_p, _dp, C.c_int, _dp, C.c_void_p]),
+}.items():
+    _f = getattr(_lib, _k)
+    _f.restype, _f.argtypes = _r, _a
+
+
+class _FrontEndMap(GridMap):
+    def __init__(self, h, owner):  # borrowed OMap* (owned by the front-end)
+        self.h = h
+        self._owner = owner
+
+    def __del__(self):
+        pass
+
+
+class FrontEnd:
+    """Oracle SlamProcessor front-end; param / result are ctypes structures with
+    the csm_frontend_param / csm_frontend_result layouts."""
+
+    def __init__(self, c_param):
+        assert _lib.oracle_frontend_param_size() == C.sizeof(c_param)
+        self._p = c_param
+        self.h = _lib.oracle_frontend_create(C.byref(c_param))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            _lib.oracle_frontend_destroy(h)
+            self.h = None
+
+    def process(self, points_m, odom, result):
+        assert _lib.oracle_frontend_result_size() == C.sizeof(result)
+        p = _pts(points_m)
+        o = _d(odom)
+        _lib.oracle_frontend_process(self.h, p.ctypes.data_as(_dp), p.shape[0], o.ctypes.data_as(_dp),
+                                     C.byref(result))
+        return result
+
+    def map(self, which: int) -> GridMap:
+        return _FrontEndMap(_lib.oracle_frontend_map(self.h, which), self)

@@ -565,7 +565,7 @@ int ensure_int_grid(csm_ctx* c) {
   c->int_ok = false;
   const int64_t n = (int64_t)c->info.size_x * c->info.size_y * c->n_grids;
   hipError_t e;
-  if ((e = c->gstats.ensure(sizeof(csm::GridStats))) != hipSuccess) return c->hip_fail(e, "hipMalloc(stats)");
+  if ((e = c->gstats.ensure(sizeof(csm::GridStats) * (1 + csm::kAnalyzeBlocks))) != hipSuccess) return c->hip_fail(e, "hipMalloc(stats)");
   if ((e = csm::launch_analyze_grid(c->d_grid, n, (csm::GridStats*)c->gstats.p, c->stream)) != hipSuccess)
     return c->hip_fail(e, "analyze_grid_kernel");
   csm::GridStats st{};

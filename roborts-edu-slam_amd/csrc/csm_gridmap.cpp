@@ -543,6 +543,23 @@ int csm_gridmap_reset(csm_gridmap* m) {
   return finish(m);
 }
 
+int csm_gridmap_update_bound(csm_gridmap* m, double min_x, double min_y, double max_x, double max_y,
+                             int32_t* inside) {
+  if (!m) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(m->mu);
+  DeviceGuard g(m->device);
+  Box b;
+  b.minx = min_x;
+  b.miny = min_y;
+  b.maxx = max_x;
+  b.maxy = max_y;
+  bool grown = false;
+  int st = update_bound(m, b, &grown);
+  if (st != CSM_OK) return st;
+  if (inside) *inside = grown ? 0 : 1;
+  return finish(m);
+}
+
 int csm_gridmap_update_by_range(csm_gridmap* m, const double* pts, int32_t n, const double origin[2],
                                 const double pose[3], int32_t use_blur, int32_t* updated) {
   if (!m || !pose || (n > 0 && !pts) || n < 0) return CSM_ERR_INVALID_ARG;
@@ -674,6 +691,7 @@ int csm_gridmap_get_state(csm_gridmap* m, csm_gridmap_state* o) {
   o->blur_states = m->blur_states ? 1 : 0;
   o->kind = m->kind;
   o->reserved = 0;
+  o->scale_factor = m->scale_factor;
   return CSM_OK;
 }
 

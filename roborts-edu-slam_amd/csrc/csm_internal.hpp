@@ -198,6 +198,8 @@ struct GridStats {
   int32_t nonfinite;
   int32_t pad;
 };
+// d_stats: 1 + kAnalyzeBlocks entries (result, then per-block partials).
+constexpr int kAnalyzeBlocks = 1024;
 hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hipStream_t stream);
 // Row pitch of gridi is a multiple of 4 cells, so 16-byte row segments are
 // aligned; size_y + kGridiPadRows rows are written, the pad zero.

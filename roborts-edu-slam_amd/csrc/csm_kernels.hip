@@ -1048,8 +1048,11 @@ namespace csm {
 namespace {
 
 // Per cell: finite? smallest power of two the value is a multiple of, and |v|.
+// Pass 1: each block reduces its cells in registers, then across its waves in
+// LDS, and writes one partial (no atomics: thousands of same-address atomics
+// serialised the old version at ~0.3 ms for a 3000 x 3000 map).
 __global__ __launch_bounds__(256) void analyze_grid_kernel(const float* __restrict__ g, int64_t n,
-                                                           GridStats* __restrict__ st) {
+                                                           GridStats* __restrict__ partials) {
   int min_g = INT32_MAX;
   uint32_t max_bits = 0;
   int bad = 0;
@@ -1072,10 +1075,48 @@ __global__ __launch_bounds__(256) void analyze_grid_kernel(const float* __restri
     max_bits = max(max_bits, (uint32_t)__shfl_down((int)max_bits, off, 64));
     bad |= __shfl_down(bad, off, 64);
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicMin(&st->min_gexp, min_g);
-    atomicMax(&st->max_abs_bits, max_bits);
-    atomicOr(&st->nonfinite, bad);
+  __shared__ GridStats w[4];
+  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = GridStats{min_g, max_bits, bad, 0};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    GridStats r = w[0];
+    for (int k = 1; k < 4; ++k) {
+      r.min_gexp = min(r.min_gexp, w[k].min_gexp);
+      r.max_abs_bits = max(r.max_abs_bits, w[k].max_abs_bits);
+      r.nonfinite |= w[k].nonfinite;
+    }
+    partials[blockIdx.x] = r;
+  }
+}
+
+// Pass 2: one block folds the partials into st[0].
+__global__ __launch_bounds__(256) void analyze_reduce_kernel(const GridStats* __restrict__ partials, int np,
+                                                             GridStats* __restrict__ st) {
+  int min_g = INT32_MAX;
+  uint32_t max_bits = 0;
+  int bad = 0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) {
+    const GridStats p = partials[i];
+    min_g = min(min_g, p.min_gexp);
+    max_bits = max(max_bits, p.max_abs_bits);
+    bad |= p.nonfinite;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    min_g = min(min_g, __shfl_down(min_g, off, 64));
+    max_bits = max(max_bits, (uint32_t)__shfl_down((int)max_bits, off, 64));
+    bad |= __shfl_down(bad, off, 64);
+  }
+  __shared__ GridStats w[4];
+  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = GridStats{min_g, max_bits, bad, 0};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    GridStats r = w[0];
+    for (int k = 1; k < 4; ++k) {
+      r.min_gexp = min(r.min_gexp, w[k].min_gexp);
+      r.max_abs_bits = max(r.max_abs_bits, w[k].max_abs_bits);
+      r.nonfinite |= w[k].nonfinite;
+    }
+    st[0] = r;
   }
 }
 
@@ -1097,12 +1138,10 @@ __global__ __launch_bounds__(256) void fixed_point_kernel(const float* __restric
 }  // namespace
 
 hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hipStream_t stream) {
-  const GridStats init{INT32_MAX, 0u, 0, 0};
-  hipError_t e = hipMemcpyAsync(d_stats, &init, sizeof(GridStats), hipMemcpyHostToDevice, stream);
-  if (e != hipSuccess) return e;
-  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
-  hipLaunchKernelGGL(analyze_grid_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0,
-                     stream, g, n, d_stats);
+  // d_stats holds 1 + kAnalyzeBlocks entries: the result, then the partials
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, kAnalyzeBlocks));
+  hipLaunchKernelGGL(analyze_grid_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, g, n, d_stats + 1);
+  hipLaunchKernelGGL(analyze_reduce_kernel, dim3(1), dim3(256), 0, stream, d_stats + 1, (int)blocks, d_stats);
   return hipGetLastError();
 }
 

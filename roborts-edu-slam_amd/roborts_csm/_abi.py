@@ -32,9 +32,12 @@ EXPORTED = (
     # include/csm_gridmap.h
     "csm_gridmap_create", "csm_gridmap_destroy", "csm_gridmap_last_error",
     "csm_gridmap_set_options", "csm_gridmap_set_cell_params", "csm_gridmap_set_map_offset",
-    "csm_gridmap_reset", "csm_gridmap_update_by_range", "csm_gridmap_init_with_range_vec",
+    "csm_gridmap_reset", "csm_gridmap_update_bound", "csm_gridmap_update_by_range", "csm_gridmap_init_with_range_vec",
     "csm_gridmap_feedback_penalty", "csm_gridmap_get_state", "csm_gridmap_download",
     "csm_gridmap_device_prob", "csm_set_grid_gridmap",
+    # include/csm_frontend.h
+    "csm_frontend_create", "csm_frontend_destroy", "csm_frontend_last_error", "csm_frontend_process",
+    "csm_frontend_map",
 )
 
 PROBABILITY_CELL, COUNT_CELL = 0, 1
@@ -107,6 +110,7 @@ class CsmGridmapState(C.Structure):
         ("blur_states", C.c_int32),
         ("kind", C.c_int32),
         ("reserved", C.c_int32),
+        ("scale_factor", C.c_double),
     ]
 
 
@@ -148,6 +152,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_gridmap_set_cell_params": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_float]),
         "csm_gridmap_set_map_offset": (C.c_int, [C.c_void_p, C.c_double, C.c_double]),
         "csm_gridmap_reset": (C.c_int, [C.c_void_p]),
+        "csm_gridmap_update_bound": (C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_double, C.c_double, _i32p]),
         "csm_gridmap_update_by_range": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, _dp, C.c_int32, _i32p]),
         "csm_gridmap_init_with_range_vec": (C.c_int, [C.c_void_p, C.c_int32, _dp, _i64p, _dp, _dp, C.c_int32,
                                                       C.c_int32]),
@@ -158,6 +163,11 @@ def _bind(lib: C.CDLL) -> C.CDLL:
                                            C.c_void_p]),
         "csm_gridmap_device_prob": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
         "csm_set_grid_gridmap": (C.c_int, [_ctx, C.c_void_p]),
+        "csm_frontend_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
+        "csm_frontend_destroy": (C.c_int, [C.c_void_p]),
+        "csm_frontend_last_error": (C.c_char_p, [C.c_void_p]),
+        "csm_frontend_process": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, C.c_void_p]),
+        "csm_frontend_map": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

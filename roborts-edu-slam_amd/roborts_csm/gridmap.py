@@ -95,6 +95,13 @@ class OccuGridMap:
     def Reset(self):
         self._check(_lib.csm_gridmap_reset(self._h))
 
+    def UpdateBound(self, min_bound, max_bound) -> bool:
+        """GridMapBase::UpdateBound (grid_map_base.h:247-264); False when the map grew."""
+        inside = C.c_int32(0)
+        self._check(_lib.csm_gridmap_update_bound(self._h, float(min_bound[0]), float(min_bound[1]),
+                                                  float(max_bound[0]), float(max_bound[1]), C.byref(inside)))
+        return bool(inside.value)
+
     # -- reference entry points -------------------------------------------------
     def UpdateMapByRange(self, points_cells, sensor_pose, use_blur: bool = False, origin=(0.0, 0.0)) -> bool:
         pts = _d(points_cells, (-1, 2))

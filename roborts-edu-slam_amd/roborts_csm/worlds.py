@@ -293,6 +293,63 @@ def make_scan_batch(world: World, n_scans: int, seed: int = 20261015, laser: Las
                      np.ascontiguousarray(init))
 
 
+@dataclass
+class ScanStream:
+    """A robot run for the online front-end (BASELINE config 5): per scan the
+    sensor-frame endpoints in metres (before CreateFrom), the true pose and the
+    odometry pose read with it."""
+
+    points_m: list
+    true_poses: np.ndarray   # [S,3] world
+    odom_poses: np.ndarray   # [S,3] odometry frame (drifting)
+
+
+def make_scan_stream(world: World, n_scans: int, seed: int = 20261015, laser: LaserSpec = None,
+                     step_m: float = 0.05, turn_rad: float = 0.02, clearance_m: float = 0.8,
+                     odom_noise=(0.004, 0.002)) -> ScanStream:
+    """A collision-free drive of n_scans steps (step_m per scan, 2 m/s at 40 Hz
+    for 0.05) with a slowly wandering heading; the robot turns away when the
+    distance transform says a wall is near. Odometry integrates the true
+    increments with multiplicative noise (odom_noise = translation, rotation)."""
+    laser = laser or LaserSpec()
+    rng = np.random.default_rng(seed)
+    edt = _edt(world.wall)
+    res = world.resolution
+    H, W = edt.shape
+
+    def clear(p):
+        cx = int(round((p[0] + world.offset[0]) / res))
+        cy = int(round((p[1] + world.offset[1]) / res))
+        return 0 <= cx < W and 0 <= cy < H and edt[cy, cx] * res > clearance_m
+
+    pose = sample_free_poses(world, 1, rng, clearance_m=1.5, edt=edt)[0]
+    poses = [pose.copy()]
+    while len(poses) < n_scans:
+        th = pose[2] + rng.normal(0.0, turn_rad)
+        for k in range(64):
+            cand = np.array([pose[0] + step_m * math.cos(th), pose[1] + step_m * math.sin(th), th])
+            if clear(cand):
+                break
+            th = pose[2] + (0.15 * (k + 1) if k % 2 == 0 else -0.15 * (k + 1))
+        else:
+            cand = np.array([pose[0], pose[1], pose[2] + 0.3])
+        pose = cand
+        poses.append(pose.copy())
+    true = np.array(poses)
+    odom = np.zeros_like(true)
+    for k in range(1, n_scans):
+        d = true[k] - true[k - 1]
+        c, s = math.cos(-true[k - 1, 2]), math.sin(-true[k - 1, 2])
+        lx, ly = c * d[0] - s * d[1], s * d[0] + c * d[1]  # increment in the robot frame
+        lx *= 1 + rng.normal(0, odom_noise[0] / max(step_m, 1e-9))
+        dth = d[2] * (1 + rng.normal(0, odom_noise[1] * 10))
+        oc, os_ = math.cos(odom[k - 1, 2]), math.sin(odom[k - 1, 2])
+        odom[k] = odom[k - 1] + np.array([oc * lx - os_ * ly, os_ * lx + oc * ly, dth])
+    rngs = raycast_ranges(world, true, laser, edt=edt)
+    pts = [scan_points(rngs[k], laser) for k in range(n_scans)]
+    return ScanStream(pts, true, odom)
+
+
 def hostile_grid(size_x: int, size_y: int, seed: int = 7) -> np.ndarray:
     """fp32 values spread over many binades (not exactly summable in fp64):
     only a kernel that keeps the reference's beam order stays bit-exact."""

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared():
     names = set()
-    for h in ("csm.h", "csm_gridmap.h"):
+    for h in ("csm.h", "csm_gridmap.h", "csm_frontend.h"):
         txt = open(os.path.join(ROOT, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         names |= set(re.findall(r"\b(csm_[a-z_0-9]+)\s*\(", txt))

@@ -1,0 +1,85 @@
+"""The online front-end (include/csm_frontend.h; SlamProcessor::process,
+slam/slam_processor.cpp:65-248; BASELINE config 5).
+
+CPU: the oracle's restatement of the loop tracks a ray-cast drive.
+GPU: the device front-end equals the oracle scan by scan (pose, matched pose,
+covariance, score, map penalty, gates) and in its three maps — bit for bit."""
+import math
+
+import numpy as np
+import pytest
+
+from roborts_csm import worlds
+
+
+def _stream(n, seed=3):
+    w = worlds.make_world(400, 400, 0.05, seed=seed)
+    return worlds.make_scan_stream(w, n, seed=seed)
+
+
+def _rel(true, k):
+    d = true[k] - true[0]
+    c, s = math.cos(-true[0, 2]), math.sin(-true[0, 2])
+    return np.array([c * d[0] - s * d[1], s * d[0] + c * d[1], d[2]])
+
+
+def test_oracle_frontend_tracks_drive():
+    import pyoracle as O
+    from roborts_csm.frontend import CsmFrontendResult, FrontEndParam
+    st = _stream(30)
+    fe = O.FrontEnd(FrontEndParam().to_c())
+    for k in range(30):
+        r = fe.process(st.points_m[k], st.odom_poses[k], CsmFrontendResult())
+        err = np.array(r.pose[:]) - _rel(st.true_poses, k)
+        assert abs(err[0]) < 0.02 and abs(err[1]) < 0.02 and abs(err[2]) < 0.01, (k, err)
+        assert r.map_updated
+
+
+@pytest.mark.gpu
+def test_device_frontend_matches_oracle():
+    import pyoracle as O
+    from map_engines import same_state
+    from roborts_csm.frontend import CsmFrontendResult, FrontEndParam, SlamFrontEnd
+    n = 24
+    st = _stream(n, seed=4)
+    prm = FrontEndParam()
+    ofe = O.FrontEnd(prm.to_c())
+    dfe = SlamFrontEnd(prm)
+    for k in range(n):
+        a = ofe.process(st.points_m[k], st.odom_poses[k], CsmFrontendResult())
+        b = dfe.process(st.points_m[k], st.odom_poses[k])
+        assert np.array_equal(np.array(a.pose[:]), b.pose), k
+        assert np.array_equal(np.array(a.match_pose[:]), b.match_pose), k
+        assert np.array_equal(np.array(a.cov[:]), b.cov), k
+        assert (a.score, a.map_penalty, a.data_index, bool(a.map_updated), bool(a.pose_accepted)) == \
+            (b.score, b.map_penalty, b.data_index, b.map_updated, b.pose_accepted), k
+
+    class _O:
+        def __init__(self, m):
+            self.m = m
+
+        def state(self):
+            i = self.m.info()
+            return {"size_x": i["size_x"], "size_y": i["size_y"], "map_update_index": i["map_update_index"],
+                    "cur_update_index": i["cur_update_index"], "offset": i["offset"], "bound": i["bound"]}
+
+        def arrays(self):
+            p, ps, h, u = self.m.cells()
+            return p, ps, h, u, self.m.touched().reshape(p.shape)
+
+    class _D:
+        def __init__(self, m):
+            self.m = m
+
+        def state(self):
+            s = self.m.state()
+            return {"size_x": s.size_x, "size_y": s.size_y, "map_update_index": s.map_update_index,
+                    "cur_update_index": s.cur_update_index, "offset": (s.offset_x, s.offset_y),
+                    "bound": (s.bound_min_x, s.bound_min_y, s.bound_max_x, s.bound_max_y)}
+
+        def arrays(self):
+            return self.m.cells()
+
+    for which in (0, 1, 2):
+        same_state(_O(ofe.map(which)), _D(dfe.map(which)))
+    dfe.close()
