@@ -25,6 +25,8 @@
  *   csm_best_window           same scoring, reduced on device to (max score, lowest flat index)
  *                             (large windows / loop-closure shards; no reference counterpart,
  *                             SURVEY.md 8e)
+ *   csm_optimize_scan_match   BasedOptimizeScanMatch::ScanMatch (Gauss-Newton)
+ *                                                        optimize_scan_matcher.h:68-221
  *   csm_scan_match with       BranchAndBoundCorrelateScanMatcher::ScanMatch (FAST type,
  *   type == CSM_FAST          dispatched from BasedCorrelationScanMatch::ScanMatch :815-821)
  *                                                        correlate_scan_matcher.h:274-502
@@ -184,6 +186,34 @@ int csm_load_scans(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
                    const int64_t* point_offsets);
 int csm_scan_matchers_loaded(csm_ctx* ctx, const csm_param levels[3], int32_t use_fine,
                              double* poses, double* covs, double* scores);
+
+/* --- Gauss-Newton scan matcher ---------------------- */
+/* OptimizeScanMatchParam (optimize_scan_matcher.h:33-58), filled by
+ * ScanMatchers::ScanMatchParamInit (scan_matchers.h:346-350). */
+typedef struct csm_optimize_param {
+  int32_t iterate_max_times;
+  int32_t reserved;
+  double cost_decrease_threshold;
+  double cost_min_threshold;
+  double max_update_distance;      /* m   */
+  double max_update_angle;         /* rad */
+} csm_optimize_param;
+
+/* BasedOptimizeScanMatch::ScanMatch (optimize_scan_matcher.h:68-132) on the
+ * current grid: Gauss-Newton on (x, y, theta) with the bilinear cell
+ * interpolation of UpdateCost (:154-221). points_xy as in csm_scan_match
+ * (cells of this grid, sensor frame); pose world in/out; *cost = the
+ * reference's return value. As the reference: an uninitialised map, an empty
+ * scan or a NaN step gives cost 1000 (kMaxCost) and leaves the pose untouched.
+ * Sums over points are the reference's sequential fp64 sums; cos/sin and the
+ * 3x3 LDLT solve (Eigen 3.3 restated) run on the host between iterations. */
+int csm_optimize_scan_match(csm_ctx* ctx, const double* points_xy, int32_t n_points,
+                            const csm_optimize_param* param, double pose[3], double* cost);
+/* n_scans independent scans on the same grid, one launch per iteration for
+ * all of them. iterations (nullable): UpdateCost evaluations per scan. */
+int csm_optimize_scan_match_batch(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
+                                  const int64_t* point_offsets, const csm_optimize_param* param,
+                                  double* poses, double* costs, int32_t* iterations);
 
 /* --- measurement ---------------------------------------------------------- */
 /* Turn HIP-event timing of every scoring launch on/off (resets the stats). */

@@ -9,10 +9,12 @@
  * Per scan (reference lines):
  *   - first scan: CreateAllMap (slam_processor.cpp:466-524) makes the PubMap
  *     (CountCell) and the coarse and fine ScanMatchMaps; the pose starts at 0;
- *   - later scans: the odometry prediction (PredictPoseByOdom :606-621), the
- *     3-level correlative match on the fine map with MapSizeCheck on both maps
- *     (ScanMatchers::ScanMatch, scan_matchers.h:179-289, use_optimize_scan_match
- *     = false as in both reference YAMLs), the map check on the PubMap
+ *   - later scans: the odometry prediction (PredictPoseByOdom :606-621),
+ *     ScanMatchers::ScanMatch (scan_matchers.h:179-289): MapSizeCheck on both
+ *     maps, optionally the Gauss-Newton matcher on the coarse map
+ *     (use_optimize_scan_match; both reference YAMLs set it false, ParamConfig
+ *     defaults it true) with the correlative coarse level as its fallback,
+ *     then fine and super-fine on the fine map; the map check on the PubMap
  *     (MapCheckPenalize :569-593 -> MapFeedbackResponsePenalty) and the
  *     score gate on the pose (:166-186);
  *   - every scan: UpdateMap (:527-567) draws the scan into the three maps when
@@ -56,6 +58,10 @@ typedef struct csm_frontend_param {
   double map_check_bound_tolerance, map_check_penalty_gain;
   double map_update_score_threshold, map_update_distance_threshold, map_update_angle_threshold;
   csm_param levels[3];             /* coarse, fine, super-fine correlative windows  */
+  int32_t use_optimize_scan_match; /* Gauss-Newton first, on the coarse map          */
+  int32_t reserved;
+  double optimize_failed_cost;     /* cost above which the correlative coarse runs   */
+  csm_optimize_param optimize;
 } csm_frontend_param;
 
 /* What one processed scan produced. */
@@ -65,6 +71,7 @@ typedef struct csm_frontend_result {
   double cov[9];          /* process_cov_matrix                                      */
   double score;           /* scan_match_score_ after the map check                   */
   double map_penalty;     /* MapCheckPenalize result (1 when not run)                */
+  double optimize_cost;   /* BasedOptimizeScanMatch cost (0 when not run)            */
   int32_t data_index;     /* current_data_index_ of the scan                          */
   int32_t matched;        /* 0 for the first scan                                     */
   int32_t map_updated;    /* UpdateMap drew the scan (it is kept)                     */

@@ -634,6 +634,10 @@ struct oracle_map_c {
 };
 double oracle_scan_matchers(const oracle_map_c* mc, const double* pts, int n, const void* levels3, int use_fine,
                             double pose[3], double cov[9]);
+double oracle_scan_match(const oracle_map_c* mc, const double* pts, int n, const void* param, double pose[3],
+                         double cov[9], int64_t* argmax_flat, int64_t* n_scored);
+double oracle_optimize_scan_match(const oracle_map_c* mc, const double* pts, int n, const void* param,
+                                  double pose[3], int* iterations);
 }
 
 namespace {
@@ -650,10 +654,16 @@ struct FeParam {  // layout of csm_frontend_param (include/csm_frontend.h)
     double size, res, aoff, ares, thr;
     int32_t use_point_size, max_depth, use_center_penalty, type;
   } levels[3];
+  int32_t use_optimize_scan_match, reserved;
+  double optimize_failed_cost;
+  struct Opt {  // csm_optimize_param
+    int32_t iterate_max_times, reserved;
+    double cost_decrease_threshold, cost_min_threshold, max_update_distance, max_update_angle;
+  } optimize;
 };
 
 struct FeResult {  // layout of csm_frontend_result
-  double pose[3], match_pose[3], cov[9], score, map_penalty;
+  double pose[3], match_pose[3], cov[9], score, map_penalty, optimize_cost;
   int32_t data_index, matched, map_updated, pose_accepted;
 };
 
@@ -689,6 +699,20 @@ std::unique_ptr<OMap> make_map(int kind, double res, int sz, double ox, double o
   m->row = m->size_x;
   init_kernel(*m, dev, res);
   return m;
+}
+
+oracle_map_c map_view(const OMap& m) {  // what oracle_scan_match* read of a ScanMatchMap
+  oracle_map_c mc;
+  mc.cells = &m.cells[0].prob;
+  mc.stride_floats = (int64_t)(sizeof(Cell) / sizeof(float));
+  mc.size_x = m.size_x;
+  mc.size_y = m.size_y;
+  mc.resolution = 1 / m.scale_factor;
+  mc.offset_x = m.off_x;
+  mc.offset_y = m.off_y;
+  mc.update_index = m.map_update_index;
+  mc.outside_value = 0.3f;
+  return mc;
 }
 
 }  // namespace
@@ -764,18 +788,31 @@ int oracle_frontend_process(void* h, const double* pts, int n, const double odom
       b.maxy = pm[1] + max_size;
       update_bound(m, b);
     }
-    OMap& fm = *f.maps[2];
-    oracle_map_c mc;
-    mc.cells = &fm.cells[0].prob;
-    mc.stride_floats = (int64_t)(sizeof(Cell) / sizeof(float));
-    mc.size_x = fm.size_x;
-    mc.size_y = fm.size_y;
-    mc.resolution = 1 / fm.scale_factor;
-    mc.offset_x = fm.off_x;
-    mc.offset_y = fm.off_y;
-    mc.update_index = fm.map_update_index;
-    mc.outside_value = 0.3f;
-    double score = oracle_scan_matchers(&mc, fp.data(), n, p.levels, 1, pose, cov);
+    const oracle_map_c mc = map_view(*f.maps[2]);
+    double score = 0.0;
+    if (!p.use_optimize_scan_match) {
+      score = oracle_scan_matchers(&mc, fp.data(), n, p.levels, 1, pose, cov);
+    } else {  // ScanMatchers::ScanMatch with the optimizer (scan_matchers.h:205-281)
+      const oracle_map_c cmc = map_view(*f.maps[1]);
+      double proc[3] = {pose[0], pose[1], pose[2]};
+      const double cost = oracle_optimize_scan_match(&cmc, cp.data(), n, &p.optimize, proc, nullptr);
+      r.optimize_cost = cost;
+      double sum = p.optimize_failed_cost / (cost + p.optimize_failed_cost);
+      int times = 1;
+      if (cost > p.optimize_failed_cost) {
+        sum = 0.0;
+        times--;
+        std::memcpy(proc, pose, sizeof(proc));
+        sum += oracle_scan_match(&mc, fp.data(), n, &p.levels[0], proc, cov, nullptr, nullptr);
+        times++;
+      }
+      for (int k = 1; k <= 2; ++k) {
+        sum += oracle_scan_match(&mc, fp.data(), n, &p.levels[k], proc, cov, nullptr, nullptr);
+        times++;
+      }
+      std::memcpy(pose, proc, sizeof(proc));
+      score = sum / times;
+    }
     std::memcpy(r.match_pose, pose, sizeof(pose));
     double penalty = 1.0;
     if (p.use_map_check_feedback)  // MapCheckPenalize (:573-595)

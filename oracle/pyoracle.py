@@ -371,3 +371,65 @@ class FrontEnd:
 
     def map(self, which: int) -> GridMap:
         return _FrontEndMap(_lib.oracle_frontend_map(self.h, which), self)
+
+
+# ---- BasedOptimizeScanMatch (opt_oracle.cpp) ----------------------------------
+class OracleOptParam(C.Structure):  # same layout as csm_optimize_param
+    _fields_ = [
+        ("iterate_max_times", C.c_int32),
+        ("reserved", C.c_int32),
+        ("cost_decrease_threshold", C.c_double),
+        ("cost_min_threshold", C.c_double),
+        ("max_update_distance", C.c_double),
+        ("max_update_angle", C.c_double),
+    ]
+
+
+for _k, (_r, _a) in {
+    "oracle_optimize_param_size": (C.c_int, []),
+    "oracle_optimize_scan_match": (C.c_double, [C.POINTER(OracleMap), _dp, C.c_int, C.c_void_p, _dp,
+                                                C.POINTER(C.c_int)]),
+    "oracle_optimize_update_cost": (C.c_double, [C.POINTER(OracleMap), _dp, C.c_int, _dp, _dp, _dp]),
+    "oracle_ldlt_solve": (None, [_dp, _dp, _dp]),
+}.items():
+    getattr(_lib, _k).restype = _r
+    getattr(_lib, _k).argtypes = _a
+assert _lib.oracle_optimize_param_size() == C.sizeof(OracleOptParam)
+
+
+def _op(param) -> OracleOptParam:
+    if isinstance(param, OracleOptParam):
+        return param
+    return OracleOptParam(int(param.iterate_max_times), 0, param.cost_decrease_threshold, param.cost_min_threshold,
+                          param.max_update_distance, param.max_update_angle)
+
+
+def optimize_scan_match(m: Map, points, param, pose):
+    """BasedOptimizeScanMatch::ScanMatch -> (cost, pose', iterations)."""
+    pts = _pts(points)
+    pose = np.array(pose, dtype=np.float64)
+    it = C.c_int(0)
+    p = _op(param)
+    cost = _lib.oracle_optimize_scan_match(C.byref(m.c), pts.ctypes.data_as(_dp), pts.shape[0], C.byref(p),
+                                           pose.ctypes.data_as(_dp), C.byref(it))
+    return cost, pose, it.value
+
+
+def optimize_update_cost(m: Map, points, est_map):
+    """One UpdateCost at a map-cell pose -> (normalised cost, H (3x3), b)."""
+    pts = _pts(points)
+    est = np.ascontiguousarray(est_map, dtype=np.float64)
+    H = np.zeros(9)
+    b = np.zeros(3)
+    c = _lib.oracle_optimize_update_cost(C.byref(m.c), pts.ctypes.data_as(_dp), pts.shape[0],
+                                         est.ctypes.data_as(_dp), H.ctypes.data_as(_dp), b.ctypes.data_as(_dp))
+    return c, H.reshape(3, 3), b
+
+
+def ldlt_solve(H, b):
+    """Eigen 3.3 LDLT<Matrix3d>::solve restated (lower triangle of H read)."""
+    h = np.ascontiguousarray(H, dtype=np.float64).reshape(9)
+    bb = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(3)
+    _lib.oracle_ldlt_solve(h.ctypes.data_as(_dp), bb.ctypes.data_as(_dp), x.ctypes.data_as(_dp))
+    return x

@@ -60,7 +60,8 @@ struct csm_frontend {
   int device = 0;
   csm_frontend_param p{};
   std::string err;
-  csm_ctx* ctx = nullptr;
+  csm_ctx* ctx = nullptr;         // matcher on the fine map
+  csm_ctx* ctx_coarse = nullptr;  // Gauss-Newton matcher on the coarse map (use_optimize_scan_match)
   csm_gridmap* maps[3] = {nullptr, nullptr, nullptr};
   int32_t data_index = 0;  // scans kept so far (SensorDataManager::current_data_index_ + 1)
   double current_pose[3] = {0, 0, 0};
@@ -125,6 +126,47 @@ int map_size_check(csm_frontend* f, csm_gridmap* m, const double* pose, double o
   return csm_gridmap_update_bound(m, cx - max_size, cy - max_size, cx + max_size, cy + max_size, &inside);
 }
 
+// ScanMatchers::ScanMatch after MapSizeCheck (scan_matchers.h:189-288): the
+// optional Gauss-Newton matcher on the coarse map, the correlative coarse
+// level when it is off or failed, then fine and super-fine; all correlative
+// levels on the fine map. Returns the mean response in *score.
+int scan_matchers(csm_frontend* f, int32_t n, double pose[3], double cov[9], double* score, double* opt_cost) {
+  const csm_frontend_param& p = f->p;
+  int st;
+  *opt_cost = 0.0;
+  if (!p.use_optimize_scan_match) {  // the three correlative levels in one call
+    if ((st = csm_scan_matchers(f->ctx, f->fine_pts.data(), n, p.levels, 1, pose, cov, score)) != CSM_OK)
+      return f->fail(st, std::string("csm_scan_matchers: ") + csm_last_error(f->ctx));
+    return CSM_OK;
+  }
+  double sum = 0.0, process[3] = {pose[0], pose[1], pose[2]}, cost = 0.0, resp = 0.0;
+  int times = 0;
+  if ((st = csm_set_grid_gridmap(f->ctx_coarse, f->maps[CSM_COARSE_MAP])) != CSM_OK ||
+      (st = csm_optimize_scan_match(f->ctx_coarse, f->coarse_pts.data(), n, &p.optimize, process, &cost)) != CSM_OK)
+    return f->fail(st, std::string("csm_optimize_scan_match: ") + csm_last_error(f->ctx_coarse));
+  *opt_cost = cost;
+  sum = p.optimize_failed_cost / (cost + p.optimize_failed_cost);  // :211
+  times++;
+  if (cost > p.optimize_failed_cost) {  // :224-242: optimisation failed
+    sum = 0.0;
+    times--;
+    std::memcpy(process, pose, sizeof(process));
+    if ((st = csm_scan_match(f->ctx, f->fine_pts.data(), n, &p.levels[0], process, cov, &resp, nullptr)) != CSM_OK)
+      return f->fail(st, std::string("csm_scan_match(coarse): ") + csm_last_error(f->ctx));
+    sum += resp;
+    times++;
+  }
+  for (int k = 1; k <= 2; ++k) {  // fine, super-fine (:247-261)
+    if ((st = csm_scan_match(f->ctx, f->fine_pts.data(), n, &p.levels[k], process, cov, &resp, nullptr)) != CSM_OK)
+      return f->fail(st, std::string("csm_scan_match: ") + csm_last_error(f->ctx));
+    sum += resp;
+    times++;
+  }
+  std::memcpy(pose, process, sizeof(process));
+  *score = sum / times;  // :281
+  return CSM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -138,7 +180,9 @@ int csm_frontend_create(int device, const csm_frontend_param* param, csm_fronten
   const char* tm = std::getenv("CSM_FE_TIMING");
   f->timing = tm && std::atoi(tm) != 0;
   int st = csm_create(device, &f->ctx);
+  if (st == CSM_OK && param->use_optimize_scan_match) st = csm_create(device, &f->ctx_coarse);
   if (st != CSM_OK) {
+    if (f->ctx) csm_destroy(f->ctx);
     delete f;
     return st;
   }
@@ -158,6 +202,7 @@ int csm_frontend_destroy(csm_frontend* f) {
   for (auto*& m : f->maps)
     if (m) csm_gridmap_destroy(m);
   if (f->ctx) csm_destroy(f->ctx);
+  if (f->ctx_coarse) csm_destroy(f->ctx_coarse);
   delete f;
   return CSM_OK;
 }
@@ -210,8 +255,7 @@ int csm_frontend_process(csm_frontend* f, const double* pts, int32_t n, const do
       return f->fail(st, std::string("csm_set_grid_gridmap: ") + csm_last_error(f->ctx));
     lap(2);
     double score = 0.0;
-    if ((st = csm_scan_matchers(f->ctx, f->fine_pts.data(), n, p.levels, 1, pose, cov, &score)) != CSM_OK)
-      return f->fail(st, std::string("csm_scan_matchers: ") + csm_last_error(f->ctx));
+    if ((st = scan_matchers(f, n, pose, cov, &score, &r->optimize_cost)) != CSM_OK) return st;
     std::memcpy(r->match_pose, pose, sizeof(pose));
     lap(3);
     // MapCheckPenalize (:573-595), use_logistic = false

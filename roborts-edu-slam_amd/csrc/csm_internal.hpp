@@ -205,6 +205,33 @@ hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hi
 // aligned; size_y + kGridiPadRows rows are written, the pad zero.
 hipError_t launch_fixed_point(const float* g, int32_t sx, int32_t sy, int32_t pitch, float outside,
                               int int_exp, int32_t* gi, hipStream_t stream);
+// ---- Gauss-Newton scan matcher (csm_optimize.hip) --------------------------
+// Per scan and iteration: the pose in map cells and the host glibc cos/sin of
+// its angle (optimize_scan_matcher.h:94-97).
+struct OptScan {
+  double c, s, tx, ty;
+  int32_t active;
+  int32_t pad;
+};
+// Sums of UpdateCost (optimize_scan_matcher.h:154-221) in point order:
+// v = {cost, H00, H10, H11, H20, H21, H22, b0, b1, b2}; valid = points in map.
+struct OptSums {
+  double v[10];
+  int32_t valid;
+  int32_t pad;
+};
+struct OptArgs {
+  const float* grid;  // packed fp32 grid, row-major
+  int32_t size_x, size_y;
+  float outside;
+  int32_t pad;
+  const double* pts;        // map-cell (x, y) points of every scan
+  const int64_t* offsets;   // n_scans + 1 prefix offsets into pts
+  const OptScan* scans;
+  OptSums* out;
+};
+hipError_t launch_optimize_cost(const OptArgs& A, int32_t n_scans, hipStream_t stream);
+
 // Reduce per-window partials (blocks_per_scan each) to one BestPartial per window.
 hipError_t launch_reduce_best(const BestPartial* d_partials, int32_t blocks_per_scan,
                               int32_t n_windows, BestPartial* d_out, hipStream_t stream);

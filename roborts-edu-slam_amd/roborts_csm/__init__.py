@@ -23,8 +23,8 @@ import numpy as np
 from . import _abi
 from ._abi import COARSE, FAST, FINE, SUPER, CsmBest, CsmMapInfo, CsmParam
 from .params import (
-    CONFIG1_PARAM, FAST_PARAM, IN_CLASS_LEVELS, PARAM_CONFIG_LEVELS, SIM_YAML_LEVELS,
-    CorrelationScanMatchParam, headline_levels,
+    CONFIG1_PARAM, FAST_PARAM, IN_CLASS_LEVELS, PARAM_CONFIG_LEVELS, PARAM_CONFIG_OPTIMIZE, SIM_YAML_LEVELS,
+    SIM_YAML_OPTIMIZE, CorrelationScanMatchParam, OptimizeScanMatchParam, headline_levels,
 )
 
 _lib = _abi.load_library()
@@ -253,6 +253,30 @@ class Context:
                                                   _dptr(covs), _dptr(scores)))
         return scores
 
+    def optimize_scan_match(self, points_cells, param, pose: np.ndarray) -> float:
+        """BasedOptimizeScanMatch::ScanMatch on the current grid; pose updated in place."""
+        pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
+        assert pose.dtype == np.float64 and pose.flags.c_contiguous and pose.size == 3
+        p = param if isinstance(param, _abi.CsmOptimizeParam) else param.to_c()
+        cost = C.c_double(0.0)
+        self._check(_lib.csm_optimize_scan_match(self._h, _dptr(pts), pts.shape[0], C.byref(p), _dptr(pose),
+                                                 C.byref(cost)))
+        return cost.value
+
+    def optimize_scan_match_batch(self, points, offsets, param, poses):
+        """Returns (costs, iterations) for n independent scans; poses updated in place."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 2)
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = off.size - 1
+        assert poses.dtype == np.float64 and poses.flags.c_contiguous and poses.size == 3 * n
+        p = param if isinstance(param, _abi.CsmOptimizeParam) else param.to_c()
+        costs = np.zeros(n)
+        iters = np.zeros(n, dtype=np.int32)
+        self._check(_lib.csm_optimize_scan_match_batch(self._h, n, _dptr(pts), _i64ptr(off), C.byref(p),
+                                                       _dptr(poses), _dptr(costs),
+                                                       iters.ctypes.data_as(C.POINTER(C.c_int32))))
+        return costs, iters
+
     def sort_order(self, keys) -> np.ndarray:
         """Device emulation of std::sort(greater) on keys (test hook)."""
         k = np.ascontiguousarray(keys, dtype=np.float64)
@@ -345,25 +369,73 @@ class BasedCorrelationScanMatch:
         return self.ctx.scan_match(range_data.points, param, current_pose, cov_matrix.reshape(-1))
 
 
-class ScanMatchers:
-    """Mirror of ScanMatchers::ScanMatch (scan_matchers.h:179-289) with the
-    correlative levels only (use_optimize_scan_match = false, both YAMLs)."""
+class BasedOptimizeScanMatch:
+    """Mirror of BasedOptimizeScanMatch (optimize_scan_matcher.h:60-237).
 
-    def __init__(self, levels=SIM_YAML_LEVELS, context: Context | None = None):
+    ScanMatch(map, range_data, param, best_pose) -> cost; best_pose (world, 3)
+    is updated in place unless the reference's early returns apply.
+    """
+
+    def __init__(self, context: Context | None = None):
+        self.ctx = context or Context(0)
+
+    def ScanMatch(self, map_: ScanMatchMap, range_data: RangeDataContainer2d, param,
+                  best_pose: np.ndarray) -> float:
+        self.ctx.set_grid(map_)
+        return self.ctx.optimize_scan_match(range_data.points, param, best_pose)
+
+
+class ScanMatchers:
+    """Mirror of ScanMatchers::ScanMatch (scan_matchers.h:179-289).
+
+    With use_optimize_scan_match (ParamConfig default; both YAMLs turn it off)
+    the Gauss-Newton matcher runs first on coarse_map with coarse_range_data
+    and the correlative coarse level only when it fails (:205-242); every
+    correlative level runs on fine_map with fine_range_data (:238,:249,:256).
+    """
+
+    def __init__(self, levels=SIM_YAML_LEVELS, context: Context | None = None,
+                 use_optimize_scan_match: bool = False, optimize=SIM_YAML_OPTIMIZE,
+                 optimize_failed_cost: float = 2.0, coarse_context: Context | None = None):
         self.levels = tuple(levels)
         self.ctx = context or Context(0)
+        self.use_optimize_scan_match = use_optimize_scan_match
+        self.optimize = optimize
+        self.optimize_failed_cost = float(optimize_failed_cost)
+        self.cctx = coarse_context or (Context(self.ctx.device) if use_optimize_scan_match else None)
 
     def ScanMatch(self, coarse_range_data, fine_range_data, coarse_map, fine_map,
                   best_pose: np.ndarray, cov_matrix: np.ndarray, use_fine_scan_match: bool = True) -> float:
-        # every correlative level runs on fine_map with fine_range_data (:238,:249,:256)
+        cov = cov_matrix.reshape(-1)
+        if not self.use_optimize_scan_match:
+            self.ctx.set_grid(fine_map)
+            return self.ctx.scan_matchers(fine_range_data.points, self.levels, best_pose, cov,
+                                          use_fine_scan_match)
+        score, times = 0.0, 0
+        process = best_pose.copy()
+        self.cctx.set_grid(coarse_map)
+        cost = self.cctx.optimize_scan_match(coarse_range_data.points, self.optimize, process)
+        score = self.optimize_failed_cost / (cost + self.optimize_failed_cost)  # :211
+        times += 1
         self.ctx.set_grid(fine_map)
-        return self.ctx.scan_matchers(fine_range_data.points, self.levels, best_pose,
-                                      cov_matrix.reshape(-1), use_fine_scan_match)
+        if not use_fine_scan_match or cost > self.optimize_failed_cost:  # :224-242
+            score, times = 0.0, times - 1
+            process[:] = best_pose
+            score += self.ctx.scan_match(fine_range_data.points, self.levels[0], process, cov)
+            times += 1
+        best_pose[:] = process
+        if use_fine_scan_match:
+            for lv in self.levels[1:]:
+                score += self.ctx.scan_match(fine_range_data.points, lv, process, cov)
+                times += 1
+        best_pose[:] = process
+        return score / times
 
 
 __all__ = [
     "Context", "CsmError", "ScanMatchMap", "RangeDataContainer2d", "BasedCorrelationScanMatch",
     "ScanMatchers", "CorrelationScanMatchParam", "SIM_YAML_LEVELS", "PARAM_CONFIG_LEVELS",
-    "IN_CLASS_LEVELS", "FAST_PARAM", "CONFIG1_PARAM", "headline_levels", "window_dims",
+    "IN_CLASS_LEVELS", "FAST_PARAM", "BasedOptimizeScanMatch", "OptimizeScanMatchParam", "SIM_YAML_OPTIMIZE",
+    "PARAM_CONFIG_OPTIMIZE", "CONFIG1_PARAM", "headline_levels", "window_dims",
     "cell_points", "COARSE", "FINE", "SUPER", "FAST", "kMapUnknownCellProb",
 ]

@@ -28,7 +28,7 @@ EXPORTED = (
     "csm_scan_match_batch", "csm_scan_matchers_batch", "csm_score_window",
     "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded",
     "csm_set_profiling", "csm_kernel_stats", "csm_sort_order",
-    "csm_set_grid_stack", "csm_best_windows",
+    "csm_set_grid_stack", "csm_best_windows", "csm_optimize_scan_match", "csm_optimize_scan_match_batch",
     # include/csm_gridmap.h
     "csm_gridmap_create", "csm_gridmap_destroy", "csm_gridmap_last_error",
     "csm_gridmap_set_options", "csm_gridmap_set_cell_params", "csm_gridmap_set_map_offset",
@@ -78,6 +78,19 @@ class CsmBest(C.Structure):
         ("x", C.c_double),
         ("y", C.c_double),
         ("angle", C.c_double),
+    ]
+
+
+class CsmOptimizeParam(C.Structure):
+    """csm_optimize_param == OptimizeScanMatchParam (optimize_scan_matcher.h:33-58)."""
+
+    _fields_ = [
+        ("iterate_max_times", C.c_int32),
+        ("reserved", C.c_int32),
+        ("cost_decrease_threshold", C.c_double),
+        ("cost_min_threshold", C.c_double),
+        ("max_update_distance", C.c_double),
+        ("max_update_angle", C.c_double),
     ]
 
 
@@ -144,6 +157,9 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_set_grid_stack": (C.c_int, [_ctx, C.c_void_p, C.c_int32, C.POINTER(CsmMapInfo), C.c_int64]),
         "csm_best_windows": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), C.c_int32, _i32p, _dp,
                                        C.POINTER(CsmBest)]),
+        "csm_optimize_scan_match": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmOptimizeParam), _dp, _dp]),
+        "csm_optimize_scan_match_batch": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, C.POINTER(CsmOptimizeParam), _dp,
+                                                    _dp, _i32p]),
         "csm_gridmap_create": (C.c_int, [C.c_int, C.c_int32, C.c_double, C.c_int32, C.c_int32, C.c_double,
                                          C.c_double, C.c_double, C.c_float, C.POINTER(C.c_void_p)]),
         "csm_gridmap_destroy": (C.c_int, [C.c_void_p]),

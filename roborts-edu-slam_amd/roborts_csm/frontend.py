@@ -15,7 +15,7 @@ import numpy as np
 
 from . import _abi
 from .gridmap import OccuGridMap
-from .params import SIM_YAML_LEVELS
+from .params import SIM_YAML_LEVELS, SIM_YAML_OPTIMIZE, SIM_YAML_OPTIMIZE_FAILED_COST
 
 _lib = _abi.load_library()
 
@@ -30,12 +30,14 @@ class CsmFrontendParam(C.Structure):
             "map_check_point_num", "use_map_update_move_check")] + [(n, C.c_double) for n in (
                 "map_check_bound_tolerance", "map_check_penalty_gain", "map_update_score_threshold",
                 "map_update_distance_threshold", "map_update_angle_threshold")] + [
-        ("levels", _abi.CsmParam * 3)]
+        ("levels", _abi.CsmParam * 3), ("use_optimize_scan_match", C.c_int32), ("reserved", C.c_int32),
+        ("optimize_failed_cost", C.c_double), ("optimize", _abi.CsmOptimizeParam)]
 
 
 class CsmFrontendResult(C.Structure):
     _fields_ = [("pose", C.c_double * 3), ("match_pose", C.c_double * 3), ("cov", C.c_double * 9),
-                ("score", C.c_double), ("map_penalty", C.c_double), ("data_index", C.c_int32),
+                ("score", C.c_double), ("map_penalty", C.c_double), ("optimize_cost", C.c_double),
+                ("data_index", C.c_int32),
                 ("matched", C.c_int32), ("map_updated", C.c_int32), ("pose_accepted", C.c_int32)]
 
 
@@ -70,6 +72,9 @@ class FrontEndParam:
     map_update_distance_threshold: float = 0.1
     map_update_angle_threshold: float = 0.01745 * 1
     levels: tuple = field(default=SIM_YAML_LEVELS)
+    use_optimize_scan_match: bool = False    # simulatin_param.yaml:40 (ParamConfig default: true)
+    optimize_failed_cost: float = SIM_YAML_OPTIMIZE_FAILED_COST
+    optimize: object = SIM_YAML_OPTIMIZE     # OptimizeScanMatchParam
 
     def to_c(self) -> CsmFrontendParam:
         c = CsmFrontendParam()
@@ -77,6 +82,8 @@ class FrontEndParam:
             if f.name == "levels":
                 for k, lv in enumerate(self.levels):
                     c.levels[k] = lv.to_c()
+            elif f.name == "optimize":
+                c.optimize = self.optimize.to_c()
             else:
                 setattr(c, f.name, type(getattr(c, f.name))(getattr(self, f.name)))
         return c
@@ -89,6 +96,7 @@ class FrontEndResult:
     cov: np.ndarray
     score: float
     map_penalty: float
+    optimize_cost: float
     data_index: int
     matched: bool
     map_updated: bool
@@ -97,7 +105,7 @@ class FrontEndResult:
     @staticmethod
     def from_c(r) -> "FrontEndResult":
         return FrontEndResult(np.array(r.pose[:]), np.array(r.match_pose[:]), np.array(r.cov[:]), r.score,
-                              r.map_penalty, r.data_index, bool(r.matched), bool(r.map_updated),
+                              r.map_penalty, r.optimize_cost, r.data_index, bool(r.matched), bool(r.map_updated),
                               bool(r.pose_accepted))
 
 

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, replace
 
-from ._abi import COARSE, FAST, FINE, SUPER, CsmParam
+from ._abi import COARSE, FAST, FINE, SUPER, CsmOptimizeParam, CsmParam
 
 
 @dataclass(frozen=True)
@@ -77,6 +77,31 @@ FAST_PARAM = CorrelationScanMatchParam(0.8, 0.01, 0.523, 0.00349, 0.5, 100, 4, F
 CONFIG1_PARAM = _lv(1.0, 0.05, 0.2617993877991494, 0.0349, 0.6, 100, COARSE)
 
 
+@dataclass(frozen=True)
+class OptimizeScanMatchParam:
+    """Mirror of OptimizeScanMatchParam (optimize_scan_matcher.h:33-58)."""
+
+    iterate_max_times: int
+    cost_decrease_threshold: float
+    cost_min_threshold: float
+    max_update_distance: float
+    max_update_angle: float
+
+    def to_c(self) -> CsmOptimizeParam:
+        return CsmOptimizeParam(int(self.iterate_max_times), 0, self.cost_decrease_threshold,
+                                self.cost_min_threshold, self.max_update_distance, self.max_update_angle)
+
+
+# config/simulatin_param.yaml:42-47 (use_optimize_scan_match: false there;
+# optimize_failed_cost 2.0)
+SIM_YAML_OPTIMIZE = OptimizeScanMatchParam(10, 0.1, 0.5, 0.5, 0.5)
+SIM_YAML_OPTIMIZE_FAILED_COST = 2.0
+# ParamConfig defaults (param_config.h:63-69; use_optimize_scan_match true,
+# optimize_failed_cost 20)
+PARAM_CONFIG_OPTIMIZE = OptimizeScanMatchParam(10, 1.0, 2.0, 0.5, 0.2)
+PARAM_CONFIG_OPTIMIZE_FAILED_COST = 20.0
+
+
 def headline_levels(use_point_size: int = 1081):
     """SIM_YAML levels with every beam summed (B = N = 1081): the BASELINE
     headline "1081-beam" configuration."""
@@ -86,5 +111,6 @@ def headline_levels(use_point_size: int = 1081):
 __all__ = [
     "CorrelationScanMatchParam", "SIM_YAML_LEVELS", "PARAM_CONFIG_LEVELS",
     "IN_CLASS_LEVELS", "FAST_PARAM", "CONFIG1_PARAM", "headline_levels",
-    "COARSE", "FINE", "SUPER", "FAST",
+    "COARSE", "FINE", "SUPER", "FAST", "OptimizeScanMatchParam", "SIM_YAML_OPTIMIZE",
+    "SIM_YAML_OPTIMIZE_FAILED_COST", "PARAM_CONFIG_OPTIMIZE", "PARAM_CONFIG_OPTIMIZE_FAILED_COST",
 ]

@@ -23,8 +23,8 @@ sys.path[:0] = [os.path.join(ROOT, "roborts-edu-slam_amd"), os.path.join(ROOT, "
 import pyoracle as O  # noqa: E402
 from roborts_csm import worlds  # noqa: E402
 from roborts_csm.params import (  # noqa: E402
-    CONFIG1_PARAM, FAST_PARAM, PARAM_CONFIG_LEVELS, SIM_YAML_LEVELS, CorrelationScanMatchParam,
-    headline_levels,
+    CONFIG1_PARAM, FAST_PARAM, PARAM_CONFIG_LEVELS, PARAM_CONFIG_OPTIMIZE, SIM_YAML_LEVELS, SIM_YAML_OPTIMIZE,
+    CorrelationScanMatchParam, headline_levels,
 )
 
 OUT = os.path.dirname(os.path.abspath(__file__))
@@ -173,9 +173,34 @@ def gen_large_window():
     print("f5 best", s, flat)
 
 
+def gen_optimize():
+    """F6: the Gauss-Newton matcher (optimize_scan_matcher.h:68-132) on the F1
+    grid: the F1 scan plus 5 ray-cast scans, both reference parameter sets
+    (simulatin_param.yaml:42-47 and ParamConfig defaults param_config.h:63-69)."""
+    f1 = np.load(os.path.join(OUT, "f1_config1.npz"))
+    res, off = float(f1["resolution"]), tuple(f1["offset"])
+    m = O.Map(f1["grid"], res, off)
+    w = worlds.World(f1["grid"], f1["grid"] >= 0.99, res, off)
+    b = worlds.make_scan_batch(w, 5, seed=SEED + 6)
+    pts = [f1["points"]] + [b.points_cells[b.offsets[k]:b.offsets[k + 1]] for k in range(5)]
+    init = np.vstack([f1["init_pose"], b.init_poses])
+    offsets = np.concatenate([[0], np.cumsum([len(p) for p in pts])]).astype(np.int64)
+    out = {"points": np.vstack(pts), "offsets": offsets, "init_poses": init}
+    for tag, prm in (("sim", SIM_YAML_OPTIMIZE), ("cfg", PARAM_CONFIG_OPTIMIZE)):
+        out[f"param_{tag}"] = np.array([prm.iterate_max_times, prm.cost_decrease_threshold, prm.cost_min_threshold,
+                                        prm.max_update_distance, prm.max_update_angle])
+        r = [O.optimize_scan_match(m, p, prm, q) for p, q in zip(pts, init)]
+        out[f"cost_{tag}"] = np.array([x[0] for x in r])
+        out[f"pose_{tag}"] = np.vstack([x[1] for x in r])
+        out[f"iters_{tag}"] = np.array([x[2] for x in r], dtype=np.int32)
+        print("f6", tag, "costs", np.round(out[f"cost_{tag}"], 3), "iters", out[f"iters_{tag}"])
+    np.savez_compressed(os.path.join(OUT, "f6_optimize.npz"), **out)
+
+
+GENERATORS = {"f1": gen_config1, "f2": gen_config2_crop, "f3": gen_ties, "f4": gen_bnb, "f5": gen_large_window,
+              "f6": gen_optimize}
+
 if __name__ == "__main__":
-    gen_config1()
-    gen_config2_crop()
-    gen_ties()
-    gen_bnb()
-    gen_large_window()
+    # python tests/golden/make_golden.py [f1 f2 ...]  (default: all, in order)
+    for name in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[name]()

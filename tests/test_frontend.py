@@ -23,11 +23,30 @@ def _rel(true, k):
     return np.array([c * d[0] - s * d[1], s * d[0] + c * d[1], d[2]])
 
 
-def test_oracle_frontend_tracks_drive():
+def _param(mode):
+    """sim: simulatin_param.yaml (no optimizer); opt_sim: with the Gauss-Newton
+    matcher and the YAML's optimize_failed_cost 2 (often falls back to the
+    correlative coarse level); opt_mixed: failed cost 0.33, so some scans take
+    the fallback and some do not; opt_cfg: ParamConfig's optimizer defaults
+    (failed cost 20: the optimizer replaces the coarse level)."""
+    from roborts_csm.frontend import FrontEndParam
+    from roborts_csm.params import PARAM_CONFIG_OPTIMIZE, PARAM_CONFIG_OPTIMIZE_FAILED_COST
+    if mode == "sim":
+        return FrontEndParam()
+    if mode == "opt_sim":
+        return FrontEndParam(use_optimize_scan_match=True)
+    if mode == "opt_mixed":  # failed cost inside the drive's cost range: both branches of :224
+        return FrontEndParam(use_optimize_scan_match=True, optimize_failed_cost=0.33)
+    return FrontEndParam(use_optimize_scan_match=True, optimize=PARAM_CONFIG_OPTIMIZE,
+                         optimize_failed_cost=PARAM_CONFIG_OPTIMIZE_FAILED_COST)
+
+
+@pytest.mark.parametrize("mode", ["sim", "opt_sim", "opt_mixed", "opt_cfg"])
+def test_oracle_frontend_tracks_drive(mode):
     import pyoracle as O
-    from roborts_csm.frontend import CsmFrontendResult, FrontEndParam
+    from roborts_csm.frontend import CsmFrontendResult
     st = _stream(30)
-    fe = O.FrontEnd(FrontEndParam().to_c())
+    fe = O.FrontEnd(_param(mode).to_c())
     for k in range(30):
         r = fe.process(st.points_m[k], st.odom_poses[k], CsmFrontendResult())
         err = np.array(r.pose[:]) - _rel(st.true_poses, k)
@@ -36,13 +55,14 @@ def test_oracle_frontend_tracks_drive():
 
 
 @pytest.mark.gpu
-def test_device_frontend_matches_oracle():
+@pytest.mark.parametrize("mode", ["sim", "opt_sim", "opt_mixed", "opt_cfg"])
+def test_device_frontend_matches_oracle(mode):
     import pyoracle as O
     from map_engines import same_state
-    from roborts_csm.frontend import CsmFrontendResult, FrontEndParam, SlamFrontEnd
+    from roborts_csm.frontend import CsmFrontendResult, SlamFrontEnd
     n = 24
     st = _stream(n, seed=4)
-    prm = FrontEndParam()
+    prm = _param(mode)
     ofe = O.FrontEnd(prm.to_c())
     dfe = SlamFrontEnd(prm)
     for k in range(n):
@@ -51,8 +71,9 @@ def test_device_frontend_matches_oracle():
         assert np.array_equal(np.array(a.pose[:]), b.pose), k
         assert np.array_equal(np.array(a.match_pose[:]), b.match_pose), k
         assert np.array_equal(np.array(a.cov[:]), b.cov), k
-        assert (a.score, a.map_penalty, a.data_index, bool(a.map_updated), bool(a.pose_accepted)) == \
-            (b.score, b.map_penalty, b.data_index, b.map_updated, b.pose_accepted), k
+        assert (a.score, a.map_penalty, a.optimize_cost, a.data_index, bool(a.map_updated),
+                bool(a.pose_accepted)) == \
+            (b.score, b.map_penalty, b.optimize_cost, b.data_index, b.map_updated, b.pose_accepted), k
 
     class _O:
         def __init__(self, m):
