@@ -215,6 +215,12 @@ int csm_optimize_scan_match_batch(csm_ctx* ctx, int32_t n_scans, const double* p
                                   const int64_t* point_offsets, const csm_optimize_param* param,
                                   double* poses, double* costs, int32_t* iterations);
 
+/* Test hook: one UpdateCost evaluation (optimize_scan_matcher.h:154-221) on
+ * the device at a map-cell pose; cost normalised as the reference (:220), H
+ * row-major (symmetric), b. */
+int csm_optimize_update_cost(csm_ctx* ctx, const double* points_xy, int32_t n_points,
+                             const double est_map[3], double* cost, double H[9], double b[3]);
+
 /* --- measurement ---------------------------------------------------------- */
 /* Turn HIP-event timing of every scoring launch on/off (resets the stats). */
 int csm_set_profiling(csm_ctx* ctx, int32_t on);

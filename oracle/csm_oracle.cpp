@@ -30,6 +30,8 @@
 #include <cstring>
 #include <vector>
 
+#include "oracle_math.hpp"
+
 namespace {
 
 // Geometry + cells of one ScanMatchMap (map/grid_map_base.h:47-71,352-354).
@@ -135,7 +137,8 @@ struct AngleLut {
     for (int a = 0; a < n_angles; ++a) {
       double angle = start_angle + a * angle_resolution;
       angles[a] = angle;
-      double cs = std::cos(angle), sn = std::sin(angle);
+      double cs, sn;
+      ref_sincos(angle, &sn, &cs);
       rows[a].resize(n);
       for (int p = 0; p < n; ++p) {
         double px = pts[2 * p], py = pts[2 * p + 1];
@@ -197,8 +200,10 @@ Cand find_best(const std::vector<Cand>& sorted, double tol) {
     if (!double_equal(sc, best.score, tol)) break;
     ax += c.x * sc;
     ay += c.y * sc;
-    tx += std::cos(c.angle) * sc;
-    ty += std::sin(c.angle) * sc;
+    double sa, ca;
+    ref_sincos(c.angle, &sa, &ca);
+    tx += ca * sc;
+    ty += sa * sc;
     ssum += sc;
     count++;
   }

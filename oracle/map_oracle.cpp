@@ -46,6 +46,8 @@
 #include <utility>
 #include <vector>
 
+#include "oracle_math.hpp"
+
 namespace {
 
 constexpr float kDefaultCellProb = 0.5f;  // grid_map_cell.h:30
@@ -374,7 +376,8 @@ bool update_by_range(OMap& m, const double* pts, int n, const double origin[2], 
   m.cur_mark_occu = m.cur_update_index + 2;
   double pm[3];
   world_to_map(m, pose, pm);
-  const double c = std::cos(pm[2]), s = std::sin(pm[2]);
+  double c, s;
+  ref_sincos(pm[2], &s, &c);
   std::vector<double> tp((size_t)2 * (n > 0 ? n : 0));
   for (int i = 0; i < n; ++i) pose_apply(c, s, pm[0], pm[1], pts[2 * i], pts[2 * i + 1], tp[2 * i], tp[2 * i + 1]);
   if (m.auto_resize && n > 0) {
@@ -440,7 +443,8 @@ double feedback_penalty(OMap& m, const double* pts, int n, const double origin[2
   double pm[3];
   world_to_map(m, best_pose, pm);
   if (!point_in_map(m, pm[0], pm[1])) return 0.0;
-  const double c = std::cos(pm[2]), s = std::sin(pm[2]);
+  double c, s;
+  ref_sincos(pm[2], &s, &c);
   double sx, sy;
   pose_apply(c, s, pm[0], pm[1], origin[0], origin[1], sx, sy);
   const int x0 = (int)(sx + 0.5), y0 = (int)(sy + 0.5);
@@ -767,7 +771,8 @@ int oracle_frontend_process(void* h, const double* pts, int n, const double odom
   if (!first) {
     if (p.use_odometry) {  // PredictPoseByOdom (:618-635)
       const double a = f.cur[2] - f.last_odom[2];
-      const double c = std::cos(a), s = std::sin(a);
+      double c, s;
+      ref_sincos(a, &s, &c);
       const double tx = f.cur[0] - (c * f.last_odom[0] + (-s) * f.last_odom[1]);
       const double ty = f.cur[1] - (s * f.last_odom[0] + c * f.last_odom[1]);
       predict[0] = (c * odom[0] + (-s) * odom[1]) + tx;

@@ -26,6 +26,8 @@
 #include <cstring>
 #include <utility>
 
+#include "oracle_math.hpp"
+
 extern "C" {
 struct oracle_map_c {  // csm_oracle.cpp
   const float* cells;
@@ -154,7 +156,8 @@ void ldlt_solve(const double Hin[9], const double b[3], double x[3]) {
 // est: map-cell pose; H row-major, all 9 entries accumulated.
 double update_cost(const oracle_map_c& m, const double* pts, int n, const double est[3], double H[9],
                    double b[3]) {
-  const double c = std::cos(est[2]), s = std::sin(est[2]);  // :96-97, :200-201
+  double s, c;  // one sincos per evaluation: rotation (:96-97) and de_s (:200-201)
+  ref_sincos(est[2], &s, &c);
   const double r00 = c, r01 = -s, r10 = s, r11 = c;
   double cost = 0.0;
   int valid_point = 1;
@@ -173,8 +176,8 @@ double update_cost(const oracle_map_c& m, const double* pts, int n, const double
     r = (r >= 0) ? ((r <= 1) ? (r) : (1)) : (0);
     const double error = 1 - r;
     cost += (error * error);
-    const double ds02 = (-std::sin(est[2]) * lx - std::cos(est[2]) * ly);
-    const double ds12 = (std::cos(est[2]) * lx - std::sin(est[2]) * ly);
+    const double ds02 = (-s * lx - c * ly);
+    const double ds12 = (c * lx - s * ly);
     const double dm0 = (((y - y0)) * (p11 - p01) + ((y1 - y)) * (p10 - p00));
     const double dm1 = (((x - x0)) * (p11 - p10) + ((x1 - x)) * (p01 - p00));
     // J = -de_m * de_s with de_s = [1 0 ds02; 0 1 ds12]

@@ -17,6 +17,7 @@
 #include "csm_internal.hpp"
 #include "csm_gridmap.h"
 #include "csm_gridmap_internal.hpp"
+#include "host_math.hpp"
 
 #include <algorithm>
 #include <atomic>
@@ -919,8 +920,7 @@ bool plan_window_into(const csm_param& P, const Dims& D, const Geometry& G, int 
   for (int a = 0; a < D.n_angles; ++a) {
     AngleEntry& ae = out[a];
     ae.angle = start + a * P.search_angle_resolution;
-    ae.cosine = std::cos(ae.angle);
-    ae.sine = std::sin(ae.angle);
+    csm::host_sincos(ae.angle, &ae.sine, &ae.cosine);
   }
   return true;
 }
@@ -1520,8 +1520,7 @@ int optimize_batch(csm_ctx* c, int32_t n_scans, const int64_t* off, const csm_op
       o.active = active[(size_t)s];
       if (!o.active) continue;
       const double* m = &est[(size_t)3 * s];
-      o.c = std::cos(m[2]);  // rotation (:96-97), de_s (:200-201)
-      o.s = std::sin(m[2]);
+      csm::host_sincos(m[2], &o.s, &o.c);  // rotation (:96-97), de_s (:200-201)
       o.tx = m[0];
       o.ty = m[1];
     }
@@ -2106,6 +2105,51 @@ int csm_optimize_scan_match(csm_ctx* c, const double* pts, int32_t n_points, con
   if (n_points < 0) return c->fail(CSM_ERR_INVALID_ARG, "negative point count");
   const int64_t off[2] = {0, n_points};
   return csm_optimize_scan_match_batch(c, 1, pts, off, param, pose, cost, nullptr);
+}
+
+int csm_optimize_update_cost(csm_ctx* c, const double* pts, int32_t n_points, const double est_map[3],
+                             double* cost, double H[9], double b[3]) {
+  if (!c || !est_map || !cost || !H || !b) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st;
+  if (n_points < 0) return c->fail(CSM_ERR_INVALID_ARG, "negative point count");
+  if ((st = check_points(c, pts, n_points)) != CSM_OK) return st;
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  if ((st = upload_points(c, pts, n_points)) != CSM_OK) return st;
+  const int64_t off[2] = {0, n_points};
+  hipError_t e;
+  if ((e = c->opt_off.ensure(sizeof(off))) != hipSuccess || (e = c->opt_scans.ensure(sizeof(csm::OptScan))) != hipSuccess ||
+      (e = c->opt_sums.ensure(sizeof(csm::OptSums))) != hipSuccess)
+    return c->hip_fail(e, "hipMalloc(optimize)");
+  csm::OptScan o{};
+  csm::host_sincos(est_map[2], &o.s, &o.c);
+  o.tx = est_map[0];
+  o.ty = est_map[1];
+  o.active = 1;
+  csm::OptArgs A{};
+  A.grid = c->d_grid;
+  A.size_x = c->info.size_x;
+  A.size_y = c->info.size_y;
+  A.outside = c->outside;
+  A.pts = (const double*)c->pts.p;
+  A.offsets = (const int64_t*)c->opt_off.p;
+  A.scans = (const csm::OptScan*)c->opt_scans.p;
+  A.out = (csm::OptSums*)c->opt_sums.p;
+  csm::OptSums r{};
+  if ((e = hipMemcpyAsync(c->opt_off.p, off, sizeof(off), hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(c->opt_scans.p, &o, sizeof(o), hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+      (e = csm::launch_optimize_cost(A, 1, c->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(&r, c->opt_sums.p, sizeof(r), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+    return c->hip_fail(e, "optimize_cost_kernel");
+  *cost = r.v[0] * (kOptCostPointSize / (1 + r.valid));
+  const double h[9] = {r.v[1], r.v[2], r.v[4], r.v[2], r.v[3], r.v[5], r.v[4], r.v[5], r.v[6]};
+  std::memcpy(H, h, sizeof(h));
+  b[0] = r.v[7];
+  b[1] = r.v[8];
+  b[2] = r.v[9];
+  return CSM_OK;
 }
 
 }  // extern "C"

@@ -18,6 +18,7 @@
 #include "csm.h"
 #include "csm_frontend.h"
 #include "csm_gridmap.h"
+#include "host_math.hpp"
 
 namespace {
 
@@ -40,7 +41,8 @@ bool pose_change_enough(const double* p1, const double* p2, double dist, double 
 // PredictPoseByOdom (slam_processor.cpp:618-635), Eigen's 2x2 products.
 void predict_by_odom(const double* last_pose, const double* last_odom, const double* cur_odom, double* out) {
   const double a = last_pose[2] - last_odom[2];
-  const double c = std::cos(a), s = std::sin(a);
+  double c, s;
+  csm::host_sincos(a, &s, &c);
   const double tx = last_pose[0] - (c * last_odom[0] + (-s) * last_odom[1]);
   const double ty = last_pose[1] - (s * last_odom[0] + c * last_odom[1]);
   out[0] = (c * cur_odom[0] + (-s) * cur_odom[1]) + tx;

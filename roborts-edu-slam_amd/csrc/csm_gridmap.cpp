@@ -26,6 +26,7 @@
 
 #include "csm_gridmap.h"
 #include "csm_gridmap_internal.hpp"
+#include "host_math.hpp"
 
 namespace {
 
@@ -339,7 +340,8 @@ int update_by_range(csm_gridmap* m, const double* pts, int n, const double origi
   // GetMapCoordsPose (grid_map_base.h:89-93)
   const double s = m->scale_factor;
   const double pmx = s * pose[0] + s * m->off_x, pmy = s * pose[1] + s * m->off_y, pth = pose[2];
-  const double c = std::cos(pth), sn = std::sin(pth);
+  double c, sn;
+  csm::host_sincos(pth, &sn, &c);
   std::vector<double> tp((size_t)2 * n);
   for (int i = 0; i < n; ++i) pose_apply(c, sn, pmx, pmy, pts[2 * i], pts[2 * i + 1], tp[2 * i], tp[2 * i + 1]);
   if (m->auto_resize && n > 0) {
@@ -628,7 +630,8 @@ int csm_gridmap_feedback_penalty(csm_gridmap* m, const double* pts, int32_t n, c
     *coeff = 0.0;
     return CSM_OK;
   }
-  const double c = std::cos(best_pose[2]), sn = std::sin(best_pose[2]);
+  double c, sn;
+  csm::host_sincos(best_pose[2], &sn, &c);
   const double zero[2] = {0.0, 0.0};
   const double* o = origin ? origin : zero;
   double sx, sy;

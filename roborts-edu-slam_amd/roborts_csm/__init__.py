@@ -277,6 +277,15 @@ class Context:
                                                        iters.ctypes.data_as(C.POINTER(C.c_int32))))
         return costs, iters
 
+    def optimize_update_cost(self, points_cells, est_map):
+        """One device UpdateCost at a map-cell pose -> (cost, H 3x3, b) (test hook)."""
+        pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
+        est = np.ascontiguousarray(est_map, dtype=np.float64)
+        cost, H, b = C.c_double(0.0), np.zeros(9), np.zeros(3)
+        self._check(_lib.csm_optimize_update_cost(self._h, _dptr(pts), pts.shape[0], _dptr(est), C.byref(cost),
+                                                  _dptr(H), _dptr(b)))
+        return cost.value, H.reshape(3, 3), b
+
     def sort_order(self, keys) -> np.ndarray:
         """Device emulation of std::sort(greater) on keys (test hook)."""
         k = np.ascontiguousarray(keys, dtype=np.float64)

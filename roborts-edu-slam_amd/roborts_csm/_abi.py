@@ -29,6 +29,7 @@ EXPORTED = (
     "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded",
     "csm_set_profiling", "csm_kernel_stats", "csm_sort_order",
     "csm_set_grid_stack", "csm_best_windows", "csm_optimize_scan_match", "csm_optimize_scan_match_batch",
+    "csm_optimize_update_cost",
     # include/csm_gridmap.h
     "csm_gridmap_create", "csm_gridmap_destroy", "csm_gridmap_last_error",
     "csm_gridmap_set_options", "csm_gridmap_set_cell_params", "csm_gridmap_set_map_offset",
@@ -160,6 +161,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_optimize_scan_match": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmOptimizeParam), _dp, _dp]),
         "csm_optimize_scan_match_batch": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, C.POINTER(CsmOptimizeParam), _dp,
                                                     _dp, _i32p]),
+        "csm_optimize_update_cost": (C.c_int, [_ctx, _dp, C.c_int32, _dp, _dp, _dp, _dp]),
         "csm_gridmap_create": (C.c_int, [C.c_int, C.c_int32, C.c_double, C.c_int32, C.c_int32, C.c_double,
                                          C.c_double, C.c_double, C.c_float, C.POINTER(C.c_void_p)]),
         "csm_gridmap_destroy": (C.c_int, [C.c_void_p]),

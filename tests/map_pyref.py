@@ -11,6 +11,8 @@ import math
 
 import numpy as np
 
+from libm import sincos
+
 F = np.float32
 FLT_MAX = float(np.finfo(np.float32).max)
 FLT_MIN = float(np.finfo(np.float32).tiny)
@@ -217,7 +219,7 @@ class PyMap:
         self.cf, self.co = self.cur + 1, self.cur + 2
         s = self.s
         px, py, th = s * pose[0] + s * self.ox, s * pose[1] + s * self.oy, pose[2]
-        c, sn = math.cos(th), math.sin(th)
+        c, sn = sincos(th)
         tp = [((c * x + (-sn) * y) + px, (sn * x + c * y) + py) for x, y in pts]
         if self.auto and tp:
             bmin = [FLT_MAX, FLT_MAX]
@@ -299,7 +301,7 @@ class PyMap:
         px, py, th = s * pose[0] + s * self.ox, s * pose[1] + s * self.oy, pose[2]
         if not self.inmap(px, py):
             return 0.0
-        c, sn = math.cos(th), math.sin(th)
+        c, sn = sincos(th)
         x0 = int(((c * origin[0] + (-sn) * origin[1]) + px) + 0.5)
         y0 = int(((sn * origin[0] + c * origin[1]) + py) + 0.5)
         n = len(pts)

@@ -12,6 +12,8 @@ import math
 
 import numpy as np
 
+from libm import sincos
+
 K_COST_POINT_SIZE = 1000.0   # optimize_scan_matcher.h:234
 K_MAX_COST = 1.0 * K_COST_POINT_SIZE
 
@@ -27,7 +29,7 @@ def _cell(grid, x, y, outside):
 def update_cost(grid, pts, est, outside=0.3):
     """UpdateCost (:154-221) -> (cost, H 3x3 list, b list)."""
     sy, sx = grid.shape
-    c, s = math.cos(est[2]), math.sin(est[2])
+    c, s = sincos(est[2])  # GCC merges the cos/sin pairs of :96-97,:200-201 into sincos
     H = [[0.0] * 3 for _ in range(3)]
     b = [0.0] * 3
     cost = 0.0

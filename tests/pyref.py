@@ -13,6 +13,7 @@ import math
 import numpy as np
 
 from introsort_ref import sort_order_greater
+from libm import sincos
 
 
 def dims(p):
@@ -43,7 +44,7 @@ def window_scores(grid: np.ndarray, pts: np.ndarray, p, center, mres: float, out
     H, W = grid.shape
     out = np.empty((na, ns, ns))
     for a in range(na):
-        c, s = math.cos(angles[a]), math.sin(angles[a])
+        c, s = sincos(angles[a])                                 # :171-172 (GCC: one sincos)
         acc = np.zeros((ns, ns))
         for q in range(0, n, step):                               # :645
             px, py = pts[q, 0], pts[q, 1]
