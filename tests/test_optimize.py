@@ -225,3 +225,33 @@ def test_device_scan_matchers_with_optimizer(ctx, failed):
             s2, p2, c2 = _oracle_scan_matchers(m, pts, SIM_YAML_LEVELS, SIM_YAML_OPTIMIZE, failed,
                                                b.init_poses[k], np.eye(3), use_fine)
             assert s == s2 and np.array_equal(pose, p2) and np.array_equal(cov.reshape(-1), c2), (k, use_fine)
+
+
+def test_sincos_is_not_cos_and_sin():
+    """The trap host_math.hpp / oracle_math.hpp guard against: glibc's sincos
+    and separate cos/sin disagree in the last bit for some arguments, so the
+    restatements must pick the one the reference's GCC build calls (sincos)."""
+    from libm import sincos
+    rng = np.random.default_rng(0)
+    xs = rng.uniform(-4, 4, 20000)
+    diff = sum((sincos(x) != (math.cos(x), math.sin(x))) for x in xs)
+    assert diff > 0  # if glibc ever makes them agree, the guard is merely redundant
+
+
+@pytest.mark.gpu
+def test_device_update_cost_matches_oracle(ctx):
+    """One UpdateCost on the device at 200 random map-cell poses (test hook)."""
+    from roborts_csm import worlds
+    w = worlds.make_world(800, 800, 0.05, seed=31)
+    b = worlds.make_scan_batch(w, 10, seed=32)
+    _set(ctx, w.grid, w.resolution, w.offset)
+    m = O.Map(w.grid, w.resolution, w.offset)
+    rng = np.random.default_rng(33)
+    for k in range(10):
+        pts = b.points_cells[b.offsets[k]:b.offsets[k + 1]]
+        e0 = O.world_to_map(m, b.init_poses[k])
+        for _ in range(20):
+            e = e0 + rng.normal(size=3) * [3.0, 3.0, 0.1]
+            c1, H1, b1 = ctx.optimize_update_cost(pts, e)
+            c2, H2, b2 = O.optimize_update_cost(m, pts, e)
+            assert c1 == c2 and np.array_equal(H1, H2) and np.array_equal(b1, b2)
