@@ -221,6 +221,18 @@ int csm_optimize_scan_match_batch(csm_ctx* ctx, int32_t n_scans, const double* p
 int csm_optimize_update_cost(csm_ctx* ctx, const double* points_xy, int32_t n_points,
                              const double est_map[3], double* cost, double H[9], double b[3]);
 
+/* --- many scans, each on its own resident grid ------------------------------ */
+/* As csm_load_scans / csm_scan_matchers_batch, with scan i matched on grid
+ * grid_index[i] of the resident stack (csm_set_grid_stack or
+ * csm_set_grid_stack_gridmaps); the grids share one geometry. Used by the
+ * back-end's batched ScanMatchInterface (csm_backend.h). */
+int csm_load_scans_grids(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
+                         const int64_t* point_offsets, const int32_t* grid_index);
+int csm_scan_matchers_batch_grids(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
+                                  const int64_t* point_offsets, const int32_t* grid_index,
+                                  const csm_param levels[3], int32_t use_fine, double* poses,
+                                  double* covs, double* scores);
+
 /* --- measurement ---------------------------------------------------------- */
 /* Turn HIP-event timing of every scoring launch on/off (resets the stats). */
 int csm_set_profiling(csm_ctx* ctx, int32_t on);

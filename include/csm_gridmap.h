@@ -128,6 +128,11 @@ int csm_gridmap_device_prob(csm_gridmap* map, const float** device_prob);
  * size, resolution, offset and update index come from the map. */
 int csm_set_grid_gridmap(csm_ctx* ctx, csm_gridmap* map);
 
+/* Make n maps of one size, resolution and offset resident as a grid stack
+ * (device-to-device copies ordered after each map's last update); scans then
+ * name their map with csm_scan_matchers_batch_grids. Replaces the grid. */
+int csm_set_grid_stack_gridmaps(csm_ctx* ctx, csm_gridmap* const* maps, int32_t n_maps);
+
 #ifdef __cplusplus
 }
 #endif

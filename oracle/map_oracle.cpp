@@ -719,6 +719,55 @@ oracle_map_c map_view(const OMap& m) {  // what oracle_scan_match* read of a Sca
   return mc;
 }
 
+// ScanMatchers::MapSizeCheck (scan_matchers.h:365-390) for one map.
+void map_size_check(OMap& m, const double pose[3], double range_max, double offset) {
+  double pm[3];
+  world_to_map(m, pose, pm);
+  const double mres = 1 / m.scale_factor;
+  const double max_size = (range_max + offset) / mres;
+  Box b;
+  b.minx = pm[0] - max_size;
+  b.miny = pm[1] - max_size;
+  b.maxx = pm[0] + max_size;
+  b.maxy = pm[1] + max_size;
+  update_bound(m, b);
+}
+
+// ScanMatchers::ScanMatch (scan_matchers.h:179-289) on a coarse and a fine
+// ScanMatchMap: MapSizeCheck on both, the optional Gauss-Newton matcher on the
+// coarse map, the correlative coarse level when it is off, failed or
+// !use_fine, then fine and super-fine on the fine map. Returns the mean.
+double matchers_on_maps(OMap& coarse, OMap& fine, const double* cp, const double* fp, int n,
+                        const FeParam::Level* levels, int use_opt, double failed, const FeParam::Opt& opt,
+                        double range_max, int use_fine, double pose[3], double cov[9], double* opt_cost) {
+  map_size_check(coarse, pose, range_max, levels[0].size);
+  map_size_check(fine, pose, range_max, levels[0].size);
+  const oracle_map_c mc = map_view(fine);
+  *opt_cost = 0.0;
+  if (!use_opt) return oracle_scan_matchers(&mc, fp, n, levels, use_fine, pose, cov);
+  const oracle_map_c cmc = map_view(coarse);
+  double proc[3] = {pose[0], pose[1], pose[2]};
+  const double cost = oracle_optimize_scan_match(&cmc, cp, n, &opt, proc, nullptr);
+  *opt_cost = cost;
+  double sum = failed / (cost + failed);
+  int times = 1;
+  if (!use_fine || cost > failed) {
+    sum = 0.0;
+    times--;
+    std::memcpy(proc, pose, sizeof(proc));
+    sum += oracle_scan_match(&mc, fp, n, &levels[0], proc, cov, nullptr, nullptr);
+    times++;
+  }
+  if (use_fine) {
+    for (int k = 1; k <= 2; ++k) {
+      sum += oracle_scan_match(&mc, fp, n, &levels[k], proc, cov, nullptr, nullptr);
+      times++;
+    }
+  }
+  std::memcpy(pose, proc, sizeof(proc));
+  return sum / times;
+}
+
 }  // namespace
 
 extern "C" {
@@ -780,44 +829,10 @@ int oracle_frontend_process(void* h, const double* pts, int n, const double odom
       predict[2] = a + odom[2];
     }
     double pose[3] = {predict[0], predict[1], predict[2]};
-    for (int k = 1; k <= 2; ++k) {  // MapSizeCheck (scan_matchers.h:365-390)
-      OMap& m = *f.maps[k];
-      double pm[3];
-      world_to_map(m, pose, pm);
-      const double mres = 1 / m.scale_factor;
-      const double max_size = (p.range_max + p.levels[0].size) / mres;
-      Box b;
-      b.minx = pm[0] - max_size;
-      b.miny = pm[1] - max_size;
-      b.maxx = pm[0] + max_size;
-      b.maxy = pm[1] + max_size;
-      update_bound(m, b);
-    }
-    const oracle_map_c mc = map_view(*f.maps[2]);
-    double score = 0.0;
-    if (!p.use_optimize_scan_match) {
-      score = oracle_scan_matchers(&mc, fp.data(), n, p.levels, 1, pose, cov);
-    } else {  // ScanMatchers::ScanMatch with the optimizer (scan_matchers.h:205-281)
-      const oracle_map_c cmc = map_view(*f.maps[1]);
-      double proc[3] = {pose[0], pose[1], pose[2]};
-      const double cost = oracle_optimize_scan_match(&cmc, cp.data(), n, &p.optimize, proc, nullptr);
-      r.optimize_cost = cost;
-      double sum = p.optimize_failed_cost / (cost + p.optimize_failed_cost);
-      int times = 1;
-      if (cost > p.optimize_failed_cost) {
-        sum = 0.0;
-        times--;
-        std::memcpy(proc, pose, sizeof(proc));
-        sum += oracle_scan_match(&mc, fp.data(), n, &p.levels[0], proc, cov, nullptr, nullptr);
-        times++;
-      }
-      for (int k = 1; k <= 2; ++k) {
-        sum += oracle_scan_match(&mc, fp.data(), n, &p.levels[k], proc, cov, nullptr, nullptr);
-        times++;
-      }
-      std::memcpy(pose, proc, sizeof(proc));
-      score = sum / times;
-    }
+    double opt_cost = 0.0;
+    double score = matchers_on_maps(*f.maps[1], *f.maps[2], cp.data(), fp.data(), n, p.levels, p.use_optimize_scan_match,
+                                    p.optimize_failed_cost, p.optimize, p.range_max, 1, pose, cov, &opt_cost);
+    r.optimize_cost = opt_cost;
     std::memcpy(r.match_pose, pose, sizeof(pose));
     double penalty = 1.0;
     if (p.use_map_check_feedback)  // MapCheckPenalize (:573-595)
@@ -875,6 +890,137 @@ int oracle_frontend_process(void* h, const double* pts, int n, const double odom
   r.score = f.score;
   r.map_updated = updated ? 1 : 0;
   std::memcpy(result, &r, sizeof(r));
+  return 0;
+}
+
+}  // extern "C"
+
+// ---- SlamProcessor::ScanMatchInterface (slam/slam_processor.cpp:250-326) -----
+// Test-infrastructure restatement of the calls include/csm_backend.h runs on
+// the device; job j of a call rebuilds and reads map pair j, in job order.
+
+namespace {
+
+struct BeParam {  // layout of csm_backend_param (include/csm_backend.h)
+  double range_max, gaussian_blur_offset, map_resolution;
+  double coarse_map_resolution, coarse_map_deviation, fine_map_resolution, fine_map_deviation;
+  int32_t coarse_map_use_blur, fine_map_use_blur, use_map_check_feedback, map_check_point_num;
+  double map_check_bound_tolerance, map_check_penalty_gain;
+  FeParam::Level levels[3];
+  int32_t use_optimize_scan_match, reserved;
+  double optimize_failed_cost;
+  FeParam::Opt optimize;
+};
+
+struct BeJob {  // layout of csm_backend_job
+  const double* points_m;
+  int32_t n_points, n_chain;
+  const int32_t* chain_ids;
+  int32_t use_fine_scan_match, reserved;
+  double pose[3], cov[9], score, map_penalty, optimize_cost;
+};
+
+struct OKept {
+  std::vector<double> coarse, fine;
+  double pose[3];
+};
+
+struct OBackEnd {
+  BeParam p;
+  std::vector<OKept> scans;
+  std::vector<std::unique_ptr<OMap>> maps[2];  // coarse, fine per job slot
+};
+
+std::vector<double> scaled(const double* pts, int n, double factor) {  // CreateFrom (:99-115)
+  std::vector<double> v((size_t)2 * n);
+  for (int i = 0; i < 2 * n; ++i) v[(size_t)i] = pts[i] * factor;
+  return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+void* oracle_backend_create(const void* param) {
+  auto* b = new OBackEnd();
+  std::memcpy(&b->p, param, sizeof(BeParam));
+  return b;
+}
+void oracle_backend_destroy(void* h) { delete static_cast<OBackEnd*>(h); }
+int oracle_backend_param_size(void) { return (int)sizeof(BeParam); }
+int oracle_backend_job_size(void) { return (int)sizeof(BeJob); }
+void* oracle_backend_map(void* h, int slot, int which) {
+  OBackEnd& b = *static_cast<OBackEnd*>(h);
+  return slot < (int)b.maps[which].size() ? b.maps[which][(size_t)slot].get() : nullptr;
+}
+
+int oracle_backend_add_scan(void* h, const double* pts, int n, const double pose[3]) {
+  OBackEnd& b = *static_cast<OBackEnd*>(h);
+  OKept k;
+  k.coarse = scaled(pts, n, 1 / b.p.coarse_map_resolution);
+  k.fine = scaled(pts, n, 1 / b.p.fine_map_resolution);
+  std::memcpy(k.pose, pose, sizeof(k.pose));
+  b.scans.push_back(std::move(k));
+  return (int)b.scans.size() - 1;
+}
+
+void oracle_backend_set_scan_pose(void* h, int id, const double pose[3]) {
+  std::memcpy(static_cast<OBackEnd*>(h)->scans[(size_t)id].pose, pose, sizeof(double) * 3);
+}
+
+int oracle_backend_scan_match(void* h, void* pub_map, const double cur[3], void* jobs_v, int n_jobs) {
+  OBackEnd& b = *static_cast<OBackEnd*>(h);
+  const BeParam& p = b.p;
+  BeJob* jobs = static_cast<BeJob*>(jobs_v);
+  for (int j = 0; j < n_jobs; ++j) {
+    BeJob& jb = jobs[j];
+    // the back-end maps (CreateScanMatchMapWithRangeVec :428-446); first contents wiped by the first reset
+    const double ims = (p.range_max + 2.0) * 2;
+    const double res[2] = {p.coarse_map_resolution, p.fine_map_resolution};
+    const double dev[2] = {p.coarse_map_deviation, p.fine_map_deviation};
+    for (int k = 0; k < 2; ++k) {
+      while ((int)b.maps[k].size() <= j)
+        b.maps[k].push_back(make_map(kProbabilityCell, res[k], (int)(ims / res[k]), 0.0, 0.0, dev[k], 0.3f));
+      OMap& m = *b.maps[k][(size_t)j];
+      // ResetScanMatchMapWithRangeVec (:448-462)
+      const double resolution = 1 / m.scale_factor;
+      m.off_x = -(cur[0] - 0.5 * m.size_x * resolution);
+      m.off_y = -(cur[1] - 0.5 * m.size_y * resolution);
+      m.auto_resize = false;
+      m.just_update_occu = true;
+      m.occu_offset = p.gaussian_blur_offset;
+      std::vector<double> pts, poses;
+      std::vector<int64_t> off(1, 0);
+      for (int c = 0; c < jb.n_chain; ++c) {
+        const OKept& ks = b.scans[(size_t)jb.chain_ids[c]];
+        const std::vector<double>& v = k ? ks.fine : ks.coarse;
+        pts.insert(pts.end(), v.begin(), v.end());
+        off.push_back(off.back() + (int64_t)(v.size() / 2));
+        poses.insert(poses.end(), ks.pose, ks.pose + 3);
+      }
+      std::vector<double> origins((size_t)2 * jb.n_chain, 0.0);
+      init_with_range_vec(m, pts.data(), off.data(), jb.n_chain, origins.data(), poses.data(),
+                          (k ? p.fine_map_use_blur : p.coarse_map_use_blur) != 0, true);
+    }
+    const std::vector<double> cp = scaled(jb.points_m, jb.n_points, 1 / p.coarse_map_resolution);  // :268-272
+    const std::vector<double> fp = scaled(jb.points_m, jb.n_points, 1 / p.fine_map_resolution);
+    const double eye[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    std::memcpy(jb.cov, eye, sizeof(eye));
+    jb.score = matchers_on_maps(*b.maps[0][(size_t)j], *b.maps[1][(size_t)j], cp.data(), fp.data(), jb.n_points,
+                                p.levels, p.use_optimize_scan_match, p.optimize_failed_cost, p.optimize, p.range_max,
+                                jb.use_fine_scan_match, jb.pose, jb.cov, &jb.optimize_cost);
+    jb.map_penalty = 1.0;
+    if (pub_map && p.use_map_check_feedback) {  // MapCheckPenalize(..., true) (:315-317, :573-595)
+      const std::vector<double> pp = scaled(jb.points_m, jb.n_points, 1 / p.map_resolution);
+      const double zero[2] = {0.0, 0.0};
+      const double penalty = feedback_penalty(*static_cast<OMap*>(pub_map), pp.data(), jb.n_points, zero, jb.pose,
+                                              p.map_check_point_num, p.map_check_bound_tolerance,
+                                              p.map_check_penalty_gain, false);
+      jb.map_penalty = (1 / (1 + std::exp(-10 * (penalty - 0.4))));
+    }
+    jb.score *= jb.map_penalty;
+    jb.score = (jb.score > 1.0) ? (1.0) : (jb.score);
+  }
   return 0;
 }
 

@@ -433,3 +433,52 @@ def ldlt_solve(H, b):
     x = np.zeros(3)
     _lib.oracle_ldlt_solve(h.ctypes.data_as(_dp), bb.ctypes.data_as(_dp), x.ctypes.data_as(_dp))
     return x
+
+
+# ---- SlamProcessor::ScanMatchInterface (map_oracle.cpp oracle_backend_*) --------
+for _k, (_r, _a) in {
+    "oracle_backend_create": (C.c_void_p, [C.c_void_p]),
+    "oracle_backend_destroy": (None, [C.c_void_p]),
+    "oracle_backend_param_size": (C.c_int, []),
+    "oracle_backend_job_size": (C.c_int, []),
+    "oracle_backend_map": (C.c_void_p, [C.c_void_p, C.c_int, C.c_int]),
+    "oracle_backend_add_scan": (C.c_int, [C.c_void_p, _dp, C.c_int, _dp]),
+    "oracle_backend_set_scan_pose": (None, [C.c_void_p, C.c_int, _dp]),
+    "oracle_backend_scan_match": (C.c_int, [C.c_void_p, C.c_void_p, _dp, C.c_void_p, C.c_int]),
+}.items():
+    _f = getattr(_lib, _k)
+    _f.restype, _f.argtypes = _r, _a
+
+
+class BackEnd:
+    """Oracle back-end scan-match service; param / jobs are ctypes structures
+    with the csm_backend_param / csm_backend_job layouts (roborts_csm.backend)."""
+
+    def __init__(self, c_param):
+        assert _lib.oracle_backend_param_size() == C.sizeof(c_param)
+        self._p = c_param
+        self.h = _lib.oracle_backend_create(C.byref(c_param))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            _lib.oracle_backend_destroy(h)
+            self.h = None
+
+    def add_scan(self, points_m, pose) -> int:
+        p, w = _pts(points_m), _d(pose)
+        return _lib.oracle_backend_add_scan(self.h, p.ctypes.data_as(_dp), p.shape[0], w.ctypes.data_as(_dp))
+
+    def set_scan_pose(self, i: int, pose):
+        w = _d(pose)
+        _lib.oracle_backend_set_scan_pose(self.h, int(i), w.ctypes.data_as(_dp))
+
+    def scan_match(self, jobs, n_jobs: int, current_pose, pub_map: GridMap | None = None):
+        assert _lib.oracle_backend_job_size() == C.sizeof(jobs[0])
+        cur = _d(current_pose)
+        _lib.oracle_backend_scan_match(self.h, pub_map.h if pub_map is not None else None, cur.ctypes.data_as(_dp),
+                                       jobs, n_jobs)
+        return jobs
+
+    def map(self, slot: int, which: int) -> GridMap:
+        return _FrontEndMap(_lib.oracle_backend_map(self.h, slot, which), self)

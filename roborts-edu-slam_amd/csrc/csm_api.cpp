@@ -477,6 +477,7 @@ struct csm_ctx {
   // scans made resident by csm_load_scans (offsets relative to pts)
   int32_t loaded_n = -1;
   std::vector<int64_t> loaded_off;
+  std::vector<int32_t> loaded_grid;  // per loaded scan: the resident grid it is matched on (empty: grid 0)
 
   // per-kernel HIP-event timing (csm_set_profiling / csm_kernel_stats)
   bool profiling = false;
@@ -1089,6 +1090,7 @@ struct LevelRun {
   std::vector<int> scan_of;
   std::vector<WindowPlan> plans;
   std::vector<int64_t> pt_off;
+  std::vector<int32_t> grid;             // resident grid of each window (empty: grid 0)
   const AngleEntry* angles = nullptr;    // pinned buffer of the slot that ran it
   const csm::FinishOut* fin = nullptr;   // ditto (device finish)
   const double* scores = nullptr;        // ditto (host finish)
@@ -1097,9 +1099,11 @@ struct LevelRun {
 };
 
 int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
-                const double* poses, double* responses, int64_t* argmax_flat, LevelRun& R) {
+                const double* poses, double* responses, int64_t* argmax_flat, LevelRun& R,
+                const int32_t* scan_grid = nullptr) {
   R.P = P;
   R.scan_of.clear();
+  R.grid.clear();
   int st = window_dims(P, R.D);
   if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
   const Dims& D = R.D;
@@ -1114,6 +1118,7 @@ int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
     if (!beam_rule(n, P.use_point_size, step, use, n_used))
       return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
     R.scan_of.push_back(s);
+    if (scan_grid) R.grid.push_back(scan_grid[s]);
   }
   const int nw = (int)R.scan_of.size();
   if (nw == 0) return CSM_OK;
@@ -1141,7 +1146,7 @@ int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
   R.dev = c->device_finish && D.n_cand <= csm::kFinishMaxCand &&
           csm::finish_lds_bytes(D.n_cand) <= 160 * 1024 && nw >= c->device_finish_min;
   const double t1 = now_ms();
-  st = run_windows(c, P, D, G, R.plans, R.pt_off, angles, n_ang_total, {}, nullptr,
+  st = run_windows(c, P, D, G, R.plans, R.pt_off, angles, n_ang_total, R.grid, nullptr,
                    R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend);
   if (st != CSM_OK) return st;
   R.fin = (const csm::FinishOut*)c->h_fin.p;
@@ -1190,10 +1195,11 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
 }
 
 int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
-                double* poses, double* covs, double* responses, int64_t* argmax_flat) {
+                double* poses, double* covs, double* responses, int64_t* argmax_flat,
+                const int32_t* scan_grid = nullptr) {
   if (P.type == CSM_FAST) return match_level_fast(c, n_scans, offsets, P, poses, covs, responses, argmax_flat);
   LevelRun R;
-  int st = level_begin(c, n_scans, offsets, P, poses, responses, argmax_flat, R);
+  int st = level_begin(c, n_scans, offsets, P, poses, responses, argmax_flat, R, scan_grid);
   if (st != CSM_OK) return st;
   return level_end(c, R, poses, covs, responses, argmax_flat);
 }
@@ -1203,7 +1209,8 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
 // completes the other half's previous level and plans its next one. Scans
 // are independent, so the split changes no result.
 int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
-                           int n_levels, double* poses, double* covs, double* sum) {
+                           int n_levels, double* poses, double* covs, double* sum,
+                           const int32_t* scan_grid = nullptr) {
   const int K = std::max(2, std::min(c->pipeline_parts, csm_ctx::kMaxParts));
   int32_t first[csm_ctx::kMaxParts], count[csm_ctx::kMaxParts];
   for (int h = 0; h < K; ++h) {
@@ -1216,7 +1223,7 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
     if (h > 0) c->swap_slot(h);
     const int32_t s0 = first[h];
     const int st = level_begin(c, count[h], offsets + s0, levels[l], poses + 3 * (size_t)s0,
-                               resp.data() + s0, nullptr, R[h]);
+                               resp.data() + s0, nullptr, R[h], scan_grid ? scan_grid + s0 : nullptr);
     if (h > 0) c->swap_slot(h);
     return st;
   };
@@ -1830,6 +1837,7 @@ int csm_load_scans(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t
   DeviceGuard g(c->device);
   int st;
   c->loaded_n = -1;
+  c->loaded_grid.clear();
   if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
   const int64_t n_total = n_scans > 0 ? offsets[n_scans] - offsets[0] : 0;
   if ((st = check_points(c, pts, n_total)) != CSM_OK) return st;
@@ -1858,13 +1866,18 @@ int csm_scan_matchers_loaded(csm_ctx* c, const csm_param levels[3], int32_t use_
   int st;
   bool fast = false;
   for (int l = 0; l < n_levels; ++l) fast |= levels[l].type == CSM_FAST;
+  const int32_t* grid = c->loaded_grid.empty() ? nullptr : c->loaded_grid.data();
+  for (int32_t s = 0; grid && s < n_scans; ++s)
+    if (grid[s] < 0 || grid[s] >= c->n_grids) return c->fail(CSM_ERR_INVALID_ARG, "scan grid outside the resident stack");
+  if (fast && grid) return c->fail(CSM_ERR_UNSUPPORTED, "FAST windows read grid 0 only");
   if (n_scans >= c->pipeline_min && !fast) {
     if ((st = match_levels_pipelined(c, n_scans, c->loaded_off.data(), levels, n_levels, poses, covs,
-                                     sum.data())) != CSM_OK)
+                                     sum.data(), grid)) != CSM_OK)
       return st;
   } else {
     for (int l = 0; l < n_levels; ++l) {
-      if ((st = match_level(c, n_scans, c->loaded_off.data(), levels[l], poses, covs, resp.data(), nullptr)) != CSM_OK)
+      if ((st = match_level(c, n_scans, c->loaded_off.data(), levels[l], poses, covs, resp.data(), nullptr,
+                            grid)) != CSM_OK)
         return st;
       for (int s = 0; s < n_scans; ++s) sum[(size_t)s] += resp[(size_t)s];
     }
@@ -2149,6 +2162,69 @@ int csm_optimize_update_cost(csm_ctx* c, const double* pts, int32_t n_points, co
   b[0] = r.v[7];
   b[1] = r.v[8];
   b[2] = r.v[9];
+  return CSM_OK;
+}
+
+int csm_load_scans_grids(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
+                         const int32_t* grid_index) {
+  int st = csm_load_scans(c, n_scans, pts, offsets);
+  if (st != CSM_OK || !grid_index) return st;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->loaded_grid.assign(grid_index, grid_index + n_scans);
+  return CSM_OK;
+}
+
+int csm_scan_matchers_batch_grids(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
+                                  const int32_t* grid_index, const csm_param levels[3], int32_t use_fine,
+                                  double* poses, double* covs, double* scores) {
+  if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
+  const int st = csm_load_scans_grids(c, n_scans, pts, offsets, grid_index);
+  if (st != CSM_OK) return st;
+  return csm_scan_matchers_loaded(c, levels, use_fine, poses, covs, scores);
+}
+
+int csm_set_grid_stack_gridmaps(csm_ctx* c, csm_gridmap* const* maps, int32_t n_maps) {
+  if (!c || !maps || n_maps <= 0) return CSM_ERR_INVALID_ARG;
+  std::vector<csm::GridMapView> v((size_t)n_maps);
+  for (int32_t i = 0; i < n_maps; ++i) {
+    if (!maps[i]) return CSM_ERR_INVALID_ARG;
+    const int st = csm::gridmap_view(maps[i], &v[(size_t)i]);
+    if (st != CSM_OK) return st;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const csm::GridMapView& a = v[0];
+  int32_t min_index = a.map_update_index;
+  for (const auto& b : v) {
+    if (b.device != c->device) return c->fail(CSM_ERR_INVALID_ARG, "map lives on another device");
+    if (b.size_x != a.size_x || b.size_y != a.size_y || b.resolution != a.resolution || b.offset_x != a.offset_x ||
+        b.offset_y != a.offset_y)
+      return c->fail(CSM_ERR_INVALID_ARG, "stacked maps must share size, resolution and offset");
+    min_index = std::min(min_index, b.map_update_index);
+  }
+  const int64_t ncell = (int64_t)a.size_x * a.size_y;
+  if (ncell >= ((int64_t)1 << 31)) return c->fail(CSM_ERR_INVALID_ARG, "grid larger than 2^31 cells");
+  hipError_t e;
+  if ((e = c->grid_buf.ensure((size_t)ncell * (size_t)n_maps * sizeof(float))) != hipSuccess)
+    return c->hip_fail(e, "hipMalloc(grid stack)");
+  for (int32_t i = 0; i < n_maps; ++i) {  // after each map's last update, on the matcher's stream
+    if ((e = hipStreamWaitEvent(c->stream, v[(size_t)i].ready, 0)) != hipSuccess ||
+        (e = hipMemcpyAsync((float*)c->grid_buf.p + (size_t)i * (size_t)ncell, v[(size_t)i].prob,
+                            (size_t)ncell * sizeof(float), hipMemcpyDeviceToDevice, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(map stack)");
+  }
+  c->info.resolution = a.resolution;
+  c->info.offset_x = a.offset_x;
+  c->info.offset_y = a.offset_y;
+  c->info.size_x = a.size_x;
+  c->info.size_y = a.size_y;
+  c->info.update_index = min_index;
+  c->d_grid = (const float*)c->grid_buf.p;
+  c->n_grids = n_maps;
+  c->has_grid = true;
+  c->int_checked = false;
+  c->key_cells = nullptr;
+  c->key_version = -1;
   return CSM_OK;
 }
 

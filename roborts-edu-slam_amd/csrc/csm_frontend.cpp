@@ -18,6 +18,7 @@
 #include "csm.h"
 #include "csm_frontend.h"
 #include "csm_gridmap.h"
+#include "csm_matchers.hpp"
 #include "host_math.hpp"
 
 namespace {
@@ -115,60 +116,6 @@ int create_all_maps(csm_frontend* f) {
   return CSM_OK;
 }
 
-// ScanMatchers::MapSizeCheck (scan_matchers.h:365-390)
-int map_size_check(csm_frontend* f, csm_gridmap* m, const double* pose, double offset) {
-  csm_gridmap_state s{};
-  int st = csm_gridmap_get_state(m, &s);
-  if (st != CSM_OK) return st;
-  // GetMapCoordsPose (scale_factor_ * w + scale_factor_ * offset) and GetCellLength
-  const double sc = s.scale_factor;
-  const double cx = sc * pose[0] + sc * s.offset_x, cy = sc * pose[1] + sc * s.offset_y;
-  const double max_size = (f->p.range_max + offset) / s.resolution;
-  int32_t inside = 0;
-  return csm_gridmap_update_bound(m, cx - max_size, cy - max_size, cx + max_size, cy + max_size, &inside);
-}
-
-// ScanMatchers::ScanMatch after MapSizeCheck (scan_matchers.h:189-288): the
-// optional Gauss-Newton matcher on the coarse map, the correlative coarse
-// level when it is off or failed, then fine and super-fine; all correlative
-// levels on the fine map. Returns the mean response in *score.
-int scan_matchers(csm_frontend* f, int32_t n, double pose[3], double cov[9], double* score, double* opt_cost) {
-  const csm_frontend_param& p = f->p;
-  int st;
-  *opt_cost = 0.0;
-  if (!p.use_optimize_scan_match) {  // the three correlative levels in one call
-    if ((st = csm_scan_matchers(f->ctx, f->fine_pts.data(), n, p.levels, 1, pose, cov, score)) != CSM_OK)
-      return f->fail(st, std::string("csm_scan_matchers: ") + csm_last_error(f->ctx));
-    return CSM_OK;
-  }
-  double sum = 0.0, process[3] = {pose[0], pose[1], pose[2]}, cost = 0.0, resp = 0.0;
-  int times = 0;
-  if ((st = csm_set_grid_gridmap(f->ctx_coarse, f->maps[CSM_COARSE_MAP])) != CSM_OK ||
-      (st = csm_optimize_scan_match(f->ctx_coarse, f->coarse_pts.data(), n, &p.optimize, process, &cost)) != CSM_OK)
-    return f->fail(st, std::string("csm_optimize_scan_match: ") + csm_last_error(f->ctx_coarse));
-  *opt_cost = cost;
-  sum = p.optimize_failed_cost / (cost + p.optimize_failed_cost);  // :211
-  times++;
-  if (cost > p.optimize_failed_cost) {  // :224-242: optimisation failed
-    sum = 0.0;
-    times--;
-    std::memcpy(process, pose, sizeof(process));
-    if ((st = csm_scan_match(f->ctx, f->fine_pts.data(), n, &p.levels[0], process, cov, &resp, nullptr)) != CSM_OK)
-      return f->fail(st, std::string("csm_scan_match(coarse): ") + csm_last_error(f->ctx));
-    sum += resp;
-    times++;
-  }
-  for (int k = 1; k <= 2; ++k) {  // fine, super-fine (:247-261)
-    if ((st = csm_scan_match(f->ctx, f->fine_pts.data(), n, &p.levels[k], process, cov, &resp, nullptr)) != CSM_OK)
-      return f->fail(st, std::string("csm_scan_match: ") + csm_last_error(f->ctx));
-    sum += resp;
-    times++;
-  }
-  std::memcpy(pose, process, sizeof(process));
-  *score = sum / times;  // :281
-  return CSM_OK;
-}
-
 }  // namespace
 
 extern "C" {
@@ -195,8 +142,7 @@ int csm_frontend_create(int device, const csm_frontend_param* param, csm_fronten
 int csm_frontend_destroy(csm_frontend* f) {
   if (!f) return CSM_OK;
   if (f->timing && f->n_timed > 0) {
-    static const char* names[6] = {"prepare", "map_size_check", "set_grid", "scan_matchers", "map_check",
-                                   "update_map"};
+    static const char* names[6] = {"prepare", "-", "-", "scan_matchers", "map_check", "update_map"};
     std::fprintf(stderr, "csm_frontend timing over %lld scans (ms/scan):", (long long)f->n_timed);
     for (int i = 0; i < 6; ++i) std::fprintf(stderr, " %s %.4f", names[i], f->t_phase[i] / f->n_timed);
     std::fprintf(stderr, "\n");
@@ -247,17 +193,14 @@ int csm_frontend_process(csm_frontend* f, const double* pts, int32_t n, const do
   if (!first) {
     if (p.use_odometry) predict_by_odom(f->current_pose, f->last_odom, odom, predict);
     double pose[3] = {predict[0], predict[1], predict[2]};
-    // ScanMatchers::ScanMatch (scan_matchers.h:179-289)
-    if ((st = map_size_check(f, f->maps[CSM_COARSE_MAP], pose, p.levels[0].search_space_size)) != CSM_OK)
-      return f->check(st, "MapSizeCheck(coarse)");
-    if ((st = map_size_check(f, f->maps[CSM_FINE_MAP], pose, p.levels[0].search_space_size)) != CSM_OK)
-      return f->check(st, "MapSizeCheck(fine)");
-    lap(1);
-    if ((st = csm_set_grid_gridmap(f->ctx, f->maps[CSM_FINE_MAP])) != CSM_OK)
-      return f->fail(st, std::string("csm_set_grid_gridmap: ") + csm_last_error(f->ctx));
-    lap(2);
+    // ScanMatchers::ScanMatch (scan_matchers.h:179-289) on the fine / coarse maps
+    csm::MatchersConfig cfg{p.levels, p.use_optimize_scan_match, p.optimize_failed_cost, p.optimize, p.range_max};
     double score = 0.0;
-    if ((st = scan_matchers(f, n, pose, cov, &score, &r->optimize_cost)) != CSM_OK) return st;
+    std::string why;
+    if ((st = csm::scan_matchers_on_maps(f->ctx, f->ctx_coarse, f->maps[CSM_COARSE_MAP], f->maps[CSM_FINE_MAP],
+                                         f->coarse_pts.data(), f->fine_pts.data(), n, cfg, 1, pose, cov, &score,
+                                         &r->optimize_cost, &why)) != CSM_OK)
+      return f->fail(st, why);
     std::memcpy(r->match_pose, pose, sizeof(pose));
     lap(3);
     // MapCheckPenalize (:573-595), use_logistic = false

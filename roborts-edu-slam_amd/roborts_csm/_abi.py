@@ -29,16 +29,19 @@ EXPORTED = (
     "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded",
     "csm_set_profiling", "csm_kernel_stats", "csm_sort_order",
     "csm_set_grid_stack", "csm_best_windows", "csm_optimize_scan_match", "csm_optimize_scan_match_batch",
-    "csm_optimize_update_cost",
+    "csm_optimize_update_cost", "csm_load_scans_grids", "csm_scan_matchers_batch_grids",
     # include/csm_gridmap.h
     "csm_gridmap_create", "csm_gridmap_destroy", "csm_gridmap_last_error",
     "csm_gridmap_set_options", "csm_gridmap_set_cell_params", "csm_gridmap_set_map_offset",
     "csm_gridmap_reset", "csm_gridmap_update_bound", "csm_gridmap_update_by_range", "csm_gridmap_init_with_range_vec",
     "csm_gridmap_feedback_penalty", "csm_gridmap_get_state", "csm_gridmap_download",
-    "csm_gridmap_device_prob", "csm_set_grid_gridmap",
+    "csm_gridmap_device_prob", "csm_set_grid_gridmap", "csm_set_grid_stack_gridmaps",
     # include/csm_frontend.h
     "csm_frontend_create", "csm_frontend_destroy", "csm_frontend_last_error", "csm_frontend_process",
     "csm_frontend_map",
+    # include/csm_backend.h
+    "csm_backend_create", "csm_backend_destroy", "csm_backend_last_error", "csm_backend_add_scan",
+    "csm_backend_set_scan_pose", "csm_backend_scan_match", "csm_backend_map",
 )
 
 PROBABILITY_CELL, COUNT_CELL = 0, 1
@@ -186,6 +189,17 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_frontend_last_error": (C.c_char_p, [C.c_void_p]),
         "csm_frontend_process": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, C.c_void_p]),
         "csm_frontend_map": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
+        "csm_load_scans_grids": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, _i32p]),
+        "csm_scan_matchers_batch_grids": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, _i32p, C.POINTER(CsmParam), C.c_int32,
+                                                    _dp, _dp, _dp]),
+        "csm_set_grid_stack_gridmaps": (C.c_int, [_ctx, C.POINTER(C.c_void_p), C.c_int32]),
+        "csm_backend_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
+        "csm_backend_destroy": (C.c_int, [C.c_void_p]),
+        "csm_backend_last_error": (C.c_char_p, [C.c_void_p]),
+        "csm_backend_add_scan": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, _i32p]),
+        "csm_backend_set_scan_pose": (C.c_int, [C.c_void_p, C.c_int32, _dp]),
+        "csm_backend_scan_match": (C.c_int, [C.c_void_p, C.c_void_p, _dp, C.c_void_p, C.c_int32]),
+        "csm_backend_map": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -1,5 +1,4 @@
-"""CPU: the C-ABI library loads, exports every symbol include/csm.h and
-include/csm_gridmap.h declare,
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declare,
 and its host-only entry points behave (no compute calls without a GPU)."""
 import ctypes as C
 import os
@@ -17,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared():
     names = set()
-    for h in ("csm.h", "csm_gridmap.h", "csm_frontend.h"):
+    for h in sorted(f for f in os.listdir(os.path.join(ROOT, "include")) if f.endswith(".h")):
         txt = open(os.path.join(ROOT, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         names |= set(re.findall(r"\b(csm_[a-z_0-9]+)\s*\(", txt))
