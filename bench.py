@@ -283,6 +283,100 @@ def online_bench(args, rank, world_size, dist, torch):
     }
 
 
+def backend_bench(args, rank, world_size, dist, torch):
+    """the back-end's ScanMatchInterface
+    (slam_processor.cpp:250-326) for a batch of pose-graph jobs per step —
+    --jobs near-chain links of a 1081-beam drive, each rebuilding its coarse
+    (8 cm) and fine (1 cm) back-end maps from a 10-scan chain, the 3-level
+    match on the fine map and the logistic PubMap check (simulatin_param.yaml
+    settings). One step = one batch. Replicas only (one back-end per rank)."""
+    from roborts_csm.backend import BackEndParam, ScanMatchService, job_results, make_jobs
+    from roborts_csm.gridmap import OccuGridMap
+    n_scans = 160
+    w = worlds_mod().make_world(1000, 1000, 0.05, seed=20261015)
+    st = worlds_mod().make_scan_stream(w, n_scans, seed=55 + rank)
+    prm = BackEndParam()
+    svc = ScanMatchService(prm, device=int(os.environ.get("LOCAL_RANK", "0")))
+    for k in range(n_scans):
+        svc.AddRangeData(st.points_m[k], st.true_poses[k])
+    pub = OccuGridMap(w.resolution, (w.size_x, w.size_y), w.offset, 0.0, 0.5, kind=1)
+    pub.set_options(True, False, 0.72, 0.2)
+    for k in range(n_scans):
+        pub.UpdateMapByRange(st.points_m[k] / w.resolution, st.true_poses[k])
+    rng = np.random.default_rng(3)
+    J = args.jobs
+    qs = list(range(n_scans - J, n_scans))
+    chains = [list(range(q - 20, q - 1, 2)) for q in qs]  # sparse 10-scan chains (LinkNearChains :131-146)
+    init = [st.true_poses[q] + rng.normal(size=3) * [0.05, 0.05, 0.02] for q in qs]
+    cur = st.true_poses[-1]
+    queries = [st.points_m[q] for q in qs]
+
+    def step():
+        return svc.scan_match_jobs(queries, chains, init, cur, pub)
+
+    for _ in range(args.warmup):
+        step()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # the same jobs one call at a time (the reference's calling pattern)
+    t1 = time.perf_counter()
+    for j in range(J):
+        svc.scan_match_jobs([queries[j]], [chains[j]], [init[j]], cur, pub)
+    seq = time.perf_counter() - t1
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    err = [float(np.hypot(*(r.pose[:2] - st.true_poses[q][:2]))) for r, q in zip(res, qs)]
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu:
+        import pyoracle as O
+        opub = O.GridMap(1, w.resolution, (w.size_x, w.size_y), w.offset, 0.0, 0.5)
+        opub.set_options(True, False, 0.72, 0.2)
+        for k in range(n_scans):
+            opub.update_by_range(st.points_m[k] / w.resolution, st.true_poses[k])
+        obe = O.BackEnd(prm.to_c())
+        for k in range(n_scans):
+            obe.add_scan(st.points_m[k], st.true_poses[k])
+        tc = time.perf_counter()
+        m = 0
+        while m < J and (m < 2 or time.perf_counter() - tc < args.cpu_seconds):
+            arr = make_jobs([queries[m]], [chains[m]], [init[m]])
+            obe.scan_match(arr, 1, cur, opub)
+            m += 1
+        dtc = time.perf_counter() - tc
+        cpu = {"value": m / dtc, "unit": "jobs/s", "cores": 1, "kind": "port",
+               "sample": f"{m} of the same jobs through the oracle's restatement of ScanMatchInterface "
+                         f"(oracle/map_oracle.cpp), single-threaded, {dtc:.1f} s on {_cpu_model()}"}
+    return {
+        "metric": "back-end ScanMatchInterface jobs/sec (f2: map pair rebuild from a 10-scan chain + 3-level "
+                  "match + logistic map check)",
+        "value": world_size * J * args.steps / elapsed, "unit": "jobs/s", "n_gpus": world_size,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic drive in the seeded 1000x1000 @5cm world; ray-cast 1081-beam scans at true poses",
+        "config": {"workload": f"backend: {J} near-chain jobs per step, simulatin_param.yaml (fine 1 cm, coarse "
+                               f"8 cm, U=100)", "parallelism": f"replicas x{world_size}",
+                   "sequential_jobs_per_s": J / seq, "median_pose_error_m": float(np.median(err))},
+        "roofline": None, "cpu_baseline": cpu,
+    }
+
+
+def worlds_mod():
+    from roborts_csm import worlds
+    return worlds
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -291,9 +385,11 @@ def main():
     ap.add_argument("--scans", type=int, default=4096, help="scans per GPU per step")
     ap.add_argument("--levels", choices=["headline", "sim"], default="headline",
                     help="headline: every beam summed (B=1081); sim: reference YAML U=100 (B=109)")
-    ap.add_argument("--workload", choices=["config2", "loop_closure", "willow", "online"], default="config2",
+    ap.add_argument("--workload", choices=["config2", "loop_closure", "willow", "online", "backend"],
+                    default="config2",
                     help="config2: the headline front-end batch; loop_closure: config 3; willow: config 4; "
-                         "online: config 5 (steps = scans)")
+                         "online: config 5 (steps = scans); backend: f2 pose-graph jobs")
+    ap.add_argument("--jobs", type=int, default=16, help="backend: ScanMatchInterface jobs per step")
     ap.add_argument("--window-m", type=float, default=20.0, help="willow: window edge (m)")
     ap.add_argument("--submaps", type=int, default=512, help="loop_closure: submaps in total")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -317,8 +413,9 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
 
-    if args.workload in ("loop_closure", "willow", "online"):
-        fn = {"loop_closure": loop_closure_bench, "willow": willow_bench, "online": online_bench}[args.workload]
+    if args.workload in ("loop_closure", "willow", "online", "backend"):
+        fn = {"loop_closure": loop_closure_bench, "willow": willow_bench, "online": online_bench,
+              "backend": backend_bench}[args.workload]
         out = fn(args, rank, world_size, dist, torch)
         if rank == 0:
             print(json.dumps(out))
