@@ -489,10 +489,16 @@ struct csm_ctx {
   // Second set of per-launch buffers: the 3-level driver keeps two halves of
   // a batch in flight (match_levels_pipelined); swap_slot() exchanges the
   // sets so run_windows works on whichever half is current.
+  // Optionally each part has its own kernel stream (CSM_PART_STREAMS=1), so one
+  // part's finish (a few latency-bound blocks) can overlap the next part's scoring.
   struct Slot {
     DevBuf scans, angles, scores, partials, best, fin;
     HostBuf h_scores, h_fin, h_angles, h_sw;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr, ev_in = nullptr, ev_k = nullptr;
+    // null (default): the part shares csm_ctx::stream. CSM_PART_STREAMS=1 gives each part its
+    // own stream; measured slower on config 2 (6.23 vs 5.96 ms per step: two concurrent
+    // box-kernel launches contend for L2 and the coarse launch goes 1.01 -> 1.57 ms).
+    hipStream_t stream = nullptr;
   };
   static constexpr int kMaxParts = 4;
   Slot alt[kMaxParts - 1];
@@ -516,7 +522,9 @@ struct csm_ctx {
     std::swap(ev_done, a.ev_done);
     std::swap(ev_in, a.ev_in);
     std::swap(ev_k, a.ev_k);
+    if (a.stream) std::swap(stream, a.stream);
   }
+  hipEvent_t ev_fork = nullptr;  // the pipelined driver's part streams start after the main stream
   std::vector<csm_kernel_stat> stats;
   void account(const char* name, float ms, double bytes, double scorings) {
     for (auto& s : stats)
@@ -601,6 +609,8 @@ int ensure_int_grid(csm_ctx* c) {
     if ((e = csm::launch_fixed_point(c->d_grid + gi * cells1, c->info.size_x, c->info.size_y, pitch, c->outside, E,
                                      (int32_t*)c->gridi.p + gi * ni, c->stream)) != hipSuccess)
       return c->hip_fail(e, "fixed_point_kernel");
+  // other parts' streams read gridi next (match_levels_pipelined)
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(gridi)");
   c->pitch = pitch;
   c->int_exp = E;
   c->int_max_abs = vmax;
@@ -1219,6 +1229,11 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
   }
   std::vector<double> resp((size_t)n_scans, 0.0);
   LevelRun R[csm_ctx::kMaxParts];
+  hipError_t he;  // part streams start after everything already on the main stream (grid, points)
+  if ((he = hipEventRecord(c->ev_fork, c->stream)) != hipSuccess) return c->hip_fail(he, "hipEventRecord(fork)");
+  for (int h = 1; h < K; ++h)
+    if (c->alt[h - 1].stream && (he = hipStreamWaitEvent(c->alt[h - 1].stream, c->ev_fork, 0)) != hipSuccess)
+      return c->hip_fail(he, "hipStreamWaitEvent(fork)");
   auto begin = [&](int l, int h) {
     if (h > 0) c->swap_slot(h);
     const int32_t s0 = first[h];
@@ -1640,6 +1655,10 @@ int csm_create(int device, csm_ctx** out) {
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
   bool ev_ok = true;
+  const char* ps = std::getenv("CSM_PART_STREAMS");
+  if (ps && std::atoi(ps) != 0)
+    for (auto& a : c->alt) ev_ok = ev_ok && hipStreamCreateWithFlags(&a.stream, hipStreamNonBlocking) == hipSuccess;
+  ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
   for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k})
     ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
   for (auto& a : c->alt)
@@ -1662,6 +1681,8 @@ int csm_destroy(csm_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->h2d);
     (void)hipStreamSynchronize(c->d2h);
+    for (auto& a : c->alt)
+      if (a.stream) (void)hipStreamSynchronize(a.stream);
     c->grid_buf.release();
     c->gridi.release();
     c->gstats.release();
@@ -1694,7 +1715,9 @@ int csm_destroy(csm_ctx* c) {
       a.h_sw.release();
       for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k})
         if (ev) (void)hipEventDestroy(ev);
+      if (a.stream) (void)hipStreamDestroy(a.stream);
     }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k})
       if (ev) (void)hipEventDestroy(ev);
     (void)hipStreamDestroy(c->h2d);
