@@ -242,8 +242,10 @@ void host_sort_finish(const double* scores, const Dims& D, const CandGeom& C, co
 // Everything BasedCorrelationScanMatch::ScanMatch does once the sorted
 // candidates are summarised in `o` (correlate_scan_matcher.h:700-707,
 // 835-869, covariance :887-1019). Returns the response.
+// skip_lists: covariances a later level overwrites (live_lists) are not
+// computed; their lists were not filled.
 double complete_window(const csm::FinishOut& o, const CandGeom& C, const csm_param& P,
-                       const Geometry& G, double pose[3], double cov[9]) {
+                       const Geometry& G, double pose[3], double cov[9], int skip_lists = 0) {
   const double best_score = o.best_score;
   const double best_x = o.best_x, best_y = o.best_y;
   double best_a = C.a(o.front_idx).angle;
@@ -299,16 +301,17 @@ double complete_window(const csm::FinishOut& o, const CandGeom& C, const csm_par
     }
     cov[8] = (norm > kDoubleTolerance) ? acc / norm : 200 * max_ang_var;
   };
+  const bool pos = !(skip_lists & 1), ang = !(skip_lists & 2);
   switch (P.type) {
     case CSM_COARSE:
-      positional();
-      angular();
+      if (pos) positional();
+      if (ang) angular();
       break;
     case CSM_FINE:
-      positional();
+      if (pos) positional();
       break;
     case CSM_SUPER:
-      angular();
+      if (ang) angular();
       break;
     default:
       break;
@@ -503,6 +506,7 @@ struct csm_ctx {
   static constexpr int kMaxParts = 4;
   Slot alt[kMaxParts - 1];
   int pipeline_min = 512;    // fewest scans the 3-level driver splits into parts (CSM_PIPELINE)
+  bool skip_dead_lists = true;  // live_lists (CSM_SKIP_DEAD_LISTS=0: every level fills both lists)
   int pipeline_parts = 2;    // parts in flight (CSM_PIPELINE_PARTS: 2..kMaxParts; 2 measured fastest)
   void swap_slot(int i) {    // i >= 1: exchange the current buffer set with alt[i - 1]
     Slot& a = alt[i - 1];
@@ -662,7 +666,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                 const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
                 const AngleEntry* angles, size_t n_angle_entries,
                 const std::vector<int32_t>& grid_index, BestPartial* best_out,
-                Finish mode = Finish::kScoresToHost, PendingRun* pend = nullptr) {
+                Finish mode = Finish::kScoresToHost, PendingRun* pend = nullptr, int skip_lists = 0) {
   if (best_out) mode = Finish::kBest;
   const int nw = (int)plans.size();
   if (nw == 0) return CSM_OK;
@@ -837,6 +841,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       A.n_space = D.n_space;
       A.step_cells = L.step_cells;
       A.lin_tol = P.search_space_resolution / G.mres;
+      A.skip_lists = skip_lists;
       const size_t fbytes = (size_t)nw * sizeof(csm::FinishOut);
       // + one "needs the exact sort" flag per window (fast finish, csm_finish.hip)
       if ((e = c->fin.ensure(fbytes + (size_t)nw * sizeof(int32_t))) != hipSuccess) return c->hip_fail(e, "hipMalloc(finish)");
@@ -1105,13 +1110,32 @@ struct LevelRun {
   const csm::FinishOut* fin = nullptr;   // ditto (device finish)
   const double* scores = nullptr;        // ditto (host finish)
   bool dev = false;
+  int skip_lists = 0;  // live_lists
   PendingRun pend;
 };
 
+// Which covariance lists of level l a caller of the 3-level driver can see,
+// as the finish's skip mask (bit 0 positional, bit 1 angular: skipped).
+// ComputePositionalCovariance resets the whole matrix (correlate_scan_matcher.h:891)
+// and ComputeAngularCovariance writes (2,2) only (:1018), by type (:835-858); a
+// later level that writes the same entries makes this level's value dead (the
+// reference's coarse covariance is always overwritten by the fine level).
+int live_lists(const csm_param* levels, int n_levels, int l) {
+  auto pos = [](int t) { return t == CSM_COARSE || t == CSM_FAST || t == CSM_FINE; };
+  auto ang = [](int t) { return t == CSM_COARSE || t == CSM_FAST || t == CSM_SUPER; };
+  int skip = 0;
+  for (int k = l + 1; k < n_levels; ++k) {
+    if (pos(levels[k].type)) return 3;
+    if (ang(levels[k].type)) skip |= 2;
+  }
+  return skip;
+}
+
 int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
                 const double* poses, double* responses, int64_t* argmax_flat, LevelRun& R,
-                const int32_t* scan_grid = nullptr) {
+                const int32_t* scan_grid = nullptr, int skip_lists = 0) {
   R.P = P;
+  R.skip_lists = skip_lists;
   R.scan_of.clear();
   R.grid.clear();
   int st = window_dims(P, R.D);
@@ -1157,7 +1181,7 @@ int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
           csm::finish_lds_bytes(D.n_cand) <= 160 * 1024 && nw >= c->device_finish_min;
   const double t1 = now_ms();
   st = run_windows(c, P, D, G, R.plans, R.pt_off, angles, n_ang_total, R.grid, nullptr,
-                   R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend);
+                   R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend, skip_lists);
   if (st != CSM_OK) return st;
   R.fin = (const csm::FinishOut*)c->h_fin.p;
   R.scores = (const double*)c->h_scores.p;
@@ -1195,7 +1219,7 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
       o = &local;
     }
     if (argmax_flat) argmax_flat[s] = o->front_idx;
-    responses[s] = complete_window(*o, C, P, G, poses + 3 * s, covs + 9 * s);
+    responses[s] = complete_window(*o, C, P, G, poses + 3 * s, covs + 9 * s, R.skip_lists);
   });
   if (c->profiling) {
     c->account("host:wait", (float)(t2 - t1), 0.0, 0.0);
@@ -1206,10 +1230,10 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
 
 int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
                 double* poses, double* covs, double* responses, int64_t* argmax_flat,
-                const int32_t* scan_grid = nullptr) {
+                const int32_t* scan_grid = nullptr, int skip_lists = 0) {
   if (P.type == CSM_FAST) return match_level_fast(c, n_scans, offsets, P, poses, covs, responses, argmax_flat);
   LevelRun R;
-  int st = level_begin(c, n_scans, offsets, P, poses, responses, argmax_flat, R, scan_grid);
+  int st = level_begin(c, n_scans, offsets, P, poses, responses, argmax_flat, R, scan_grid, skip_lists);
   if (st != CSM_OK) return st;
   return level_end(c, R, poses, covs, responses, argmax_flat);
 }
@@ -1238,7 +1262,8 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
     if (h > 0) c->swap_slot(h);
     const int32_t s0 = first[h];
     const int st = level_begin(c, count[h], offsets + s0, levels[l], poses + 3 * (size_t)s0,
-                               resp.data() + s0, nullptr, R[h], scan_grid ? scan_grid + s0 : nullptr);
+                               resp.data() + s0, nullptr, R[h], scan_grid ? scan_grid + s0 : nullptr,
+                               c->skip_dead_lists ? live_lists(levels, n_levels, l) : 0);
     if (h > 0) c->swap_slot(h);
     return st;
   };
@@ -1652,6 +1677,7 @@ int csm_create(int device, csm_ctx** out) {
     const int v = std::atoi(env);
     c->pipeline_min = v > 0 ? v : INT32_MAX;
   }
+  if (const char* env = std::getenv("CSM_SKIP_DEAD_LISTS")) c->skip_dead_lists = std::atoi(env) != 0;
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
   bool ev_ok = true;
@@ -1900,7 +1926,7 @@ int csm_scan_matchers_loaded(csm_ctx* c, const csm_param levels[3], int32_t use_
   } else {
     for (int l = 0; l < n_levels; ++l) {
       if ((st = match_level(c, n_scans, c->loaded_off.data(), levels[l], poses, covs, resp.data(), nullptr,
-                            grid)) != CSM_OK)
+                            grid, c->skip_dead_lists ? live_lists(levels, n_levels, l) : 0)) != CSM_OK)
         return st;
       for (int s = 0; s < n_scans; ++s) sum[(size_t)s] += resp[(size_t)s];
     }

@@ -417,7 +417,8 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     // stage 1: FindBest's prefix and the positional list's 20
     // (small windows sort whole: the limits' extra passes cost more there)
     const bool full = sh->nan || A.order_out != nullptr || n < kPartialMinCand;
-    sh->plim = full ? n : min(n, max(sh->cnt_a, kCovPoints));
+    const int need = (A.skip_lists & 1) ? 1 : kCovPoints;  // the positional list reads 20
+    sh->plim = full ? n : min(n, max(sh->cnt_a, need));
   }
   __syncthreads();
   auto run_levels = [&]() {
@@ -528,11 +529,12 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     const bool ey = dy < 0.0 ? dy >= -fabs(tol) : dy <= fabs(tol);
     return ex && ey;
   };
+  const bool want_pos = !(A.skip_lists & 1), want_ang = !(A.skip_lists & 2);
   // Stage 2: the angular list reads the sorted order of every element with
   // score >= bound while it still needs near-best ones: all of them when at
   // most 20 are near the best, else up to the 20th near one in sorted order,
   // i.e. every element scoring at least the 20th largest near-best score.
-  {
+  if (want_ang) {  // uniform over the block
     int cm = 0, cr = 0;
     for (int i = threadIdx.x; i < n; i += 64 * kWaves) {
       const double x = keys[i];
@@ -593,7 +595,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
   // positional list (:915-928): the sorted prefix with score > bound, <= 20
   {
     int npos = 0;
-    for (int base = 0; base < n && npos < kCovPoints; base += 64) {
+    for (int base = 0; want_pos && base < n && npos < kCovPoints; base += 64) {
       const int p = base + lane;
       const bool ok = p < n && keys[p] > bound;
       const uint64_t m = __ballot(ok);
@@ -610,7 +612,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
   // angular list (:990-1003): score >= bound and (x, y) within lin_tol of the best
   {
     int nang = 0;
-    for (int base = 0; base < n && nang < kCovPoints; base += 64) {
+    for (int base = 0; want_ang && base < n && nang < kCovPoints; base += 64) {
       const int p = base + lane;
       bool ok = false;
       bool above = false;
@@ -733,9 +735,11 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     }
   }
   __syncthreads();
-  // 2. the smallest level whose cumulative count reaches 20 (or all > bound)
-  int L = kFastLevels - 1, cum = 0;
-  for (int k = 0; k < kFastLevels; ++k) {
+  // 2. the smallest level whose cumulative count reaches 20 (or all > bound);
+  // without the positional list, level 0 (exactly FindBest's prefix set)
+  const bool want_pos = !(A.skip_lists & 1), want_ang = !(A.skip_lists & 2);
+  int L = want_pos ? kFastLevels - 1 : 0, cum = 0;
+  for (int k = 0; want_pos && k < kFastLevels; ++k) {
     cum += cnt_s[k];
     if (cum >= kCovPoints) {
       L = k;
@@ -775,7 +779,7 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     }
     const double d = v - best;
     const bool inF = d < 0.0 ? d >= -1e-2 : d <= 1e-2;  // DoubleEqual(s, best, 1e-2)
-    if (eq > 1 && (inF || r <= kCovPoints)) flag_s = 1;
+    if (eq > 1 && (inF || (want_pos && r <= kCovPoints))) flag_s = 1;
     sk[r] = v;  // distinct ranks whenever nothing is flagged
     si[r] = ci[t];
   }
@@ -824,7 +828,7 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     o->best_x = sbx;
     o->best_y = sby;
     // positional list (:915-928): the sorted prefix with score > bound, <= 20
-    const int np = min(nC, kCovPoints);
+    const int np = want_pos ? min(nC, kCovPoints) : 0;
     for (int r = 0; r < np; ++r) {
       o->pos_idx[r] = si[r];
       o->pos_score[r] = sk[r];
@@ -833,6 +837,13 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   }
   __syncthreads();
   // 3. angular list (:990-1003): near the best, score >= bound
+  if (!want_ang) {
+    if (tid == 0) {
+      o->n_ang = 0;
+      *need = 0;
+    }
+    return;
+  }
   const double bx = sbx, by = sby, tol = A.lin_tol;
   for (int i0 = tid - lane; i0 < n; i0 += kFastThreads) {
     const int i = i0 + lane;

@@ -76,7 +76,10 @@ constexpr int64_t kFinishMaxCand = 10240;  // windows above this finish on the h
 struct FinishArgs {
   int64_t n_cand;
   int32_t n_space;
-  int32_t pad;
+  // Covariance lists nobody reads (bit 0: positional, bit 1: angular). In the
+  // 3-level driver a later level overwrites them (csm_api.cpp live_lists);
+  // the finish then decides and fills only FindBest's prefix and the rest.
+  int32_t skip_lists;
   double step_cells;   // res / map_resolution
   double lin_tol;      // search_space_resolution / map_resolution (:840,:852)
   int32_t* order_out;  // optional: the sorted permutation, n_cand per window

@@ -639,3 +639,40 @@ def test_pipelined_three_level_driver(world2000, finish, parts):
         assert st["host:wait"] == 3 * parts  # 3 levels x parts
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("order,use_fine", [((0, 1, 2), True), ((0, 1, 2), False), ((1, 0, 2), True),
+                                            ((0, 2, 1), True), ((2, 2, 0), True)])
+def test_dead_covariance_lists_skipped_exactly(world2000, order, use_fine):
+    """The 3-level driver fills only the covariance lists a later level does
+    not overwrite (live_lists: the fine level's ComputePositionalCovariance
+    resets the matrix, :891). Device finish + pipelined driver, the default
+    and CSM_SKIP_DEAD_LISTS=0, and odd level orders: all equal the oracle."""
+    import roborts_csm
+    from roborts_csm.params import SIM_YAML_LEVELS, headline_levels
+    w, b = world2000
+    base = headline_levels()
+    # level k takes the window of headline level k and the type of order[k]
+    levels = tuple(base[k].with_(correlation_scan_match_type=SIM_YAML_LEVELS[order[k]].correlation_scan_match_type)
+                   for k in range(3))
+    m = O.Map(w.grid, w.resolution, w.offset)
+    eye = np.tile(np.eye(3).reshape(1, 9), (b.init_poses.shape[0], 1))
+    s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells, b.offsets, levels, b.init_poses, eye.copy(),
+                                       use_fine=use_fine)
+    for skip in ("1", "0"):
+        os.environ["CSM_PIPELINE"] = "16"
+        os.environ["CSM_FINISH"] = "device"
+        os.environ["CSM_SKIP_DEAD_LISTS"] = skip
+        try:
+            c = roborts_csm.Context(0)
+        finally:
+            for k in ("CSM_PIPELINE", "CSM_FINISH", "CSM_SKIP_DEAD_LISTS"):
+                del os.environ[k]
+        try:
+            c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+            poses = np.ascontiguousarray(b.init_poses.copy())
+            covs = eye.copy()
+            s = c.scan_matchers_batch(b.points_cells, b.offsets, levels, poses, covs, use_fine=use_fine)
+            assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2), skip
+        finally:
+            c.close()
