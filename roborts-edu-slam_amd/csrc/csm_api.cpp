@@ -428,6 +428,12 @@ struct csm_ctx {
   // the kernels by events: a part's inputs go up while the other part's
   // kernels run, its results come down while the next kernels run.
   hipStream_t h2d = nullptr, d2h = nullptr;
+  // CSM_FINISH_STREAM=1: the device finish runs on a stream of its own, so one
+  // part's finish (latency-bound, a few blocks wide at its exact pass) can
+  // overlap the next part's scoring launch; its results go down only after it
+  // (ev_k on this stream). Opt-in: measured no faster on config 2 (5.72-6.41
+  // vs 5.78-6.19 ms/step interleaved, the host plan slows down under it).
+  hipStream_t fin_stream = nullptr;
   std::mutex mu;
   std::string err;
   float outside = 0.3f;  // kMapUnknownCellProb (slam/slam_processor.h:264)
@@ -458,6 +464,8 @@ struct csm_ctx {
   bool tile_kernel = false;   // CSM_KERNEL=v5 opts into the beam-tile kernel (exact; measured
                               // slower than v4 on config 2: 8.3 vs 7.0 ms, profiles/r01)
   int tile_beams = 8;         // beams per box of the beam-tile kernel (CSM_TILE_BEAMS: 4 or 8)
+  bool phase_kernel = true;   // v7 phase kernel for sub-cell window steps (CSM_KERNEL=v7 or unset)
+  int phase_margin_log2 = 20; // CSM_PHASE_MARGIN_LOG2 (tests: a wider margin sends more beams to the exact path)
   bool box_kernel = true;     // v6 box kernel for one-cell window steps; any CSM_KERNEL other
                               // than v6 turns it off (CSM_KERNEL=v4: the LDS-DMA row kernel)
   std::vector<float> h_pack;
@@ -660,6 +668,49 @@ int wait_run(csm_ctx* c, const PendingRun& p) {
   return CSM_OK;
 }
 
+// Phase buckets of a sub-cell window step f (csm_phase.hip): candidate j of a
+// beam with phase p = frac((lx + x0) + 0.5) reads column floor(p + j*f) past
+// the beam's cell; that changes only where p + j*f crosses an integer, at the
+// breakpoints ceil(j*f) - j*f. Breakpoints closer than 4 margins merge into
+// one cluster; each gap between clusters, shrunk by the margin on both sides,
+// is a bucket with fixed offsets ox[q][j]. Computed in long double, where
+// j*f and the differences are exact (f has 53 bits, j < 2^11).
+bool phase_table(double f, int ns, int margin_log2, csm::PhaseTable& T) {
+  T = csm::PhaseTable{};
+  if (!(f > 0.0 && f < 1.0) || ns < 1 || ns > csm::kPhaseMaxSpace) return false;
+  const long double M = std::ldexp(1.0L, -margin_log2);
+  std::vector<long double> bp = {0.0L, 1.0L};
+  for (int j = 0; j < ns; ++j) {
+    const long double jf = (long double)j * (long double)f;
+    bp.push_back(std::ceil(jf) - jf);
+  }
+  std::sort(bp.begin(), bp.end());
+  std::vector<std::pair<long double, long double>> cl;  // clusters [first, last]
+  for (long double b : bp) {
+    if (!cl.empty() && b - cl.back().second < 4 * M) cl.back().second = b;
+    else cl.push_back({b, b});
+  }
+  int cells = 0;
+  for (size_t i = 0; i + 1 < cl.size(); ++i) {
+    const long double lo = cl[i].second + M, hi = cl[i + 1].first - M;
+    if (!(hi > lo)) continue;
+    if (T.nq == csm::kPhaseMaxBuckets) return false;
+    const long double mid = (lo + hi) / 2;
+    for (int j = 0; j < ns; ++j) {
+      const long double o = std::floor(mid + (long double)j * (long double)f);
+      if (o < 0 || o > 15) return false;
+      T.ox[T.nq][j] = (int8_t)o;
+      cells = std::max(cells, (int)o + 1);
+    }
+    // rounded inwards: a phase the device accepts lies inside [lo, hi]
+    T.lo[T.nq] = std::nextafter((double)lo, 2.0);
+    T.hi[T.nq] = std::nextafter((double)hi, -1.0);
+    T.nq++;
+  }
+  T.cells = cells;
+  return T.nq > 0;
+}
+
 // With pend == nullptr the call returns once results are on the host; with
 // pend it returns as soon as the work is enqueued (join with wait_run).
 int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
@@ -719,10 +770,17 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const bool box = !tiles && use_int && c->box_kernel && f == 1.0 && csm::box_supported(D.n_space) &&
                    c->pitch >= c->info.size_x + csm::kGridiPadCols;
   if (box) rows_sq = 0;
+  // v7 phase kernel: sub-cell window step with an instantiated bucket shape
+  csm::PhaseTable PT{};
+  const bool phase = !tiles && !box && use_int && c->phase_kernel && f < 1.0 &&
+                     phase_table(f, D.n_space, c->phase_margin_log2, PT) &&
+                     csm::phase_supported(D.n_space, PT.cells, PT.nq) &&
+                     c->pitch >= c->info.size_x + csm::kGridiPadCols;
+  if (phase) rows_sq = 0;
   const int cpl = pick_cpl(D.n_cand);
   const int64_t per_block = (int64_t)csm::kBlock * cpl;
   const int64_t rows_groups = (rows_sq || tiles) ? 64 / D.n_space : 1;
-  const int64_t bps = box ? D.n_angles
+  const int64_t bps = (box || phase) ? D.n_angles
                       : (rows_sq || tiles) ? (D.n_angles + rows_groups - 1) / rows_groups
                       : v2    ? col_blocks * ktiles
                               : (D.n_cand + per_block - 1) / per_block;
@@ -791,6 +849,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   char kname[48];
   if (box)
     std::snprintf(kname, sizeof(kname), "score_box_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
+  else if (phase)
+    std::snprintf(kname, sizeof(kname), "score_phase_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (tiles)
     std::snprintf(kname, sizeof(kname), "score_tiles_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (rows_sq)
@@ -812,6 +872,10 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       e = csm::launch_score_box(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                 (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
                                 c->stream);
+    else if (phase)
+      e = csm::launch_score_phase(L, PT, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
+                                  c->stream);
     else if (tiles)
       e = csm::launch_score_tiles(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                   (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
@@ -848,14 +912,19 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       A.need_exact = c->fast_finish ? (int32_t*)((char*)c->fin.p + fbytes) : nullptr;
       if ((e = c->h_fin.ensure(fbytes + (size_t)nw * sizeof(int32_t))) != hipSuccess)
         return c->hip_fail(e, "hipHostMalloc(finish)");
+      // the finish stream starts after the scoring kernel (ev_k, re-recorded below
+      // once the finish is queued: a wait binds to the record before it)
+      hipStream_t fs = c->fin_stream ? c->fin_stream : c->stream;
+      if (fs != c->stream &&
+          ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(fs, c->ev_k, 0)) != hipSuccess))
+        return c->hip_fail(e, "finish stream event");
       if ((e = csm::launch_finish(A, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
-                                  (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw,
-                                  c->stream)) != hipSuccess)
+                                  (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw, fs)) != hipSuccess)
         return c->hip_fail(e, "finish_kernel");
-      if (c->profiling && (e = hipEventRecord(c->ev2, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+      if (c->profiling && (e = hipEventRecord(c->ev2, fs)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
       // with profiling on, the flags come back too: how many windows needed the exact sort
       const size_t cbytes = fbytes + ((c->profiling && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
-      if ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
+      if ((e = hipEventRecord(c->ev_k, fs)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
         return c->hip_fail(e, "kernels event");
       if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, cbytes, hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
         return c->hip_fail(e, "hipMemcpyAsync(finish)");
@@ -872,6 +941,10 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       e = csm::launch_score_box(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                 (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
                                 D.n_space, c->stream);
+    else if (phase)
+      e = csm::launch_score_phase(L, PT, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                  (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
+                                  D.n_space, c->stream);
     else if (tiles)
       e = csm::launch_score_tiles(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                   (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
@@ -1670,8 +1743,11 @@ int csm_create(int device, csm_ctx** out) {
     c->row_kernel = std::strcmp(env, "v1") != 0 && std::strcmp(env, "v2") != 0;
     c->row_dma = std::strcmp(env, "v3") != 0;
     c->tile_kernel = std::strcmp(env, "v5") == 0;
-    c->box_kernel = std::strcmp(env, "v6") == 0;
+    c->box_kernel = std::strcmp(env, "v6") == 0 || std::strcmp(env, "v7") == 0;
+    c->phase_kernel = std::strcmp(env, "v7") == 0;
   }
+  if (const char* env = std::getenv("CSM_PHASE_MARGIN_LOG2"))
+    c->phase_margin_log2 = std::max(2, std::min(std::atoi(env), 20));
   if (const char* env = std::getenv("CSM_TILE_BEAMS")) c->tile_beams = std::atoi(env) == 4 ? 4 : 8;
   if (const char* env = std::getenv("CSM_PIPELINE")) {  // 0: never split the 3-level batch
     const int v = std::atoi(env);
@@ -1684,6 +1760,9 @@ int csm_create(int device, csm_ctx** out) {
   const char* ps = std::getenv("CSM_PART_STREAMS");
   if (ps && std::atoi(ps) != 0)
     for (auto& a : c->alt) ev_ok = ev_ok && hipStreamCreateWithFlags(&a.stream, hipStreamNonBlocking) == hipSuccess;
+  const char* fsn = std::getenv("CSM_FINISH_STREAM");
+  if (!(ps && std::atoi(ps) != 0) && fsn && std::atoi(fsn) != 0)
+    ev_ok = ev_ok && hipStreamCreateWithFlags(&c->fin_stream, hipStreamNonBlocking) == hipSuccess;
   ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
   for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k})
     ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
@@ -1709,6 +1788,7 @@ int csm_destroy(csm_ctx* c) {
     (void)hipStreamSynchronize(c->d2h);
     for (auto& a : c->alt)
       if (a.stream) (void)hipStreamSynchronize(a.stream);
+    if (c->fin_stream) (void)hipStreamSynchronize(c->fin_stream);
     c->grid_buf.release();
     c->gridi.release();
     c->gstats.release();
@@ -1746,6 +1826,7 @@ int csm_destroy(csm_ctx* c) {
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k})
       if (ev) (void)hipEventDestroy(ev);
+    if (c->fin_stream) (void)hipStreamDestroy(c->fin_stream);
     (void)hipStreamDestroy(c->h2d);
     (void)hipStreamDestroy(c->d2h);
     (void)hipStreamDestroy(c->stream);

@@ -188,6 +188,21 @@ bool box_supported(int ns);
 hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                             const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
                             hipStream_t stream);
+// Phase kernel (v7, csm_phase.hip): INT mode, sub-cell window step f < 1.
+// A beam's cell offset for candidate j is floor(phase + j*f), constant over
+// each phase bucket; the host builds the buckets (csm_api.cpp phase_table).
+constexpr int kPhaseMaxBuckets = 8;
+constexpr int kPhaseMaxSpace = 16;
+struct PhaseTable {
+  int32_t nq;                                  // buckets in use (<= the kernel's NQ)
+  int32_t cells;                               // distinct offsets per axis: max ox + 1
+  double lo[kPhaseMaxBuckets], hi[kPhaseMaxBuckets];  // bucket q: lo[q] <= phase <= hi[q]
+  int8_t ox[kPhaseMaxBuckets][kPhaseMaxSpace]; // floor(phase + j*f) inside bucket q
+};
+bool phase_supported(int ns, int cells, int nq);
+hipError_t launch_score_phase(const LevelWork& L, const PhaseTable& T, const ScanWork* d_scans, const double* d_pts,
+                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
+                              hipStream_t stream);
 // gridi layout: row pitch = round4(size_x + kGridiPadCols) cells, size_y +
 // kGridiPadRows rows; every cell outside [0,size_x) x [0,size_y) is zero, so a
 // 16 x 16 box whose corner lies on the grid never leaves the buffer.

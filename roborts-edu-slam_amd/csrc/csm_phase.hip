@@ -1,0 +1,402 @@
+// csm_phase.hip — v7 "phase" scoring kernel: window levels whose step f is
+// below one map cell (the fine level of every shipped parameter set on a
+// 5 cm map: 11 steps of f = 0.4 cells).
+//
+// Candidate (j, k) of angle a reads, for beam b, cell
+// (trunc((lx + x_j) + 0.5), trunc((ly + y_k) + 0.5)) with x_j = x0 + j*f
+// (correlate_scan_matcher.h:569-572, :637-662). Write t = (lx + x0) + 0.5 =
+// X + phase (X = floor(t)). The column of candidate j is then
+// X + floor(phase + j*f): as the phase runs over [0, 1) the offsets change
+// only at the breakpoints ceil(j*f) - j*f, so inside a bucket q between two
+// breakpoints the columns are X + ox[q][j], fixed. A beam is thus a C x C box
+// of cells (C = max ox + 1) at corner (X, Y) plus a bucket pair (qx, qy), and
+// it adds box cell (ox[qy][k], ox[qx][j]) to candidate (j, k).
+//
+// So the kernel sums boxes per bucket pair — C*C cells per beam instead of
+// NS*NS candidate reads — and expands the pair sums to candidates once, at
+// the end. One wave per (window, angle):
+//   1. classify every beam (rotation, phases, buckets, margin test), count it
+//      into its pair, scatter its box corner into the pair's list in LDS
+//      (lists padded to whole groups of SL beams);
+//   2. walk the lists: lane (slot, cell) gathers one dword of its slot's beam
+//      box, one group of SL beams per wave instruction, kD groups in flight;
+//      at a pair boundary the slots' sums fold into accum[pair][cell];
+//   3. candidate (j, k) = sum over pairs of accum[pair][ox[qy][k]][ox[qx][j]].
+// Sums are exact integers over the fixed-point grid (gridi), so their order
+// is free (csm_set_grid). Rounding, as for the box kernel (csm_box.hip): the
+// computed t_j is within 2^-27 of T + j*f (T = lx + x0 + 0.5, real), so a
+// phase at least 2^-20 from every bucket edge gives trunc(t_j) =
+// X + floor(phase + j*f) exactly. Beams that fail (a phase inside a margin,
+// t < 0) are summed cell by cell with the reference's expressions.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "csm_device.hpp"
+#include "csm_internal.hpp"
+
+namespace csm {
+namespace {
+
+constexpr int kSeg = 576;            // beams classified per segment (lists in LDS)
+constexpr int kEntG = 5;             // groups per list entry: 6 slots * 5 * (2^26 - 1) < 2^31
+constexpr int kChunks = kSeg / 64;   // 64-beam chunks per segment, classified in registers
+#ifndef CSM_PHASE_DEPTH
+#define CSM_PHASE_DEPTH 16
+#endif
+constexpr int kD = CSM_PHASE_DEPTH;  // groups of loads in flight
+static_assert(kD <= 32, "int32 partial sums fold every kD groups");
+
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+
+template <int NS, int C, int NQ, bool BEST>
+__global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable T,
+                                                         const ScanWork* __restrict__ scans,
+                                                         const double2* __restrict__ pts,
+                                                         const AngleEntry* __restrict__ angles,
+                                                         double* __restrict__ out,
+                                                         BestPartial* __restrict__ partials) {
+  constexpr int NP = NQ * NQ;   // bucket pairs
+  constexpr int NPC = (C + 3) / 4;  // 16-byte pieces per box row
+  constexpr int CW = 4 * NPC;   // accumulated columns per box row (those >= C are never read)
+  constexpr int LPS = C * NPC;  // lanes per slot: one row piece each
+  constexpr int SL = 64 / LPS;  // beams (slots) per wave instruction
+  static_assert(LPS <= 64 && NP <= 64 && NS <= kPhaseMaxSpace && NQ <= kPhaseMaxBuckets, "layout");
+  // padded lists, whole kD blocks of groups and the issue-ahead slack
+  static_assert(SL * kEntG * ((1 << 26) - 1) < 2147483647LL, "an entry's int32 sums");
+  constexpr int kList = kSeg + NP * (SL - 1) + 2 * SL * kD + 64;
+  constexpr int kMaxGroups = kList / SL + 1;
+  constexpr int kMaxEnt = NP + (kSeg / SL + NP) / kEntG + 2;  // + the spare entry
+  constexpr int ECELLS = C * CW;                              // int32 sums per entry
+  __shared__ int32_t list[kList];
+  __shared__ int32_t cursor[NP];
+  __shared__ int32_t ngroups_s, nent_s;
+  __shared__ uint8_t gentry[kMaxGroups];  // list entry of each group
+  __shared__ int8_t ent_pair[kMaxEnt];    // bucket pair of each entry (-1: the spare)
+  __shared__ int32_t esum[kMaxEnt * ECELLS];
+  __shared__ int32_t dummy[64 * 4];       // per-lane target of the flushes between boundaries
+  __shared__ int8_t oxs[NQ][kPhaseMaxSpace];
+
+  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int win = bid / L.n_angles;
+  const int a = bid - win * L.n_angles;
+  const ScanWork S = scans[win];
+  const AngleEntry ae = angles[S.angle_off + a];
+  const int lane = threadIdx.x;
+  // lane (slot, box row cv, piece ch); lanes past SL slots repeat slot 0's
+  // row 0 piece 0 (same cache lines) and never fold into accum
+  const bool cact = lane < SL * LPS;
+  const int slot = cact ? lane / LPS : 0;
+  const int within = cact ? lane - slot * LPS : 0;
+  const int cv = within / NPC;  // box row (y offset)
+  const int ch = within - cv * NPC;
+  const double f = L.step_cells;
+  const double x_0 = S.x0 + 0 * f;  // :569 at j = 0
+  const double y_0 = S.y0 + 0 * f;  // :572 at k = 0
+  const int sx = L.size_x, sy = L.size_y;
+  const int pitch4 = L.pitch * 4;
+  const int zero_off = sy * pitch4;  // first of the zero rows
+  const double2* __restrict__ P = pts + S.pts_off;
+  const int step = S.step;
+  const int n_used = S.n_used;
+  const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
+  const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
+  const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)ghi << 32) | glo), (short)0, (int)(L.gridi_stride * 4), 0x00020000);
+  const int voff = cv * pitch4 + ch * 16;
+
+  for (int i = lane; i < NQ * kPhaseMaxSpace; i += 64) oxs[i / kPhaseMaxSpace][i % kPhaseMaxSpace] =
+      T.ox[i / kPhaseMaxSpace][i % kPhaseMaxSpace];
+
+  auto bucket = [&](double ph, bool& ok) -> int {
+    int q = 0;
+    bool hit = false;
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) {
+      const bool in = b < T.nq && ph >= T.lo[b] && ph <= T.hi[b];
+      q = in ? b : q;
+      hit |= in;
+    }
+    ok = ok && hit;
+    return q;
+  };
+  // Beam cb + lane (live below lim): its box offset and pair (pair < 0: it adds
+  // nothing here — not live, box wholly past the grid's high edges, or rejected).
+  auto classify = [&](const double2 p, int cb, int lim, double& lx, double& ly, bool& rejected) -> int2 {
+    lx = ae.cosine * p.x - ae.sine * p.y;  // :179
+    ly = ae.sine * p.x + ae.cosine * p.y;  // :180
+    const double tx = (lx + x_0) + 0.5;
+    const double ty = (ly + y_0) + 0.5;
+    bool ok = tx >= 0.0 && ty >= 0.0;
+    const double fx = tx - floor(tx);
+    const double fy = ty - floor(ty);
+    const int qx = bucket(fx, ok);
+    const int qy = bucket(fy, ok);
+    const bool live = cb + lane < lim;
+    rejected = live && !ok;
+    const int ix0 = ok ? (int)tx : 0;
+    const int iy0 = ok ? (int)ty : 0;
+    const bool use = live && ok && ix0 < sx && iy0 < sy;
+    return make_int2(use ? iy0 * pitch4 + ix0 * 4 : 0, use ? qx * NQ + qy : -1);
+  };
+  auto point = [&](int b) { return P[(int64_t)min(b, n_used - 1) * step]; };
+
+  // per lane: its candidates' box offsets in every bucket, 4 bits each
+  constexpr int NC = NS * NS;
+  constexpr int R = (NC + 63) / 64;
+  __syncthreads();  // oxs
+  uint32_t oxj[R], oyk[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = lane + 64 * r;
+    const int j = t < NC ? t / NS : 0;
+    const int k = t < NC ? t - j * NS : 0;
+    oxj[r] = 0;
+    oyk[r] = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      oxj[r] |= (uint32_t)oxs[q][j] << (4 * q);
+      oyk[r] |= (uint32_t)oxs[q][k] << (4 * q);
+    }
+  }
+  int64_t sum[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) sum[r] = 0;
+  const int lane_cell = (cv * CW + 4 * ch) * 4;  // byte offset of this lane's 4 sums in an entry
+
+  uint64_t slow = 0;  // bit c: 64-beam chunk c holds a rejected beam (bit 63: some chunk >= 63)
+  for (int s0 = 0; s0 < n_used; s0 += kSeg) {
+    const int s1 = min(n_used, s0 + kSeg);
+    // 1a. every point of the segment in flight at once, then classify into
+    // registers (offset, pair) and count per pair
+    double2 pq[kChunks];
+#pragma unroll
+    for (int u = 0; u < kChunks; ++u) pq[u] = point(s0 + 64 * u + lane);
+    if (lane < NP) cursor[lane] = 0;
+    __syncthreads();
+    int offr[kChunks], pairr[kChunks];
+#pragma unroll
+    for (int u = 0; u < kChunks; ++u) {
+      const int cb = s0 + 64 * u;
+      double lx, ly;
+      bool rej;
+      const int2 c = classify(pq[u], cb, s1, lx, ly, rej);
+      slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(rej) != 0) << min(cb >> 6, 63);
+      offr[u] = c.x;
+      pairr[u] = c.y;
+      if (c.y >= 0) atomicAdd(&cursor[c.y], 1);
+    }
+    __syncthreads();
+    // 1b. lists: pair p gets whole groups of SL beams, its groups split into
+    // entries of at most kEntG groups (an entry's sums fit int32)
+    {
+      const int cnt = lane < NP ? cursor[lane] : 0;
+      const int g = (cnt + SL - 1) / SL;
+      const int e = (g + kEntG - 1) / kEntG;
+      int gi_ = g, ei = e;  // inclusive scans over lanes
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int tg = __shfl_up(gi_, o, 64);
+        const int te = __shfl_up(ei, o, 64);
+        if (lane >= o) {
+          gi_ += tg;
+          ei += te;
+        }
+      }
+      const int g0p = gi_ - g, e0p = ei - e;
+      if (lane < NP) {
+        cursor[lane] = g0p * SL;
+        for (int k = 0; k < g; ++k) gentry[g0p + k] = (uint8_t)(e0p + k / kEntG);
+        for (int m = 0; m < e; ++m) ent_pair[e0p + m] = (int8_t)lane;
+      }
+      if (lane == NP - 1) {
+        ngroups_s = gi_;
+        nent_s = ei;
+        ent_pair[ei] = -1;  // the spare: groups past the lists
+      }
+    }
+    __syncthreads();
+    const int ngroups = __builtin_amdgcn_readfirstlane(ngroups_s);
+    const int nent = __builtin_amdgcn_readfirstlane(nent_s);
+    // Whole blocks of kD groups and no branch in the unrolled loop below, so
+    // the compiler keeps exactly kD loads in flight across iterations.
+    // Padding entries, the groups past the lists and the issue-ahead slack
+    // read the zero block; the groups past the lists go to the spare entry.
+    const int ng_pad = (ngroups + kD - 1) / kD * kD;
+    for (int i = lane; i < (ng_pad + kD) * SL; i += 64) list[i] = zero_off;
+    for (int i = ngroups + lane; i < ng_pad + kD; i += 64) gentry[i] = (uint8_t)nent;
+    for (int i = lane; i < (nent + 1) * ECELLS; i += 64) esum[i] = 0;
+    __syncthreads();
+    // 1c. scatter box corners into their pair's list
+#pragma unroll
+    for (int u = 0; u < kChunks; ++u)
+      if (pairr[u] >= 0) list[atomicAdd(&cursor[pairr[u]], 1)] = offr[u];
+    __syncthreads();
+    // 2. gather: group g = list entries g*SL .. g*SL + SL - 1 (slot s takes
+    // g*SL + s); one 16-byte row piece per lane (buffer_load_dwordx4: the TA
+    // coalesces a slot's row into its cache lines, a dword gather costs an
+    // access per lane). A lane's sums of the current entry are flushed into
+    // esum when the next group starts a new entry, branch-free: every group
+    // issues the four LDS adds, into the lane's dummy cells when no entry
+    // ends there.
+    if (ngroups > 0) {
+      v4i buf[kD];
+#pragma unroll
+      for (int j = 0; j < kD; ++j) {  // issued in order: the loop consumes buf[0] first
+        buf[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, list[j * SL + slot] + voff, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      int32_t part[4] = {0, 0, 0, 0};
+      int e_prev = __builtin_amdgcn_readfirstlane((int)gentry[0]);
+      const uint32_t esum_b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int32_t*)esum;
+      const uint32_t dummy_b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int32_t*)dummy + lane * 16;
+      int gev = gentry[lane & (kD - 1)];
+      for (int g0 = 0; g0 < ng_pad; g0 += kD) {
+        const int gev_next = gentry[g0 + kD + (lane & (kD - 1))];  // next block's entries
+#pragma unroll
+        for (int j = 0; j < kD; ++j) {
+          const int g = g0 + j;
+          const int ej = __builtin_amdgcn_readlane(gev, j);
+          const bool nb = ej != e_prev;  // uniform
+          // lanes past the slots always flush into their dummy cells
+          const uint32_t addr = (nb && cact) ? esum_b + (uint32_t)(e_prev * ECELLS * 4 + lane_cell) : dummy_b;
+          __attribute__((address_space(3))) int32_t* dst = (__attribute__((address_space(3))) int32_t*)(uintptr_t)addr;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) __hip_atomic_fetch_add(dst + t, part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) part[t] = nb ? 0 : part[t];
+          e_prev = ej;
+          v4i v = buf[j];
+          asm volatile("" : "+v"(v));  // consume group g here, in order
+          part[0] += v.x;
+          part[1] += v.y;
+          part[2] += v.z;
+          part[3] += v.w;
+          buf[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, list[(g + kD) * SL + slot] + voff, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        gev = gev_next;
+      }
+      if (cact) {
+        __attribute__((address_space(3))) int32_t* dst =
+            (__attribute__((address_space(3))) int32_t*)(uintptr_t)(esum_b + (uint32_t)(e_prev * ECELLS * 4 + lane_cell));
+#pragma unroll
+        for (int t = 0; t < 4; ++t) __hip_atomic_fetch_add(dst + t, part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    __syncthreads();
+    // 3a. this segment's entries into the candidates: candidate (j, k) takes
+    // box cell (ox[qy][k], ox[qx][j]) of every entry of pair (qx, qy)
+    for (int e = 0; e < nent; ++e) {
+      const int pr = __builtin_amdgcn_readfirstlane((int)ent_pair[e]);
+      const int qx = pr / NQ, qy = pr - (pr / NQ) * NQ;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int u = (oxj[r] >> (4 * qx)) & 15;
+        const int v = (oyk[r] >> (4 * qy)) & 15;
+        sum[r] += esum[e * ECELLS + v * CW + u];
+      }
+    }
+    __syncthreads();  // the next segment rewrites the lists and entries
+  }
+
+  // rejected beams, cell by cell with the reference's expressions
+  for (uint64_t m = slow; m != 0; m &= m - 1) {
+    const int c0 = (int)__builtin_ctzll(m);
+    const int c_end = c0 == 63 ? (n_used + 63) / 64 : c0 + 1;
+    for (int c = c0; c < c_end; ++c) {
+      const int cb = c * 64;
+      double lx, ly;
+      bool rej;
+      (void)classify(point(cb + lane), cb, n_used, lx, ly, rej);
+      for (uint64_t rm = __builtin_amdgcn_ballot_w64(rej); rm != 0; rm &= rm - 1) {
+        const int l = (int)__builtin_ctzll(rm);  // uniform: one beam for the whole wave
+        const double bx = dev::bcast_lane(lx, l);
+        const double by = dev::bcast_lane(ly, l);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int t = lane + 64 * r;
+          if (t < NC) {
+            const int j = t / NS, k = t - (t / NS) * NS;
+            const int gx = (int)((bx + (S.x0 + j * f)) + 0.5);
+            const int gy = (int)((by + (S.y0 + k * f)) + 0.5);
+            const bool in = (unsigned)gx < (unsigned)sx && (unsigned)gy < (unsigned)sy;
+            sum[r] += gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)sy * L.pitch];
+          }
+        }
+      }
+    }
+  }
+
+  double bs = -1.0e300;
+  int64_t bf = INT64_MAX;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = lane + 64 * r;
+    if (t < NC) {
+      const int j = t / NS, k = t - (t / NS) * NS;
+      const double accd = (double)(sum[r] + (int64_t)n_used * L.outside_i) * L.int_scale;
+      const double xj = S.x0 + j * f;  // :569
+      const double yk = S.y0 + k * f;  // :572
+      const double score = dev::penalized(L, S, accd, xj, yk, ae.angle);
+      const int64_t flat = ((int64_t)a * NS + j) * NS + k;
+      if (BEST) {
+        if (dev::better(score, flat, bs, bf)) {
+          bs = score;
+          bf = flat;
+        }
+      } else {
+        out[S.out_off + flat] = score;
+      }
+    }
+  }
+  if (BEST) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double os = __shfl_down(bs, o, 64);
+      const int64_t of = __shfl_down(bf, o, 64);
+      if (dev::better(os, of, bs, bf)) {
+        bs = os;
+        bf = of;
+      }
+    }
+    if (lane == 0) partials[(int64_t)win * L.blocks_per_scan + a] = BestPartial{bs, bf};
+  }
+}
+
+template <int NS, int C, int NQ>
+hipError_t launch_phase(const LevelWork& L, const PhaseTable& T, const ScanWork* s, const double2* p,
+                        const AngleEntry* an, double* out, BestPartial* part, unsigned nblk, hipStream_t stream) {
+  if (part)
+    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, true>), dim3(nblk), dim3(64), 0, stream, L, T, s, p, an, out,
+                       part);
+  else
+    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, false>), dim3(nblk), dim3(64), 0, stream, L, T, s, p, an,
+                       out, part);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// Instantiated shape: the fine level of the shipped parameter sets on a 5 cm
+// map (11 steps of 0.4 cells: 5 buckets, 5 x 5 boxes). Other sub-cell windows
+// use the row-segment kernel.
+bool phase_supported(int ns, int cells, int nq) { return ns == 11 && cells == 5 && nq == 5; }
+
+hipError_t launch_score_phase(const LevelWork& L, const PhaseTable& T, const ScanWork* d_scans, const double* d_pts,
+                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
+                              hipStream_t stream) {
+  const int64_t nblk = (int64_t)L.n_scans * L.n_angles;
+  if (nblk <= 0 || nblk > INT32_MAX || !L.int_mode || !(L.step_cells < 1.0) || L.blocks_per_scan != L.n_angles ||
+      L.pitch < L.size_x + kGridiPadCols || L.pitch % 4 != 0 || !phase_supported(ns, T.cells, T.nq) ||
+      T.cells > kGridiPadCols + 1)
+    return hipErrorInvalidValue;
+  for (int q = 0; q < T.nq; ++q)
+    for (int j = 0; j < ns; ++j)
+      if (T.ox[q][j] < 0 || T.ox[q][j] >= T.cells) return hipErrorInvalidValue;
+  const double2* p = reinterpret_cast<const double2*>(d_pts);
+  return launch_phase<11, 5, 5>(L, T, d_scans, p, d_angles, d_out, d_partials, (unsigned)nblk, stream);
+}
+
+}  // namespace csm

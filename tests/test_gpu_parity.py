@@ -232,9 +232,10 @@ def test_batch_three_level_bit_exact(ctx, world2000, which):
 
 
 def test_headline_runs_row_segment_kernels(ctx, world2000):
-    """The config-2 levels run on the box kernel (coarse: one-cell step) and the
-    LDS-DMA row-segment kernels (fine, super-fine), not a fallback, and the
-    device finish, and the result is the oracle's bit for bit."""
+    """The config-2 levels run on the box kernel (coarse: one-cell step), the
+    phase kernel (fine: 0.4-cell step) and the LDS-DMA row-segment kernel
+    (super-fine), not a fallback, and the device finish, and the result is the
+    oracle's bit for bit."""
     from roborts_csm.params import headline_levels
     w, b = world2000
     ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
@@ -245,7 +246,7 @@ def test_headline_runs_row_segment_kernels(ctx, world2000):
     s = ctx.scan_matchers_batch(b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(), poses, covs)
     names = {k["name"] for k in ctx.kernel_stats()}
     ctx.set_profiling(False)
-    for want in ("score_box_kernel<13,all>", "score_rowsd_kernel<11,2,all>",
+    for want in ("score_box_kernel<13,all>", "score_phase_kernel<11,all>",
                  "score_rowsd_kernel<3,1,all>", "finish_kernel<5070>"):
         assert want in names, names
     m = O.Map(w.grid, w.resolution, w.offset)
@@ -364,7 +365,7 @@ def test_kernel_variants_agree(f1, grid_kind):
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
     ctxs = []
-    for kern in ("v1", "v2", "v3", "v4", "v5", None):  # None: default (v6 box kernel / v4 where eligible)
+    for kern in ("v1", "v2", "v3", "v4", "v5", "v6", None):  # None: default (v6 box / v7 phase / v4 where eligible)
         if kern:
             os.environ["CSM_KERNEL"] = kern
         try:
@@ -676,3 +677,75 @@ def test_dead_covariance_lists_skipped_exactly(world2000, order, use_fine):
             assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2), skip
         finally:
             c.close()
+
+
+@pytest.mark.parametrize("margin_log2", [None, "5"])
+def test_phase_kernel_edge_beams(world2000, margin_log2):
+    """v7 phase kernel (sub-cell window step) on its margin cases: beams whose
+    phase sits on or near a bucket edge (origin points with window phases at
+    the breakpoints 0, 0.2, 0.4, ...), beams off the grid's low edge (negative
+    t) and past its high edges, windows at inexact step sums; with the default
+    2^-20 margin and with a 1/32 margin that sends ~half the beams down the exact
+    path. All scores and the argmax against the oracle and the v4 row kernel."""
+    import roborts_csm
+    from roborts_csm.params import SIM_YAML_LEVELS
+    w, b = world2000
+    m = O.Map(w.grid, w.resolution, w.offset)
+    pts = b.points_cells[b.offsets[0]:b.offsets[1]]
+    extra = np.array([[0.0, 0.0], [0.0, 0.0], [1.0, -2.0], [-1500.0, 3.0], [2.0, -1500.0],
+                      [900.0, 900.0], [-3000.0, -3000.0], [0.25, 0.0], [0.2, 0.6], [-0.4, 0.8]])
+    pts = np.ascontiguousarray(np.concatenate([pts, extra]))
+    lv = SIM_YAML_LEVELS[1].with_(use_point_size=pts.shape[0])
+    half = (lv.search_space_size / w.resolution) * 0.5
+    centers = [[100.5 + half, 200.5 + half, 0.0], [100.7 + half, 200.9 + half, 1.3],
+               [100.3 + half, 200.1 + half, -0.4],
+               [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
+               [1.2, 0.1, -2.5], [1998.0, 1990.0, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
+    ctxs = []
+    for kern in (None, "v4"):
+        if kern:
+            os.environ["CSM_KERNEL"] = kern
+        if margin_log2:
+            os.environ["CSM_PHASE_MARGIN_LOG2"] = margin_log2
+        try:
+            ctxs.append(roborts_csm.Context(0))
+        finally:
+            os.environ.pop("CSM_KERNEL", None)
+            os.environ.pop("CSM_PHASE_MARGIN_LOG2", None)
+    for c in ctxs:
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+    ctxs[0].set_profiling(True)
+    for cen in centers:
+        cen = np.array(cen)
+        want = O.score_window(m, pts, lv, cen, 11 * 11 * 11)
+        for c in ctxs:
+            assert np.array_equal(c.score_window(pts, lv, cen), want), cen
+            got = c.best_window(pts, lv, cen)
+            s, flat = O.best_window(m, pts, lv, cen)
+            assert got.score == s and got.flat_index == flat
+    names = {k["name"] for k in ctxs[0].kernel_stats()}
+    assert "score_phase_kernel<11,all>" in names and "score_phase_kernel<11,best>" in names, names
+    for c in ctxs:
+        c.close()
+
+
+def test_phase_kernel_batch_segments(world2000):
+    """Scans longer than one classification segment (1152 beams, every beam
+    summed) and short ones in one phase launch, against the oracle."""
+    from roborts_csm.params import SIM_YAML_LEVELS
+    import roborts_csm
+    w, b = world2000
+    m = O.Map(w.grid, w.resolution, w.offset)
+    rng = np.random.default_rng(5)
+    scans = [np.ascontiguousarray(np.concatenate([b.points_cells[b.offsets[k]:b.offsets[k + 1]]] * r))
+             for k, r in ((0, 3), (1, 1), (2, 2))]
+    scans.append(rng.uniform(-60, 60, size=(7, 2)))
+    c = roborts_csm.Context(0)
+    try:
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+        for pts in scans:
+            lv = SIM_YAML_LEVELS[1].with_(use_point_size=pts.shape[0])
+            cen = O.world_to_map(m, b.init_poses[0])
+            assert np.array_equal(c.score_window(pts, lv, cen), O.score_window(m, pts, lv, cen, 1331))
+    finally:
+        c.close()
