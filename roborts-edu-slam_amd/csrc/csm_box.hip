@@ -181,14 +181,20 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
       // otherwise (one dependent load per 64 beams)
       double2 pq[kPF];
 #pragma unroll
-      for (int u = 0; u < kPF; ++u) pq[u] = point(s0 + 64 * u);
+      for (int u = 0; u < kPF; ++u) {  // issued in the order the loop consumes them
+        pq[u] = point(s0 + 64 * u);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       for (int cb0 = s0; cb0 < s1; cb0 += 64 * kPF) {
 #pragma unroll
         for (int u = 0; u < kPF; ++u) {
+          // no early exit: a chunk at or past s1 adds no run (live is false for
+          // every lane), and an exit here made the compiler drain vmcnt(0) per
+          // chunk instead of keeping kPF chunks of points in flight
           const int cb = cb0 + 64 * u;
-          if (cb >= s1) break;
           const double2 pcur = pq[u];
           pq[u] = point(cb + 64 * kPF);
+          __builtin_amdgcn_sched_barrier(0);
           const int off = offsets(pcur, cb, slow);
           const bool live = cb + lane < s1;
           // previous beam's corner (lane 0: none)

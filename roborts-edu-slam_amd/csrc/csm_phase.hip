@@ -74,7 +74,7 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
   __shared__ uint8_t gentry[kMaxGroups];  // list entry of each group
   __shared__ int8_t ent_pair[kMaxEnt];    // bucket pair of each entry (-1: the spare)
   __shared__ int32_t esum[kMaxEnt * ECELLS];
-  __shared__ int32_t dummy[64 * 4];       // per-lane target of the flushes between boundaries
+  __shared__ int32_t dummy[64 * 4 + 4];   // per-lane target of the flushes between boundaries
   __shared__ int8_t oxs[NQ][kPhaseMaxSpace];
 
   const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
@@ -250,7 +250,10 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
       int32_t part[4] = {0, 0, 0, 0};
       int e_prev = __builtin_amdgcn_readfirstlane((int)gentry[0]);
       const uint32_t esum_b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int32_t*)esum;
-      const uint32_t dummy_b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int32_t*)dummy + lane * 16;
+      // lane l's four dummy cells at dword 4l + (l >> 4): the 64 lanes of each
+      // of the four adds hit 64 distinct banks (4l alone is a 4-way conflict)
+      const uint32_t dummy_b =
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int32_t*)dummy + lane * 16 + (lane >> 4) * 4;
       int gev = gentry[lane & (kD - 1)];
       for (int g0 = 0; g0 < ng_pad; g0 += kD) {
         const int gev_next = gentry[g0 + kD + (lane & (kD - 1))];  // next block's entries
