@@ -46,7 +46,7 @@ constexpr int kWaves = 4;
 // stage's limit to the 20th near-best score (20 block-wide rounds) instead of
 // every element >= bound.
 #ifndef CSM_PARTIAL_MIN
-#define CSM_PARTIAL_MIN 2048
+#define CSM_PARTIAL_MIN 256
 #endif
 #ifndef CSM_NEAR_ROUNDS
 #define CSM_NEAR_ROUNDS 0
@@ -57,6 +57,22 @@ constexpr bool kNearRounds = CSM_NEAR_ROUNDS != 0;
 struct Seg {
   int32_t first, last, depth;
 };
+
+// CSM_FINISH_TRACE builds: wall-clock stamps of the exact pass's phases for
+// the first kTraceWindows windows that take it (tools/finish_trace.py).
+#ifdef CSM_FINISH_TRACE
+constexpr int kTraceWindows = 256;
+__device__ unsigned long long g_trace[kTraceWindows][10];
+__device__ int g_trace_n;
+#define CSM_STAMP(i)                                          \
+  do {                                                        \
+    if (threadIdx.x == 0 && tr >= 0) g_trace[tr][i] = wall_clock64(); \
+  } while (0)
+#else
+#define CSM_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
 
 struct WaveScratch {      // per-wave LDS scratch of the register sort
   uint8_t T[72], U[72];   // lane of the k-th right / left stop
@@ -188,6 +204,10 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 // ---- large segments: one wave, LDS -------------------------------------------
 // Parallel std::__unguarded_partition(first+1, last, pivot=first). lpos/rpos
 // are the window-sized scratch arrays; this segment uses [first, first+cap).
+// Every pass takes kU chunks of 64 per iteration, their LDS reads issued
+// together (one wave works a segment alone: nothing else hides the latency);
+// ranks are still assigned chunk by chunk in order.
+constexpr int kU = 4;
 __device__ int partition_lds(double* k, uint16_t* v, uint16_t* lpos_all, uint16_t* rpos_all,
                              int first, int last) {
   const int lane = lane_id();
@@ -197,43 +217,95 @@ __device__ int partition_lds(double* k, uint16_t* v, uint16_t* lpos_all, uint16_
   uint16_t* rpos = rpos_all + first - 1;
   const double P = k[first];
   int totR = 0;
-  for (int base = first + 1; base < last; base += 64) {
-    const int p = base + lane;
-    const bool ok = p < last;
-    const bool isR = ok && !gt(P, ok ? k[p] : 0.0);
-    totR += popc(__ballot(isR));
+  for (int base = first + 1; base < last; base += 64 * kU) {
+    double key[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = base + 64 * u + lane;
+      key[u] = p < last ? k[p] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = base + 64 * u + lane;
+      totR += popc(__ballot(p < last && !gt(P, key[u])));
+    }
   }
   int cntL = 0, cntR = 0;
-  for (int base = first + 1; base < last; base += 64) {
-    const int p = base + lane;
-    const bool ok = p < last;
-    const double key = ok ? k[p] : 0.0;
-    const bool isL = ok && !gt(key, P);
-    const bool isR = ok && !gt(P, key);
-    const uint64_t mL = __ballot(isL), mR = __ballot(isR);
-    const int rl = cntL + popc(mL & below_mask(lane)) + 1;
-    const int rr = totR - (cntR + popc(mR & below_mask(lane))) ;  // rank from the right
-    if (isL && rl <= cap) lpos[rl] = (uint16_t)p;
-    if (isR && rr <= cap) rpos[rr] = (uint16_t)p;
-    cntL += popc(mL);
-    cntR += popc(mR);
+  for (int base = first + 1; base < last; base += 64 * kU) {
+    double key[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = base + 64 * u + lane;
+      key[u] = p < last ? k[p] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = base + 64 * u + lane;
+      const bool ok = p < last;
+      const bool isL = ok && !gt(key[u], P);
+      const bool isR = ok && !gt(P, key[u]);
+      const uint64_t mL = __ballot(isL), mR = __ballot(isR);
+      const int rl = cntL + popc(mL & below_mask(lane)) + 1;
+      const int rr = totR - (cntR + popc(mR & below_mask(lane)));  // rank from the right
+      if (isL && rl <= cap) lpos[rl] = (uint16_t)p;
+      if (isR && rr <= cap) rpos[rr] = (uint16_t)p;
+      cntL += popc(mL);
+      cntR += popc(mR);
+    }
   }
   const int totL = cntL;
   const int kmax = min(min(totL, totR), cap);
+  // the pairs (l_k < r_k) are a prefix of the ranks: l_k rises, r_k falls
   int npairs = 0;
-  for (int kb = 1; kb <= kmax; kb += 64) {
-    const int kk = kb + lane;
-    const bool okp = kk <= kmax && lpos[kk] < rpos[kk];
-    const uint64_t mk = __ballot(okp);
-    npairs += popc(mk);
-    if (mk != ~0ull) break;
+  bool open = true;
+  for (int kb = 1; open && kb <= kmax; kb += 64 * kU) {
+    int lp[kU], rp[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int kk = kb + 64 * u + lane;
+      lp[u] = kk <= kmax ? (int)lpos[kk] : 0;
+      rp[u] = kk <= kmax ? (int)rpos[kk] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int kk = kb + 64 * u + lane;
+      const uint64_t mk = __ballot(kk <= kmax && lp[u] < rp[u]);
+      if (open) npairs += popc(mk);
+      open = open && mk == ~0ull;
+    }
   }
   int cut = INT32_MAX;
   if (npairs + 1 <= totL) cut = lpos[npairs + 1];
   if (npairs >= 1) cut = min(cut, (int)rpos[npairs]);
-  for (int kb = 1; kb <= npairs; kb += 64) {
-    const int kk = kb + lane;
-    if (kk <= npairs) swap_kv(k, v, lpos[kk], rpos[kk]);
+  // the swapped positions are all distinct: the kU chunks' swaps are independent
+  for (int kb = 1; kb <= npairs; kb += 64 * kU) {
+    int lp[kU], rp[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int kk = kb + 64 * u + lane;
+      lp[u] = kk <= npairs ? (int)lpos[kk] : -1;
+      rp[u] = kk <= npairs ? (int)rpos[kk] : -1;
+    }
+    double kl[kU], kr[kU];
+    uint16_t vl[kU], vr[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (lp[u] >= 0) {
+        kl[u] = k[lp[u]];
+        kr[u] = k[rp[u]];
+        vl[u] = v[lp[u]];
+        vr[u] = v[rp[u]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (lp[u] >= 0) {
+        k[lp[u]] = kr[u];
+        k[rp[u]] = kl[u];
+        v[lp[u]] = vr[u];
+        v[rp[u]] = vl[u];
+      }
+    }
   }
   return uni(cut);
 }
@@ -353,6 +425,17 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
   const int w = blockIdx.x;
   if (A.need_exact && A.need_exact[w] == 0) return;  // the fast finish settled this window
   const int n = (int)A.n_cand;
+#ifdef CSM_FINISH_TRACE
+  __shared__ int tr_s;
+  if (threadIdx.x == 0) {
+    tr_s = atomicAdd(&g_trace_n, 1);
+    if (tr_s >= kTraceWindows) tr_s = -1;
+  }
+  __syncthreads();
+  const int tr = tr_s;
+  if (threadIdx.x == 0 && tr >= 0) g_trace[tr][9] = (unsigned long long)n;
+#endif
+  CSM_STAMP(0);
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   const FinishLayout Lo = finish_layout(n);
@@ -378,6 +461,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     lmax = x > lmax ? x : lmax;
   }
   lmax = block_max(lmax, sh, wave);
+  CSM_STAMP(1);
   if (threadIdx.x == 0) {
     sh->nan = 0;
     sh->cnt_a = 0;
@@ -421,6 +505,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     sh->plim = full ? n : min(n, max(sh->cnt_a, need));
   }
   __syncthreads();
+  CSM_STAMP(2);
   auto run_levels = [&]() {
     const int plim = sh->plim;
     for (int level = 0;; ++level) {
@@ -473,6 +558,10 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
   };
   run_levels();
   __syncthreads();
+  CSM_STAMP(3);
+#ifdef CSM_FINISH_TRACE
+  if (threadIdx.x == 0 && tr >= 0) g_trace[tr][8] = (unsigned long long)sh->plim;
+#endif
 
   // ---- ordered scans over the sorted candidates -----------------------------
   const ScanWork S = scans[w];
@@ -519,6 +608,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     o->best_y = sh->by;
   }
   __syncthreads();
+  CSM_STAMP(4);
   const double bx = sh->bx, by = sh->by;
   const double lo = best - 0.1;
   const double bound = (0.5 < lo) ? 0.5 : lo;  // std::min(best - 0.1, 0.5) (:912,:986)
@@ -587,6 +677,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     run_levels();
     __syncthreads();
   }
+  CSM_STAMP(5);
   if (A.order_out)
     for (int i = threadIdx.x; i < n; i += 64 * kWaves) A.order_out[(int64_t)w * n + i] = vals[i];
   if (threadIdx.x == 0 && sh->pad) o->count = -1;
@@ -632,6 +723,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
     }
     if (lane == 0) o->n_ang = min(nang, kCovPoints);
   }
+  CSM_STAMP(6);
 }
 
 // ---- fast finish: no sort when no tie can matter ----------------------------
@@ -904,7 +996,11 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel),
+#ifdef CSM_FINISH_TRACE
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);  // + static trace slot
+#else
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+#endif
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -922,3 +1018,18 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
 }
 
 }  // namespace csm
+
+#ifdef CSM_FINISH_TRACE
+// Trace readout for tools/finish_trace.py: copies and resets the stamps.
+extern "C" int csm_debug_finish_trace(unsigned long long* out, int max_windows) {
+  int n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(csm::g_trace_n), sizeof(int)) != hipSuccess) return -1;
+  n = n < max_windows ? n : max_windows;
+  n = n < csm::kTraceWindows ? n : csm::kTraceWindows;
+  if (n > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(csm::g_trace), (size_t)n * 10 * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  const int zero = 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(csm::g_trace_n), &zero, sizeof(int));
+  return n;
+}
+#endif
