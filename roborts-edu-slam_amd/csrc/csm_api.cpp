@@ -908,8 +908,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       A.skip_lists = skip_lists;
       const size_t fbytes = (size_t)nw * sizeof(csm::FinishOut);
       // + one "needs the exact sort" flag per window (fast finish, csm_finish.hip)
-      if ((e = c->fin.ensure(fbytes + (size_t)nw * sizeof(int32_t))) != hipSuccess) return c->hip_fail(e, "hipMalloc(finish)");
+      // + the flags' compacted list (count, then windows)
+      if ((e = c->fin.ensure(fbytes + (size_t)(2 * nw + 1) * sizeof(int32_t))) != hipSuccess)
+        return c->hip_fail(e, "hipMalloc(finish)");
       A.need_exact = c->fast_finish ? (int32_t*)((char*)c->fin.p + fbytes) : nullptr;
+      A.exact_list = c->fast_finish ? A.need_exact + nw : nullptr;
       if ((e = c->h_fin.ensure(fbytes + (size_t)nw * sizeof(int32_t))) != hipSuccess)
         return c->hip_fail(e, "hipHostMalloc(finish)");
       // the finish stream starts after the scoring kernel (ev_k, re-recorded below

@@ -81,11 +81,13 @@ struct WaveScratch {      // per-wave LDS scratch of the register sort
 
 static_assert(sizeof(WaveScratch) <= kFinishWaveScratch, "finish_layout wave scratch");
 
-struct Shared {           // misc block of the LDS carve (finish_layout: 64 B + waves)
+struct Shared {           // misc block of the LDS carve (finish_layout: 128 B)
   int plim, top, pending, pad;
   double bx, by;
   int ndef, cnt_a, cnt_b, nan;
   double red[kWaves];
+  int wl[kWaves], wr[kWaves];  // partition_block: per-wave counts
+  int fail;                    // partition_block: first rank that is not a pair
 };
 static_assert(sizeof(Shared) <= 128, "finish_layout misc block");
 
@@ -310,6 +312,97 @@ __device__ int partition_lds(double* k, uint16_t* v, uint16_t* lpos_all, uint16_
   return uni(cut);
 }
 
+// The same partition by the whole 4-wave block, for a level holding one
+// large segment (the partial sort's chain down to the prefix): the waves
+// count and rank contiguous quarters (ranks offset by the earlier quarters'
+// counts, so every rank is the one the single-wave pass assigns), find the
+// first rank that is not a pair together, and share the swaps.
+constexpr int kCoopMin = 256;
+__device__ int partition_block(double* k, uint16_t* v, uint16_t* lpos_all, uint16_t* rpos_all, int first,
+                               int last, Shared* sh, int wave) {
+  const int lane = lane_id();
+  const int m = last - first;
+  const int cap = m / 2 + 2;
+  uint16_t* lpos = lpos_all + first - 1;
+  uint16_t* rpos = rpos_all + first - 1;
+  if (threadIdx.x == 0) {
+    move_median_to_first(k, v, first, first + 1, first + m / 2, last - 1);
+    sh->fail = INT32_MAX;
+  }
+  __syncthreads();
+  const double P = k[first];
+  const int cq = ((m - 1 + 63) / 64 + kWaves - 1) / kWaves;  // 64-chunks per quarter
+  const int q0 = min(first + 1 + wave * cq * 64, last), q1 = min(first + 1 + (wave + 1) * cq * 64, last);
+  int cL = 0, cR = 0;
+  for (int base = q0; base < q1; base += 64 * kU) {
+    double key[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = base + 64 * u + lane;
+      key[u] = p < q1 ? k[p] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = base + 64 * u + lane;
+      cL += popc(__ballot(p < q1 && !gt(key[u], P)));
+      cR += popc(__ballot(p < q1 && !gt(P, key[u])));
+    }
+  }
+  if (lane == 0) {
+    sh->wl[wave] = cL;
+    sh->wr[wave] = cR;
+  }
+  __syncthreads();
+  int cntL = 0, cntR = 0, totL = 0, totR = 0;
+  for (int w = 0; w < kWaves; ++w) {
+    totL += sh->wl[w];
+    totR += sh->wr[w];
+    if (w < wave) {
+      cntL += sh->wl[w];
+      cntR += sh->wr[w];
+    }
+  }
+  for (int base = q0; base < q1; base += 64 * kU) {
+    double key[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = base + 64 * u + lane;
+      key[u] = p < q1 ? k[p] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = base + 64 * u + lane;
+      const bool ok = p < q1;
+      const bool isL = ok && !gt(key[u], P);
+      const bool isR = ok && !gt(P, key[u]);
+      const uint64_t mL = __ballot(isL), mR = __ballot(isR);
+      const int rl = cntL + popc(mL & below_mask(lane)) + 1;
+      const int rr = totR - (cntR + popc(mR & below_mask(lane)));
+      if (isL && rl <= cap) lpos[rl] = (uint16_t)p;
+      if (isR && rr <= cap) rpos[rr] = (uint16_t)p;
+      cntL += popc(mL);
+      cntR += popc(mR);
+    }
+  }
+  __syncthreads();
+  const int kmax = min(min(totL, totR), cap);
+  for (int kk = 1 + (int)threadIdx.x; kk <= kmax; kk += 64 * kWaves)
+    if (!(lpos[kk] < rpos[kk])) {  // ranks past the pairs fail from here on
+      atomicMin(&sh->fail, kk);
+      break;
+    }
+  __syncthreads();
+  const int f = sh->fail;
+  const int npairs = f == INT32_MAX ? kmax : f - 1;
+  int cut = INT32_MAX;
+  if (npairs + 1 <= totL) cut = lpos[npairs + 1];
+  if (npairs >= 1) cut = min(cut, (int)rpos[npairs]);
+  __syncthreads();  // every thread read the cut before the swaps move elements
+  for (int kk = 1 + (int)threadIdx.x; kk <= npairs; kk += 64 * kWaves) swap_kv(k, v, lpos[kk], rpos[kk]);
+  __syncthreads();
+  return cut;
+}
+
 // ---- small segments: one wave, registers ----------------------------------------
 // Finishes [base, base+m), m <= 64, entirely: introsort recursion from depth
 // `depth`, heap sort where a sub-segment runs out of depth, stable sort of the
@@ -416,14 +509,11 @@ __device__ void sort_small(double* keys, uint16_t* vals, int base, int m, int de
 
 }  // namespace
 
-// scores: window-major, n_cand per window (penalty applied). 4 waves/window.
-__global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const ScanWork* __restrict__ scans,
-                                                             const AngleEntry* __restrict__ angles,
-                                                             const double* __restrict__ scores,
-                                                             FinishOut* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int w = blockIdx.x;
-  if (A.need_exact && A.need_exact[w] == 0) return;  // the fast finish settled this window
+// The exact pass over one window (4 waves). Waves 1-3 return before the
+// list scans; the caller's barrier joins them.
+__device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ scans,
+                              const AngleEntry* __restrict__ angles, const double* __restrict__ scores,
+                              FinishOut* __restrict__ out, const int w, char* smem) {
   const int n = (int)A.n_cand;
 #ifdef CSM_FINISH_TRACE
   __shared__ int tr_s;
@@ -515,6 +605,16 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
         if (threadIdx.x == 0) sh->pad = 1;
         break;
       }
+      const Seg s0 = cur[0];
+      if (ncur == 1 && s0.first < plim && s0.last - s0.first > kCoopMin && s0.depth > 0) {
+        // one large segment: the whole block partitions it
+        const int cut = partition_block(keys, vals, lpos, rpos, s0.first, s0.last, sh, wave);
+        if (threadIdx.x == 0) {
+          nxt[0] = Seg{cut, s0.last, s0.depth - 1};
+          nxt[1] = Seg{s0.first, cut, s0.depth - 1};
+          sh->pending = 2;
+        }
+      } else
       for (int i = wave; i < ncur; i += kWaves) {
         const Seg s = cur[i];
         const int first = uni(s.first), last = uni(s.last), depth = uni(s.depth);
@@ -726,6 +826,28 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
   CSM_STAMP(6);
 }
 
+// scores: window-major, n_cand per window (penalty applied). 4 waves/window.
+// With the fast finish's list of flagged windows, a small grid walks the list
+// (a block per window of all n_windows cost ~50 us of dispatch at 2048
+// windows even though almost every block exits at once).
+__global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const ScanWork* __restrict__ scans,
+                                                             const AngleEntry* __restrict__ angles,
+                                                             const double* __restrict__ scores,
+                                                             FinishOut* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (A.exact_list) {
+    const int cnt = A.exact_list[0];
+    for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+      finish_window(A, scans, angles, scores, out, A.exact_list[1 + i], smem);
+      __syncthreads();  // the next window reuses the LDS carve
+    }
+    return;
+  }
+  const int w = blockIdx.x;
+  if (A.need_exact && A.need_exact[w] == 0) return;  // the fast finish settled this window
+  finish_window(A, scans, angles, scores, out, w, smem);
+}
+
 // ---- fast finish: no sort when no tie can matter ----------------------------
 // Everything the sorted candidates feed is decided by the elements with
 // score >= bound = min(best - 0.1, 0.5) (:912,:986; FindBestCandidate's
@@ -776,6 +898,10 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double* sc = scores + (int64_t)w * A.n_cand;
   int32_t* need = A.need_exact + w;
+  auto flag = [&]() {  // thread 0: the exact pass takes this window
+    *need = 1;
+    if (A.exact_list) A.exact_list[1 + atomicAdd(A.exact_list, 1)] = w;
+  };
   if (tid < kFastLevels) cnt_s[tid] = 0;
   if (tid == 0) {
     nC_s = 0;
@@ -797,7 +923,7 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   __syncthreads();
   const double best = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
   if (flag_s || n <= 0) {
-    if (tid == 0) *need = 1;
+    if (tid == 0) flag();
     return;
   }
   const double lo = best - 0.1;
@@ -841,7 +967,7 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   int nC = 0;
   for (int k = 0; k <= L; ++k) nC += cnt_s[k];
   if (nC > kFastCap) {
-    if (tid == 0) *need = 1;
+    if (tid == 0) flag();
     return;
   }
   for (int i0 = tid - lane; i0 < n; i0 += kFastThreads) {
@@ -877,7 +1003,7 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   }
   __syncthreads();
   if (flag_s) {
-    if (tid == 0) *need = 1;
+    if (tid == 0) flag();
     return;
   }
   const ScanWork S = scans[w];
@@ -965,7 +1091,7 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   __syncthreads();
   const int nN = nN_s;
   if (nN > kFastNearCap) {
-    if (tid == 0) *need = 1;
+    if (tid == 0) flag();
     return;
   }
   for (int t = tid; t < nN; t += kFastThreads) {
@@ -985,7 +1111,8 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   __syncthreads();
   if (tid == 0) {
     o->n_ang = min(nN, kCovPoints);
-    *need = flag_s ? 1 : 0;
+    if (flag_s) flag();
+    else *need = 0;
   }
 }
 
@@ -1004,6 +1131,11 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  const bool listed = A.need_exact && A.exact_list && !A.order_out;
+  if (listed) {
+    hipError_t e = hipMemsetAsync(A.exact_list, 0, sizeof(int32_t), stream);
+    if (e != hipSuccess) return e;
+  }
   if (A.need_exact && !A.order_out) {  // fast pass first; the exact pass only where it flagged
     hipLaunchKernelGGL(finish_fast_kernel, dim3(n_windows), dim3(kFastThreads), 0, stream, A, d_scans,
                        d_angles, d_scores, d_out);
@@ -1012,7 +1144,8 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
   }
   FinishArgs B = A;
   if (A.order_out) B.need_exact = nullptr;  // the permutation hook always sorts
-  hipLaunchKernelGGL(finish_kernel, dim3(n_windows), dim3(64 * kWaves), lds, stream, B, d_scans,
+  if (!listed) B.exact_list = nullptr;
+  hipLaunchKernelGGL(finish_kernel, dim3(listed ? std::min(n_windows, 512) : n_windows), dim3(64 * kWaves), lds, stream, B, d_scans,
                      d_angles, d_scores, d_out);
   return hipGetLastError();
 }

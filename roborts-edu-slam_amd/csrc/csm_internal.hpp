@@ -84,6 +84,7 @@ struct FinishArgs {
   double lin_tol;      // search_space_resolution / map_resolution (:840,:852)
   int32_t* order_out;  // optional: the sorted permutation, n_cand per window
   int32_t* need_exact; // per window: 1 = the fast finish saw a tie that matters (device scratch)
+  int32_t* exact_list; // [0] = count, then the flagged windows (device scratch, n_windows + 1)
 };
 
 // What the host needs to complete BasedCorrelationScanMatch::ScanMatch for
