@@ -351,6 +351,13 @@ class ThreadPool {
       std::lock_guard<std::mutex> lk(mu_);
       job_ = &job;
       n_items_ = n;
+      // items are claimed in chunks: one shared counter bumped per item cost
+      // more than the work itself at ~1 us per window (cache-line contention)
+      static const bool per_item = [] {  // CSM_POOL_CHUNK=1: one item per claim (A/B)
+        const char* e = std::getenv("CSM_POOL_CHUNK");
+        return e && std::atoi(e) == 1;
+      }();
+      chunk_ = per_item ? 1 : std::max(1, n / (threads * 8));
       next_.store(0);
       active_ = threads - 1;
       ++epoch_;
@@ -364,10 +371,12 @@ class ThreadPool {
 
  private:
   void drain(const std::function<void(int)>& job, int n) {
+    const int chunk = chunk_;
     for (;;) {
-      const int i = next_.fetch_add(1);
-      if (i >= n) break;
-      job(i);
+      const int i0 = next_.fetch_add(chunk);
+      if (i0 >= n) break;
+      const int i1 = std::min(n, i0 + chunk);
+      for (int i = i0; i < i1; ++i) job(i);
     }
   }
   void start(int want) {
@@ -403,7 +412,7 @@ class ThreadPool {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(int)>* job_ = nullptr;
-  int n_items_ = 0, active_ = 0, wanted_ = 0;
+  int n_items_ = 0, active_ = 0, wanted_ = 0, chunk_ = 1;
   uint64_t epoch_ = 0;
   std::atomic<int> next_{0};
   bool stop_ = false;
