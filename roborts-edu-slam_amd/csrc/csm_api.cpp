@@ -467,6 +467,18 @@ struct csm_ctx {
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
   bool fast_finish = true;    // CSM_FINISH=exact: always the full device std::sort emulation
   int device_finish_min = 1;  // fewest windows per launch that finish on the device
+  // Windows of at least this many candidates that the fast finish flags are
+  // sorted on the host (libstdc++ std::sort, what the reference runs) instead
+  // of by the device's exact pass: a handful per launch, so the host does them
+  // while the device scores the other part, and the level's device time loses
+  // the exact pass's tail (one window's sort chain). CSM_HOST_EXACT_MIN (e.g.
+  // 4096); 0, the default: off. Measured slower on config 2: the coarse
+  // finish drops 0.188 -> 0.062 ms per launch, but the host sorts (5070
+  // candidates each) land on the pipeline's critical path, 4.70-4.82 ->
+  // 5.24-5.40 ms per step (profiles/r01/experiments/ab_host_exact.txt).
+  int64_t host_exact_min = 0;
+  hipStream_t x2h = nullptr;  // copies of the flagged windows' scores
+  HostBuf h_exact;            // ... their pinned staging
   bool column_kernel = true;  // CSM_KERNEL=v1 selects the lane-per-candidate kernels
   bool row_kernel = true;     // CSM_KERNEL=v2 (or v1) turns the row-segment kernels off
   bool row_dma = true;        // CSM_KERNEL=v3: register-staged row segments instead of LDS-DMA
@@ -653,8 +665,10 @@ struct PendingRun {
   double alg_bytes = 0.0, scorings = 0.0, finish_bytes = 0.0;
   bool device_finish = false, timed = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, done = nullptr;
-  const int32_t* flags = nullptr;  // need-exact flags on the host (profiling)
+  const int32_t* flags = nullptr;  // need-exact flags on the host (profiling, host_exact)
   int n_flags = 0;
+  bool host_exact = false;          // flagged windows finish on the host (level_end)
+  const double* d_scores = nullptr; // their scores on the device
 };
 
 int wait_run(csm_ctx* c, const PendingRun& p) {
@@ -874,6 +888,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
 
   const int32_t* flags_h = nullptr;
   int n_flags = 0;
+  bool host_exact = false;
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
@@ -930,12 +945,14 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       if (fs != c->stream &&
           ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(fs, c->ev_k, 0)) != hipSuccess))
         return c->hip_fail(e, "finish stream event");
+      host_exact = pend && A.need_exact && c->host_exact_min > 0 && D.n_cand >= c->host_exact_min;
       if ((e = csm::launch_finish(A, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
-                                  (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw, fs)) != hipSuccess)
+                                  (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw, fs,
+                                  !host_exact)) != hipSuccess)
         return c->hip_fail(e, "finish_kernel");
       if (c->profiling && (e = hipEventRecord(c->ev2, fs)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
       // with profiling on, the flags come back too: how many windows needed the exact sort
-      const size_t cbytes = fbytes + ((c->profiling && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
+      const size_t cbytes = fbytes + (((c->profiling || host_exact) && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
       if ((e = hipEventRecord(c->ev_k, fs)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
         return c->hip_fail(e, "kernels event");
       if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, cbytes, hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
@@ -987,6 +1004,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   PendingRun& p = pend ? *pend : local;
   p.flags = flags_h;
   p.n_flags = n_flags;
+  p.host_exact = host_exact;
+  p.d_scores = (const double*)c->scores.p;
   std::snprintf(p.kname, sizeof(p.kname), "%s", kname);
   std::snprintf(p.fname, sizeof(p.fname), "finish_kernel<%lld>", (long long)D.n_cand);
   p.alg_bytes = alg_bytes;
@@ -1287,8 +1306,31 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
   const Geometry G(c->info);
   if (R.dev)
     for (int i = 0; i < nw; ++i)
-      if (R.fin[i].count < 0) return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
+      if (R.fin[i].count < 0 && !(R.pend.host_exact && R.pend.flags && R.pend.flags[i]))
+        return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
   const double f = P.search_space_resolution / G.mres;
+  // windows the fast finish flagged and left to the host: their scores come
+  // down (pinned staging, one stream sync) and std::sort orders them below
+  std::vector<int> slot_of;  // window -> staging slot (-1: the device finished it)
+  const double* xs = nullptr;
+  if (R.dev && R.pend.host_exact && R.pend.flags) {
+    slot_of.assign((size_t)nw, -1);
+    int nx = 0;
+    for (int i = 0; i < nw; ++i)
+      if (R.pend.flags[i]) slot_of[(size_t)i] = nx++;
+    if (nx > 0) {
+      const size_t wb = (size_t)D.n_cand * sizeof(double);
+      hipError_t e;
+      if ((e = c->h_exact.ensure((size_t)nx * wb)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(exact)");
+      for (int i = 0; i < nw; ++i)
+        if (slot_of[(size_t)i] >= 0 &&
+            (e = hipMemcpyAsync((char*)c->h_exact.p + (size_t)slot_of[(size_t)i] * wb, R.pend.d_scores + (size_t)i * D.n_cand,
+                                wb, hipMemcpyDeviceToHost, c->x2h)) != hipSuccess)
+          return c->hip_fail(e, "hipMemcpyAsync(exact scores)");
+      if ((e = hipStreamSynchronize(c->x2h)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(exact)");
+      xs = (const double*)c->h_exact.p;
+    }
+  }
   const int threads = (nw >= 64) ? c->host_threads : 1;
   c->parallel_for(nw, threads, [&](int i) {
     thread_local std::vector<Entry> scratch;
@@ -1297,7 +1339,10 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
                      (int64_t)D.n_space * D.n_space};
     csm::FinishOut local;
     const csm::FinishOut* o = nullptr;
-    if (R.dev) {
+    if (R.dev && xs && slot_of[(size_t)i] >= 0) {
+      host_sort_finish(xs + (size_t)slot_of[(size_t)i] * (size_t)D.n_cand, D, C, P, G, scratch, local);
+      o = &local;
+    } else if (R.dev) {
       o = R.fin + i;
     } else {
       host_sort_finish(R.scores + (size_t)i * (size_t)D.n_cand, D, C, P, G, scratch, local);
@@ -1766,6 +1811,7 @@ int csm_create(int device, csm_ctx** out) {
     c->pipeline_min = v > 0 ? v : INT32_MAX;
   }
   if (const char* env = std::getenv("CSM_SKIP_DEAD_LISTS")) c->skip_dead_lists = std::atoi(env) != 0;
+  if (const char* env = std::getenv("CSM_HOST_EXACT_MIN")) c->host_exact_min = std::atoll(env);
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
   bool ev_ok = true;
@@ -1776,6 +1822,7 @@ int csm_create(int device, csm_ctx** out) {
   if (!(ps && std::atoi(ps) != 0) && fsn && std::atoi(fsn) != 0)
     ev_ok = ev_ok && hipStreamCreateWithFlags(&c->fin_stream, hipStreamNonBlocking) == hipSuccess;
   ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
+  ev_ok = ev_ok && hipStreamCreateWithFlags(&c->x2h, hipStreamNonBlocking) == hipSuccess;
   for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k})
     ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
   for (auto& a : c->alt)
@@ -1801,7 +1848,9 @@ int csm_destroy(csm_ctx* c) {
     for (auto& a : c->alt)
       if (a.stream) (void)hipStreamSynchronize(a.stream);
     if (c->fin_stream) (void)hipStreamSynchronize(c->fin_stream);
+    if (c->x2h) (void)hipStreamSynchronize(c->x2h);
     c->grid_buf.release();
+    c->h_exact.release();
     c->gridi.release();
     c->gstats.release();
     c->pts.release();
@@ -1839,6 +1888,7 @@ int csm_destroy(csm_ctx* c) {
     for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k})
       if (ev) (void)hipEventDestroy(ev);
     if (c->fin_stream) (void)hipStreamDestroy(c->fin_stream);
+    if (c->x2h) (void)hipStreamDestroy(c->x2h);
     (void)hipStreamDestroy(c->h2d);
     (void)hipStreamDestroy(c->d2h);
     (void)hipStreamDestroy(c->stream);

@@ -1117,7 +1117,8 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
 }
 
 hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const AngleEntry* d_angles,
-                         const double* d_scores, FinishOut* d_out, int32_t n_windows, hipStream_t stream) {
+                         const double* d_scores, FinishOut* d_out, int32_t n_windows, hipStream_t stream,
+                         bool exact_on_device) {
   const size_t lds = finish_lds_bytes(A.n_cand);
   if (A.n_cand <= 0 || A.n_cand > kFinishMaxCand || lds > 160 * 1024 || n_windows <= 0) return hipErrorInvalidValue;
   static bool attr_set = false;
@@ -1142,6 +1143,7 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+  if (!exact_on_device && A.need_exact && !A.order_out) return hipSuccess;  // flagged windows: the host
   FinishArgs B = A;
   if (A.order_out) B.need_exact = nullptr;  // the permutation hook always sorts
   if (!listed) B.exact_list = nullptr;
