@@ -451,7 +451,9 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    ctx.set_profiling(True)
+    # HIP events around every launch feed the live roofline below; the A/B knob
+    # CSM_BENCH_NO_EVENTS=1 leaves them out to price their overhead
+    ctx.set_profiling(os.environ.get("CSM_BENCH_NO_EVENTS") != "1")
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -491,6 +493,9 @@ def main():
             dist.destroy_process_group()
         return
 
+    if os.environ.get("CSM_BENCH_NO_EVENTS") == "1":  # A/B of the event overhead only: no roofline
+        print(json.dumps({"ms_per_step": elapsed / args.steps * 1e3, "events": False}))
+        return
     # device kernels only; "host:*" entries are wall-clock phases of the driver
     kstats = [s for s in stats if not s["name"].startswith("host:")]
     dom = max(kstats, key=lambda s: s["total_ms"])

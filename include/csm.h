@@ -244,6 +244,15 @@ int csm_kernel_stats(csm_ctx* ctx, csm_kernel_stat* out, int32_t capacity, int32
  * n <= 10240. order receives n indices. */
 int csm_sort_order(csm_ctx* ctx, const double* keys, int64_t n, int64_t* order);
 
+/* Test hook (host only, no device): the phase buckets the v7 phase kernel
+ * uses for a window step of step_cells (< 1) map cells over n_space
+ * positions (csm_phase.hip; correlate_scan_matcher.h:569-572 enumeration).
+ * Bucket q holds the phases lo[q] <= p <= hi[q] of t = (lx + x0) + 0.5, in
+ * which candidate j reads column floor(t) + ox[q * 16 + j]. Arrays hold 8
+ * buckets (ox: 8 x 16). Returns CSM_ERR_UNSUPPORTED when no table exists. */
+int csm_phase_buckets(double step_cells, int32_t n_space, int32_t margin_log2, int32_t* n_buckets,
+                      int32_t* cells, double* lo, double* hi, int8_t* ox);
+
 /* --- raw scoring --------------------------------------------------------- */
 /* Every candidate score of one window (after the centre penalty when
  * param->use_center_penalty), in reference enumeration order. center_map is

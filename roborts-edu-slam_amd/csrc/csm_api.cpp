@@ -2269,6 +2269,21 @@ int csm_set_grid_stack(csm_ctx* c, const float* cells, int32_t n_grids, const cs
   return CSM_OK;
 }
 
+int csm_phase_buckets(double step_cells, int32_t n_space, int32_t margin_log2, int32_t* n_buckets,
+                      int32_t* cells, double* lo, double* hi, int8_t* ox) {
+  if (!n_buckets || !cells || !lo || !hi || !ox || margin_log2 < 2 || margin_log2 > 40) return CSM_ERR_INVALID_ARG;
+  csm::PhaseTable T{};
+  if (!phase_table(step_cells, n_space, margin_log2, T)) return CSM_ERR_UNSUPPORTED;
+  *n_buckets = T.nq;
+  *cells = T.cells;
+  for (int q = 0; q < csm::kPhaseMaxBuckets; ++q) {
+    lo[q] = T.lo[q];
+    hi[q] = T.hi[q];
+    for (int j = 0; j < csm::kPhaseMaxSpace; ++j) ox[q * csm::kPhaseMaxSpace + j] = T.ox[q][j];
+  }
+  return CSM_OK;
+}
+
 int csm_sort_order(csm_ctx* c, const double* keys, int64_t n, int64_t* order) {
   if (!c || !keys || !order) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);

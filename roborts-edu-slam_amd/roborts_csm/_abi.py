@@ -27,7 +27,7 @@ EXPORTED = (
     "csm_window_dims", "csm_scan_match", "csm_scan_matchers",
     "csm_scan_match_batch", "csm_scan_matchers_batch", "csm_score_window",
     "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded",
-    "csm_set_profiling", "csm_kernel_stats", "csm_sort_order",
+    "csm_set_profiling", "csm_kernel_stats", "csm_sort_order", "csm_phase_buckets",
     "csm_set_grid_stack", "csm_best_windows", "csm_optimize_scan_match", "csm_optimize_scan_match_batch",
     "csm_optimize_update_cost", "csm_load_scans_grids", "csm_scan_matchers_batch_grids",
     # include/csm_gridmap.h
@@ -158,6 +158,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_set_profiling": (C.c_int, [_ctx, C.c_int32]),
         "csm_kernel_stats": (C.c_int, [_ctx, C.POINTER(CsmKernelStat), C.c_int32, _i32p]),
         "csm_sort_order": (C.c_int, [_ctx, _dp, C.c_int64, _i64p]),
+        "csm_phase_buckets": (C.c_int, [C.c_double, C.c_int32, C.c_int32, C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_int32), _dp, _dp, C.POINTER(C.c_int8)]),
         "csm_set_grid_stack": (C.c_int, [_ctx, C.c_void_p, C.c_int32, C.POINTER(CsmMapInfo), C.c_int64]),
         "csm_best_windows": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), C.c_int32, _i32p, _dp,
                                        C.POINTER(CsmBest)]),
