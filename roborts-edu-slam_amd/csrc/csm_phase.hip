@@ -38,7 +38,10 @@
 namespace csm {
 namespace {
 
-constexpr int kSeg = 576;            // beams classified per segment (lists in LDS)
+#ifndef CSM_PHASE_SEG
+#define CSM_PHASE_SEG 576  // 576: 0.42 ms per fine launch; 1152: 0.48 (register and LDS pressure); 384: 0.43
+#endif
+constexpr int kSeg = CSM_PHASE_SEG;  // beams classified per segment (lists in LDS)
 constexpr int kEntG = 5;             // groups per list entry: 6 slots * 5 * (2^26 - 1) < 2^31
 constexpr int kChunks = kSeg / 64;   // 64-beam chunks per segment, classified in registers
 #ifndef CSM_PHASE_DEPTH
