@@ -13,28 +13,52 @@ Multi-GPU: one process per GPU; each rank matches its own batch (weak scaling,
 no data-path collective — independent scans). Timing: barrier +
 synchronize on both sides of exactly --steps steps, max over ranks.
 
-Roofline: the dominant kernel's algorithmic bytes (4 B per summed beam per
-candidate) over its HIP-event time, measured live on the stream it runs on.
+Roofline: the dominant kernel is placed against every ceiling its counters
+can be priced on (HBM bytes, TA address-unit busy cycles, VALU issue cycles),
+each from rocprofv3 --pmc passes of the same build (tools/pmc_roofline.sh ->
+profiles/<round>/counters.json) divided by the kernel's average launch time
+measured live with HIP events on the stream it runs on. `bound` is the ceiling
+with the highest fraction; a fraction above 1 is refused (printed as null).
+The algorithmic rate (4 B per summed beam per candidate) is kept
+beside it as `algorithmic_GBs`: those reads are served from L2 / Infinity
+Cache and deduplicated by the kernels, so it is not an HBM rate.
 cpu_baseline: the oracle (single-threaded restatement of the reference) on a
-bounded sample of the same workload, rank 0 at N=1 only.
+bounded sample of the same workload, rank 0 at N=1 only, plus its all-cores
+variant (OpenMP over theta) and the reference-default B=109 levels.
+
+Multi-GPU: `python bench.py --gpus N` with no torch.distributed environment
+spawns N child processes itself (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set before
+any GPU call) and prints rank 0's line; under torchrun it joins the given group.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import math
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# the CPU baseline's OpenMP threads sleep between windows instead of spinning
+# (read by libgomp when the oracle library loads)
+os.environ.setdefault("OMP_WAIT_POLICY", "passive")
 sys.path[:0] = [os.path.join(ROOT, "roborts-edu-slam_amd"), os.path.join(ROOT, "oracle")]
 
 import numpy as np  # noqa: E402
 
 METRIC = "candidate-pose scorings/sec (1081-beam scan, 2000×2000 grid) at 1/2/4/8 GPUs"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s (spec), 256 CUs x 4 SIMD-32,
+# 2400 MHz max clock; a 64-lane VALU instruction issues over 2 cycles (4 for
+# fp64 arithmetic: FP64 vector peak = half the FP32 rate).
+HBM_PEAK_GBS = 8000.0
+N_CU, N_SIMD, CLK_GHZ = 256, 1024, 2.4
+COUNTERS_JSON = os.path.join(ROOT, "profiles", "r02", "counters.json")
+CSRC = os.path.join(ROOT, "roborts-edu-slam_amd", "csrc")
 
 
 def _cpu_model() -> str:
@@ -48,9 +72,22 @@ def _cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(world, batch, levels, seconds: float):
-    """Oracle (test infrastructure, CPU restatement) on a bounded sample."""
+def _host_threads() -> int:
+    """The box's CPU share (OMP_NUM_THREADS is set to it there; nproc shows the
+    whole machine)."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(n or (os.cpu_count() or 1), os.cpu_count() or 1, 16))
+
+
+def cpu_baseline(world, batch, levels, seconds: float, threads: int = 1, label: str = ""):
+    """Oracle (test infrastructure, CPU restatement) on a bounded sample.
+    threads > 1: the all-cores variant (OpenMP over theta inside each window;
+    identical results)."""
     import pyoracle as O
+    O.set_threads(threads)
     m = O.Map(world.grid, world.resolution, world.offset)
     eye = np.tile(np.eye(3).reshape(1, 9), (1, 1))
 
@@ -65,10 +102,90 @@ def cpu_baseline(world, batch, levels, seconds: float):
     probe = run(0, 2) / 2
     n = int(max(2, min(batch.offsets.size - 1, seconds / max(probe, 1e-6))))
     dt = run(0, n)
+    O.set_threads(1)
     per_scan = sum(_window_cands(l) for l in levels)
-    return {"value": n * per_scan / dt, "unit": "scorings/s", "cores": 1, "kind": "port",
-            "sample": f"{n} scans x 3 levels ({n * per_scan} scorings, {dt:.1f} s) single-threaded "
+    how = "single-threaded" if threads == 1 else f"{threads} threads (OpenMP over theta)"
+    return {"value": n * per_scan / dt, "unit": "scorings/s", "cores": threads, "kind": "port",
+            "sample": f"{label}{n} scans x 3 levels ({n * per_scan} scorings, {dt:.1f} s) {how} "
                       f"oracle/csm_oracle.cpp on {_cpu_model()}"}
+
+
+def source_digest() -> str:
+    """SHA-1 over the HIP/C++ sources of the library: ties counters.json (and a
+    bench line) to the build it was measured on."""
+    h = hashlib.sha1()
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith((".hip", ".cpp", ".hpp")):
+            with open(os.path.join(CSRC, f), "rb") as fh:
+                h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:12]
+
+
+def load_counters(path: str):
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def roofline(kernel: str, avg_ms: float, algorithmic_bytes: float, counters, counters_path: str):
+    """The kernel against each ceiling its PMC counters price (per launch, from
+    tools/pmc_roofline.sh) over the live average launch time. frac > 1 is
+    refused: the ceiling or the counter reading would be wrong."""
+    t = avg_ms * 1e-3
+    out = {"kernel": kernel, "avg_launch_ms": avg_ms,
+           "algorithmic_bytes_per_launch": algorithmic_bytes,
+           "algorithmic_GBs": algorithmic_bytes / t / 1e9,
+           "algorithmic_note": "4 B per summed beam per candidate (SURVEY 8d); served from L2/MALL and "
+                               "deduplicated on chip, so not an HBM rate"}
+    ks = (counters or {}).get("kernels", {}).get(kernel)
+    if ks is None:
+        out.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
+                    "traffic": None, "note": f"no PMC counters for {kernel} in {counters_path}"})
+        return out
+    ceilings = {}
+    hbm = ks.get("hbm_bytes_per_launch")
+    if hbm is not None:
+        ceilings["hbm"] = (hbm / t / 1e9, HBM_PEAK_GBS, "GB/s")
+    if ks.get("TA_BUSY_avr") is not None:  # busy cycles of one TA (one per CU)
+        ceilings["ta"] = (ks["TA_BUSY_avr"] / t / 1e9, CLK_GHZ, "TA-busy Gcycles/s per CU")
+    if ks.get("SQ_INSTS_VALU") is not None:
+        f64 = ks.get("valu_f64_insts")
+        cyc = 2.0 * ks["SQ_INSTS_VALU"] + (2.0 * f64 if f64 else 0.0)
+        ceilings["valu"] = (cyc / N_SIMD / t / 1e9, CLK_GHZ, "VALU issue Gcycles/s per SIMD")
+    if ks.get("SQ_INSTS_LDS") is not None and ks.get("SQ_LDS_BANK_CONFLICT") is not None:
+        # ds instructions at >= 1 cycle each plus the measured conflict cycles, per CU
+        cyc = ks["SQ_INSTS_LDS"] + ks["SQ_LDS_BANK_CONFLICT"]
+        ceilings["lds"] = (cyc / N_CU / t / 1e9, CLK_GHZ, "LDS Gcycles/s per CU (lower bound)")
+    fr = {k: a / p for k, (a, p, _) in ceilings.items()}
+    bad = {k: v for k, v in fr.items() if v > 1.0}
+    out["ceilings"] = {k: {"achieved": a, "peak": p, "unit": u, "frac": (a / p if k not in bad else None)}
+                       for k, (a, p, u) in ceilings.items()}
+    good = {k: v for k, v in fr.items() if k not in bad}
+    if bad:
+        out["refused"] = {k: f"frac {v:.2f} > 1 refused" for k, v in bad.items()}
+    b = max(good, key=good.get) if good else None
+    if b is not None:
+        a, p, u = ceilings[b]
+        out.update({"bound": b, "achieved": a, "peak": p, "unit": u, "frac": a / p})
+    else:
+        out.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None})
+    out["traffic"] = hbm
+    out["hbm_frac"] = fr.get("hbm")
+    if ks.get("SQ_WAVE_CYCLES") and ks.get("GRBM_GUI_ACTIVE"):
+        cyc = ks["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
+        out["waves_per_simd"] = ks["SQ_WAVE_CYCLES"] * 4.0 / N_SIMD / cyc
+        out["effective_clock_GHz"] = cyc / t / 1e9
+        if ks.get("SQ_WAIT_ANY"):
+            out["wait_frac"] = ks["SQ_WAIT_ANY"] / ks["SQ_WAVE_CYCLES"]
+    if b is not None and fr[b] < 0.6:
+        out["limiter"] = (f"latency: best ceiling {b} at {fr[b]:.2f}; "
+                          f"{out.get('waves_per_simd', float('nan')):.1f} waves/SIMD, "
+                          f"{out.get('wait_frac', float('nan')):.0%} of wave time parked on waitcnt")
+    out["counters_source"] = os.path.relpath(counters_path, ROOT)
+    out["counters_build"] = (counters or {}).get("source_digest")
+    out["counters_stale"] = (counters or {}).get("source_digest") != source_digest()
+    return out
 
 
 def _window_cands(p) -> int:
@@ -123,7 +240,11 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
     kst = [s for s in stats if not s["name"].startswith("host:")]
     dom = max(kst, key=lambda s: s["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
-    achieved = dom["algorithmic_bytes"] / dom["launches"] / (avg_ms * 1e-3) / 1e9
+    rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"],
+                  load_counters(args.counters_json), args.counters_json)
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu:
+        cpu = lc_cpu_baseline(bases, pts, param, pose, args.cpu_seconds, na * ns * ns)
     return {
         "metric": METRIC, "value": total / elapsed, "unit": "scorings/s", "n_gpus": world_size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -132,12 +253,34 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
         "config": {"workload": f"config3: loop closure, 1 query x {n_sub} submaps 800x800 @5cm, "
                                f"+-8 m / +-pi window ({na}x{ns}^2 candidates per submap), B=109",
                    "parallelism": f"submaps sharded x{world_size}, MAX/MIN all-reduce"},
-        "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "avg_launch_ms": avg_ms},
+        "roofline": rl,
         "result": {"score": r.score, "submap": r.submap, "global_index": r.global_index},
-        "kernels": stats, "cpu_baseline": None,
+        "kernels": stats, "cpu_baseline": cpu,
     }
+
+
+def lc_cpu_baseline(bases, pts, param, pose, seconds, per_submap):
+    """Config-3 CPU leg: the oracle's argmax over whole submap windows (the
+    reference's GetResponse loop over 181 x 321^2 candidates), all host
+    threads (OpenMP over theta); one submap takes seconds, so the sample is
+    the submaps that fit in `seconds`."""
+    import pyoracle as O
+    from roborts_csm.loop_closure import world_to_map
+    th = _host_threads()
+    O.set_threads(th)
+    b = bases[0]
+    m = O.Map(b.grid, b.resolution, b.offset)
+    c = world_to_map(pose, b.resolution, b.offset)
+    t = time.perf_counter()
+    n = 0
+    while n < 1 or time.perf_counter() - t < seconds:
+        O.best_window(m, pts, param, c)
+        n += 1
+    dt = time.perf_counter() - t
+    O.set_threads(1)
+    return {"value": n * per_submap / dt, "unit": "scorings/s", "cores": th, "kind": "port",
+            "sample": f"{n} submap window(s) of {per_submap} candidates, B=109, {dt:.1f} s, oracle "
+                      f"best_window with {th} threads (OpenMP over theta) on {_cpu_model()}"}
 
 
 def willow_bench(args, rank, world_size, dist, torch):
@@ -189,7 +332,25 @@ def willow_bench(args, rank, world_size, dist, torch):
     kst = [s for s in stats if not s["name"].startswith("host:")]
     dom = max(kst, key=lambda s: s["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
-    achieved = dom["algorithmic_bytes"] / dom["launches"] / (avg_ms * 1e-3) / 1e9
+    rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"],
+                  load_counters(args.counters_json), args.counters_json)
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu:
+        import pyoracle as O
+        th = _host_threads()
+        O.set_threads(th)
+        om = O.Map(w.grid, w.resolution, w.offset)
+        tc = time.perf_counter()
+        m = 0
+        while m < 1 or time.perf_counter() - tc < args.cpu_seconds:
+            pts = batch.points_cells[batch.offsets[m]:batch.offsets[m + 1]]
+            O.best_window(om, pts, param, world_to_map(batch.init_poses[m], w.resolution, w.offset))
+            m += 1
+        dtc = time.perf_counter() - tc
+        O.set_threads(1)
+        cpu = {"value": m * na * ns * ns / dtc, "unit": "scorings/s", "cores": th, "kind": "port",
+               "sample": f"{m} of the same queries ({na}x{ns}^2 candidates, all beams), {dtc:.1f} s, oracle "
+                         f"best_window with {th} threads (OpenMP over theta) on {_cpu_model()}"}
     return {
         "metric": METRIC, "value": total / elapsed, "unit": "scorings/s", "n_gpus": world_size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -199,10 +360,8 @@ def willow_bench(args, rank, world_size, dist, torch):
         "config": {"workload": f"config4: willow 1565x1345 @5cm, {args.window_m} m / +-pi window "
                                f"({na}x{ns}^2 candidates), all beams",
                    "mean_beams": beams / args.steps, "parallelism": f"replicas x{world_size}"},
-        "roofline": {"bound": "hbm", "kernel": dom["name"], "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "avg_launch_ms": avg_ms},
-        "kernels": stats, "cpu_baseline": None,
+        "roofline": rl,
+        "kernels": stats, "cpu_baseline": cpu,
     }
 
 
@@ -372,6 +531,65 @@ def backend_bench(args, rank, world_size, dist, torch):
     }
 
 
+def plumbing_bench(args, rank, world_size, dist, torch):
+    """The launcher and timing protocol without the matcher (CPU tests of
+    `--gpus N`): barrier, --steps timed sleeps of 1 ms, max over ranks, sum of
+    per-rank units."""
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(1e-3)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    units = float(args.steps)
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64)
+        u = torch.tensor([units], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        elapsed, units = float(e.item()), float(u.item())
+    return {"metric": "plumbing", "value": units / elapsed, "unit": "steps/s", "n_gpus": world_size,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "rank_units": units}
+
+
+def world_info(dist) -> dict:
+    """What actually ran: world size and backend of the process group."""
+    if dist is None:
+        return {"world_size": 1, "backend": None}
+    return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend())}
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh child processes, one
+    per GPU, with the torch.distributed environment set. The parent never
+    touches the GPU and never re-execs; it relays rank 0's stdout and returns
+    the first non-zero exit status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0]
+    codes = [p.wait() for p in procs]
+    # only the result line goes to stdout (communication libraries print
+    # their own status lines to the process's stdout)
+    for line in out.decode().splitlines():
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line + "\n")
+    sys.stdout.flush()
+    return next((c for c in codes if c != 0), 0)
+
+
 def worlds_mod():
     from roborts_csm import worlds
     return worlds
@@ -385,7 +603,7 @@ def main():
     ap.add_argument("--scans", type=int, default=4096, help="scans per GPU per step")
     ap.add_argument("--levels", choices=["headline", "sim"], default="headline",
                     help="headline: every beam summed (B=1081); sim: reference YAML U=100 (B=109)")
-    ap.add_argument("--workload", choices=["config2", "loop_closure", "willow", "online", "backend"],
+    ap.add_argument("--workload", choices=["config2", "loop_closure", "willow", "online", "backend", "plumbing"],
                     default="config2",
                     help="config2: the headline front-end batch; loop_closure: config 3; willow: config 4; "
                          "online: config 5 (steps = scans); backend: f2 pose-graph jobs")
@@ -397,27 +615,40 @@ def main():
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-scan latency probe (profiling runs: keeps rocprof "
                          "per-kernel averages equal to the timed steps' launches)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch per kernel (tools/pmc_run.sh -> "
-                         "tools/pmc_traffic.py; FETCH_SIZE and WRITE_SIZE passes of the same command)")
+    ap.add_argument("--counters-json", default=COUNTERS_JSON,
+                    help="per-kernel PMC counters per launch (tools/pmc_roofline.sh -> tools/pmc_roofline.py)")
+    ap.add_argument("--no-b109", action="store_true",
+                    help="config2: skip the reference-default B=109 (U=100) line beside the headline")
+    ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
+                    help="torch.distributed backend (auto: nccl = RCCL on a GPU box, gloo on CPU)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+
     rank = int(os.environ.get("RANK", "0"))
-    world_size = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_size}")
     dist = None
     import torch
     if world_size > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        backend = args.backend if args.backend != "auto" else (
+            "nccl" if torch.cuda.is_available() else "gloo")
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend)
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
 
-    if args.workload in ("loop_closure", "willow", "online", "backend"):
+    if args.workload in ("loop_closure", "willow", "online", "backend", "plumbing"):
         fn = {"loop_closure": loop_closure_bench, "willow": willow_bench, "online": online_bench,
-              "backend": backend_bench}[args.workload]
+              "backend": backend_bench, "plumbing": plumbing_bench}[args.workload]
         out = fn(args, rank, world_size, dist, torch)
         if rank == 0:
+            out["world"] = world_info(dist)
             print(json.dumps(out))
         if dist is not None:
             dist.barrier()
@@ -485,7 +716,34 @@ def main():
         t = time.perf_counter()
         ctx.scan_matchers(one_pts, levels, pose, cov)
         lat.append(time.perf_counter() - t)
+    # the PCIe-inclusive cost of the host-buffer entry points: one H2D copy of
+    # the batch's points (never part of `value`)
+    t = time.perf_counter()
     ctx.load_scans(batch.points_cells, batch.offsets)
+    h2d_ms = (time.perf_counter() - t) * 1e3
+
+    # the reference-default beam rule next to the headline: sim-YAML U=100 -> B=109
+    b109 = None
+    if args.levels == "headline" and not args.no_b109:
+        def step109():
+            p, c = poses0.copy(), covs0.copy()
+            ctx.scan_matchers_loaded(SIM_YAML_LEVELS, p, c)
+        for _ in range(args.warmup):
+            step109()
+        barrier()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            step109()
+        barrier()
+        e109 = time.perf_counter() - t
+        if dist is not None:
+            e = torch.tensor([e109], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            e109 = float(e.item())
+        ps = sum(_window_cands(l) for l in SIM_YAML_LEVELS)
+        b109 = {"value": world_size * args.scans * ps * args.steps / e109, "unit": "scorings/s",
+                "ms_per_step": e109 / args.steps * 1e3, "beams_summed": 109,
+                "levels": "sim YAML (U=100 at every level: B=109)"}
 
     if rank != 0:
         if dist is not None:
@@ -500,13 +758,8 @@ def main():
     kstats = [s for s in stats if not s["name"].startswith("host:")]
     dom = max(kstats, key=lambda s: s["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
-    bytes_per_launch = dom["algorithmic_bytes"] / dom["launches"]
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            tj = json.load(f)  # tools/pmc_traffic.py output, keyed by kernel
-        traffic = tj.get(dom["name"], {}).get("hbm_bytes_per_launch")
+    rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"],
+                  load_counters(args.counters_json), args.counters_json)
     kernel_total_ms = sum(s["total_ms"] for s in kstats)
     kernel_scorings = sum(s["scorings"] for s in kstats)
 
@@ -533,29 +786,30 @@ def main():
             "scans_per_gpu": args.scans,
             "scorings_per_scan": per_scan,
             "parallelism": f"replicas x{world_size} (scan-sharded, no collective)",
+            "inputs": "grid and scans resident in HBM before the timed region (csm_load_scans); the "
+                      f"host-buffer entry points add one H2D copy of the points: "
+                      f"{batch.points_cells.nbytes / 1e6:.1f} MB per step here, timed below as h2d_ms",
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": dom["name"],
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_source": (os.path.relpath(args.traffic_json, ROOT) if traffic is not None else None),
-            "avg_launch_ms": avg_ms,
-            "algorithmic_bytes_per_launch": bytes_per_launch,
-        },
+        "roofline": rl,
         "kernel_scorings_per_s": kernel_scorings / (kernel_total_ms * 1e-3) if kernel_total_ms else None,
         "kernel_share_of_step": kernel_total_ms * 1e-3 / elapsed,
         "single_scan_latency_ms": float(np.median(lat) * 1e3) if lat else None,
         "median_pose_error_m": float(np.median(err)),
         "kernels": stats,
     }
+    out["h2d_ms"] = h2d_ms
+    if b109 is not None:
+        out["b109"] = b109
     if not args.no_cpu and world_size == 1:
         out["cpu_baseline"] = cpu_baseline(world, batch, levels, args.cpu_seconds)
+        th = _host_threads()
+        out["cpu_baseline_all_cores"] = cpu_baseline(world, batch, levels, args.cpu_seconds / 2, threads=th)
+        if b109 is not None:
+            b109["cpu_baseline"] = cpu_baseline(world, batch, SIM_YAML_LEVELS, args.cpu_seconds / 2,
+                                                label="B=109 (sim YAML, U=100): ")
     else:
         out["cpu_baseline"] = None
+    out["world"] = world_info(dist)
     print(json.dumps(out))
     if dist is not None:
         dist.barrier()

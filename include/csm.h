@@ -14,6 +14,8 @@
  *   csm_map_info              GridMapBase geometry       grid_map_base.h:47-71,307-309,371-378
  *   csm_set_grid              OccuGridMap cell storage read by GetGridProbValue
  *                                                        occu_grid_map.h:395-397, grid_map_base.h:352-354
+ *   csm_update_grid_cells/rows  the cells UpdateMapByRange / ResetValueSpeedup rewrite
+ *                                                        occu_grid_map.h:258-329, grid_map_base.h:114-120
  *   csm_scan_match            BasedCorrelationScanMatch::ScanMatch
  *                                                        correlate_scan_matcher.h:784-875
  *   csm_scan_matchers         ScanMatchers::ScanMatch (3-level coarse->fine->super)
@@ -136,6 +138,24 @@ int csm_set_outside_value(csm_ctx* ctx, float value);
  * unchanged key skips the upload. Pass version = -1 to force the upload. */
 int csm_set_grid(csm_ctx* ctx, const void* cells, int64_t cell_stride_bytes,
                  const csm_map_info* info, int64_t version);
+/* Incremental refresh of a grid made resident by csm_set_grid (the same
+ * cells pointer, stride and geometry; otherwise the whole grid is uploaded).
+ * Replaces re-uploading the map after OccuGridMap::UpdateMapByRange
+ * (occu_grid_map.h:258-329): the reference rewrites only the cells it lists
+ * in map_update_point_ (occu_grid_map.h:509,528,571) and resets only those in
+ * ResetValueSpeedup (grid_map_base.h:114-120).
+ *   csm_update_grid_cells: the listed cells (indices y*size_x + x, any order,
+ *                          duplicates allowed) are re-read from cells.
+ *   csm_update_grid_rows:  rows [row_begin, row_end) are re-read.
+ * The grid's key takes the new version. Up to four host maps stay resident at
+ * once, keyed on their cells pointer (least recently used evicted), so the
+ * front end's and the back end's maps do not evict each other. */
+int csm_update_grid_cells(csm_ctx* ctx, const void* cells, int64_t cell_stride_bytes,
+                          const csm_map_info* info, int64_t version,
+                          const int32_t* cell_indices, int64_t n_indices);
+int csm_update_grid_rows(csm_ctx* ctx, const void* cells, int64_t cell_stride_bytes,
+                         const csm_map_info* info, int64_t version,
+                         int32_t row_begin, int32_t row_end);
 /* Borrow a packed float grid that already lives in device memory of this
  * context's device (size_y * size_x floats). The caller keeps it alive. */
 int csm_set_grid_device(csm_ctx* ctx, const float* device_prob,

@@ -34,6 +34,8 @@
 
 namespace {
 
+int g_threads = 1;  // oracle_set_threads: 1 = single-threaded like the reference
+
 // Geometry + cells of one ScanMatchMap (map/grid_map_base.h:47-71,352-354).
 struct OracleMap {
   const float* cells;      // &cell[0].prob_value_
@@ -236,21 +238,27 @@ void enumerate_scores(const OracleMap& m, const double* pts, int n, const Oracle
   double sx0 = center[0] - (ssize / mres) * 0.5;
   double sy0 = center[1] - (ssize / mres) * 0.5;
   double f = sres / mres;
-  cands.clear();
-  cands.reserve((size_t)n_ang * n_space * n_space);
-  Cand cur;
-  int64_t flat = 0;
+  // The reference re-runs the beam rule inside the angle loop (:561-566); it is
+  // idempotent after the first angle, so it is evaluated once here.
+  step = beam_step(n, use);
+  const int64_t per_angle = (int64_t)n_space * n_space;
+  cands.assign((size_t)(n_ang * per_angle), Cand());
+  // g_threads > 1: the all-cores CPU baseline (OpenMP over theta, the loop the
+  // reference's commented-out OpenMP pragma sat on, grid_map_base.h:98). Each
+  // candidate is computed by the same expressions, so results are identical.
+#pragma omp parallel for schedule(dynamic, 1) num_threads(g_threads) if (g_threads > 1)
   for (int a = 0; a < n_ang; ++a) {
+    Cand cur;
     cur.angle_index = a;
     cur.angle = lut.angles[a];
-    step = beam_step(n, use);
+    int64_t flat = a * per_angle;
     for (int xi = 0; xi < n_space; ++xi) {
       cur.x = sx0 + xi * f;
       for (int yi = 0; yi < n_space; ++yi) {
         cur.y = sy0 + yi * f;
         cur.score = response_at(m, cur.x, cur.y, lut.rows[a].data(), n, step, use);
-        cur.flat = flat++;
-        cands.push_back(cur);
+        cur.flat = flat;
+        cands[(size_t)flat++] = cur;
       }
     }
   }
@@ -538,6 +546,8 @@ static OracleParam to_param(const void* p) {
 }
 
 int oracle_param_size(void) { return (int)sizeof(OracleParam); }
+// Threads for the candidate enumeration (CPU baseline's all-cores variant).
+void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
 int oracle_map_size(void) { return (int)sizeof(oracle_map_c); }
 
 // All candidate scores (after penalty) in enumeration order (theta, x, y).

@@ -65,6 +65,7 @@ def _load():
         "oracle_map_to_world": (None, [C.POINTER(OracleMap), _dp, _dp]),
         "oracle_best_window": (C.c_double, [C.POINTER(OracleMap), _dp, C.c_int, C.c_void_p, _dp, _i64p]),
         "oracle_std_sort_order": (None, [_dp, C.c_int64, _i64p]),
+        "oracle_set_threads": (None, [C.c_int]),
     }
     for k, (r, a) in sig.items():
         f = getattr(lib, k)
@@ -152,6 +153,12 @@ def scan_matchers(m: Map, points, levels, pose, cov, use_fine: bool = True):
     r = _lib.oracle_scan_matchers(C.byref(m.c), pts.ctypes.data_as(_dp), pts.shape[0], lv,
                                   1 if use_fine else 0, pose.ctypes.data_as(_dp), cov.ctypes.data_as(_dp))
     return r, pose, cov
+
+
+def set_threads(n: int) -> None:
+    """Threads for the candidate enumeration (OpenMP over theta; 1 = the
+    reference's single-threaded loop). Results do not depend on it."""
+    _lib.oracle_set_threads(int(n))
 
 
 def scan_matchers_batch(m: Map, points, offsets, levels, poses, covs, use_fine: bool = True):

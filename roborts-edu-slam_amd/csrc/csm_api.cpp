@@ -509,7 +509,55 @@ struct csm_ctx {
   int phase_margin_log2 = 20; // CSM_PHASE_MARGIN_LOG2 (tests: a wider margin sends more beams to the exact path)
   bool box_kernel = true;     // v6 box kernel for one-cell window steps; any CSM_KERNEL other
                               // than v6 turns it off (CSM_KERNEL=v4: the LDS-DMA row kernel)
-  std::vector<float> h_pack;
+  HostBuf h_pack;  // pinned staging of packed grid rows / cell updates (grid uploads)
+  DevBuf d_updates;  // csm_update_grid_cells entries on the device
+
+  // Resident grids of other host maps. csm_set_grid keys a grid on the host
+  // cells pointer (the map's identity); switching between maps (the front
+  // end's fine map, the back end's maps) swaps the current grid with a parked
+  // one instead of re-uploading it. The least recently used is evicted.
+  struct GridSlot {
+    csm_map_info info{};
+    bool has_grid = false;
+    const float* d_grid = nullptr;
+    DevBuf grid_buf, gridi;
+    const void* key_cells = nullptr;
+    int64_t key_stride = 0, key_version = -1;
+    int32_t key_sx = -1, key_sy = -1;
+    bool int_checked = false, int_ok = false;
+    int int_exp = 0;
+    int32_t pitch = 0, n_grids = 1, outside_i = 0;
+    double int_max_abs = 0.0;
+    uint64_t last_use = 0;
+  };
+  static constexpr int kParkedGrids = 3;
+  GridSlot parked[kParkedGrids];
+  uint64_t grid_clock = 0, cur_use = 0;
+  void swap_grid(GridSlot& g) {
+    std::swap(info, g.info);
+    std::swap(has_grid, g.has_grid);
+    std::swap(d_grid, g.d_grid);
+    std::swap(grid_buf, g.grid_buf);
+    std::swap(gridi, g.gridi);
+    std::swap(key_cells, g.key_cells);
+    std::swap(key_stride, g.key_stride);
+    std::swap(key_version, g.key_version);
+    std::swap(key_sx, g.key_sx);
+    std::swap(key_sy, g.key_sy);
+    std::swap(int_checked, g.int_checked);
+    std::swap(int_ok, g.int_ok);
+    std::swap(int_exp, g.int_exp);
+    std::swap(pitch, g.pitch);
+    std::swap(n_grids, g.n_grids);
+    std::swap(outside_i, g.outside_i);
+    std::swap(int_max_abs, g.int_max_abs);
+    std::swap(cur_use, g.last_use);
+  }
+  // The current grid is a host map's own copy (worth keeping when another
+  // grid takes its place).
+  bool owns_host_grid() const {
+    return has_grid && key_cells != nullptr && d_grid == (const float*)grid_buf.p;
+  }
 
   // Gauss-Newton matcher (csm_optimize_scan_match*): per-scan state up, sums down
   DevBuf opt_off, opt_scans, opt_sums;
@@ -674,6 +722,110 @@ int ensure_int_grid(csm_ctx* c) {
   c->outside_i = (int32_t)((double)c->outside * scale);
   c->int_ok = true;
   return CSM_OK;
+}
+
+// Make the grid keyed on `cells` current: it is current already, or parked
+// (swapped in), or new (the current host-map grid is parked first, evicting
+// the least recently used slot). Returns true when the grid was found.
+bool select_grid(csm_ctx* c, const void* cells) {
+  c->cur_use = ++c->grid_clock;
+  if (c->owns_host_grid() && c->key_cells == cells) return true;
+  for (auto& g : c->parked)
+    if (g.has_grid && g.key_cells == cells) {
+      if (c->owns_host_grid()) {
+        c->swap_grid(g);
+      } else {  // a borrowed or empty current grid is not kept
+        csm_ctx::GridSlot tmp;
+        c->swap_grid(tmp);
+        c->swap_grid(g);
+        std::swap(g, tmp);
+        tmp.grid_buf.release();
+        tmp.gridi.release();
+      }
+      c->cur_use = ++c->grid_clock;
+      return true;
+    }
+  if (c->owns_host_grid()) {
+    csm_ctx::GridSlot* v = &c->parked[0];
+    for (auto& g : c->parked) {
+      if (!g.has_grid) {
+        v = &g;
+        break;
+      }
+      if (g.last_use < v->last_use) v = &g;
+    }
+    v->grid_buf.release();
+    v->gridi.release();
+    *v = csm_ctx::GridSlot();
+    c->swap_grid(*v);  // the current grid is parked; the empty slot becomes current
+    c->cur_use = ++c->grid_clock;
+  }
+  c->has_grid = false;
+  c->key_cells = nullptr;
+  c->key_version = -1;
+  return false;
+}
+
+// A borrowed device grid or a stack replaces the current grid: keep the
+// current host-map grid parked so a later csm_set_grid of it is free.
+void park_current(csm_ctx* c) {
+  if (c->owns_host_grid()) select_grid(c, nullptr);
+}
+
+// Pack rows [y0, y1) of a strided host grid into dst (row-major fp32) on the
+// context's host threads, and gather the values' fixed-point statistics
+// (smallest power-of-two granularity, largest magnitude, non-finite).
+struct PackStats {
+  int min_g = INT32_MAX;
+  float max_abs = 0.f;
+  bool nonfinite = false;
+};
+PackStats pack_rows(csm_ctx* c, const void* cells, int64_t stride, int32_t sx, int32_t y0, int32_t y1, float* dst) {
+  const int rows = y1 - y0;
+  const int chunks = std::max(1, std::min(rows, c->host_threads * 4));
+  std::vector<PackStats> part((size_t)chunks);
+  c->parallel_for(chunks, c->host_threads, [&](int t) {
+    const int r0 = y0 + (int)((int64_t)rows * t / chunks), r1 = y0 + (int)((int64_t)rows * (t + 1) / chunks);
+    PackStats ps;
+    for (int y = r0; y < r1; ++y) {
+      const char* src = (const char*)cells + ((int64_t)y * sx) * stride;
+      float* out = dst + (int64_t)(y - y0) * sx;
+      if (stride == 4) {
+        std::memcpy(out, src, (size_t)sx * 4);
+      } else {
+        for (int32_t x = 0; x < sx; ++x) std::memcpy(out + x, src + (int64_t)x * stride, 4);
+      }
+      for (int32_t x = 0; x < sx; ++x) {
+        const float v = out[x];
+        if (!std::isfinite(v)) ps.nonfinite = true;
+        bool z;
+        ps.min_g = std::min(ps.min_g, float_granularity(v, &z));
+        ps.max_abs = std::max(ps.max_abs, std::fabs(v));
+      }
+    }
+    part[(size_t)t] = ps;
+  });
+  PackStats all;
+  for (const auto& p : part) {
+    all.min_g = std::min(all.min_g, p.min_g);
+    all.max_abs = std::max(all.max_abs, p.max_abs);
+    all.nonfinite = all.nonfinite || p.nonfinite;
+  }
+  return all;
+}
+
+// New cell values keep the exact fixed-point copy valid when they are
+// multiples of 2^-E and within its range (ensure_int_grid's conditions);
+// otherwise the copy is rebuilt before the next match.
+void note_new_values(csm_ctx* c, const PackStats& ps) {
+  if (!c->int_checked || !c->int_ok) return;
+  const double scale = std::ldexp(1.0, c->int_exp);
+  if (ps.nonfinite || (ps.min_g != INT32_MAX && ps.min_g < -c->int_exp) ||
+      ((double)ps.max_abs + std::fabs((double)c->outside)) * scale >= std::ldexp(1.0, 26)) {
+    c->int_checked = false;
+    return;
+  }
+  c->int_max_abs = std::max(c->int_max_abs, (double)ps.max_abs);
 }
 
 // Scores windows_n windows of one level on the device. plans[i] describes
@@ -1899,6 +2051,12 @@ int csm_destroy(csm_ctx* c) {
     c->grid_buf.release();
     c->h_exact.release();
     c->gridi.release();
+    c->h_pack.release();
+    c->d_updates.release();
+    for (auto& pg : c->parked) {
+      pg.grid_buf.release();
+      pg.gridi.release();
+    }
     c->gstats.release();
     c->pts.release();
     c->scans.release();
@@ -1949,7 +2107,10 @@ const char* csm_last_error(const csm_ctx* c) { return c ? c->err.c_str() : "null
 int csm_set_outside_value(csm_ctx* c, float value) {
   if (!c) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  if (value != c->outside) c->int_checked = false;  // the fixed-point copy is shifted by it
+  if (value != c->outside) {  // every fixed-point copy is shifted by it
+    c->int_checked = false;
+    for (auto& g : c->parked) g.int_checked = false;
+  }
   c->outside = value;
   return CSM_OK;
 }
@@ -1964,34 +2125,32 @@ int csm_window_dims(const csm_param* p, int32_t* n_angles, int32_t* n_space) {
   return CSM_OK;
 }
 
-int csm_set_grid(csm_ctx* c, const void* cells, int64_t stride, const csm_map_info* info,
-                 int64_t version) {
-  if (!c || !info) return CSM_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
+namespace {
+
+int check_grid_args(csm_ctx* c, const void* cells, int64_t stride, const csm_map_info* info) {
   if (info->size_x <= 0 || info->size_y <= 0 || !(info->resolution > 0.0))
     return c->fail(CSM_ERR_INVALID_ARG, "grid size and resolution must be positive");
   if ((int64_t)info->size_x * info->size_y >= ((int64_t)1 << 31))
     return c->fail(CSM_ERR_INVALID_ARG, "grid larger than 2^31 cells");
-  if (!cells || stride < 4 || stride % 4 != 0) return c->fail(CSM_ERR_INVALID_ARG, "cells must be non-null with a stride that is a multiple of 4 bytes");
-  const bool same = c->has_grid && c->d_grid == c->grid_buf.p && version >= 0 && cells == c->key_cells &&
-                    stride == c->key_stride && version == c->key_version && info->size_x == c->key_sx &&
-                    info->size_y == c->key_sy;
-  c->info = *info;
-  if (same) return CSM_OK;
+  if (!cells || stride < 4 || stride % 4 != 0)
+    return c->fail(CSM_ERR_INVALID_ARG, "cells must be non-null with a stride that is a multiple of 4 bytes");
+  return CSM_OK;
+}
+
+// Whole-grid upload into the current slot (selected by the caller): rows are
+// packed on the host threads into pinned staging, then one H2D copy.
+int upload_grid(csm_ctx* c, const void* cells, int64_t stride, const csm_map_info* info, int64_t version) {
   const size_t ncell = (size_t)info->size_x * (size_t)info->size_y;
   hipError_t e;
   if ((e = c->grid_buf.ensure(ncell * sizeof(float))) != hipSuccess) return c->hip_fail(e, "hipMalloc(grid)");
-  const float* src = (const float*)cells;
-  if (stride != 4) {
-    c->h_pack.resize(ncell);
-    const char* b = (const char*)cells;
-    for (size_t i = 0; i < ncell; ++i) std::memcpy(&c->h_pack[i], b + i * (size_t)stride, 4);
-    src = c->h_pack.data();
-  }
-  if ((e = hipMemcpyAsync(c->grid_buf.p, src, ncell * sizeof(float), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+  if ((e = c->h_pack.ensure(ncell * sizeof(float))) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(grid)");
+  pack_rows(c, cells, stride, info->size_x, 0, info->size_y, (float*)c->h_pack.p);
+  if ((e = hipMemcpyAsync(c->grid_buf.p, c->h_pack.p, ncell * sizeof(float), hipMemcpyHostToDevice, c->stream)) !=
+      hipSuccess)
     return c->hip_fail(e, "hipMemcpyAsync(grid)");
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(grid)");
+  if (c->profiling) c->account("grid:upload", 0.f, (double)(ncell * sizeof(float)), 0.0);
+  c->info = *info;
   c->d_grid = (const float*)c->grid_buf.p;
   c->n_grids = 1;
   c->has_grid = true;
@@ -2004,6 +2163,127 @@ int csm_set_grid(csm_ctx* c, const void* cells, int64_t stride, const csm_map_in
   return CSM_OK;
 }
 
+// The current slot holds this map at this geometry (an incremental refresh
+// applies); otherwise the caller uploads the whole grid.
+bool same_geometry(const csm_ctx* c, const void* cells, int64_t stride, const csm_map_info* info) {
+  return c->owns_host_grid() && c->n_grids == 1 && c->key_cells == cells && c->key_stride == stride &&
+         c->key_sx == info->size_x && c->key_sy == info->size_y && c->info.resolution == info->resolution &&
+         c->info.offset_x == info->offset_x && c->info.offset_y == info->offset_y;
+}
+
+}  // namespace
+
+int csm_set_grid(csm_ctx* c, const void* cells, int64_t stride, const csm_map_info* info,
+                 int64_t version) {
+  if (!c || !info) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st = check_grid_args(c, cells, stride, info);
+  if (st != CSM_OK) return st;
+  select_grid(c, cells);
+  if (version >= 0 && same_geometry(c, cells, stride, info) && version == c->key_version) {
+    c->info = *info;
+    return CSM_OK;
+  }
+  return upload_grid(c, cells, stride, info, version);
+}
+
+int csm_update_grid_rows(csm_ctx* c, const void* cells, int64_t stride, const csm_map_info* info, int64_t version,
+                         int32_t row_begin, int32_t row_end) {
+  if (!c || !info) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st = check_grid_args(c, cells, stride, info);
+  if (st != CSM_OK) return st;
+  if (row_begin < 0 || row_end > info->size_y || row_begin > row_end)
+    return c->fail(CSM_ERR_INVALID_ARG, "row range outside the grid");
+  select_grid(c, cells);
+  if (!same_geometry(c, cells, stride, info)) return upload_grid(c, cells, stride, info, version);
+  c->info = *info;
+  c->key_version = version;
+  if (row_begin == row_end) return CSM_OK;
+  const int32_t sx = info->size_x;
+  const size_t n = (size_t)(row_end - row_begin) * (size_t)sx;
+  hipError_t e;
+  if ((e = c->h_pack.ensure(n * sizeof(float))) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(rows)");
+  const PackStats ps = pack_rows(c, cells, stride, sx, row_begin, row_end, (float*)c->h_pack.p);
+  float* dst = (float*)c->grid_buf.p + (int64_t)row_begin * sx;
+  if ((e = hipMemcpyAsync(dst, c->h_pack.p, n * sizeof(float), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(rows)");
+  note_new_values(c, ps);
+  if (c->int_checked && c->int_ok &&
+      (e = csm::launch_fixed_point(dst, sx, row_end - row_begin, c->pitch, c->outside, c->int_exp,
+                                   (int32_t*)c->gridi.p + (int64_t)row_begin * c->pitch, c->stream, false)) !=
+          hipSuccess)
+    return c->hip_fail(e, "fixed_point_kernel(rows)");
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(rows)");
+  if (c->profiling) c->account("grid:rows", 0.f, (double)(n * sizeof(float)), 0.0);
+  return CSM_OK;
+}
+
+int csm_update_grid_cells(csm_ctx* c, const void* cells, int64_t stride, const csm_map_info* info, int64_t version,
+                          const int32_t* cell_indices, int64_t n_indices) {
+  if (!c || !info) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st = check_grid_args(c, cells, stride, info);
+  if (st != CSM_OK) return st;
+  if (n_indices < 0 || (n_indices > 0 && !cell_indices)) return c->fail(CSM_ERR_INVALID_ARG, "cell index list");
+  select_grid(c, cells);
+  if (!same_geometry(c, cells, stride, info)) return upload_grid(c, cells, stride, info, version);
+  const int64_t ncell = (int64_t)info->size_x * info->size_y;
+  hipError_t e;
+  if ((e = c->h_pack.ensure((size_t)std::max<int64_t>(n_indices, 1) * sizeof(csm::CellUpdate))) != hipSuccess)
+    return c->hip_fail(e, "hipHostMalloc(cell updates)");
+  csm::CellUpdate* u = (csm::CellUpdate*)c->h_pack.p;
+  const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(c->host_threads * 4, n_indices / 4096 + 1));
+  std::vector<PackStats> part((size_t)chunks);
+  std::atomic<bool> bad{false};
+  c->parallel_for(chunks, c->host_threads, [&](int t) {
+    const int64_t i0 = n_indices * t / chunks, i1 = n_indices * (t + 1) / chunks;
+    PackStats ps;
+    for (int64_t i = i0; i < i1; ++i) {
+      const int32_t k = cell_indices[i];
+      if (k < 0 || k >= ncell) {
+        bad = true;
+        return;
+      }
+      float v;
+      std::memcpy(&v, (const char*)cells + (int64_t)k * stride, 4);
+      u[i].index = k;
+      u[i].value = v;
+      if (!std::isfinite(v)) ps.nonfinite = true;
+      bool z;
+      ps.min_g = std::min(ps.min_g, float_granularity(v, &z));
+      ps.max_abs = std::max(ps.max_abs, std::fabs(v));
+    }
+    part[(size_t)t] = ps;
+  });
+  if (bad) return c->fail(CSM_ERR_INVALID_ARG, "cell index outside the grid");
+  c->info = *info;
+  c->key_version = version;
+  if (n_indices == 0) return CSM_OK;
+  PackStats all;
+  for (const auto& p : part) {
+    all.min_g = std::min(all.min_g, p.min_g);
+    all.max_abs = std::max(all.max_abs, p.max_abs);
+    all.nonfinite = all.nonfinite || p.nonfinite;
+  }
+  note_new_values(c, all);
+  const size_t bytes = (size_t)n_indices * sizeof(csm::CellUpdate);
+  if ((e = c->d_updates.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(cell updates)");
+  if ((e = hipMemcpyAsync(c->d_updates.p, u, bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipMemcpyAsync(cell updates)");
+  const bool fixed = c->int_checked && c->int_ok;
+  if ((e = csm::launch_update_cells((const csm::CellUpdate*)c->d_updates.p, n_indices, (float*)c->grid_buf.p,
+                                    info->size_x, fixed ? (int32_t*)c->gridi.p : nullptr, c->pitch, c->outside,
+                                    c->int_exp, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "update_cells_kernel");
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(cells)");
+  if (c->profiling) c->account("grid:cells", 0.f, (double)bytes, 0.0);
+  return CSM_OK;
+}
+
 int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) {
   if (!c || !info) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -2011,6 +2291,7 @@ int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) 
     return c->fail(CSM_ERR_INVALID_ARG, "invalid device grid");
   if ((int64_t)info->size_x * info->size_y >= ((int64_t)1 << 31))
     return c->fail(CSM_ERR_INVALID_ARG, "grid larger than 2^31 cells");
+  park_current(c);
   c->info = *info;
   c->d_grid = dev;
   c->n_grids = 1;
@@ -2273,7 +2554,8 @@ int csm_set_grid_stack(csm_ctx* c, const float* cells, int32_t n_grids, const cs
     return c->fail(CSM_ERR_INVALID_ARG, "grid size and resolution must be positive");
   const int64_t ncell = (int64_t)info->size_x * info->size_y;
   if (ncell >= ((int64_t)1 << 31)) return c->fail(CSM_ERR_INVALID_ARG, "grid larger than 2^31 cells");
-  const bool same = c->has_grid && c->d_grid == c->grid_buf.p && version >= 0 && (const void*)cells == c->key_cells &&
+  select_grid(c, cells);
+  const bool same = c->owns_host_grid() && version >= 0 && (const void*)cells == c->key_cells &&
                     c->key_stride == -n_grids && version == c->key_version && info->size_x == c->key_sx &&
                     info->size_y == c->key_sy;
   c->info = *info;
@@ -2447,6 +2729,7 @@ int csm_set_grid_stack_gridmaps(csm_ctx* c, csm_gridmap* const* maps, int32_t n_
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  park_current(c);
   const csm::GridMapView& a = v[0];
   int32_t min_index = a.map_update_index;
   for (const auto& b : v) {

@@ -224,8 +224,17 @@ constexpr int kAnalyzeBlocks = 1024;
 hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hipStream_t stream);
 // Row pitch of gridi is a multiple of 4 cells, so 16-byte row segments are
 // aligned; size_y + kGridiPadRows rows are written, the pad zero.
+// pad = false converts rows only (a row range of a resident grid, no pad rows).
 hipError_t launch_fixed_point(const float* g, int32_t sx, int32_t sy, int32_t pitch, float outside,
-                              int int_exp, int32_t* gi, hipStream_t stream);
+                              int int_exp, int32_t* gi, hipStream_t stream, bool pad = true);
+// One cell of an incremental grid refresh (csm_update_grid_cells).
+struct CellUpdate {
+  int32_t index;  // y * size_x + x
+  float value;
+};
+// gi null: no fixed-point copy to keep in step.
+hipError_t launch_update_cells(const CellUpdate* d_updates, int64_t n, float* g, int32_t sx, int32_t* gi,
+                               int32_t pitch, float outside, int int_exp, hipStream_t stream);
 // ---- Gauss-Newton scan matcher (csm_optimize.hip) --------------------------
 // Per scan and iteration: the pose in map cells and the host glibc cos/sin of
 // its angle (optimize_scan_matcher.h:94-97).

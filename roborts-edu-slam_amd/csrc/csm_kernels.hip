@@ -1125,8 +1125,9 @@ __global__ __launch_bounds__(256) void analyze_reduce_kernel(const GridStats* __
 // and the appended zero row y = sy (what DMA reads for rows off the grid) = 0.
 __global__ __launch_bounds__(256) void fixed_point_kernel(const float* __restrict__ g, int32_t sx,
                                                           int32_t sy, int32_t pitch, float outside,
-                                                          double scale, int32_t* __restrict__ gi) {
-  const int64_t n = (int64_t)pitch * (sy + kGridiPadRows);
+                                                          double scale, int32_t* __restrict__ gi,
+                                                          int32_t pad_rows) {
+  const int64_t n = (int64_t)pitch * (sy + pad_rows);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t y = i / pitch;
@@ -1146,11 +1147,42 @@ hipError_t launch_analyze_grid(const float* g, int64_t n, GridStats* d_stats, hi
 }
 
 hipError_t launch_fixed_point(const float* g, int32_t sx, int32_t sy, int32_t pitch, float outside,
-                              int int_exp, int32_t* gi, hipStream_t stream) {
-  const int64_t n = (int64_t)pitch * (sy + kGridiPadRows);
+                              int int_exp, int32_t* gi, hipStream_t stream, bool pad) {
+  const int32_t pad_rows = pad ? kGridiPadRows : 0;
+  const int64_t n = (int64_t)pitch * (sy + pad_rows);
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(fixed_point_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0,
-                     stream, g, sx, sy, pitch, outside, ldexp(1.0, int_exp), gi);
+                     stream, g, sx, sy, pitch, outside, ldexp(1.0, int_exp), gi, pad_rows);
+  return hipGetLastError();
+}
+
+namespace {
+// Incremental refresh of a resident grid (csm_update_grid_cells): each entry
+// rewrites one fp32 cell and, when the exact fixed-point copy exists, its
+// int32 image with the fixed_point_kernel's expression. Duplicate indices
+// carry the same value, so their order does not matter.
+__global__ __launch_bounds__(256) void update_cells_kernel(const CellUpdate* __restrict__ u, int64_t n,
+                                                           float* __restrict__ g, int32_t sx,
+                                                           int32_t* __restrict__ gi, int32_t pitch,
+                                                           float outside, double scale) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const CellUpdate c = u[i];
+    g[c.index] = c.value;
+    if (gi) {
+      const int32_t y = c.index / sx;
+      const int32_t x = c.index - y * sx;
+      gi[(int64_t)y * pitch + x] = (int32_t)(((double)c.value - (double)outside) * scale);
+    }
+  }
+}
+}  // namespace
+
+hipError_t launch_update_cells(const CellUpdate* d_updates, int64_t n, float* g, int32_t sx, int32_t* gi,
+                               int32_t pitch, float outside, int int_exp, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(update_cells_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, d_updates, n, g, sx, gi,
+                     pitch, outside, ldexp(1.0, int_exp));
   return hipGetLastError();
 }
 

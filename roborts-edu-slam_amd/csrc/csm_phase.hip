@@ -45,10 +45,13 @@ constexpr int kSeg = CSM_PHASE_SEG;  // beams classified per segment (lists in L
 constexpr int kEntG = 5;             // groups per list entry: 6 slots * 5 * (2^26 - 1) < 2^31
 constexpr int kChunks = kSeg / 64;   // 64-beam chunks per segment, classified in registers
 #ifndef CSM_PHASE_DEPTH
-#define CSM_PHASE_DEPTH 8  // 8: 0.418-0.423 ms per fine launch, 16: 0.426, 24: 0.45, 4: 0.424
+#define CSM_PHASE_DEPTH 8  // 8: 0.418-0.423 ms per fine launch, 16: 0.426, 4: 0.424 (24 was a wrong build)
 #endif
 constexpr int kD = CSM_PHASE_DEPTH;  // groups of loads in flight
 static_assert(kD <= 32, "int32 partial sums fold every kD groups");
+// gentry[lane & (kD - 1)] and the group-window slides index by masking
+static_assert((kD & (kD - 1)) == 0, "CSM_PHASE_DEPTH must be a power of two");
+static_assert(kSeg % 64 == 0, "CSM_PHASE_SEG must be whole 64-beam chunks");
 // 1: flush a lane's sums only where an entry ends (a uniform branch; 0.465 ->
 // 0.427 ms per fine launch); 0: every group adds into dummy cells, branch-free
 #ifndef CSM_PHASE_BRANCH_FLUSH

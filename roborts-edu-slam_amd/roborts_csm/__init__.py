@@ -178,10 +178,50 @@ class Context:
             stride = cells.dtype.itemsize
         else:
             raise TypeError("grid cells must be float32 or a ProbabilityCell structured array")
-        self._grid_ref = cells  # keep the host copy alive (key is its address)
+        self._keep(cells)
         info = m.info()
         self._check(_lib.csm_set_grid(self._h, cells.ctypes.data_as(C.c_void_p), stride,
                                       C.byref(info), -1 if force else int(m.version)))
+
+    def _keep(self, cells):
+        """Keep host grids alive while the library may key resident copies on
+        their address (up to four maps stay resident)."""
+        refs = self.__dict__.setdefault("_grid_refs", {})
+        refs.pop(cells.ctypes.data, None)
+        refs[cells.ctypes.data] = cells
+        while len(refs) > 8:
+            refs.pop(next(iter(refs)))
+
+    @staticmethod
+    def _cells_of(m: ScanMatchMap):
+        cells = m.cells
+        if cells.dtype == np.float32:
+            stride = 4
+        elif cells.dtype.names and "prob_value_" in cells.dtype.names:
+            stride = cells.dtype.itemsize
+        else:
+            raise TypeError("grid cells must be float32 or a ProbabilityCell structured array")
+        if not cells.flags.c_contiguous:
+            raise ValueError("incremental refresh needs the map's own contiguous cell array")
+        return cells, stride
+
+    def update_grid_cells(self, m: ScanMatchMap, cell_indices):
+        """csm_update_grid_cells: re-read the listed cells (y*size_x + x) of a
+        resident map after an in-place update; m.version is the new key."""
+        cells, stride = self._cells_of(m)
+        self._keep(cells)
+        idx = np.ascontiguousarray(cell_indices, dtype=np.int32).ravel()
+        info = m.info()
+        self._check(_lib.csm_update_grid_cells(self._h, cells.ctypes.data_as(C.c_void_p), stride, C.byref(info),
+                                               int(m.version), idx.ctypes.data_as(_abi._i32p), idx.size))
+
+    def update_grid_rows(self, m: ScanMatchMap, row_begin: int, row_end: int):
+        """csm_update_grid_rows: re-read rows [row_begin, row_end)."""
+        cells, stride = self._cells_of(m)
+        self._keep(cells)
+        info = m.info()
+        self._check(_lib.csm_update_grid_rows(self._h, cells.ctypes.data_as(C.c_void_p), stride, C.byref(info),
+                                              int(m.version), int(row_begin), int(row_end)))
 
     def set_grid_device(self, dev_ptr: int, m: ScanMatchMap):
         info = m.info()

@@ -23,7 +23,8 @@ COARSE, FINE, SUPER, FAST = 0, 1, 2, 3
 # Every function include/csm.h declares (checked by tests/test_abi.py).
 EXPORTED = (
     "csm_create", "csm_destroy", "csm_last_error", "csm_abi_version",
-    "csm_set_outside_value", "csm_set_grid", "csm_set_grid_device",
+    "csm_set_outside_value", "csm_set_grid", "csm_set_grid_device", "csm_update_grid_cells",
+    "csm_update_grid_rows",
     "csm_window_dims", "csm_scan_match", "csm_scan_matchers",
     "csm_scan_match_batch", "csm_scan_matchers_batch", "csm_score_window",
     "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded",
@@ -146,6 +147,10 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_set_outside_value": (C.c_int, [_ctx, C.c_float]),
         "csm_set_grid": (C.c_int, [_ctx, C.c_void_p, C.c_int64, C.POINTER(CsmMapInfo), C.c_int64]),
         "csm_set_grid_device": (C.c_int, [_ctx, C.c_void_p, C.POINTER(CsmMapInfo)]),
+        "csm_update_grid_cells": (C.c_int, [_ctx, C.c_void_p, C.c_int64, C.POINTER(CsmMapInfo), C.c_int64, _i32p,
+                                            C.c_int64]),
+        "csm_update_grid_rows": (C.c_int, [_ctx, C.c_void_p, C.c_int64, C.POINTER(CsmMapInfo), C.c_int64,
+                                           C.c_int32, C.c_int32]),
         "csm_window_dims": (C.c_int, [C.POINTER(CsmParam), _i32p, _i32p]),
         "csm_scan_match": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), _dp, _dp, _dp, _i64p]),
         "csm_scan_matchers": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), C.c_int32, _dp, _dp, _dp]),

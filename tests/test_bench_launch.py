@@ -1,0 +1,33 @@
+"""bench.py's multi-GPU launch protocol on the CPU (gloo): `--gpus N` with no
+torch.distributed environment spawns N ranks itself, times with barriers, takes
+the max over ranks and sums the units; rank 0 prints exactly one JSON line."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_self_launch_gloo(n):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--workload",
+                        "plumbing", "--backend", "gloo", "--steps", "4"],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["world"] == {"world_size": n, "backend": "gloo"}
+    assert out["n_gpus"] == n
+    assert out["rank_units"] == 4.0 * n  # every rank's units summed
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload",
+                        "plumbing"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
