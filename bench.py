@@ -531,6 +531,43 @@ def backend_bench(args, rank, world_size, dist, torch):
     }
 
 
+def adapter_bench(args, rank, world_size, dist, torch):
+    """The reference-side drop-in (include/csm_reference_adapter.hpp) as the
+    reference calls it: ScanMatchers::ScanMatch's three levels per scan
+    (scan_matchers.h:238,249,256) on the front end's 1 cm fine map (3000 x
+    3000 AoS ProbabilityCell, slam_processor.cpp:469,499-500) with ~1e5 cells
+    rewritten between scans (UpdateMapByRange). Timed in C++ by
+    tests/cpp/adapter_run: per-scan latency including the grid refresh, with
+    the incremental refresh (csm_update_grid_cells) and with whole-grid
+    uploads, next to the oracle's CPU matcher on the same scans. Replicas
+    only; rank 0 reports."""
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "adapter_run")
+    if not os.path.exists(exe):
+        raise SystemExit("tests/cpp/build/adapter_run missing: run __graft_entry__.build()")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("LOCAL_RANK", "0")) if world_size > 1 else None
+    r = subprocess.run([exe, "bench", str(max(args.steps, 3) + 1), "3000"], capture_output=True, text=True,
+                       timeout=600, env=env)
+    if r.returncode != 0:
+        raise SystemExit(f"adapter_run failed ({r.returncode}): {r.stdout[-2000:]} {r.stderr[-2000:]}")
+    a = json.loads(r.stdout.strip().splitlines()[-1])
+    lat = a["adapter_incremental_ms_p50"]
+    return {
+        "metric": "drop-in adapter 3-level ScanMatch latency per scan (config 5 shape, incl. grid refresh)",
+        "value": 1e3 / lat, "unit": "scans/s", "n_gpus": world_size, "steps": a["scans"] - 1,
+        "warmup": 1, "ms_per_step": lat, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic 3000x3000 @1cm AoS map with walls; 1081-beam ray-marched scans; "
+                                "1e5 random cells rewritten between scans",
+        "config": {"workload": "adapter: BasedCorrelationScanMatchGpu x 3 levels per scan (sim YAML, U=100)",
+                   "incremental_ms_p50": lat, "whole_upload_ms_p50": a["adapter_whole_upload_ms_p50"],
+                   "host_map_mutation_ms_p50": a["host_map_mutation_ms_p50"],
+                   "parallelism": f"replicas x{world_size}"},
+        "roofline": None,
+        "cpu_baseline": {"value": 1e3 / a["oracle_cpu_ms_p50"], "unit": "scans/s", "cores": 1, "kind": "port",
+                         "sample": f"the same {a['scans'] - 1} scans x 3 levels through oracle_scan_match "
+                                   f"(single-threaded restatement of the reference) on {_cpu_model()}"},
+    }
+
+
 def plumbing_bench(args, rank, world_size, dist, torch):
     """The launcher and timing protocol without the matcher (CPU tests of
     `--gpus N`): barrier, --steps timed sleeps of 1 ms, max over ranks, sum of
@@ -603,7 +640,8 @@ def main():
     ap.add_argument("--scans", type=int, default=4096, help="scans per GPU per step")
     ap.add_argument("--levels", choices=["headline", "sim"], default="headline",
                     help="headline: every beam summed (B=1081); sim: reference YAML U=100 (B=109)")
-    ap.add_argument("--workload", choices=["config2", "loop_closure", "willow", "online", "backend", "plumbing"],
+    ap.add_argument("--workload", choices=["config2", "loop_closure", "willow", "online", "backend", "adapter",
+                                           "plumbing"],
                     default="config2",
                     help="config2: the headline front-end batch; loop_closure: config 3; willow: config 4; "
                          "online: config 5 (steps = scans); backend: f2 pose-graph jobs")
@@ -643,9 +681,9 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
 
-    if args.workload in ("loop_closure", "willow", "online", "backend", "plumbing"):
+    if args.workload in ("loop_closure", "willow", "online", "backend", "adapter", "plumbing"):
         fn = {"loop_closure": loop_closure_bench, "willow": willow_bench, "online": online_bench,
-              "backend": backend_bench, "plumbing": plumbing_bench}[args.workload]
+              "backend": backend_bench, "adapter": adapter_bench, "plumbing": plumbing_bench}[args.workload]
         out = fn(args, rank, world_size, dist, torch)
         if rank == 0:
             out["world"] = world_info(dist)

@@ -125,7 +125,11 @@ int csm_gridmap_download(csm_gridmap* map, float* prob, float* pass_count, float
 int csm_gridmap_device_prob(csm_gridmap* map, const float** device_prob);
 
 /* Point the scan matcher at this map (borrowed, like csm_set_grid_device):
- * size, resolution, offset and update index come from the map. */
+ * size, resolution, offset and update index come from the map.
+ * Ordering, both ways: the matcher's work runs after the map's last update,
+ * and the map's later updates (update_by_range, reset, init, update_bound)
+ * wait for every match or copy already enqueued on that matcher context, so
+ * a map may be updated right after set_grid returns, from any thread. */
 int csm_set_grid_gridmap(csm_ctx* ctx, csm_gridmap* map);
 
 /* Make n maps of one size, resolution and offset resident as a grid stack

@@ -2048,6 +2048,9 @@ int csm_destroy(csm_ctx* c) {
       if (a.stream) (void)hipStreamSynchronize(a.stream);
     if (c->fin_stream) (void)hipStreamSynchronize(c->fin_stream);
     if (c->x2h) (void)hipStreamSynchronize(c->x2h);
+    csm::gridmap_drop_reader(c->stream);
+    for (auto& a : c->alt)
+      if (a.stream) csm::gridmap_drop_reader(a.stream);
     c->grid_buf.release();
     c->h_exact.release();
     c->gridi.release();
@@ -2311,9 +2314,13 @@ int csm_set_grid_gridmap(csm_ctx* c, csm_gridmap* map) {
   {
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
-    // the matcher's kernels run after the map's last update
+    // the matcher's kernels run after the map's last update, and the map's
+    // next update after the matcher's reads (csm::gridmap_add_reader)
     hipError_t e = hipStreamWaitEvent(c->stream, v.ready, 0);
     if (e != hipSuccess) return c->fail(CSM_ERR_HIP, hipGetErrorString(e));
+    csm::gridmap_add_reader(map, c->stream);
+    for (auto& a : c->alt)
+      if (a.stream) csm::gridmap_add_reader(map, a.stream);
   }
   csm_map_info info{};
   info.resolution = v.resolution;
@@ -2745,6 +2752,7 @@ int csm_set_grid_stack_gridmaps(csm_ctx* c, csm_gridmap* const* maps, int32_t n_
   if ((e = c->grid_buf.ensure((size_t)ncell * (size_t)n_maps * sizeof(float))) != hipSuccess)
     return c->hip_fail(e, "hipMalloc(grid stack)");
   for (int32_t i = 0; i < n_maps; ++i) {  // after each map's last update, on the matcher's stream
+    csm::gridmap_add_reader(maps[i], c->stream);  // and the map's next update after the copy
     if ((e = hipStreamWaitEvent(c->stream, v[(size_t)i].ready, 0)) != hipSuccess ||
         (e = hipMemcpyAsync((float*)c->grid_buf.p + (size_t)i * (size_t)ncell, v[(size_t)i].prob,
                             (size_t)ncell * sizeof(float), hipMemcpyDeviceToDevice, c->stream)) != hipSuccess)

@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -95,6 +96,7 @@ struct csm_gridmap {
   hipStream_t stream = nullptr;
   hipEvent_t ready = nullptr;       // after the last enqueued update
   hipEvent_t staged = nullptr;      // the last H2D copy out of h_ends has been consumed
+  hipEvent_t read_done = nullptr;   // reader streams' work so far (wait_readers)
   std::mutex mu;
   std::string err;
 
@@ -400,7 +402,38 @@ int finish(csm_gridmap* m) {
 
 }  // namespace
 
+namespace {
+// Matcher streams that read a map's cells (csm_set_grid_gridmap borrows them
+// until the next set_grid; csm_set_grid_stack_gridmaps copies them on its
+// stream). A map update first waits for the work already enqueued on those
+// streams, so an update issued after a set_grid* call can never overwrite
+// cells a pending match or copy still reads.
+std::mutex g_readers_mu;
+std::map<const csm_gridmap*, std::vector<hipStream_t>> g_readers;
+
+int wait_readers(csm_gridmap* m) {
+  std::lock_guard<std::mutex> lk(g_readers_mu);
+  auto it = g_readers.find(m);
+  if (it == g_readers.end()) return CSM_OK;
+  for (hipStream_t s : it->second) {
+    GM_HIP(hipEventRecord(m->read_done, s));
+    GM_HIP(hipStreamWaitEvent(m->stream, m->read_done, 0));
+  }
+  return CSM_OK;
+}
+}  // namespace
+
 namespace csm {
+void gridmap_add_reader(csm_gridmap* m, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_readers_mu);
+  auto& v = g_readers[m];
+  if (std::find(v.begin(), v.end(), s) == v.end()) v.push_back(s);
+}
+void gridmap_drop_reader(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_readers_mu);
+  for (auto& kv : g_readers) kv.second.erase(std::remove(kv.second.begin(), kv.second.end(), s), kv.second.end());
+}
+
 int gridmap_view(csm_gridmap* m, GridMapView* v) {
   if (!m || !v) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(m->mu);
@@ -433,6 +466,7 @@ int csm_gridmap_create(int device, int32_t kind, double resolution, int32_t size
   DeviceGuard g(device);
   if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&m->ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->read_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->staged, hipEventDisableTiming) != hipSuccess) {
     csm_gridmap_destroy(m);
     return CSM_ERR_HIP;
@@ -486,8 +520,13 @@ int csm_gridmap_destroy(csm_gridmap* m) {
                     &m->count})
       b->release();
     if (m->h_ends) (void)hipHostFree(m->h_ends);
+    {
+      std::lock_guard<std::mutex> lk(g_readers_mu);
+      g_readers.erase(m);
+    }
     if (m->ready) (void)hipEventDestroy(m->ready);
     if (m->staged) (void)hipEventDestroy(m->staged);
+    if (m->read_done) (void)hipEventDestroy(m->read_done);
     if (m->stream) (void)hipStreamDestroy(m->stream);
   }
   delete m;
@@ -538,6 +577,7 @@ int csm_gridmap_reset(csm_gridmap* m) {
   if (!m) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(m->mu);
   DeviceGuard g(m->device);
+  if (int rst = wait_readers(m)) return rst;
   int st;
   if ((st = flush_pending(m)) != CSM_OK) return st;
   // Reset (grid_map_base.h:95-103) leaves map_update_point_ as it is.
@@ -550,6 +590,7 @@ int csm_gridmap_update_bound(csm_gridmap* m, double min_x, double min_y, double 
   if (!m) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(m->mu);
   DeviceGuard g(m->device);
+  if (int rst = wait_readers(m)) return rst;
   Box b;
   b.minx = min_x;
   b.miny = min_y;
@@ -567,6 +608,7 @@ int csm_gridmap_update_by_range(csm_gridmap* m, const double* pts, int32_t n, co
   if (!m || !pose || (n > 0 && !pts) || n < 0) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(m->mu);
   DeviceGuard g(m->device);
+  if (int rst = wait_readers(m)) return rst;
   const double zero[2] = {0.0, 0.0};
   bool up = false;
   int st = update_by_range(m, pts, n, origin ? origin : zero, pose, use_blur != 0, &up);
@@ -581,6 +623,7 @@ int csm_gridmap_init_with_range_vec(csm_gridmap* m, int32_t n_scans, const doubl
   if (!m || n_scans < 0 || (n_scans > 0 && (!offsets || !poses))) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(m->mu);
   DeviceGuard g(m->device);
+  if (int rst = wait_readers(m)) return rst;
   for (int k = 0; k < n_scans; ++k)
     if (offsets[k + 1] < offsets[k] || (offsets[k + 1] > offsets[k] && !pts)) return CSM_ERR_INVALID_ARG;
   int mode = 0, st;

@@ -62,5 +62,9 @@ struct GridMapView {
 struct csm_gridmap;
 namespace csm {
 int gridmap_view(csm_gridmap* m, GridMapView* v);
+// A matcher stream reads the map: the map's next updates wait for the work
+// enqueued on it so far. drop_reader: the stream is going away.
+void gridmap_add_reader(csm_gridmap* m, hipStream_t s);
+void gridmap_drop_reader(hipStream_t s);
 
 }  // namespace csm

@@ -94,3 +94,36 @@ def test_matcher_reads_device_map():
     om = O.Map(prob, st.resolution, (st.offset_x, st.offset_y), st.map_update_index)
     s2, pose2, cov2 = O.scan_matchers(om, scans[3], SIM_YAML_LEVELS, init, np.eye(3))
     assert s == s2 and np.array_equal(pose, pose2) and np.array_equal(cov, cov2)
+
+
+def test_map_update_after_set_grid_is_ordered():
+    """csm_set_grid_gridmap borrows the cells until the next set_grid; a map
+    update issued right after it (no match in between) must wait for the
+    matcher's reads: the match sees the cells as they were when the update was
+    issued after the match was enqueued, so here (update after the match call
+    returns) the matcher result is the oracle's on the pre-update cells, and a
+    second match after the update sees the updated cells."""
+    import pyoracle as O
+    import roborts_csm
+    from roborts_csm.gridmap import OccuGridMap, set_matcher_grid
+    from roborts_csm.params import SIM_YAML_LEVELS
+    scans, poses = _fine_map_stream(6)
+    res = 0.01
+    off = (-(poses[0][0] - 0.5 * 1500 * res), -(poses[0][1] - 0.5 * 1500 * res))
+    m = OccuGridMap(res, (1500, 1500), off, 0.03, 0.3)
+    m.set_options(True, True, 0.88, 0.2)
+    for k in range(3):
+        m.UpdateMapByRange(scans[k], poses[k], use_blur=True)
+    with roborts_csm.Context(0) as ctx:
+        for k in (3, 4):
+            st = m.state()
+            prob = m.cells()[0].copy()
+            set_matcher_grid(ctx, m)
+            init = poses[k] + np.array([0.03, -0.02, 0.02])
+            pose = init.copy()
+            cov = np.eye(3).reshape(9).copy()
+            s = ctx.scan_matchers(scans[k], SIM_YAML_LEVELS, pose, cov)
+            m.UpdateMapByRange(scans[k], poses[k], use_blur=True)  # right after: ordered after the reads
+            om = O.Map(prob, st.resolution, (st.offset_x, st.offset_y), st.map_update_index)
+            s2, pose2, cov2 = O.scan_matchers(om, scans[k], SIM_YAML_LEVELS, init, np.eye(3))
+            assert s == s2 and np.array_equal(pose, pose2) and np.array_equal(cov, cov2), k
