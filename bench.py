@@ -219,7 +219,11 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
     ctx = roborts_csm.Context(int(os.environ.get("LOCAL_RANK", "0")))
     ctx.set_grid_stack(stack, res, version=1)
     dev = "cuda" if torch.cuda.is_available() else "cpu"
-    lc = ShardedLoopClosure(ctx, n_sub, res, offsets, rank=rank, world=world_size, device=dev)
+    lc = ShardedLoopClosure(ctx, n_sub, res, offsets, rank=rank, world=world_size, device=dev,
+                            search=args.search)
+    if args.search == "pyramid" and args.depth >= 0:
+        sw = ctx.search_windows
+        ctx.search_windows = lambda *a, **k: sw(*a, max_depth=args.depth, **k)
     for _ in range(args.warmup):
         lc.match(pts, param, pose)
     ctx.set_profiling(True)
@@ -242,6 +246,25 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
     avg_ms = dom["total_ms"] / dom["launches"]
     rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"],
                   load_counters(args.counters_json), args.counters_json)
+    search = None
+    if args.search == "pyramid":
+        st = lc.last_stats or {}
+        search = {"kind": "admissible multi-resolution branch and bound (csm_search_windows)",
+                  "depth": st.get("depth"), "nodes_per_level": st.get("nodes"),
+                  "probe_leaves": st.get("probe_leaves"),
+                  "nodes_scored_per_query_rank0": (sum(st.get("nodes", [])) + st.get("probe_leaves", 0)),
+                  "beam_reads_per_query_rank0": st.get("beam_reads"),
+                  "candidates_per_query_rank0": st.get("candidates"),
+                  "value_note": "value counts every candidate of every window as resolved (the answer equals "
+                                "the exhaustive argmax, tests/test_gpu_search.py); the nodes actually scored "
+                                "are nodes_scored_per_query_rank0"}
+        if world_size == 1:  # the exhaustive search of the same query, same run
+            ex = ShardedLoopClosure(ctx, n_sub, res, offsets, search="exhaustive")
+            ex.match(pts, param, pose)
+            te = time.perf_counter()
+            r2 = ex.match(pts, param, pose)
+            search["exhaustive_ms_per_query"] = (time.perf_counter() - te) * 1e3
+            search["same_answer_as_exhaustive"] = bool(r2.global_index == r.global_index and r2.score == r.score)
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu:
         cpu = lc_cpu_baseline(bases, pts, param, pose, args.cpu_seconds, na * ns * ns)
@@ -252,9 +275,11 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
         "data": "synthetic (8 seeded 800x800 wall maps, shifted into 512 submaps; one ray-cast query)",
         "config": {"workload": f"config3: loop closure, 1 query x {n_sub} submaps 800x800 @5cm, "
                                f"+-8 m / +-pi window ({na}x{ns}^2 candidates per submap), B=109",
+                   "search": args.search,
                    "parallelism": f"submaps sharded x{world_size}, MAX/MIN all-reduce"},
         "roofline": rl,
         "result": {"score": r.score, "submap": r.submap, "global_index": r.global_index},
+        "search": search,
         "kernels": stats, "cpu_baseline": cpu,
     }
 
@@ -301,9 +326,16 @@ def willow_bench(args, rank, world_size, dist, torch):
     ctx.set_grid(roborts_csm.ScanMatchMap(w.grid, w.resolution, w.offset, 0, 1))
     from roborts_csm.loop_closure import world_to_map
 
-    def query(k):
+    last = {}
+
+    def query(k, search=args.search):
         pts = batch.points_cells[batch.offsets[k]:batch.offsets[k + 1]]
-        return ctx.best_window(pts, param, world_to_map(batch.init_poses[k], w.resolution, w.offset))
+        c = world_to_map(batch.init_poses[k], w.resolution, w.offset)
+        if search == "exhaustive":
+            return ctx.best_window(pts, param, c)
+        b, _, st = ctx.search_windows(pts, param, [0], c.reshape(1, 3), max_depth=args.depth)
+        last.update(st)
+        return b
 
     for k in range(args.warmup):
         query(args.steps + k)
@@ -319,6 +351,23 @@ def willow_bench(args, rank, world_size, dist, torch):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stats = ctx.kernel_stats()
+    search = None
+    if args.search == "pyramid":
+        search = {"kind": "admissible multi-resolution branch and bound (csm_search_windows)",
+                  "depth": last.get("depth"), "nodes_per_level_last_query": last.get("nodes"),
+                  "beam_reads_last_query": last.get("beam_reads"),
+                  "value_note": "value counts every candidate of the window as resolved (the answer equals "
+                                "the exhaustive argmax, tests/test_gpu_search.py)"}
+        if world_size == 1:
+            same = True
+            te = time.perf_counter()
+            for k in range(args.steps):
+                b1 = query(k, "exhaustive")
+            search["exhaustive_ms_per_query"] = (time.perf_counter() - te) / args.steps * 1e3
+            for k in range(min(args.steps, 3)):
+                b1, b2 = query(k, "exhaustive"), query(k)
+                same = same and b1.score == b2.score and b1.flat_index == b2.flat_index
+            search["same_answer_as_exhaustive"] = bool(same)
     local = float(na * ns * ns * args.steps)
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     if dist is not None:
@@ -343,8 +392,9 @@ def willow_bench(args, rank, world_size, dist, torch):
         tc = time.perf_counter()
         m = 0
         while m < 1 or time.perf_counter() - tc < args.cpu_seconds:
-            pts = batch.points_cells[batch.offsets[m]:batch.offsets[m + 1]]
-            O.best_window(om, pts, param, world_to_map(batch.init_poses[m], w.resolution, w.offset))
+            q = m % args.steps  # the timed queries, cycled
+            pts = batch.points_cells[batch.offsets[q]:batch.offsets[q + 1]]
+            O.best_window(om, pts, param, world_to_map(batch.init_poses[q], w.resolution, w.offset))
             m += 1
         dtc = time.perf_counter() - tc
         O.set_threads(1)
@@ -358,9 +408,9 @@ def willow_bench(args, rank, world_size, dist, torch):
         "data": "willow-full-0.05 occupancy (tests/golden/willow_walls.npz) with the blur splat; "
                 "ray-cast scans at free poses",
         "config": {"workload": f"config4: willow 1565x1345 @5cm, {args.window_m} m / +-pi window "
-                               f"({na}x{ns}^2 candidates), all beams",
+                               f"({na}x{ns}^2 candidates), all beams", "search": args.search,
                    "mean_beams": beams / args.steps, "parallelism": f"replicas x{world_size}"},
-        "roofline": rl,
+        "roofline": rl, "search": search,
         "kernels": stats, "cpu_baseline": cpu,
     }
 
@@ -648,6 +698,10 @@ def main():
     ap.add_argument("--jobs", type=int, default=16, help="backend: ScanMatchInterface jobs per step")
     ap.add_argument("--window-m", type=float, default=20.0, help="willow: window edge (m)")
     ap.add_argument("--submaps", type=int, default=512, help="loop_closure: submaps in total")
+    ap.add_argument("--search", choices=["pyramid", "exhaustive"], default="pyramid",
+                    help="loop_closure / willow: the admissible multi-resolution search (csm_search_windows) "
+                         "or every candidate scored (csm_best_windows); both give the same answer")
+    ap.add_argument("--depth", type=int, default=-1, help="pyramid search: top level (-1: automatic)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true",

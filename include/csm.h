@@ -27,6 +27,10 @@
  *   csm_best_window           same scoring, reduced on device to (max score, lowest flat index)
  *                             (large windows / loop-closure shards; no reference counterpart,
  *                             SURVEY.md 8e)
+ *   csm_search_windows        the same argmax over many windows by an admissible
+ *                             multi-resolution branch and bound (max-pooled levels);
+ *                             the reference's FAST matcher is the non-admissible form
+ *                                                        correlate_scan_matcher.h:271-502
  *   csm_optimize_scan_match   BasedOptimizeScanMatch::ScanMatch (Gauss-Newton)
  *                                                        optimize_scan_matcher.h:68-221
  *   csm_scan_match with       BranchAndBoundCorrelateScanMatcher::ScanMatch (FAST type,
@@ -302,6 +306,49 @@ int csm_set_grid_stack(csm_ctx* ctx, const float* cells, int32_t n_grids,
 int csm_best_windows(csm_ctx* ctx, const double* points_xy, int32_t n_points,
                      const csm_param* param, int32_t n_windows, const int32_t* grid_index,
                      const double* centers_map, csm_best* best);
+
+/* --- admissible multi-resolution search (north_star: branch-and-bound
+ *     across resolution levels; SURVEY.md 8e, BASELINE configs 3 and 4) ---- */
+/* The best candidate of n_windows windows of one scan (window i on grid
+ * grid_index[i], centred at centers_map[3i..3i+2], as csm_best_windows):
+ * the maximum score, ties to the lowest (window, flat index) -- exactly what
+ * reducing csm_best_windows' per-window results gives, and what the
+ * reference's exhaustive MultiResolutionCorrelateScanMatcher::ScanMatch
+ * (correlate_scan_matcher.h:516-603) ranks first, minus its sort.
+ *
+ * Unlike the reference's FAST matcher (BranchAndBoundCorrelateScanMatcher,
+ * :271-502), whose lowest level reads the raw grid and so may prune the best
+ * candidate, every level d >= 1 here reads a max-pooled copy of the grid
+ * ((2^d + 1)^2 cells per anchor), so a node's score bounds every candidate
+ * below it and the answer equals the exhaustive one. The pooled levels are
+ * built once per resident grid (stack) and kept until it changes.
+ *
+ * Applies to windows with a step of exactly one map cell on a grid the exact
+ * fixed-point path accepts; any other window is searched exhaustively on the
+ * device (stats->exhaustive = 1), with the same result. */
+typedef struct csm_search_options {
+  int32_t max_depth;       /* top level: nodes of 2^max_depth x 2^max_depth candidates;
+                              < 0: automatic (the smallest with ceil(n_space / 2^d) <= 32) */
+  int32_t probe_min_nodes; /* below the top, a level of at least this many nodes first
+                              scores its best node's leaves exactly (0: 4096) */
+  int64_t node_capacity;   /* nodes per level list (0: 2^22); larger levels are split */
+} csm_search_options;
+
+typedef struct csm_search_stats {
+  int32_t depth;           /* top level used                                          */
+  int32_t exhaustive;      /* 1: the window did not qualify, searched exhaustively    */
+  int64_t candidates;      /* n_windows * n_angles * n_space^2                        */
+  int64_t nodes[11];       /* nodes scored at each level (nodes[0]: exact candidates)  */
+  int64_t probe_leaves;    /* candidates scored exactly by incumbent probes           */
+  int64_t beam_reads;      /* grid reads in all: (sum of nodes + probe_leaves) * B     */
+  double build_ms;         /* pooled levels built by this call (0: cached)            */
+  int64_t syncs;           /* node counts the host read back (level passes it waited on) */
+} csm_search_stats;
+
+int csm_search_windows(csm_ctx* ctx, const double* points_xy, int32_t n_points,
+                       const csm_param* param, int32_t n_windows, const int32_t* grid_index,
+                       const double* centers_map, const csm_search_options* options,
+                       csm_best* best, int32_t* best_window, csm_search_stats* stats);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,7 @@
 #include "csm_gridmap.h"
 #include "csm_gridmap_internal.hpp"
 #include "host_math.hpp"
+#include "csm_pyramid.hpp"
 
 #include <algorithm>
 #include <atomic>
@@ -552,6 +553,7 @@ struct csm_ctx {
     std::swap(outside_i, g.outside_i);
     std::swap(int_max_abs, g.int_max_abs);
     std::swap(cur_use, g.last_use);
+    grid_gen = ++gen_clock;
   }
   // The current grid is a host map's own copy (worth keeping when another
   // grid takes its place).
@@ -565,6 +567,11 @@ struct csm_ctx {
 
   // exact fixed-point copy of the grid (ensure_int_grid)
   DevBuf gridi, gstats;
+  // Changes whenever the current fixed-point grid may have (rebuilt, cells or
+  // rows refreshed, another grid swapped in): keys the pooled levels of the
+  // multi-resolution search.
+  uint64_t grid_gen = 0, gen_clock = 0;
+  csm::PyramidSearch pyramid;
   bool int_checked = false, int_ok = false;
   int int_exp = 0;
   int32_t pitch = 0;  // gridi row pitch (cells)
@@ -721,6 +728,7 @@ int ensure_int_grid(csm_ctx* c) {
   c->int_max_abs = vmax;
   c->outside_i = (int32_t)((double)c->outside * scale);
   c->int_ok = true;
+  c->grid_gen = ++c->gen_clock;
   return CSM_OK;
 }
 
@@ -1211,6 +1219,7 @@ bool plan_window_into(const csm_param& P, const Dims& D, const Geometry& G, int 
   const double ssize = P.search_space_size;
   W.x0 = center[0] - (ssize / G.mres) * 0.5;
   W.y0 = center[1] - (ssize / G.mres) * 0.5;
+  if (!out) return true;  // angle rows shared with an earlier window of the same centre angle
   const double offset = (P.search_angle_offset * 2) / 2;
   const double start = center[2] - offset;
   for (int a = 0; a < D.n_angles; ++a) {
@@ -1227,6 +1236,32 @@ bool plan_window(const csm_param& P, const Dims& D, const Geometry& G, int n_poi
   angles.resize(base + (size_t)D.n_angles);
   W.angle_off = (int64_t)base;
   return plan_window_into(P, D, G, n_points, center, angles.data() + base, W);
+}
+
+// Many windows of one scan (loop closure: one pose against many submaps share
+// the centre angle): windows with an equal centre angle share their angle
+// rows (the same host cos/sin, bit for bit), so the host computes and uploads
+// them once.
+bool plan_windows_shared(const csm_param& P, const Dims& D, const Geometry& G, int n_points, int n_windows,
+                         const double* centers, std::vector<AngleEntry>& angles, std::vector<WindowPlan>& plans) {
+  std::vector<std::pair<uint64_t, int64_t>> seen;
+  for (int i = 0; i < n_windows; ++i) {
+    const double* c = centers + 3 * i;
+    uint64_t key;
+    std::memcpy(&key, &c[2], sizeof(key));
+    WindowPlan& W = plans[(size_t)i];
+    int64_t off = -1;
+    for (const auto& kv : seen)
+      if (kv.first == key) off = kv.second;
+    if (off >= 0) {
+      W.angle_off = off;
+      if (!plan_window_into(P, D, G, n_points, c, nullptr, W)) return false;
+    } else {
+      if (!plan_window(P, D, G, n_points, c, angles, W)) return false;
+      if (seen.size() < 64) seen.push_back({key, W.angle_off});
+    }
+  }
+  return true;
 }
 
 int upload_points(csm_ctx* c, const double* pts, int64_t n_total) {
@@ -2220,6 +2255,7 @@ int csm_update_grid_rows(csm_ctx* c, const void* cells, int64_t stride, const cs
           hipSuccess)
     return c->hip_fail(e, "fixed_point_kernel(rows)");
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(rows)");
+  c->grid_gen = ++c->gen_clock;
   if (c->profiling) c->account("grid:rows", 0.f, (double)(n * sizeof(float)), 0.0);
   return CSM_OK;
 }
@@ -2283,6 +2319,7 @@ int csm_update_grid_cells(csm_ctx* c, const void* cells, int64_t stride, const c
                                     c->int_exp, c->stream)) != hipSuccess)
     return c->hip_fail(e, "update_cells_kernel");
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(cells)");
+  c->grid_gen = ++c->gen_clock;
   if (c->profiling) c->account("grid:cells", 0.f, (double)bytes, 0.0);
   return CSM_OK;
 }
@@ -2531,9 +2568,8 @@ int csm_best_windows(csm_ctx* c, const double* pts, int32_t n_points, const csm_
   const Geometry G(c->info);
   std::vector<WindowPlan> plans((size_t)n_windows);
   std::vector<AngleEntry> angles;
-  for (int i = 0; i < n_windows; ++i)
-    if (!plan_window(*param, D, G, n_points, centers_map + 3 * i, angles, plans[(size_t)i]))
-      return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+  if (!plan_windows_shared(*param, D, G, n_points, n_windows, centers_map, angles, plans))
+    return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
   if ((st = upload_points(c, pts, n_points)) != CSM_OK) return st;
   std::vector<BestPartial> bp((size_t)n_windows);
   std::vector<int64_t> pt_off((size_t)n_windows, 0);
@@ -2549,6 +2585,176 @@ int csm_best_windows(csm_ctx* c, const double* pts, int32_t n_points, const csm_
     best[i].y = W.y0 + (int)(bp[(size_t)i].flat % ns) * f;
     best[i].angle = angles[(size_t)(W.angle_off + bp[(size_t)i].flat / nss)].angle;
   }
+  return CSM_OK;
+}
+
+namespace {
+
+// csm_search_windows' fallback: the exhaustive per-window argmax, reduced to
+// the lowest (window, flat) among the best scores.
+int search_exhaustive(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
+                      const std::vector<WindowPlan>& plans, const std::vector<AngleEntry>& angles,
+                      const std::vector<int32_t>& gidx, BestPartial* out) {
+  std::vector<BestPartial> bp(plans.size());
+  std::vector<int64_t> pt_off(plans.size(), 0);
+  int st = run_windows(c, P, D, G, plans, pt_off, angles.data(), angles.size(), gidx, bp.data());
+  if (st != CSM_OK) return st;
+  BestPartial b{-DBL_MAX, INT64_MAX};
+  for (size_t i = 0; i < bp.size(); ++i) {
+    const int64_t gf = (int64_t)i * D.n_cand + bp[i].flat;
+    if (bp[i].score > b.score || (bp[i].score == b.score && gf < b.flat)) b = BestPartial{bp[i].score, gf};
+  }
+  *out = b;
+  return CSM_OK;
+}
+
+}  // namespace
+
+int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const csm_param* param, int32_t n_windows,
+                       const int32_t* grid_index, const double* centers_map, const csm_search_options* options,
+                       csm_best* best, int32_t* best_window, csm_search_stats* stats) {
+  if (!c || !param || !centers_map || !best || !best_window || n_windows <= 0) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  Dims D;
+  int st = window_dims(*param, D);
+  if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
+  if (n_points <= 0) return c->fail(CSM_ERR_INVALID_ARG, "no points");
+  if ((st = check_points(c, pts, n_points)) != CSM_OK) return st;
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  std::vector<int32_t> gidx((size_t)n_windows, 0);
+  for (int i = 0; i < n_windows; ++i) {
+    gidx[(size_t)i] = grid_index ? grid_index[i] : 0;
+    if (gidx[(size_t)i] < 0 || gidx[(size_t)i] >= c->n_grids)
+      return c->fail(CSM_ERR_INVALID_ARG, "grid_index outside the resident grid stack");
+  }
+  const Geometry G(c->info);
+  std::vector<WindowPlan> plans((size_t)n_windows);
+  std::vector<AngleEntry> angles;
+  if (!plan_windows_shared(*param, D, G, n_points, n_windows, centers_map, angles, plans))
+    return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+  if ((st = upload_points(c, pts, n_points)) != CSM_OK) return st;
+  if ((st = ensure_int_grid(c)) != CSM_OK) return st;
+  csm_search_stats S{};
+  S.candidates = (int64_t)n_windows * D.n_cand;
+  const double f = param->search_space_resolution / G.mres;
+  const WindowPlan& W0 = plans[0];
+  // the pooled search: one-cell steps, the exact fixed-point grid, the beams
+  // staged in LDS (64 KB), every index int-castable, node fields in range
+  bool ok = f == 1.0 && c->int_ok && W0.n_used <= 4096 && n_windows < (1 << 20) && D.n_angles < 4096 &&
+            D.n_space < 65536 &&
+            (double)W0.n_used * c->int_max_abs * std::ldexp(1.0, c->int_exp) <= std::ldexp(1.0, 53);
+  int depth = options ? options->max_depth : -1;
+  if (depth < 0) {  // the shallowest top level with at most 32 x 32 nodes per angle (measured
+                    // best on configs 3 and 4: profiles/r02/search_depth_sweep.txt)
+    depth = 0;
+    while (((D.n_space + (1 << depth) - 1) >> depth) > 32 && depth < csm::kPyrMaxDepth) ++depth;
+  }
+  depth = std::min(depth, csm::kPyrMaxDepth);
+  for (const WindowPlan& W : plans) {
+    if (!ok) break;
+    const double far = (double)(D.n_space - 1) * f;
+    const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
+                                 std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
+    const double R = c->pts_maxabs * (1.0 + 1e-9) + span + 2.0 + (double)(1 << depth);
+    if (!(R < std::ldexp(1.0, 29))) ok = false;
+  }
+  BestPartial b{};
+  if (!ok) {
+    S.exhaustive = 1;
+    if ((st = search_exhaustive(c, *param, D, G, plans, angles, gidx, &b)) != CSM_OK) return st;
+    S.nodes[0] = S.candidates;
+    S.beam_reads = S.candidates * W0.n_used;
+  } else {
+    hipError_t e;
+    const int nw = n_windows;
+    if ((e = c->h_sw.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scans)");
+    ScanWork* sw = (ScanWork*)c->h_sw.p;
+    for (int i = 0; i < nw; ++i) {
+      const WindowPlan& W = plans[(size_t)i];
+      ScanWork& s = sw[i];
+      s = ScanWork{};
+      s.angle_off = W.angle_off;
+      s.out_off = (int64_t)i * D.n_cand;
+      s.n_used = W.n_used;
+      s.step = W.step;
+      s.divisor = (double)W.use;
+      s.x0 = W.x0;
+      s.y0 = W.y0;
+      s.cx = W.center[0];
+      s.cy = W.center[1];
+      s.ct = W.center[2];
+      s.grid_index = gidx[(size_t)i];
+    }
+    if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
+    if ((e = c->angles.ensure(angles.size() * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
+    if ((e = hipMemcpyAsync(c->scans.p, sw, (size_t)nw * sizeof(ScanWork), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(scans)");
+    if ((e = hipMemcpyAsync(c->angles.p, angles.data(), angles.size() * sizeof(AngleEntry), hipMemcpyHostToDevice,
+                            c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(angles)");
+    csm::PyrInputs in{};
+    in.stream = c->stream;
+    LevelWork& L = in.L;
+    L.n_angles = D.n_angles;
+    L.n_space = D.n_space;
+    L.n_cand = D.n_cand;
+    L.n_scans = nw;
+    L.step_cells = f;
+    L.use_penalty = param->use_center_penalty ? 1 : 0;
+    L.dist_gain = (param->type == CSM_COARSE) ? 0.4 : 0.2;  // :759-761
+    L.size = param->search_space_size;
+    L.mres = G.mres;
+    L.outside_i = c->outside_i;
+    L.int_mode = 1;
+    L.int_scale = std::ldexp(1.0, -c->int_exp);
+    in.level0 = csm::PyrGrid{(const int32_t*)c->gridi.p,
+                             (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows), c->pitch, 0,
+                             c->info.size_x, c->info.size_y, 0, c->info.size_x};
+    in.n_grids = c->n_grids;
+    in.grid_gen = c->grid_gen;
+    in.scans = (const ScanWork*)c->scans.p;
+    in.angles = (const AngleEntry*)c->angles.p;
+    in.pts = (const double*)c->pts.p;
+    in.n_used = W0.n_used;
+    in.step = W0.step;
+    in.depth = depth;
+    c->pyramid.configure(options ? options->node_capacity : 0, options ? options->probe_min_nodes : 0);
+    csm::PyrStats ps;
+    std::string what;
+    float ms = 0.f;
+    if (c->profiling && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+    if ((e = c->pyramid.run(in, &b, &ps, &what)) != hipSuccess) return c->hip_fail(e, what.c_str());
+    if (c->profiling) {
+      if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess || (e = hipEventSynchronize(c->ev1)) != hipSuccess ||
+          (e = hipEventElapsedTime(&ms, c->ev0, c->ev1)) != hipSuccess)
+        return c->hip_fail(e, "pyramid timing");
+    }
+    S.depth = ps.depth;
+    int64_t scored = ps.probe_leaves;
+    for (int d = 0; d <= csm::kPyrMaxDepth; ++d) {
+      S.nodes[d] = ps.nodes[d];
+      scored += ps.nodes[d];
+    }
+    S.probe_leaves = ps.probe_leaves;
+    S.beam_reads = scored * W0.n_used;
+    S.build_ms = ps.build_ms;
+    S.syncs = ps.syncs;
+    // one grid read per beam per scored node (the pooled levels included)
+    if (c->profiling) c->account("pyramid_search", ms, (double)S.beam_reads * 4.0, (double)S.candidates);
+  }
+  if (b.flat == INT64_MAX) return c->fail(CSM_ERR_HIP, "search found no candidate");
+  const int32_t w = (int32_t)(b.flat / D.n_cand);
+  const int64_t flat = b.flat - (int64_t)w * D.n_cand;
+  const int64_t ns = D.n_space, nss = ns * ns;
+  const WindowPlan& W = plans[(size_t)w];
+  best->score = b.score;
+  best->flat_index = flat;
+  best->x = W.x0 + (int)((flat / ns) % ns) * f;
+  best->y = W.y0 + (int)(flat % ns) * f;
+  best->angle = angles[(size_t)(W.angle_off + flat / nss)].angle;
+  *best_window = w;
+  if (stats) *stats = S;
   return CSM_OK;
 }
 

@@ -1,0 +1,478 @@
+// csm_pyramid.hip — kernels of the admissible multi-resolution search
+// (csm_pyramid.hpp): max-pooled grid levels, node bounds, pruning/expansion.
+//
+// Exactness of the bound. A node at depth d covers candidates j in
+// [j0, j0 + 2^d) (j0 = J 2^d), k likewise, at one angle. For a beam, the
+// column a candidate reads is trunc(fl(fl(lx + x_j) + 0.5)) with
+// x_j = fl(x0 + j) (correlate_scan_matcher.h:569,647; step exactly one cell).
+// fp addition and trunc are monotone, so the columns of the node's
+// candidates lie in [g0, trunc(t_j1)], g0 the anchor candidate's own column;
+// t_j1 - t_j0 <= 2^d - 1 + (rounding < 2^-20), so trunc(t_j1) <= g0 + 2^d
+// (for t < 0, trunc = ceil, and ceil(a + b) <= ceil(a) + ceil(b) gives the
+// same bound). Level d stores at anchor g0 the maximum over [g0, g0 + 2^d],
+// off-grid cells counting as the outside value (0 in the fixed-point copy),
+// hence sum_beams level_d[anchor] >= the integer sum of every candidate of
+// the node. The score is monotone in that sum ((double)(S + n outside_i) *
+// 2^-E / divisor: exact scaling, monotone rounding), and the centre penalty
+// (:718-745) multiplies by a factor in [0.45, 1] (0.45 = 0.5 * 0.9, its
+// floors), so the bound is the raw score if >= 0 and 0.45 times it if < 0.
+#include <hip/hip_runtime.h>
+
+#include "csm_device.hpp"
+#include "csm_pyramid.hpp"
+
+#pragma clang fp contract(off)
+
+namespace csm {
+namespace {
+
+using dev::better;
+using dev::penalized;
+
+constexpr int kPB = 256;  // threads per block (4 waves)
+
+__device__ __forceinline__ void node_decode(uint64_t nd, int& w, int& a, int& J, int& K) {
+  w = (int)(nd >> 44);
+  a = (int)((nd >> 32) & 0xFFF);
+  J = (int)((nd >> 16) & 0xFFFF);
+  K = (int)(nd & 0xFFFF);
+}
+
+__device__ __forceinline__ int64_t pyr_col(const PyrGrid& L, int xs) {
+  return (int64_t)(xs & ((1 << L.lg) - 1)) * L.q + (xs >> L.lg);
+}
+
+// Level d (>= 1): anchor (x, y) = (xs - 2^d, ys - 2^d) holds the maximum of
+// the source over anchors x + t, t in taps (d = 1: the grid at 0, 1, 2;
+// d >= 2: level d - 1 at 0 and 2^(d-1)), rows likewise. Every stored cell of
+// the buffer is written (pad columns zero).
+__global__ __launch_bounds__(256) void pyr_pool_kernel(PyrGrid src, PyrGrid dst, int t1, int t2, int ntaps,
+                                                       int64_t total) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t gidx = i / dst.stride;
+    const int64_t r = i - gidx * dst.stride;
+    const int ys = (int)(r / dst.pitch), c = (int)(r - (int64_t)ys * dst.pitch);
+    const int ph = c / dst.q, qx = c - ph * dst.q;
+    const int xs = (qx << dst.lg) + ph;  // logical column of storage column c
+    int32_t m = 0;
+    if (ph < (1 << dst.lg) && xs < dst.width && ys < dst.height) {
+      const int ax = xs - dst.shift + src.shift, ay = ys - dst.shift + src.shift;
+      const int32_t* g = src.g + gidx * src.stride;
+      const int tap[3] = {0, t1, t2};
+      bool any = false;
+      for (int ty = 0; ty < ntaps; ++ty) {
+        const int yy = ay + tap[ty];
+        for (int tx = 0; tx < ntaps; ++tx) {
+          const int xx = ax + tap[tx];
+          const bool in = (unsigned)xx < (unsigned)src.width && (unsigned)yy < (unsigned)src.height;
+          const int32_t v = in ? g[(int64_t)yy * src.pitch + pyr_col(src, xx)] : 0;  // off-grid: outside
+          m = any ? max(m, v) : v;
+          any = true;
+        }
+      }
+    }
+    const_cast<int32_t*>(dst.g)[i] = m;
+  }
+}
+
+__global__ __launch_bounds__(256) void pyr_top_kernel(LevelWork L, int32_t nj, int64_t first, int64_t n,
+                                                      uint64_t* __restrict__ out) {
+  const int64_t per_angle = (int64_t)nj * nj;
+  const int64_t per_window = per_angle * L.n_angles;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = first + i;
+    const int64_t w = q / per_window;
+    const int64_t rw = q - w * per_window;
+    const int64_t a = rw / per_angle;
+    const int64_t ra = rw - a * per_angle;
+    const int64_t K = ra / nj, J = ra - K * nj;  // J fastest
+    out[i] = pyr_node((uint32_t)w, (uint32_t)a, (uint32_t)J, (uint32_t)K);
+  }
+}
+
+__device__ __forceinline__ void block_best(double v, int64_t f, uint64_t nd, PyrPartial* __restrict__ out) {
+  __shared__ double rs[kPB / 64];
+  __shared__ int64_t rf[kPB / 64];
+  __shared__ uint64_t rn[kPB / 64];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ov = __shfl_down(v, off, 64);
+    const int64_t of = __shfl_down(f, off, 64);
+    const uint64_t on = __shfl_down(nd, off, 64);
+    if (better(ov, of, v, f)) {
+      v = ov;
+      f = of;
+      nd = on;
+    }
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    rs[wave] = v;
+    rf[wave] = f;
+    rn[wave] = nd;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kPB / 64; ++k)
+      if (better(rs[k], rf[k], v, f)) {
+        v = rs[k];
+        f = rf[k];
+        nd = rn[k];
+      }
+    *out = PyrPartial{v, f, nd};
+  }
+}
+
+// One lane per node (blocks stride over the list): the sum over the scan's
+// beams of the level-d value at the anchor candidate's cell (GetResponse
+// :645-654 with the pooled level in place of the grid); d = 0 is the
+// candidate's exact, penalised score.
+__global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev, int d,
+                                                        const ScanWork* __restrict__ scans,
+                                                        const AngleEntry* __restrict__ angles,
+                                                        const double2* __restrict__ pts, int32_t n_used,
+                                                        int32_t step, const uint64_t* __restrict__ nodes,
+                                                        int64_t n_host, const unsigned long long* __restrict__ n_dev,
+                                                        double* __restrict__ vals,
+                                                        PyrPartial* __restrict__ partials,
+                                                        unsigned long long* __restrict__ scored) {
+  extern __shared__ double2 beams[];
+  for (int b = threadIdx.x; b < n_used; b += kPB) beams[b] = pts[(int64_t)b * step];
+  __syncthreads();
+  const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
+  if (scored && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(scored, (unsigned long long)n);
+  double bv = -1.0e300;
+  int64_t bf = INT64_MAX;
+  uint64_t bn = kPyrNoNode;
+  const int sh = lev.shift, W = lev.width, H = lev.height, pitch = lev.pitch, lg = lev.lg, qc = lev.q;
+  const int pm = (1 << lg) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kPB) {
+    const uint64_t nd = nodes[i];
+    int w, a, J, K;
+    node_decode(nd, w, a, J, K);
+    const int j0 = J << d, k0 = K << d;
+    const bool valid = nd != kPyrNoNode && w < L.n_scans && a < L.n_angles && j0 < L.n_space && k0 < L.n_space;
+    double v = -1.0e300;
+    int64_t gflat = INT64_MAX;
+    if (valid) {
+      const ScanWork S = scans[w];
+      const AngleEntry ae = angles[S.angle_off + a];
+      const double x = S.x0 + j0 * L.step_cells;  // :569
+      const double y = S.y0 + k0 * L.step_cells;  // :572
+      const int32_t* __restrict__ g = lev.g + (int64_t)S.grid_index * lev.stride;
+      int64_t sum = 0;
+      auto cell = [&](int b) -> int32_t {
+        const double2 p = beams[b];
+        const double lx = ae.cosine * p.x - ae.sine * p.y;
+        const double ly = ae.sine * p.x + ae.cosine * p.y;
+        const int gx = (int)((lx + x) + 0.5) + sh;
+        const int gy = (int)((ly + y) + 0.5) + sh;
+        const bool in = (unsigned)gx < (unsigned)W && (unsigned)gy < (unsigned)H;
+        const int64_t idx = (int64_t)gy * pitch + (int64_t)(gx & pm) * qc + (gx >> lg);
+        const int32_t c = g[in ? idx : 0];
+        return in ? c : 0;
+      };
+      int b = 0;
+      for (; b + 8 <= n_used; b += 8) {  // 8 gathers in flight per lane
+        int32_t c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = cell(b + u);
+        // |c| < 2^26: eight fit an int32
+        sum += (int64_t)(((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7])));
+      }
+      for (; b < n_used; ++b) sum += cell(b);
+      const double acc = (double)(sum + (int64_t)n_used * L.outside_i) * L.int_scale;
+      if (d == 0) {
+        v = penalized(L, S, acc, x, y, ae.angle);
+      } else {
+        const double raw = acc / S.divisor;
+        v = (L.use_penalty && raw < 0.0) ? raw * 0.45 : raw;
+      }
+      gflat = (int64_t)w * L.n_cand + ((int64_t)a * L.n_space + j0) * L.n_space + k0;
+    }
+    vals[i] = v;
+    if (better(v, gflat, bv, bf)) {
+      bv = v;
+      bf = gflat;
+      bn = nd;
+    }
+  }
+  block_best(bv, bf, bn, partials + blockIdx.x);
+}
+
+// The whole top level at once, laid out as the exhaustive column kernel
+// (csm_kernels.hip score_cols_kernel): lane = one (angle, J) column of a
+// window, kt rows K per lane, so a beam's rotation and column are computed
+// once per lane and shared by its rows, and adjacent J lanes gather adjacent
+// phase-split cells. Writes every top node and its bound in list order
+// ((window, angle, K, J), J fastest) and one best per block.
+constexpr int kTopKT = 16;
+__global__ __launch_bounds__(kPB) void pyr_top_bound_kernel(LevelWork L, PyrGrid lev, int d, int32_t nj,
+                                                            int32_t ktiles, int32_t kt, int32_t col_blocks,
+                                                            const ScanWork* __restrict__ scans,
+                                                            const AngleEntry* __restrict__ angles,
+                                                            const double2* __restrict__ pts, int32_t n_used,
+                                                            int32_t step, uint64_t* __restrict__ nodes,
+                                                            double* __restrict__ vals,
+                                                            PyrPartial* __restrict__ partials) {
+  extern __shared__ double2 beams[];
+  for (int b = threadIdx.x; b < n_used; b += kPB) beams[b] = pts[(int64_t)b * step];
+  __syncthreads();
+  const int per_window = col_blocks * ktiles;
+  const int w = blockIdx.x / per_window;
+  const int r = blockIdx.x - w * per_window;
+  const int cb = r / ktiles, ktile = r - cb * ktiles;
+  const int col = cb * kPB + threadIdx.x;
+  const bool valid = col < L.n_angles * nj;
+  const int a = valid ? col / nj : 0;
+  const int J = valid ? col - a * nj : 0;
+  const int K0 = ktile * kt;
+  const int krem = min(kt, nj - K0);
+  const ScanWork S = scans[w];
+  const AngleEntry ae = angles[S.angle_off + a];
+  const double x = S.x0 + (J << d) * L.step_cells;  // :569
+  double y[kTopKT];
+#pragma unroll
+  for (int kk = 0; kk < kTopKT; ++kk) y[kk] = S.y0 + ((K0 + kk) << d) * L.step_cells;  // :572
+  const int32_t* __restrict__ g = lev.g + (int64_t)S.grid_index * lev.stride;
+  const int sh = lev.shift, W = lev.width, H = lev.height, pitch = lev.pitch, lg = lev.lg, qc = lev.q;
+  const int pm = (1 << lg) - 1;
+  int64_t sum[kTopKT];
+#pragma unroll
+  for (int kk = 0; kk < kTopKT; ++kk) sum[kk] = 0;
+  for (int b = 0; b < n_used; ++b) {
+    const double2 p = beams[b];
+    const double lx = ae.cosine * p.x - ae.sine * p.y;
+    const double ly = ae.sine * p.x + ae.cosine * p.y;
+    const int gx = (int)((lx + x) + 0.5) + sh;
+    const bool inx = (unsigned)gx < (unsigned)W;
+    const int64_t cx = (int64_t)(gx & pm) * qc + (gx >> lg);
+    int32_t c[kTopKT];
+#pragma unroll
+    for (int kk = 0; kk < kTopKT; ++kk) {
+      const int gy = (int)((ly + y[kk]) + 0.5) + sh;
+      const bool in = inx && (unsigned)gy < (unsigned)H && kk < krem;
+      const int32_t v = g[in ? (int64_t)gy * pitch + cx : 0];
+      c[kk] = in ? v : 0;
+    }
+#pragma unroll
+    for (int kk = 0; kk < kTopKT; ++kk) sum[kk] += c[kk];
+  }
+  double bv = -1.0e300;
+  int64_t bf = INT64_MAX;
+  uint64_t bn = kPyrNoNode;
+  const int64_t wbase = ((int64_t)w * L.n_angles + a) * nj;
+#pragma unroll
+  for (int kk = 0; kk < kTopKT; ++kk) {
+    if (valid && kk < krem) {
+      const int K = K0 + kk;
+      const double acc = (double)(sum[kk] + (int64_t)n_used * L.outside_i) * L.int_scale;
+      const double raw = acc / S.divisor;
+      const double v = (L.use_penalty && raw < 0.0) ? raw * 0.45 : raw;
+      const int64_t idx = (wbase + K) * nj + J;
+      const uint64_t nd = pyr_node((uint32_t)w, (uint32_t)a, (uint32_t)J, (uint32_t)K);
+      nodes[idx] = nd;
+      vals[idx] = v;
+      const int64_t gflat = (int64_t)w * L.n_cand + ((int64_t)a * L.n_space + (J << d)) * L.n_space + (K << d);
+      if (better(v, gflat, bv, bf)) {
+        bv = v;
+        bf = gflat;
+        bn = nd;
+      }
+    }
+  }
+  block_best(bv, bf, bn, partials + blockIdx.x);
+}
+
+// merge (one block): fold the best partial into the incumbent. Otherwise
+// block i picks the best of the i-th of gridDim.x equal segments of the
+// partials (different windows / angle ranges: diverse probe roots) when it
+// beats the incumbent (kPyrNoNode otherwise).
+__global__ __launch_bounds__(kPB) void pyr_final_kernel(const PyrPartial* __restrict__ in, int64_t n, int merge,
+                                                        BestPartial* __restrict__ inc,
+                                                        uint64_t* __restrict__ probe) {
+  const BestPartial cur = *inc;
+  const int64_t lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
+  double v = -1.0e300;
+  int64_t f = INT64_MAX;
+  uint64_t nd = kPyrNoNode;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kPB) {
+    const PyrPartial p = in[i];
+    if (better(p.v, p.gflat, v, f)) {
+      v = p.v;
+      f = p.gflat;
+      nd = p.node;
+    }
+  }
+  __shared__ PyrPartial out;
+  block_best(v, f, nd, &out);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const bool win = out.gflat != INT64_MAX && better(out.v, out.gflat, cur.score, cur.flat);
+    if (merge) {
+      if (win) *inc = BestPartial{out.v, out.gflat};
+    } else {
+      probe[blockIdx.x] = win ? out.node : kPyrNoNode;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void pyr_probe_kernel(int d, int n_probe, const uint64_t* __restrict__ probe,
+                                                        uint64_t* __restrict__ out) {
+  const int64_t per = (int64_t)1 << (2 * d);
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < per * n_probe;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t % per;
+    const uint64_t nd = probe[t / per];
+    int w, a, J, K;
+    node_decode(nd, w, a, J, K);
+    if (nd == kPyrNoNode) {
+      out[t] = kPyrNoNode;
+      continue;
+    }
+    const uint32_t dk = (uint32_t)(i >> d), dj = (uint32_t)(i & ((1 << d) - 1));  // J fastest
+    const uint32_t j = ((uint32_t)J << d) + dj, k = ((uint32_t)K << d) + dk;
+    out[t] = (j < 0x10000u && k < 0x10000u) ? pyr_node((uint32_t)w, (uint32_t)a, j, k) : kPyrNoNode;
+  }
+}
+
+// Children in the order (2J, 2K), (2J+1, 2K), (2J, 2K+1), (2J+1, 2K+1): J
+// pairs adjacent, as the next level's gathers want them.
+__global__ __launch_bounds__(256) void pyr_expand_kernel(LevelWork L, int d, const uint64_t* __restrict__ nodes,
+                                                         const double* __restrict__ bounds, int64_t n_host,
+                                                         const unsigned long long* __restrict__ n_dev,
+                                                         const BestPartial* __restrict__ inc,
+                                                         uint64_t* __restrict__ out,
+                                                         unsigned long long* __restrict__ count, int64_t cap) {
+  const BestPartial cur = *inc;
+  const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
+  const int lane = threadIdx.x & 63;
+  const int h = d - 1;
+  // whole waves step together (the append below is wave-wide)
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = i0 + threadIdx.x;
+    int w = 0, a = 0, J = 0, K = 0;
+    uint32_t mask = 0;  // children kept: bit (2 dk + dj)
+    if (i < n) {
+      const uint64_t nd = nodes[i];
+      node_decode(nd, w, a, J, K);
+      const double b = bounds[i];
+      const int64_t lowest = (int64_t)w * L.n_cand + ((int64_t)a * L.n_space + (J << d)) * L.n_space + (K << d);
+      if (nd != kPyrNoNode && better(b, lowest, cur.score, cur.flat)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cj = 2 * J + (q & 1), ck = 2 * K + (q >> 1);
+          if ((cj << h) < L.n_space && (ck << h) < L.n_space) mask |= 1u << q;
+        }
+      }
+    }
+    // wave-aggregated append: one atomic per wave
+    const int cnt = __builtin_popcount(mask);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    const int total = __shfl(incl, 63, 64);
+    unsigned long long base = 0;
+    if (lane == 63 && total > 0) base = atomicAdd(count, (unsigned long long)total);
+    base = __shfl(base, 63, 64);
+    int64_t o = (int64_t)base + (incl - cnt);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (mask & (1u << q)) {
+        if (o < cap)
+          out[o] = pyr_node((uint32_t)w, (uint32_t)a, (uint32_t)(2 * J + (q & 1)), (uint32_t)(2 * K + (q >> 1)));
+        ++o;
+      }
+    }
+  }
+}
+
+int blocks_for(int64_t n, int per) {
+  int64_t b = (n + per - 1) / per;
+  if (b > 65536) b = 65536;
+  return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+hipError_t launch_pyr_pool(const PyrGrid& src, const PyrGrid& dst, int d, int32_t n_grids, hipStream_t stream) {
+  const int64_t total = dst.stride * n_grids;
+  const int t1 = d == 1 ? 1 : (1 << (d - 1));
+  const int t2 = d == 1 ? 2 : 0;
+  const int ntaps = d == 1 ? 3 : 2;
+  hipLaunchKernelGGL(pyr_pool_kernel, dim3(blocks_for(total, 256)), dim3(256), 0, stream, src, dst, t1, t2, ntaps,
+                     total);
+  return hipGetLastError();
+}
+
+hipError_t launch_pyr_top(const LevelWork& L, int32_t nj, int64_t first, int64_t n, uint64_t* out,
+                          hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pyr_top_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, stream, L, nj, first, n, out);
+  return hipGetLastError();
+}
+
+int pyr_blocks(int64_t upper) {
+  int64_t b = (upper + kPB - 1) / kPB;
+  if (b > 4096) b = 4096;  // 16 waves per CU; blocks stride over longer lists
+  return (int)(b < 1 ? 1 : b);
+}
+
+hipError_t launch_pyr_bound(const LevelWork& L, const PyrGrid& lev, int d, const ScanWork* scans,
+                            const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
+                            const uint64_t* nodes, int64_t n, const unsigned long long* n_dev, int64_t upper,
+                            double* vals, PyrPartial* partials, unsigned long long* scored, hipStream_t stream) {
+  if (upper <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pyr_bound_kernel, dim3(pyr_blocks(upper)), dim3(kPB), (size_t)n_used * sizeof(double2), stream,
+                     L, lev, d, scans, angles, reinterpret_cast<const double2*>(pts), n_used, step, nodes, n, n_dev,
+                     vals, partials, scored);
+  return hipGetLastError();
+}
+
+hipError_t launch_pyr_final(const PyrPartial* partials, int64_t n, bool merge, int n_probe, BestPartial* inc,
+                            uint64_t* probe, hipStream_t stream) {
+  hipLaunchKernelGGL(pyr_final_kernel, dim3(merge ? 1 : n_probe), dim3(kPB), 0, stream, partials, n, merge ? 1 : 0,
+                     inc, probe);
+  return hipGetLastError();
+}
+
+int pyr_top_blocks(const LevelWork& L, int32_t nj, int32_t* ktiles, int32_t* kt, int32_t* col_blocks) {
+  *ktiles = (nj + kTopKT - 1) / kTopKT;
+  *kt = (nj + *ktiles - 1) / *ktiles;
+  *col_blocks = (int32_t)(((int64_t)L.n_angles * nj + kPB - 1) / kPB);
+  const int64_t b = (int64_t)L.n_scans * *col_blocks * *ktiles;
+  return b > INT32_MAX ? -1 : (int)b;
+}
+
+hipError_t launch_pyr_top_bound(const LevelWork& L, const PyrGrid& lev, int d, int32_t nj, const ScanWork* scans,
+                                const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
+                                uint64_t* nodes, double* vals, PyrPartial* partials, hipStream_t stream) {
+  int32_t ktiles, kt, col_blocks;
+  const int blocks = pyr_top_blocks(L, nj, &ktiles, &kt, &col_blocks);
+  if (blocks <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pyr_top_bound_kernel, dim3(blocks), dim3(kPB), (size_t)n_used * sizeof(double2), stream, L, lev,
+                     d, nj, ktiles, kt, col_blocks, scans, angles, reinterpret_cast<const double2*>(pts), n_used,
+                     step, nodes, vals, partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_pyr_probe(int d, int n_probe, const uint64_t* probe, uint64_t* out, hipStream_t stream) {
+  const int64_t n = ((int64_t)1 << (2 * d)) * n_probe;
+  hipLaunchKernelGGL(pyr_probe_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, stream, d, n_probe, probe, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pyr_expand(const LevelWork& L, int d, const uint64_t* nodes, const double* bounds, int64_t n,
+                             const unsigned long long* n_dev, int64_t upper, const BestPartial* inc, uint64_t* out,
+                             unsigned long long* count, int64_t cap, hipStream_t stream) {
+  if (upper <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pyr_expand_kernel, dim3(pyr_blocks(upper)), dim3(256), 0, stream, L, d, nodes, bounds, n, n_dev,
+                     inc, out, count, cap);
+  return hipGetLastError();
+}
+
+}  // namespace csm

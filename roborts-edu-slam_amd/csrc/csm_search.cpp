@@ -1,0 +1,296 @@
+// csm_search.cpp — host driver of the admissible multi-resolution search
+// (csm_pyramid.hpp). The host walks the resolution levels; the device bounds
+// every node of a level in one launch and compacts the survivors' children.
+//
+//   top depth D: every (window, angle, J, K) node, bounded on level D
+//   probe: the best node's 4^d leaves are scored exactly, raising the
+//          incumbent before the level is pruned (the first probe at the top
+//          usually finds the answer; later ones tighten it)
+//   expand: children of the nodes whose bound is not below the incumbent
+//   depth 0: exact candidate scores, folded into the incumbent
+//
+// A level's child list is bounded by the node capacity: a parent list larger
+// than capacity / 4 is expanded in slices, each descended before the next
+// (depth-first over slices, level-synchronous inside one), so memory stays
+// fixed whatever the pruning rate.
+#include "csm_pyramid.hpp"
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <climits>
+#include <vector>
+
+namespace csm {
+
+namespace {
+
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  ~Buf() { release(); }
+};
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct PyramidSearch::Impl {
+  // pooled levels 1..kPyrMaxDepth of the current fixed-point grid
+  Buf level[kPyrMaxDepth + 1];
+  PyrGrid lev[kPyrMaxDepth + 1]{};
+  const int32_t* key_g = nullptr;
+  uint64_t key_gen = 0;
+  int32_t key_sx = -1, key_sy = -1, key_grids = -1, built = 0;
+  // per-depth node lists, their values and counts (counts[d]: nodes[d]'s
+  // length as the expand that filled it left it)
+  Buf nodes[kPyrMaxDepth + 1], vals[kPyrMaxDepth + 1];
+  Buf partials, inc, probe_slot, probe_nodes, probe_vals, counts, scored;
+  unsigned long long* h_counts = nullptr;  // pinned: counts read back, then scored
+  int64_t cap = (int64_t)1 << 24;
+  int probe_min = 4096;
+  static constexpr int kRoots = 8;  // probe roots per probe (best partials of distinct blocks)
+  PyrInputs in{};
+  PyrStats* st = nullptr;
+
+  ~Impl() {
+    if (h_counts) (void)hipHostFree(h_counts);
+  }
+
+  hipError_t build(const PyrInputs& x) {
+    const int32_t sx = x.level0.width, sy = x.level0.height;
+    if (key_g != x.level0.g || key_gen != x.grid_gen || key_sx != sx || key_sy != sy || key_grids != x.n_grids) {
+      built = 0;
+      key_g = x.level0.g;
+      key_gen = x.grid_gen;
+      key_sx = sx;
+      key_sy = sy;
+      key_grids = x.n_grids;
+    }
+    lev[0] = x.level0;
+    if (built >= x.depth) return hipSuccess;
+    const double t0 = now_ms();
+    hipError_t e;
+    for (int d = built + 1; d <= x.depth; ++d) {
+      PyrGrid& L = lev[d];
+      L.shift = 1 << d;
+      L.width = sx + L.shift;
+      L.height = sy + L.shift;
+      L.lg = d;
+      L.q = (L.width + L.shift - 1) >> d;
+      L.pitch = ((L.q << d) + 3) & ~3;
+      L.stride = (int64_t)L.pitch * L.height;
+      if ((e = level[d].ensure((size_t)L.stride * (size_t)x.n_grids * sizeof(int32_t))) != hipSuccess) return e;
+      L.g = (const int32_t*)level[d].p;
+      if ((e = launch_pyr_pool(lev[d - 1], L, d, x.n_grids, x.stream)) != hipSuccess) return e;
+    }
+    if ((e = hipStreamSynchronize(x.stream)) != hipSuccess) return e;
+    built = x.depth;
+    if (st) st->build_ms = now_ms() - t0;
+    return hipSuccess;
+  }
+
+  hipError_t ensure_lists(int D) {
+    hipError_t e;
+    for (int d = 0; d <= D; ++d) {
+      if ((e = nodes[d].ensure((size_t)cap * sizeof(uint64_t))) != hipSuccess) return e;
+      if ((e = vals[d].ensure((size_t)cap * sizeof(double))) != hipSuccess) return e;
+    }
+    const int64_t np = ((int64_t)1 << (2 * D)) * kRoots;
+    if ((e = partials.ensure((size_t)pyr_blocks(INT64_MAX / 2) * sizeof(PyrPartial))) != hipSuccess) return e;
+    if ((e = inc.ensure(sizeof(BestPartial))) != hipSuccess) return e;
+    if ((e = probe_slot.ensure(kRoots * sizeof(uint64_t))) != hipSuccess) return e;
+    if ((e = probe_nodes.ensure((size_t)np * sizeof(uint64_t))) != hipSuccess) return e;
+    if ((e = probe_vals.ensure((size_t)np * sizeof(double))) != hipSuccess) return e;
+    if ((e = counts.ensure((kPyrMaxDepth + 1) * sizeof(unsigned long long))) != hipSuccess) return e;
+    if ((e = scored.ensure((kPyrMaxDepth + 1) * sizeof(unsigned long long))) != hipSuccess) return e;
+    if (!h_counts && (e = hipHostMalloc((void**)&h_counts, 2 * (kPyrMaxDepth + 1) * sizeof(unsigned long long),
+                                        hipHostMallocDefault)) != hipSuccess)
+      return e;
+    return hipSuccess;
+  }
+
+  unsigned long long* count_dev(int d) { return (unsigned long long*)counts.p + d; }
+
+  // nodes (n on the host, or *n_dev), at most `upper` of them
+  hipError_t bound(int d, const uint64_t* list, double* out, int64_t n, const unsigned long long* n_dev,
+                   int64_t upper) {
+    return launch_pyr_bound(in.L, lev[d], d, in.scans, in.angles, in.pts, in.n_used, in.step, list, n, n_dev, upper,
+                            out, (PyrPartial*)partials.p, (unsigned long long*)scored.p + d, in.stream);
+  }
+
+  // Score the leaves of the best nodes of n_partials block partials exactly
+  // (the incumbent only ever rises).
+  hipError_t probe(int d, int64_t n_partials) {
+    hipError_t e;
+    if ((e = launch_pyr_final((const PyrPartial*)partials.p, n_partials, false, kRoots, (BestPartial*)inc.p,
+                              (uint64_t*)probe_slot.p, in.stream)) != hipSuccess)
+      return e;
+    if ((e = launch_pyr_probe(d, kRoots, (const uint64_t*)probe_slot.p, (uint64_t*)probe_nodes.p, in.stream)) !=
+        hipSuccess)
+      return e;
+    const int64_t np = ((int64_t)1 << (2 * d)) * kRoots;
+    if ((e = launch_pyr_bound(in.L, lev[0], 0, in.scans, in.angles, in.pts, in.n_used, in.step,
+                              (const uint64_t*)probe_nodes.p, np, nullptr, np, (double*)probe_vals.p,
+                              (PyrPartial*)partials.p, nullptr, in.stream)) != hipSuccess)
+      return e;
+    if ((e = launch_pyr_final((const PyrPartial*)partials.p, pyr_blocks(np), true, 0, (BestPartial*)inc.p, nullptr,
+                              in.stream)) != hipSuccess)
+      return e;
+    st->probe_leaves += np;
+    return hipSuccess;
+  }
+
+  // Children of nodes[d][s, s + k) (k on the host, or *n_dev) into nodes[d-1].
+  hipError_t expand(int d, int64_t s, int64_t k, const unsigned long long* n_dev, int64_t upper) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(count_dev(d - 1), 0, sizeof(unsigned long long), in.stream)) != hipSuccess) return e;
+    st->slices += 1;
+    return launch_pyr_expand(in.L, d, (const uint64_t*)nodes[d].p + s, (const double*)vals[d].p + s, k, n_dev, upper,
+                             (const BestPartial*)inc.p, (uint64_t*)nodes[d - 1].p, count_dev(d - 1), cap, in.stream);
+  }
+
+  // counts[d - 1] and counts[d] to the host
+  hipError_t read_counts(int d) {
+    hipError_t e;
+    if ((e = hipMemcpyAsync(h_counts, count_dev(d - 1), 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                            in.stream)) != hipSuccess)
+      return e;
+    st->syncs += 1;
+    return hipStreamSynchronize(in.stream);
+  }
+
+  // nodes[d] holds n nodes (n >= 0 known on the host; n < 0: counts[d]),
+  // at most `upper`: bound them and descend. The host reads a count back
+  // only when 4 * upper children might not fit the next list.
+  hipError_t level_pass(int d, int64_t n, int64_t upper, bool top) {
+    hipError_t e;
+    const unsigned long long* nd = n >= 0 ? nullptr : count_dev(d);
+    if ((e = bound(d, (const uint64_t*)nodes[d].p, (double*)vals[d].p, n, nd, upper)) != hipSuccess) return e;
+    return descend(d, n, upper, top, pyr_blocks(upper));
+  }
+
+  // nodes[d] and vals[d] are in place, the block bests in partials.
+  hipError_t descend(int d, int64_t n, int64_t upper, bool top, int64_t n_partials) {
+    hipError_t e;
+    const unsigned long long* nd = n >= 0 ? nullptr : count_dev(d);
+    if (d == 0)
+      return launch_pyr_final((const PyrPartial*)partials.p, n_partials, true, 0, (BestPartial*)inc.p, nullptr,
+                              in.stream);
+    if ((top || n >= probe_min) && (e = probe(d, n_partials)) != hipSuccess) return e;
+    if (4 * upper <= cap) {
+      if ((e = expand(d, 0, n, nd, upper)) != hipSuccess) return e;
+      return level_pass(d - 1, -1, 4 * upper, false);
+    }
+    // optimistic: expand everything, then look at the count
+    if ((e = expand(d, 0, n, nd, upper)) != hipSuccess) return e;
+    if ((e = read_counts(d)) != hipSuccess) return e;
+    const int64_t m = (int64_t)h_counts[0];
+    if (n < 0) n = (int64_t)h_counts[1];
+    if (m <= cap) return m > 0 ? level_pass(d - 1, m, m, false) : hipSuccess;
+    // overflow (children dropped): slices of cap / 4 parents, each descended
+    const int64_t slice = std::max<int64_t>(1, cap / 4);
+    for (int64_t s = 0; s < n; s += slice) {
+      const int64_t k = std::min(slice, n - s);
+      if ((e = expand(d, s, k, nullptr, k)) != hipSuccess) return e;
+      if ((e = level_pass(d - 1, -1, 4 * k, false)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+};
+
+PyramidSearch::PyramidSearch() : p_(new Impl) {}
+PyramidSearch::~PyramidSearch() { delete p_; }
+
+void PyramidSearch::release() {
+  delete p_;
+  p_ = new Impl;
+}
+
+void PyramidSearch::configure(int64_t node_capacity, int probe_min_nodes) {
+  p_->cap = node_capacity > 0 ? std::max<int64_t>(node_capacity, 4) : ((int64_t)1 << 24);
+  p_->probe_min = probe_min_nodes > 0 ? probe_min_nodes : 4096;
+}
+
+int64_t PyramidSearch::level_cells(int32_t sx, int32_t sy, int d) {
+  const int32_t w = sx + (1 << d), h = sy + (1 << d);
+  return (int64_t)((w + 3) & ~3) * h;
+}
+
+hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* stats, std::string* what) {
+  Impl& I = *p_;
+  PyrStats local;
+  I.st = stats ? stats : &local;
+  *I.st = PyrStats{};
+  I.st->depth = x.depth;
+  I.in = x;
+  hipError_t e;
+  auto fail = [&](hipError_t err, const char* msg) {
+    if (what) *what = msg;
+    return err;
+  };
+  if (x.depth < 0 || x.depth > kPyrMaxDepth) return fail(hipErrorInvalidValue, "pyramid depth out of range");
+  if ((e = I.build(x)) != hipSuccess) return fail(e, "pyramid levels");
+  const int64_t nj = ((int64_t)x.L.n_space + (1 << x.depth) - 1) >> x.depth;
+  const int64_t n_top = (int64_t)x.L.n_scans * x.L.n_angles * nj * nj;
+  if ((e = I.ensure_lists(x.depth)) != hipSuccess) return fail(e, "pyramid node lists");
+  const BestPartial init{-DBL_MAX, INT64_MAX};
+  if ((e = hipMemcpyAsync(I.inc.p, &init, sizeof(init), hipMemcpyHostToDevice, x.stream)) != hipSuccess)
+    return fail(e, "incumbent");
+  if ((e = hipMemsetAsync(I.scored.p, 0, (kPyrMaxDepth + 1) * sizeof(unsigned long long), x.stream)) != hipSuccess)
+    return fail(e, "node counters");
+  int32_t ktiles, kt, col_blocks;
+  const int top_blocks = pyr_top_blocks(x.L, (int32_t)nj, &ktiles, &kt, &col_blocks);
+  const int D = x.depth;
+  int64_t top_scored = 0;
+  if (D > 0 && top_blocks > 0 && n_top <= ((int64_t)1 << 28)) {
+    // the whole top level in one launch (column layout), then descend
+    if ((e = I.nodes[D].ensure((size_t)n_top * sizeof(uint64_t))) != hipSuccess ||
+        (e = I.vals[D].ensure((size_t)n_top * sizeof(double))) != hipSuccess)
+      return fail(e, "pyramid top level");
+    if ((e = I.partials.ensure((size_t)std::max<int64_t>(top_blocks, pyr_blocks(INT64_MAX / 2)) *
+                               sizeof(PyrPartial))) != hipSuccess)
+      return fail(e, "pyramid partials");
+    if ((e = launch_pyr_top_bound(x.L, I.lev[D], D, (int32_t)nj, x.scans, x.angles, x.pts, x.n_used, x.step,
+                                  (uint64_t*)I.nodes[D].p, (double*)I.vals[D].p, (PyrPartial*)I.partials.p,
+                                  x.stream)) != hipSuccess)
+      return fail(e, "pyr_top_bound_kernel");
+    top_scored = n_top;
+    if ((e = I.descend(D, n_top, n_top, true, top_blocks)) != hipSuccess) return fail(e, "pyramid level pass");
+  } else {
+    for (int64_t first = 0; first < n_top; first += I.cap) {
+      const int64_t m = std::min(I.cap, n_top - first);
+      if ((e = launch_pyr_top(x.L, (int32_t)nj, first, m, (uint64_t*)I.nodes[D].p, x.stream)) != hipSuccess)
+        return fail(e, "pyr_top_kernel");
+      if ((e = I.level_pass(D, m, m, true)) != hipSuccess) return fail(e, "pyramid level pass");
+    }
+  }
+  if ((e = hipMemcpyAsync(best, I.inc.p, sizeof(BestPartial), hipMemcpyDeviceToHost, x.stream)) != hipSuccess)
+    return fail(e, "incumbent copy");
+  unsigned long long* h_scored = I.h_counts + kPyrMaxDepth + 1;
+  if ((e = hipMemcpyAsync(h_scored, I.scored.p, (kPyrMaxDepth + 1) * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, x.stream)) != hipSuccess)
+    return fail(e, "node counters copy");
+  if ((e = hipStreamSynchronize(x.stream)) != hipSuccess) return fail(e, "pyramid search");
+  for (int d = 0; d <= kPyrMaxDepth; ++d) I.st->nodes[d] = (int64_t)h_scored[d];
+  I.st->nodes[D] += top_scored;
+  return hipSuccess;
+}
+
+}  // namespace csm

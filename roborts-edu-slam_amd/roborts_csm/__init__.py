@@ -388,6 +388,30 @@ class Context:
                 np.array([out[i].angle for i in range(n)]))
 
 
+    def search_windows(self, points_cells, param, grid_index, centers_map, max_depth: int = -1,
+                       probe_min_nodes: int = 0, node_capacity: int = 0):
+        """Best candidate of one scan over many windows by the admissible
+        multi-resolution search (csm_search_windows) -> (CsmBest, window, stats
+        dict). Same answer as reducing best_windows: max score, lowest
+        (window, flat index)."""
+        pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
+        p = _as_param(param)
+        gi = np.ascontiguousarray(grid_index, dtype=np.int32)
+        ctr = np.ascontiguousarray(centers_map, dtype=np.float64).reshape(-1, 3)
+        assert gi.size == ctr.shape[0]
+        opt = _abi.CsmSearchOptions(int(max_depth), int(probe_min_nodes), int(node_capacity))
+        b = CsmBest()
+        w = C.c_int32(-1)
+        st = _abi.CsmSearchStats()
+        self._check(_lib.csm_search_windows(self._h, _dptr(pts), pts.shape[0], C.byref(p), gi.size,
+                                            gi.ctypes.data_as(C.POINTER(C.c_int32)), _dptr(ctr), C.byref(opt),
+                                            C.byref(b), C.byref(w), C.byref(st)))
+        stats = dict(depth=st.depth, exhaustive=bool(st.exhaustive), candidates=st.candidates,
+                     nodes=list(st.nodes), probe_leaves=st.probe_leaves, beam_reads=st.beam_reads,
+                     build_ms=st.build_ms, syncs=st.syncs)
+        return b, int(w.value), stats
+
+
 def window_dims(param) -> tuple[int, int]:
     p = _as_param(param)
     na, ns = C.c_int32(), C.c_int32()

@@ -31,6 +31,7 @@ EXPORTED = (
     "csm_set_profiling", "csm_kernel_stats", "csm_sort_order", "csm_phase_buckets",
     "csm_set_grid_stack", "csm_best_windows", "csm_optimize_scan_match", "csm_optimize_scan_match_batch",
     "csm_optimize_update_cost", "csm_load_scans_grids", "csm_scan_matchers_batch_grids",
+    "csm_search_windows",
     # include/csm_gridmap.h
     "csm_gridmap_create", "csm_gridmap_destroy", "csm_gridmap_last_error",
     "csm_gridmap_set_options", "csm_gridmap_set_cell_params", "csm_gridmap_set_map_offset",
@@ -83,6 +84,28 @@ class CsmBest(C.Structure):
         ("x", C.c_double),
         ("y", C.c_double),
         ("angle", C.c_double),
+    ]
+
+
+class CsmSearchOptions(C.Structure):
+    """csm_search_options (include/csm.h): the admissible multi-resolution search."""
+    _fields_ = [
+        ("max_depth", C.c_int32),
+        ("probe_min_nodes", C.c_int32),
+        ("node_capacity", C.c_int64),
+    ]
+
+
+class CsmSearchStats(C.Structure):
+    _fields_ = [
+        ("depth", C.c_int32),
+        ("exhaustive", C.c_int32),
+        ("candidates", C.c_int64),
+        ("nodes", C.c_int64 * 11),
+        ("probe_leaves", C.c_int64),
+        ("beam_reads", C.c_int64),
+        ("build_ms", C.c_double),
+        ("syncs", C.c_int64),
     ]
 
 
@@ -168,6 +191,9 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_set_grid_stack": (C.c_int, [_ctx, C.c_void_p, C.c_int32, C.POINTER(CsmMapInfo), C.c_int64]),
         "csm_best_windows": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), C.c_int32, _i32p, _dp,
                                        C.POINTER(CsmBest)]),
+        "csm_search_windows": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), C.c_int32, _i32p, _dp,
+                                         C.POINTER(CsmSearchOptions), C.POINTER(CsmBest), _i32p,
+                                         C.POINTER(CsmSearchStats)]),
         "csm_optimize_scan_match": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmOptimizeParam), _dp, _dp]),
         "csm_optimize_scan_match_batch": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, C.POINTER(CsmOptimizeParam), _dp,
                                                     _dp, _i32p]),

@@ -19,8 +19,11 @@ answer is the single best candidate over all of them. Here:
   not depend on the rank count or order.
 
 The scorer is anything with ``best_windows(points, param, grid_index,
-centers) -> (scores, flat, x, y, angle)``: the HIP context
-(roborts_csm.Context) in production.
+centers) -> (scores, flat, x, y, angle)`` (search="exhaustive") or
+``search_windows(points, param, grid_index, centers) -> (best, window,
+stats)`` (search="pyramid", the admissible multi-resolution branch and
+bound of csrc/csm_pyramid.hip: same answer, a fraction of the scorings):
+the HIP context (roborts_csm.Context) in production.
 """
 from __future__ import annotations
 
@@ -59,8 +62,11 @@ class ShardedLoopClosure:
     """One rank's share of the submaps and the exchange that merges ranks."""
 
     def __init__(self, scorer, n_submaps: int, resolution: float, offsets: np.ndarray,
-                 rank: int = 0, world: int = 1, group=None, device=None):
+                 rank: int = 0, world: int = 1, group=None, device=None, search: str = "pyramid"):
+        assert search in ("pyramid", "exhaustive")
         self.scorer = scorer
+        self.search = search
+        self.last_stats = None
         self.n_submaps = int(n_submaps)
         self.resolution = float(resolution)
         self.lo, self.hi = shard_range(self.n_submaps, rank, world)
@@ -75,6 +81,10 @@ class ShardedLoopClosure:
         na, ns = window_dims(param)
         n_cand = na * ns * ns
         centers = np.stack([world_to_map(pose_world, self.resolution, o) for o in self.offsets])
+        if self.search == "pyramid":
+            b, w, self.last_stats = self.scorer.search_windows(points_cells, param, np.arange(n_loc), centers)
+            return LoopClosureResult(float(b.score), int((self.lo + w) * n_cand + b.flat_index), self.lo + w,
+                                     float(b.x), float(b.y), float(b.angle))
         sc, flat, x, y, a = self.scorer.best_windows(points_cells, param, np.arange(n_loc), centers)
         gidx = (np.arange(self.lo, self.hi, dtype=np.int64) * n_cand + flat.astype(np.int64))
         best = np.max(sc)

@@ -41,6 +41,17 @@ class OracleScorer:
             out[4].append((c[2] - (param.search_angle_offset * 2) / 2) + (flat // (ns * ns)) * param.search_angle_resolution)
         return tuple(np.array(v) for v in out)
 
+    def search_windows(self, points, param, grid_index, centers):
+        """csm_search_windows' contract: the best over all windows, ties to
+        the lowest (window, flat)."""
+        import roborts_csm
+        from roborts_csm._abi import CsmBest
+        na, ns = roborts_csm.window_dims(param)
+        sc, flat, x, y, a = self.best_windows(points, param, grid_index, centers)
+        gidx = np.arange(sc.size) * (na * ns * ns) + flat
+        k = int(np.argmin(np.where(sc == sc.max(), gidx, np.iinfo(np.int64).max)))
+        return CsmBest(sc[k], int(flat[k]), x[k], y[k], a[k]), k, {}
+
 
 def _world():
     rng = np.random.default_rng(77)
@@ -63,14 +74,15 @@ def test_shard_range_covers():
             assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
 
 
-def _single(grids, offsets, pts, pose):
-    lc = ShardedLoopClosure(OracleScorer(grids), grids.shape[0], RES, offsets)
+def _single(grids, offsets, pts, pose, search="exhaustive"):
+    lc = ShardedLoopClosure(OracleScorer(grids), grids.shape[0], RES, offsets, search=search)
     return lc.match(pts, PARAM, pose)
 
 
-def test_world1_matches_bruteforce():
+@pytest.mark.parametrize("search", ["exhaustive", "pyramid"])
+def test_world1_matches_bruteforce(search):
     grids, offsets, pts, pose = _world()
-    r = _single(grids, offsets, pts, pose)
+    r = _single(grids, offsets, pts, pose, search)
     import roborts_csm
     na, ns = roborts_csm.window_dims(PARAM)
     best = (-np.inf, None)
@@ -83,7 +95,7 @@ def test_world1_matches_bruteforce():
     assert (r.score, r.global_index) == best
 
 
-def _rank_main(rank, world, port, out_dir):
+def _rank_main(rank, world, port, out_dir, search):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -91,7 +103,7 @@ def _rank_main(rank, world, port, out_dir):
     grids, offsets, pts, pose = _world()
     lo, hi = shard_range(grids.shape[0], rank, world)
     lc = ShardedLoopClosure(OracleScorer(grids[lo:hi]), grids.shape[0], RES, offsets[lo:hi],
-                            rank=rank, world=world)
+                            rank=rank, world=world, search=search)
     r = lc.match(pts, PARAM, pose)
     np.save(os.path.join(out_dir, f"r{rank}.npy"),
             np.array([r.score, r.global_index, r.submap, r.x, r.y, r.angle], dtype=np.float64))
@@ -105,10 +117,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_shards_agree_with_single_process(tmp_path, world):
+@pytest.mark.parametrize("world,search", [(2, "exhaustive"), (3, "exhaustive"), (2, "pyramid"), (3, "pyramid")])
+def test_gloo_shards_agree_with_single_process(tmp_path, world, search):
     import torch.multiprocessing as mp
-    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path), search), nprocs=world, join=True)
     grids, offsets, pts, pose = _world()
     ref = _single(grids, offsets, pts, pose)
     want = np.array([ref.score, ref.global_index, ref.submap, ref.x, ref.y, ref.angle])
