@@ -41,6 +41,9 @@ EXPORTED = (
     # include/csm_frontend.h
     "csm_frontend_create", "csm_frontend_destroy", "csm_frontend_last_error", "csm_frontend_process",
     "csm_frontend_map",
+    # include/csm_loop_closure.h
+    "csm_loop_closure_create", "csm_loop_closure_destroy", "csm_loop_closure_last_error",
+    "csm_loop_closure_set_submaps", "csm_loop_closure_match",
     # include/csm_backend.h
     "csm_backend_create", "csm_backend_destroy", "csm_backend_last_error", "csm_backend_add_scan",
     "csm_backend_set_scan_pose", "csm_backend_scan_match", "csm_backend_map",
@@ -106,6 +109,20 @@ class CsmSearchStats(C.Structure):
         ("beam_reads", C.c_int64),
         ("build_ms", C.c_double),
         ("syncs", C.c_int64),
+    ]
+
+
+class CsmLoopClosureResult(C.Structure):
+    """csm_loop_closure_result (include/csm_loop_closure.h)."""
+    _fields_ = [
+        ("score", C.c_double),
+        ("global_index", C.c_int64),
+        ("submap", C.c_int32),
+        ("n_devices", C.c_int32),
+        ("x", C.c_double),
+        ("y", C.c_double),
+        ("angle", C.c_double),
+        ("pose_world", C.c_double * 3),
     ]
 
 
@@ -226,6 +243,13 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_scan_matchers_batch_grids": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, _i32p, C.POINTER(CsmParam), C.c_int32,
                                                     _dp, _dp, _dp]),
         "csm_set_grid_stack_gridmaps": (C.c_int, [_ctx, C.POINTER(C.c_void_p), C.c_int32]),
+        "csm_loop_closure_create": (C.c_int, [C.c_int32, _i32p, C.POINTER(C.c_void_p)]),
+        "csm_loop_closure_destroy": (C.c_int, [C.c_void_p]),
+        "csm_loop_closure_last_error": (C.c_char_p, [C.c_void_p]),
+        "csm_loop_closure_set_submaps": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(CsmMapInfo), _dp,
+                                                   C.c_int64]),
+        "csm_loop_closure_match": (C.c_int, [C.c_void_p, _dp, C.c_int32, C.POINTER(CsmParam), _dp, C.c_int32,
+                                             C.POINTER(CsmLoopClosureResult)]),
         "csm_backend_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
         "csm_backend_destroy": (C.c_int, [C.c_void_p]),
         "csm_backend_last_error": (C.c_char_p, [C.c_void_p]),

@@ -110,3 +110,69 @@ class ShardedLoopClosure:
         dist.all_reduce(row, op=dist.ReduceOp.SUM, group=self.group)
         r = row.cpu().numpy()
         return LoopClosureResult(float(s.item()), win, int(r[0]), float(r[1]), float(r[2]), float(r[3]))
+
+
+class DeviceLoopClosure:
+    """The same search and exchange behind the C-ABI (include/csm_loop_closure.h):
+    one process, the submaps sharded over `devices`, an in-process RCCL
+    communicator per device (ncclCommInitAll) carrying the MAX / MIN / SUM
+    all-reduces. What the reference's C++ back end (TryCloseLoop,
+    range_scan_pose_graph.cpp:299-355) would call; no torch involved."""
+
+    def __init__(self, devices=(0,)):
+        import ctypes as C
+        from . import _lib
+        self._C, self._lib = C, _lib
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        h = C.c_void_p()
+        st = _lib.csm_loop_closure_create(devs.size, devs.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(h))
+        if st != 0:
+            msg = _lib.csm_loop_closure_last_error(h).decode() if h.value else "create failed"
+            if h.value:
+                _lib.csm_loop_closure_destroy(h)
+            from . import CsmError
+            raise CsmError(st, msg)
+        self._h = h
+        self.n_devices = devs.size
+
+    def _check(self, st):
+        if st != 0:
+            from . import CsmError
+            raise CsmError(st, self._lib.csm_loop_closure_last_error(self._h).decode())
+
+    def set_submaps(self, grids: np.ndarray, resolution: float, offsets, version: int = -1):
+        from ._abi import CsmMapInfo
+        C = self._C
+        g = np.ascontiguousarray(grids, dtype=np.float32)
+        self._grids = g  # resident by host pointer: keep alive
+        off = np.ascontiguousarray(offsets, dtype=np.float64).reshape(-1, 2)
+        assert off.shape[0] == g.shape[0]
+        info = CsmMapInfo(float(resolution), 0.0, 0.0, g.shape[2], g.shape[1], 0, 0)
+        self._check(self._lib.csm_loop_closure_set_submaps(self._h, g.ctypes.data_as(C.c_void_p), g.shape[0],
+                                                           C.byref(info), off.ctypes.data_as(C.POINTER(C.c_double)),
+                                                           int(version)))
+
+    def match(self, points_cells, param, pose_world, search: str = "pyramid") -> LoopClosureResult:
+        from . import _as_param
+        from ._abi import CsmLoopClosureResult
+        C = self._C
+        pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
+        pose = np.ascontiguousarray(pose_world, dtype=np.float64)
+        p = _as_param(param)
+        r = CsmLoopClosureResult()
+        self._check(self._lib.csm_loop_closure_match(self._h, pts.ctypes.data_as(C.POINTER(C.c_double)), pts.shape[0],
+                                                     C.byref(p), pose.ctypes.data_as(C.POINTER(C.c_double)),
+                                                     0 if search == "pyramid" else 1, C.byref(r)))
+        self.last_pose_world = np.array(r.pose_world[:])
+        return LoopClosureResult(r.score, r.global_index, r.submap, r.x, r.y, r.angle)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.csm_loop_closure_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -75,3 +75,15 @@ def test_create_without_gpu_fails_cleanly():
 def test_package_import_is_loud_about_missing_library(tmp_path):
     with pytest.raises(OSError):
         _abi.load_library(str(tmp_path / "nope.so"))
+
+
+def test_loop_closure_create_without_gpu_fails_cleanly():
+    """csm_loop_closure_create loads RCCL privately, then fails on the
+    missing device with a message (no crash, no partial handle leak)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from roborts_csm import CsmError
+    from roborts_csm.loop_closure import DeviceLoopClosure
+    with pytest.raises(CsmError):
+        DeviceLoopClosure([0])
