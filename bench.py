@@ -453,6 +453,18 @@ def online_bench(args, rank, world_size, dist, torch):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     lat_ms = np.array(lat) * 1e3
+    # SlamProcessor::CorrectPoseAndMap (slam_processor.cpp:329-370) after the
+    # drive: every kept scan's pose nudged as a pose-graph solve would, all
+    # three maps rebuilt on the device from every kept scan
+    kept = fe.kept_poses()
+    rng = np.random.default_rng(5)
+    ids = np.arange(kept.shape[0], dtype=np.int32)
+    corr = kept + rng.uniform(-1, 1, size=kept.shape) * np.array([0.02, 0.02, 0.005])
+    tcp = time.perf_counter()
+    fe.correct_pose_and_map(ids, corr)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    correct_ms = (time.perf_counter() - tcp) * 1e3
     # pose error against the drive (the SLAM frame is the first scan's pose)
     t0p = stream.true_poses[0]
     c, s = math.cos(-t0p[2]), math.sin(-t0p[2])
@@ -474,6 +486,13 @@ def online_bench(args, rank, world_size, dist, torch):
         cpu = {"value": (m - args.warmup) / dtc, "unit": "scans/s", "cores": 1, "kind": "port",
                "sample": f"scans {args.warmup}..{m - 1} of the same stream through the oracle's restatement "
                          f"of the front-end (oracle/map_oracle.cpp), single-threaded, {dtc:.1f} s on {_cpu_model()}"}
+        if m == n:  # the oracle kept the same scans: time its CorrectPoseAndMap too
+            tco = time.perf_counter()
+            try:
+                ofe.correct_pose_and_map(ids, corr)
+                cpu["correct_pose_and_map_ms"] = (time.perf_counter() - tco) * 1e3
+            except ValueError:
+                pass
     return {
         "metric": "front-end scans/sec (config 5 online: 1081-beam stream, 3-level match + map check + 3 map "
                   "updates)",
@@ -487,7 +506,10 @@ def online_bench(args, rank, world_size, dist, torch):
                    "latency_ms": {"mean": float(lat_ms.mean()), "p50": float(np.median(lat_ms)),
                                   "p99": float(np.percentile(lat_ms, 99)), "max": float(lat_ms.max())},
                    "rate_40hz_headroom": float(world_size * args.steps / elapsed / 40.0),
-                   "median_pose_error_m": float(np.median(perr)), "max_pose_error_m": float(perr.max())},
+                   "median_pose_error_m": float(np.median(perr)), "max_pose_error_m": float(perr.max()),
+                   "correct_pose_and_map": {"kept_scans": int(kept.shape[0]), "ms": correct_ms,
+                                            "what": "CorrectPoseAndMap: all kept poses corrected, PubMap + coarse + "
+                                                    "fine rebuilt from every kept scan on the device"}},
         "roofline": None, "cpu_baseline": cpu,
     }
 

@@ -4,7 +4,8 @@
  * (slam/slam_processor.cpp:66-258) with every map and the scan matcher on the
  * GPU. It is what BASELINE config 5 ("online mode: scan stream against a
  * growing map") measures; the pose-graph back-end is out of scope (SURVEY.md
- * 8f), so loop closure and map correction are not run.
+ * 8f); its result, the corrected poses, comes back through
+ * csm_frontend_correct_pose_and_map (SlamProcessor::CorrectPoseAndMap).
  *
  * Per scan (reference lines):
  *   - first scan: CreateAllMap (slam_processor.cpp:466-524) makes the PubMap
@@ -93,6 +94,18 @@ int csm_frontend_process(csm_frontend* fe, const double* points_xy, int32_t n_po
 /* Borrow one of the front-end's maps (owned by the front-end; null before the
  * first scan). */
 int csm_frontend_map(csm_frontend* fe, int32_t which, csm_gridmap** map);
+
+/* SlamProcessor::CorrectPoseAndMap (slam/slam_processor.cpp:329-370): the
+ * pose-graph back end's corrected world poses for kept scans ids[0..n)
+ * (0 = the first kept scan; UpdateRangeData :597-602) replace their poses,
+ * then all three maps are rebuilt on the device from every kept scan
+ * (InitMapWithRangeVec, occu_grid_map.h:222-255): the PubMap from ids
+ * 0..last plus map_min_passthrough_ more copies of scan 0, the coarse and fine
+ * ScanMatchMaps with their blur settings. An id beyond the kept scans is
+ * CSM_ERR_INVALID_ARG (the reference's CHECK_LE aborts). */
+int csm_frontend_correct_pose_and_map(csm_frontend* fe, int32_t n, const int32_t* ids, const double* poses);
+/* Kept scans so far (*n in: capacity of poses, out: count) and their poses. */
+int csm_frontend_kept_scans(csm_frontend* fe, int32_t* n, double* poses);
 
 #ifdef __cplusplus
 }

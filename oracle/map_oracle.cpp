@@ -678,6 +678,11 @@ struct OFrontEnd {
   double cur[3] = {0, 0, 0}, last_odom[3] = {0, 0, 0}, last_update[3] = {0, 0, 0};
   double score = 0.0;
   int penalize_times = 0;
+  // the kept scans (SensorDataManager's range data of the maps, :216-221):
+  // sensor-frame points (m) and the pose each was drawn at
+  std::vector<double> kept_pts;
+  std::vector<int64_t> kept_off{0};
+  std::vector<double> kept_pose;
 };
 
 double norm_angle(double a) {  // util::NormalizeAngle (util/slam_util.h:103-111)
@@ -884,12 +889,52 @@ int oracle_frontend_process(void* h, const double* pts, int n, const double odom
   if (updated) {
     f.data_index++;
     std::memcpy(f.last_odom, odom, sizeof(f.last_odom));
+    f.kept_pts.insert(f.kept_pts.end(), pts, pts + 2 * (size_t)n);
+    f.kept_off.push_back((int64_t)(f.kept_pts.size() / 2));
+    f.kept_pose.insert(f.kept_pose.end(), f.cur, f.cur + 3);
   }
   std::memcpy(r.pose, f.cur, sizeof(r.pose));
   std::memcpy(r.cov, cov, sizeof(cov));
   r.score = f.score;
   r.map_updated = updated ? 1 : 0;
   std::memcpy(result, &r, sizeof(r));
+  return 0;
+}
+
+// SlamProcessor::CorrectPoseAndMap (slam/slam_processor.cpp:329-370): the
+// corrected poses replace the kept scans' poses (UpdateRangeData :597-602),
+// then each map is rebuilt from every kept scan (InitMapWithRangeVec): the
+// PubMap from ids 0..last plus map_min_passthrough_ more copies of scan 0,
+// the scan-match maps with their blur settings. Returns 1 on an id beyond the
+// kept scans (the reference's CHECK_LE aborts).
+int oracle_frontend_correct(void* h, int n, const int32_t* ids, const double* poses) {
+  OFrontEnd& f = *static_cast<OFrontEnd*>(h);
+  const FeParam& p = f.p;
+  const int kept = (int)f.kept_off.size() - 1;
+  for (int i = 0; i < n; ++i)
+    if (ids[i] < 0 || ids[i] >= kept) return 1;
+  if (kept == 0) return 0;
+  for (int i = 0; i < n; ++i) std::memcpy(&f.kept_pose[3 * (size_t)ids[i]], poses + 3 * i, 3 * sizeof(double));
+  std::vector<int> pub_ids;
+  for (int i = 0; i < kept; ++i) pub_ids.push_back(i);
+  for (int i = 0; i < p.map_min_passthrough; ++i) pub_ids.push_back(0);
+  const double res[3] = {p.map_resolution, p.coarse_map_resolution, p.fine_map_resolution};
+  const bool blur[3] = {false, p.coarse_map_use_blur != 0, p.fine_map_use_blur != 0};
+  for (int k = 0; k < 3; ++k) {
+    std::vector<int> use = pub_ids;
+    if (k > 0) use.resize((size_t)kept);
+    const double factor = 1 / res[k];  // CreateFrom (sensor_data_manager.h:99-115)
+    std::vector<double> pts, ps;
+    std::vector<int64_t> off{0};
+    for (int id : use) {
+      for (int64_t j = 2 * f.kept_off[(size_t)id]; j < 2 * f.kept_off[(size_t)id + 1]; ++j)
+        pts.push_back(f.kept_pts[(size_t)j] * factor);
+      off.push_back((int64_t)(pts.size() / 2));
+      ps.insert(ps.end(), &f.kept_pose[3 * (size_t)id], &f.kept_pose[3 * (size_t)id] + 3);
+    }
+    std::vector<double> org(2 * use.size(), 0.0);
+    init_with_range_vec(*f.maps[k], pts.data(), off.data(), (int)use.size(), org.data(), ps.data(), blur[k], false);
+  }
   return 0;
 }
 

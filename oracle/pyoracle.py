@@ -339,6 +339,7 @@ for _k, (_r, _a) in {
     "oracle_frontend_result_size": (C.c_int, []),
     "oracle_frontend_map": (C.c_void_p, [C.c_void_p, C.c_int]),
     "oracle_frontend_process": (C.c_int, [C.c_void_p, _dp, C.c_int, _dp, C.c_void_p]),
+    "oracle_frontend_correct": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int32), _dp]),
 }.items():
     _f = getattr(_lib, _k)
     _f.restype, _f.argtypes = _r, _a
@@ -378,6 +379,16 @@ class FrontEnd:
 
     def map(self, which: int) -> GridMap:
         return _FrontEndMap(_lib.oracle_frontend_map(self.h, which), self)
+
+    def correct_pose_and_map(self, ids, poses) -> None:
+        """SlamProcessor::CorrectPoseAndMap (slam_processor.cpp:329-370)."""
+        i = np.ascontiguousarray(ids, dtype=np.int32)
+        p = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 3)
+        assert p.shape[0] == i.size
+        st = _lib.oracle_frontend_correct(self.h, i.size, i.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          p.ctypes.data_as(_dp))
+        if st != 0:
+            raise ValueError("corrected id beyond the kept scans")
 
 
 # ---- BasedOptimizeScanMatch (opt_oracle.cpp) ----------------------------------

@@ -73,6 +73,12 @@ struct csm_frontend {
   double scan_match_score = 0.0;
   int map_penalize_times = 0;
   std::vector<double> pub_pts, coarse_pts, fine_pts;
+  // the kept scans (SensorDataManager's multiresolution range data,
+  // slam_processor.cpp:216-221): sensor-frame points (m), the pose each was
+  // drawn at (:196-205); CorrectPoseAndMap rebuilds the maps from them
+  std::vector<double> kept_pts;
+  std::vector<int64_t> kept_off{0};
+  std::vector<double> kept_pose;
   // CSM_FE_TIMING=1: host wall time per phase, printed at destroy
   bool timing = false;
   double t_phase[6] = {0, 0, 0, 0, 0, 0};
@@ -264,11 +270,62 @@ int csm_frontend_process(csm_frontend* f, const double* pts, int32_t n, const do
   if (updated) {  // the scan is kept (AddMultiresolutionRangeData); else ClearCurrentData
     f->data_index++;
     std::memcpy(f->last_odom, odom, sizeof(f->last_odom));
+    f->kept_pts.insert(f->kept_pts.end(), pts, pts + 2 * (size_t)n);
+    f->kept_off.push_back((int64_t)(f->kept_pts.size() / 2));
+    f->kept_pose.insert(f->kept_pose.end(), f->current_pose, f->current_pose + 3);
   }
   std::memcpy(r->pose, f->current_pose, sizeof(r->pose));
   std::memcpy(r->cov, cov, sizeof(cov));
   r->score = f->scan_match_score;
   r->map_updated = updated ? 1 : 0;
+  return CSM_OK;
+}
+
+int csm_frontend_correct_pose_and_map(csm_frontend* f, int32_t n, const int32_t* ids, const double* poses) {
+  if (!f || n < 0 || (n > 0 && (!ids || !poses))) return CSM_ERR_INVALID_ARG;
+  const csm_frontend_param& p = f->p;
+  const int kept = (int)f->kept_off.size() - 1;
+  for (int i = 0; i < n; ++i)  // CHECK_LE(id, current_data_index_) (:341)
+    if (ids[i] < 0 || ids[i] >= kept) return f->fail(CSM_ERR_INVALID_ARG, "corrected id beyond the kept scans");
+  if (kept == 0) return CSM_OK;
+  for (int i = 0; i < n; ++i)  // UpdateRangeData (:597-602)
+    std::memcpy(&f->kept_pose[3 * (size_t)ids[i]], poses + 3 * i, 3 * sizeof(double));
+  // the PubMap's scans: every kept id, then map_min_passthrough_ more copies of
+  // scan 0 (:349-355); the scan-match maps: every kept scan (:357-366)
+  std::vector<int> pub_ids;
+  for (int i = 0; i < kept; ++i) pub_ids.push_back(i);
+  for (int i = 0; i < p.map_min_passthrough; ++i) pub_ids.push_back(0);
+  const double res[3] = {p.map_resolution, p.coarse_map_resolution, p.fine_map_resolution};
+  const int32_t blur[3] = {0, p.coarse_map_use_blur, p.fine_map_use_blur};
+  std::vector<double> pts, ps;
+  std::vector<int64_t> off;
+  for (int k = 0; k < 3; ++k) {
+    const size_t use = k == 0 ? pub_ids.size() : (size_t)kept;
+    const double factor = 1 / res[k];  // CreateFrom (sensor_data_manager.h:99-115)
+    pts.clear();
+    ps.clear();
+    off.assign(1, 0);
+    for (size_t u = 0; u < use; ++u) {
+      const int id = pub_ids[u];
+      for (int64_t j = 2 * f->kept_off[(size_t)id]; j < 2 * f->kept_off[(size_t)id + 1]; ++j)
+        pts.push_back(f->kept_pts[(size_t)j] * factor);
+      off.push_back((int64_t)(pts.size() / 2));
+      ps.insert(ps.end(), &f->kept_pose[3 * (size_t)id], &f->kept_pose[3 * (size_t)id] + 3);
+    }
+    // InitMapWithRangeVec (occu_grid_map.h:222-255) on the device map: the
+    // scan-match maps' blur splats of every scan go down in one launch
+    const int st = csm_gridmap_init_with_range_vec(f->maps[k], (int32_t)use, pts.data(), off.data(), nullptr,
+                                                   ps.data(), blur[k], 0);
+    if (st != CSM_OK) return f->fail(st, std::string("InitMapWithRangeVec: ") + csm_gridmap_last_error(f->maps[k]));
+  }
+  return CSM_OK;
+}
+
+int csm_frontend_kept_scans(csm_frontend* f, int32_t* n, double* poses) {
+  if (!f || !n) return CSM_ERR_INVALID_ARG;
+  const int kept = (int)f->kept_off.size() - 1;
+  if (poses && *n >= kept) std::memcpy(poses, f->kept_pose.data(), 3 * (size_t)kept * sizeof(double));
+  *n = kept;
   return CSM_OK;
 }
 

@@ -164,3 +164,23 @@ class SlamFrontEnd:
         if st != _abi.CSM_OK or not h.value:
             raise RuntimeError("front-end map not available (no scan processed yet?)")
         return _BorrowedMap(h, self)
+
+    def correct_pose_and_map(self, ids, poses) -> None:
+        """SlamProcessor::CorrectPoseAndMap (slam/slam_processor.cpp:329-370):
+        corrected world poses for kept scans `ids`, then the three maps are
+        rebuilt on the device from every kept scan."""
+        i = np.ascontiguousarray(ids, dtype=np.int32)
+        p = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 3)
+        assert p.shape[0] == i.size
+        st = _lib.csm_frontend_correct_pose_and_map(self._h, i.size, i.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                    p.ctypes.data_as(C.POINTER(C.c_double)))
+        if st != _abi.CSM_OK:
+            raise RuntimeError(f"csm_frontend_correct_pose_and_map: status {st}: "
+                               f"{_lib.csm_frontend_last_error(self._h).decode()}")
+
+    def kept_poses(self) -> np.ndarray:
+        n = C.c_int32(0)
+        _lib.csm_frontend_kept_scans(self._h, C.byref(n), None)
+        out = np.zeros((max(n.value, 1), 3))
+        _lib.csm_frontend_kept_scans(self._h, C.byref(n), out.ctypes.data_as(C.POINTER(C.c_double)))
+        return out[:n.value]

@@ -58,7 +58,6 @@ def test_oracle_frontend_tracks_drive(mode):
 @pytest.mark.parametrize("mode", ["sim", "opt_sim", "opt_mixed", "opt_cfg"])
 def test_device_frontend_matches_oracle(mode):
     import pyoracle as O
-    from map_engines import same_state
     from roborts_csm.frontend import CsmFrontendResult, SlamFrontEnd
     n = 24
     st = _stream(n, seed=4)
@@ -74,6 +73,13 @@ def test_device_frontend_matches_oracle(mode):
         assert (a.score, a.map_penalty, a.optimize_cost, a.data_index, bool(a.map_updated),
                 bool(a.pose_accepted)) == \
             (b.score, b.map_penalty, b.optimize_cost, b.data_index, b.map_updated, b.pose_accepted), k
+
+    _same_maps(ofe, dfe)
+    dfe.close()
+
+
+def _same_maps(ofe, dfe):
+    from map_engines import same_state
 
     class _O:
         def __init__(self, m):
@@ -103,4 +109,65 @@ def test_device_frontend_matches_oracle(mode):
 
     for which in (0, 1, 2):
         same_state(_O(ofe.map(which)), _D(dfe.map(which)))
-    dfe.close()
+
+
+def _corrections(kept, k_ids=(1, 4, 9, 13)):
+    """A pose-graph style correction: some kept scans move a few cm / mrad."""
+    rng = np.random.default_rng(17)
+    ids = np.array([i for i in k_ids if i < kept.shape[0]], dtype=np.int32)
+    poses = kept[ids] + rng.uniform(-1, 1, size=(ids.size, 3)) * np.array([0.04, 0.04, 0.01])
+    return ids, poses
+
+
+def test_oracle_correct_pose_and_map():
+    """CPU: the oracle's CorrectPoseAndMap (slam_processor.cpp:329-370)
+    rebuilds its maps and the loop keeps tracking; a bad id is refused."""
+    import pyoracle as O
+    from roborts_csm.frontend import CsmFrontendResult
+    st = _stream(26, seed=5)
+    fe = O.FrontEnd(_param("sim").to_c())
+    for k in range(20):
+        fe.process(st.points_m[k], st.odom_poses[k], CsmFrontendResult())
+    with pytest.raises(ValueError):
+        fe.correct_pose_and_map([99], [[0.0, 0.0, 0.0]])
+    fe.correct_pose_and_map([2, 5], [[0.01, 0.0, 0.0], [0.0, 0.02, 0.005]])
+    for k in range(20, 26):
+        r = fe.process(st.points_m[k], st.odom_poses[k], CsmFrontendResult())
+        err = np.array(r.pose[:]) - _rel(st.true_poses, k)
+        assert abs(err[0]) < 0.05 and abs(err[1]) < 0.05 and abs(err[2]) < 0.02, (k, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["sim", "opt_sim"])
+def test_device_correct_pose_and_map_matches_oracle(mode):
+    """SlamProcessor::CorrectPoseAndMap on the device: corrected poses, the
+    three maps rebuilt from every kept scan (PubMap with the passthrough
+    copies of scan 0, blurred scan-match maps), bit for bit against the
+    oracle; then the front-end runs on over the rebuilt maps, still equal."""
+    import pyoracle as O
+    from roborts_csm.frontend import CsmFrontendResult, SlamFrontEnd
+    st = _stream(30, seed=6)
+    prm = _param(mode)
+    ofe = O.FrontEnd(prm.to_c())
+    dfe = SlamFrontEnd(prm)
+    try:
+        for k in range(22):
+            ofe.process(st.points_m[k], st.odom_poses[k], CsmFrontendResult())
+            dfe.process(st.points_m[k], st.odom_poses[k])
+        kept = dfe.kept_poses()
+        assert kept.shape[0] >= 10
+        ids, poses = _corrections(kept)
+        ofe.correct_pose_and_map(ids, poses)
+        dfe.correct_pose_and_map(ids, poses)
+        assert np.array_equal(dfe.kept_poses()[ids], poses)
+        _same_maps(ofe, dfe)
+        for k in range(22, 30):
+            a = ofe.process(st.points_m[k], st.odom_poses[k], CsmFrontendResult())
+            b = dfe.process(st.points_m[k], st.odom_poses[k])
+            assert np.array_equal(np.array(a.pose[:]), b.pose), k
+            assert (a.score, a.map_penalty, bool(a.map_updated)) == (b.score, b.map_penalty, b.map_updated), k
+        _same_maps(ofe, dfe)
+        with pytest.raises(RuntimeError):
+            dfe.correct_pose_and_map([10 ** 6], [[0.0, 0.0, 0.0]])
+    finally:
+        dfe.close()
