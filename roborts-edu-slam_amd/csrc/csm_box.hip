@@ -54,6 +54,169 @@ constexpr int kPF = CSM_BOX_PF;  // chunks of beam points in flight while a run 
 static_assert(kRunSeg % 64 == 0, "segments of whole 64-beam chunks");
 
 
+// One wave's view of its (window, angle): the beam points, the box test and
+// the per-segment run list (shared by the run-list and the grouped kernels).
+struct BoxWave {
+  const ScanWork& S;
+  const AngleEntry& ae;
+  const double2* __restrict__ P;
+  int step, n_used, lane, sx, sy, pitch4, zero_off;
+  double x_0, y_0;
+
+  // The box test of one beam point; on success (ix0, iy0) is the box corner.
+  __device__ __forceinline__ bool box_test(const double2 p, double& lx, double& ly, int& ix0, int& iy0) const {
+    lx = ae.cosine * p.x - ae.sine * p.y;  // :179
+    ly = ae.sine * p.x + ae.cosine * p.y;  // :180
+    const double tx = (lx + x_0) + 0.5;
+    const double ty = (ly + y_0) + 0.5;
+    const double fx = tx - floor(tx);
+    const double fy = ty - floor(ty);
+    const bool clean = tx >= 0.0 && ty >= 0.0 && fx >= kBoxMargin && fx <= 1.0 - kBoxMargin &&
+                       fy >= kBoxMargin && fy <= 1.0 - kBoxMargin;
+    ix0 = clean ? (int)tx : 0;
+    iy0 = clean ? (int)ty : 0;
+    return clean;
+  }
+  // Lane l: the box byte offset of beam cb + l (the zero block for beams past
+  // n_used, boxes wholly past the grid's high edges and rejected beams).
+  // slow: bit c marks 64-beam chunk c as holding a rejected beam (bit 63:
+  // some chunk >= 63), for the cell-by-cell pass at the end.
+  __device__ __forceinline__ int offsets(const double2 p, int cb, uint64_t& slow) const {
+    double lx, ly;
+    int ix0, iy0;
+    const bool clean = box_test(p, lx, ly, ix0, iy0);
+    const bool live = cb + lane < n_used;
+    slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean) != 0) << min(cb >> 6, 63);
+    return (live && clean && ix0 < sx && iy0 < sy) ? iy0 * pitch4 + ix0 * 4 : zero_off;
+  }
+  __device__ __forceinline__ double2 point(int cb) const { return P[(int64_t)min(cb + lane, n_used - 1) * step]; }
+
+  // Run list of beams [s0, s1): consecutive beams with the same box corner
+  // (common: at a few metres, neighbouring beams of a 0.25 deg scanner land in
+  // the same cell) form one run, (corner offset, count) at run_off / run_cnt;
+  // runs of boxes wholly off the grid and of rejected beams are dropped (they
+  // read zeros). Slots from `scratch` on take the non-run lanes' writes
+  // (branch-free). Returns the run count.
+  __device__ __forceinline__ int build_runs(int s0, int s1, int32_t* run_off, int32_t* run_cnt, int scratch,
+                                            uint64_t& slow) const {
+    int nruns = 0;
+    // points of kPF chunks in flight: the list build is latency-bound
+    // otherwise (one dependent load per 64 beams)
+    double2 pq[kPF];
+#pragma unroll
+    for (int u = 0; u < kPF; ++u) {  // issued in the order the loop consumes them
+      pq[u] = point(s0 + 64 * u);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    for (int cb0 = s0; cb0 < s1; cb0 += 64 * kPF) {
+#pragma unroll
+      for (int u = 0; u < kPF; ++u) {
+        // no early exit: a chunk at or past s1 adds no run (live is false for
+        // every lane), and an exit here made the compiler drain vmcnt(0) per
+        // chunk instead of keeping kPF chunks of points in flight
+        const int cb = cb0 + 64 * u;
+        const double2 pcur = pq[u];
+        pq[u] = point(cb + 64 * kPF);
+        __builtin_amdgcn_sched_barrier(0);
+        const int off = offsets(pcur, cb, slow);
+        const bool live = cb + lane < s1;
+        // previous beam's corner (lane 0: none)
+        const int prev = __builtin_amdgcn_mov_dpp(off, 0x138, 0xF, 0xF, false);  // wave_shr:1
+        const bool edge = live && (lane == 0 || off != prev);  // a new corner starts here
+        const uint64_t E = __builtin_amdgcn_ballot_w64(edge);
+        const int nlive = min(64, s1 - cb);
+        const uint64_t above = lane == 63 ? 0ull : (E >> (lane + 1)) << (lane + 1);
+        const int next = above ? (int)__builtin_ctzll(above) : nlive;
+        const bool head = edge && off != zero_off;
+        const uint64_t Hm = __builtin_amdgcn_ballot_w64(head);
+        const int rank = __builtin_popcountll(Hm & ((1ull << lane) - 1));
+        const int slot = head ? nruns + rank : scratch + lane;
+        run_off[slot] = off;
+        run_cnt[slot] = next - lane;
+        nruns += __builtin_popcountll(Hm);
+      }
+    }
+    return nruns;
+  }
+};
+
+// Rejected beams, cell by cell with the reference's expressions: only the
+// marked chunks are revisited, and only their rejected beams summed into the
+// lane's candidates (j = 4q .. 4q+3, row k).
+template <int NS>
+__device__ __forceinline__ void slow_beams(const BoxWave& B, const LevelWork& L, const int32_t* gi, uint64_t slow,
+                                           int k, int q, int64_t (&acc)[4]) {
+  const double f = L.step_cells;
+  for (uint64_t m = slow; m != 0; m &= m - 1) {
+    const int c0 = (int)__builtin_ctzll(m);
+    const int c_end = c0 == 63 ? (B.n_used + 63) / 64 : c0 + 1;
+    for (int c = c0; c < c_end; ++c) {
+      const int cb = c * 64;
+      double lx, ly;
+      int ix0, iy0;
+      const bool clean = B.box_test(B.point(cb), lx, ly, ix0, iy0);
+      for (uint64_t rej = __builtin_amdgcn_ballot_w64(cb + B.lane < B.n_used && !clean); rej != 0; rej &= rej - 1) {
+        const int l = (int)__builtin_ctzll(rej);  // uniform: one beam for the whole wave
+        const double bx = dev::bcast_lane(lx, l);
+        const double by = dev::bcast_lane(ly, l);
+        const int gy = (int)((by + (B.S.y0 + k * f)) + 0.5);
+        const bool iny = (unsigned)gy < (unsigned)B.sy;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = 4 * q + t;
+          if (j < NS) {
+            const int gx = (int)((bx + (B.S.x0 + j * f)) + 0.5);
+            const bool in = iny && (unsigned)gx < (unsigned)B.sx;
+            acc[t] += gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)B.sy * L.pitch];
+          }
+        }
+      }
+    }
+  }
+}
+
+// Scores of the lane's candidates (j = 4q .. 4q+3, row k) from their integer
+// sums: written out, or reduced to the wave's best.
+template <int NS, bool BEST>
+__device__ __forceinline__ void box_epilogue(const LevelWork& L, const ScanWork& S, const AngleEntry& ae, int win,
+                                             int a, bool act, int k, int q, const int64_t (&acc)[4],
+                                             double* __restrict__ out, BestPartial* __restrict__ partials) {
+  const double f = L.step_cells;
+  double bs = -1.0e300;
+  int64_t bf = INT64_MAX;
+  const double yk = S.y0 + k * f;  // :572
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int j = 4 * q + t;
+    if (act && j < NS) {
+      const double accd = (double)(acc[t] + (int64_t)S.n_used * L.outside_i) * L.int_scale;
+      const double xj = S.x0 + j * f;  // :569
+      const double score = dev::penalized(L, S, accd, xj, yk, ae.angle);
+      const int64_t flat = ((int64_t)a * NS + j) * NS + k;
+      if (BEST) {
+        if (dev::better(score, flat, bs, bf)) {
+          bs = score;
+          bf = flat;
+        }
+      } else {
+        out[S.out_off + flat] = score;
+      }
+    }
+  }
+  if (BEST) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double os = __shfl_down(bs, o, 64);
+      const int64_t of = __shfl_down(bf, o, 64);
+      if (dev::better(os, of, bs, bf)) {
+        bs = os;
+        bf = of;
+      }
+    }
+    if (threadIdx.x == 0) partials[(int64_t)win * L.blocks_per_scan + a] = BestPartial{bs, bf};
+  }
+}
+
 template <int NS, int D, bool RUNS, bool BEST>
 __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWork* __restrict__ scans,
                                                        const double2* __restrict__ pts,
@@ -73,15 +236,12 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   // idle lanes repeat row 0's addresses (no extra cache lines)
   const int k = act ? lane / NQ : 0;
   const int q = act ? lane - k * NQ : lane % NQ;
-  const double f = L.step_cells;     // 1.0 (host)
-  const double x_0 = S.x0 + 0 * f;   // :569 at j = 0
-  const double y_0 = S.y0 + 0 * f;   // :572 at k = 0
-  const int sx = L.size_x, sy = L.size_y;
   const int pitch4 = L.pitch * 4;
-  const int zero_off = sy * pitch4;  // first of the zero rows
-  const double2* __restrict__ P = pts + S.pts_off;
-  const int step = S.step;
+  const BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, pitch4,
+                  L.size_y * pitch4 /* first of the zero rows */, S.x0 + 0 * L.step_cells /* :569, j = 0 */,
+                  S.y0 + 0 * L.step_cells /* :572, k = 0 */};
   const int n_used = S.n_used;
+  const int zero_off = B.zero_off;
   const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
   const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
   const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
@@ -89,42 +249,14 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
       (void*)(((uint64_t)ghi << 32) | glo), (short)0, (int)(L.gridi_stride * 4), 0x00020000);
   const int voff = k * pitch4 + 16 * q;
 
-  // The box test of one beam point; on success (ix0, iy0) is the box corner.
-  auto box_test = [&](const double2 p, double& lx, double& ly, int& ix0, int& iy0) -> bool {
-    lx = ae.cosine * p.x - ae.sine * p.y;  // :179
-    ly = ae.sine * p.x + ae.cosine * p.y;  // :180
-    const double tx = (lx + x_0) + 0.5;
-    const double ty = (ly + y_0) + 0.5;
-    const double fx = tx - floor(tx);
-    const double fy = ty - floor(ty);
-    const bool clean = tx >= 0.0 && ty >= 0.0 && fx >= kBoxMargin && fx <= 1.0 - kBoxMargin &&
-                       fy >= kBoxMargin && fy <= 1.0 - kBoxMargin;
-    ix0 = clean ? (int)tx : 0;
-    iy0 = clean ? (int)ty : 0;
-    return clean;
-  };
-  // Lane l: the box byte offset of beam cb + l (the zero block for beams past
-  // n_used, boxes wholly past the grid's high edges and rejected beams).
-  // slow: bit c marks 64-beam chunk c as holding a rejected beam (bit 63:
-  // some chunk >= 63), for the cell-by-cell pass at the end.
-  auto offsets = [&](const double2 p, int cb, uint64_t& slow) -> int {
-    double lx, ly;
-    int ix0, iy0;
-    const bool clean = box_test(p, lx, ly, ix0, iy0);
-    const bool live = cb + lane < n_used;
-    slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean) != 0) << min(cb >> 6, 63);
-    return (live && clean && ix0 < sx && iy0 < sy) ? iy0 * pitch4 + ix0 * 4 : zero_off;
-  };
-  auto point = [&](int cb) { return P[(int64_t)min(cb + lane, n_used - 1) * step]; };
-
   auto load = [&](int soff) { return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0); };
   int64_t acc[4] = {0, 0, 0, 0};
   uint64_t slow = 0;
   v4i buf[D];
   if constexpr (!RUNS) {
-    int offA = offsets(point(0), 0, slow);    // beams of the current chunk
-    int offB = offsets(point(64), 64, slow);  // and of the next one
-    double2 pn = point(128);                  // points of the chunk after, in flight
+    int offA = B.offsets(B.point(0), 0, slow);    // beams of the current chunk
+    int offB = B.offsets(B.point(64), 64, slow);  // and of the next one
+    double2 pn = B.point(128);                    // points of the chunk after, in flight
     // soffset of beam cb + r, 0 <= r < 128
     auto off_of = [&](int r) -> int {
       return r < 64 ? __builtin_amdgcn_readlane(offA, r) : __builtin_amdgcn_readlane(offB, r - 64);
@@ -161,58 +293,19 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
         for (int t = 0; t < 4; ++t) acc[t] += part[t];
       }
       offA = offB;
-      offB = offsets(pn, (c + 2) * 64, slow);
-      pn = point((c + 3) * 64);
+      offB = B.offsets(pn, (c + 2) * 64, slow);
+      pn = B.point((c + 3) * 64);
     }
   } else {
-    // Run list: consecutive beams with the same box corner (common: at a few
-    // metres, neighbouring beams of a 0.25 deg scanner land in the same cell)
-    // form one run; a run is one load whose values are added count times.
-    // Runs of boxes wholly off the grid and of rejected beams are dropped
-    // (they read zeros). Lists are built per segment of kRunSeg beams.
-    // list, padding, then one scratch slot per lane (branch-free list writes)
+    // Run list: a run is one load whose values are added count times. Lists
+    // are built per segment of kRunSeg beams (list, padding, then one scratch
+    // slot per lane for the branch-free list writes).
     constexpr int kScratch = kRunSeg + 64 + 2 * D;
     __shared__ int32_t run_off[kScratch + 64];
     __shared__ int32_t run_cnt[kScratch + 64];
     for (int s0 = 0; s0 < n_used; s0 += kRunSeg) {
       const int s1 = min(n_used, s0 + kRunSeg);
-      int nruns = 0;
-      // points of kPF chunks in flight: the list build is latency-bound
-      // otherwise (one dependent load per 64 beams)
-      double2 pq[kPF];
-#pragma unroll
-      for (int u = 0; u < kPF; ++u) {  // issued in the order the loop consumes them
-        pq[u] = point(s0 + 64 * u);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      for (int cb0 = s0; cb0 < s1; cb0 += 64 * kPF) {
-#pragma unroll
-        for (int u = 0; u < kPF; ++u) {
-          // no early exit: a chunk at or past s1 adds no run (live is false for
-          // every lane), and an exit here made the compiler drain vmcnt(0) per
-          // chunk instead of keeping kPF chunks of points in flight
-          const int cb = cb0 + 64 * u;
-          const double2 pcur = pq[u];
-          pq[u] = point(cb + 64 * kPF);
-          __builtin_amdgcn_sched_barrier(0);
-          const int off = offsets(pcur, cb, slow);
-          const bool live = cb + lane < s1;
-          // previous beam's corner (lane 0: none)
-          const int prev = __builtin_amdgcn_mov_dpp(off, 0x138, 0xF, 0xF, false);  // wave_shr:1
-          const bool edge = live && (lane == 0 || off != prev);  // a new corner starts here
-          const uint64_t E = __builtin_amdgcn_ballot_w64(edge);
-          const int nlive = min(64, s1 - cb);
-          const uint64_t above = lane == 63 ? 0ull : (E >> (lane + 1)) << (lane + 1);
-          const int next = above ? (int)__builtin_ctzll(above) : nlive;
-          const bool head = edge && off != zero_off;
-          const uint64_t Hm = __builtin_amdgcn_ballot_w64(head);
-          const int rank = __builtin_popcountll(Hm & ((1ull << lane) - 1));
-          const int slot = head ? nruns + rank : kScratch + lane;
-          run_off[slot] = off;
-          run_cnt[slot] = next - lane;
-          nruns += __builtin_popcountll(Hm);
-        }
-      }
+      const int nruns = B.build_runs(s0, s1, run_off, run_cnt, kScratch, slow);
       // whole groups of D, then empty runs (zero block, count 0) far enough
       // past the list for the issue-ahead window below
       const int npad = (nruns + D - 1) / D * D;
@@ -258,69 +351,8 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
       __syncthreads();  // the next segment rewrites the list
     }
   }
-
-  // Rejected beams, cell by cell with the reference's expressions: only the
-  // marked chunks are revisited, and only their rejected beams summed.
-  for (uint64_t m = slow; m != 0; m &= m - 1) {
-    const int c0 = (int)__builtin_ctzll(m);
-    const int c_end = c0 == 63 ? (n_used + 63) / 64 : c0 + 1;
-    for (int c = c0; c < c_end; ++c) {
-      const int cb = c * 64;
-      double lx, ly;
-      int ix0, iy0;
-      const bool clean = box_test(point(cb), lx, ly, ix0, iy0);
-      for (uint64_t rej = __builtin_amdgcn_ballot_w64(cb + lane < n_used && !clean); rej != 0; rej &= rej - 1) {
-        const int l = (int)__builtin_ctzll(rej);  // uniform: one beam for the whole wave
-        const double bx = dev::bcast_lane(lx, l);
-        const double by = dev::bcast_lane(ly, l);
-        const int gy = (int)((by + (S.y0 + k * f)) + 0.5);
-        const bool iny = (unsigned)gy < (unsigned)sy;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = 4 * q + t;
-          if (j < NS) {
-            const int gx = (int)((bx + (S.x0 + j * f)) + 0.5);
-            const bool in = iny && (unsigned)gx < (unsigned)sx;
-            acc[t] += gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)sy * L.pitch];
-          }
-        }
-      }
-    }
-  }
-
-  double bs = -1.0e300;
-  int64_t bf = INT64_MAX;
-  const double yk = S.y0 + k * f;  // :572
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int j = 4 * q + t;
-    if (act && j < NS) {
-      const double accd = (double)(acc[t] + (int64_t)n_used * L.outside_i) * L.int_scale;
-      const double xj = S.x0 + j * f;  // :569
-      const double score = dev::penalized(L, S, accd, xj, yk, ae.angle);
-      const int64_t flat = ((int64_t)a * NS + j) * NS + k;
-      if (BEST) {
-        if (dev::better(score, flat, bs, bf)) {
-          bs = score;
-          bf = flat;
-        }
-      } else {
-        out[S.out_off + flat] = score;
-      }
-    }
-  }
-  if (BEST) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double os = __shfl_down(bs, o, 64);
-      const int64_t of = __shfl_down(bf, o, 64);
-      if (dev::better(os, of, bs, bf)) {
-        bs = os;
-        bf = of;
-      }
-    }
-    if (lane == 0) partials[(int64_t)win * L.blocks_per_scan + a] = BestPartial{bs, bf};
-  }
+  slow_beams<NS>(B, L, gi, slow, k, q, acc);
+  box_epilogue<NS, BEST>(L, S, ae, win, a, act, k, q, acc, out, partials);
 }
 
 template <int NS, int D, bool RUNS>
@@ -340,7 +372,8 @@ hipError_t launch_ns(const LevelWork& L, const ScanWork* s, const double2* p, co
 bool box_supported(int ns) { return ns >= 9 && ns <= 16; }
 
 // CSM_BOX=beams: one load per beam (no run list); CSM_BOX_DEPTH=16: 16 loads
-// in flight per wave instead of 8.
+// in flight per wave instead of 8. (Grouping runs of nearby corners into one
+// shared load measured slower: profiles/r02/experiments/ab_box_groups.txt.)
 int box_mode() {
   static const int m = [] {
     const char* env = std::getenv("CSM_BOX_DEPTH");
@@ -362,7 +395,7 @@ hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const d
   const int mode = box_mode();
 #define CSM_BOX_CASE(N)                                                                        \
   case N:                                                                                      \
-    switch (mode) {                                                                            \
+    switch (mode & 3) {                                                                        \
       case 0:                                                                                  \
         return launch_ns<N, 8, true>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);   \
       case 1:                                                                                  \
