@@ -2710,7 +2710,7 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
     L.int_scale = std::ldexp(1.0, -c->int_exp);
     in.level0 = csm::PyrGrid{(const int32_t*)c->gridi.p,
                              (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows), c->pitch, 0,
-                             c->info.size_x, c->info.size_y, 0, c->info.size_x};
+                             c->info.size_x, c->info.size_y, 0, c->info.size_x, 0, 0};
     in.n_grids = c->n_grids;
     in.grid_gen = c->grid_gen;
     in.scans = (const ScanWork*)c->scans.p;

@@ -44,10 +44,15 @@ __device__ __forceinline__ int64_t pyr_col(const PyrGrid& L, int xs) {
 
 // Level d (>= 1): anchor (x, y) = (xs - 2^d, ys - 2^d) holds the maximum of
 // the source over anchors x + t, t in taps (d = 1: the grid at 0, 1, 2;
-// d >= 2: level d - 1 at 0 and 2^(d-1)), rows likewise. Every stored cell of
+// d >= 2: level d - 1 at 0 and 2^(d-1)), rows likewise, quantised upwards to
+// int16 (level 1 from the int32 grid: ceil(max / 2^qs); later levels take
+// the max of already quantised values, the same thing). Every stored cell of
 // the buffer is written (pad columns zero).
+template <typename TS>
 __global__ __launch_bounds__(256) void pyr_pool_kernel(PyrGrid src, PyrGrid dst, int t1, int t2, int ntaps,
                                                        int64_t total) {
+  const TS* __restrict__ sg = (const TS*)src.g;
+  int16_t* __restrict__ dg = (int16_t*)const_cast<void*>(dst.g);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t gidx = i / dst.stride;
@@ -58,7 +63,7 @@ __global__ __launch_bounds__(256) void pyr_pool_kernel(PyrGrid src, PyrGrid dst,
     int32_t m = 0;
     if (ph < (1 << dst.lg) && xs < dst.width && ys < dst.height) {
       const int ax = xs - dst.shift + src.shift, ay = ys - dst.shift + src.shift;
-      const int32_t* g = src.g + gidx * src.stride;
+      const TS* g = sg + gidx * src.stride;
       const int tap[3] = {0, t1, t2};
       bool any = false;
       for (int ty = 0; ty < ntaps; ++ty) {
@@ -66,13 +71,15 @@ __global__ __launch_bounds__(256) void pyr_pool_kernel(PyrGrid src, PyrGrid dst,
         for (int tx = 0; tx < ntaps; ++tx) {
           const int xx = ax + tap[tx];
           const bool in = (unsigned)xx < (unsigned)src.width && (unsigned)yy < (unsigned)src.height;
-          const int32_t v = in ? g[(int64_t)yy * src.pitch + pyr_col(src, xx)] : 0;  // off-grid: outside
+          const int32_t v = in ? (int32_t)g[(int64_t)yy * src.pitch + pyr_col(src, xx)] : 0;  // off-grid: outside
           m = any ? max(m, v) : v;
           any = true;
         }
       }
+      const int dq = dst.qs - src.qs;  // quantise: ceil(m / 2^dq) (arithmetic shift floors)
+      if (dq > 0) m = (m + (1 << dq) - 1) >> dq;
     }
-    const_cast<int32_t*>(dst.g)[i] = m;
+    dg[i] = (int16_t)m;
   }
 }
 
@@ -91,10 +98,11 @@ __global__ __launch_bounds__(256) void pyr_top_kernel(LevelWork L, int32_t nj, i
   }
 }
 
+template <int NT = kPB>
 __device__ __forceinline__ void block_best(double v, int64_t f, uint64_t nd, PyrPartial* __restrict__ out) {
-  __shared__ double rs[kPB / 64];
-  __shared__ int64_t rf[kPB / 64];
-  __shared__ uint64_t rn[kPB / 64];
+  __shared__ double rs[NT / 64];
+  __shared__ int64_t rf[NT / 64];
+  __shared__ uint64_t rn[NT / 64];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const double ov = __shfl_down(v, off, 64);
@@ -114,7 +122,7 @@ __device__ __forceinline__ void block_best(double v, int64_t f, uint64_t nd, Pyr
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int k = 1; k < kPB / 64; ++k)
+    for (int k = 1; k < NT / 64; ++k)
       if (better(rs[k], rf[k], v, f)) {
         v = rs[k];
         f = rf[k];
@@ -128,6 +136,7 @@ __device__ __forceinline__ void block_best(double v, int64_t f, uint64_t nd, Pyr
 // beams of the level-d value at the anchor candidate's cell (GetResponse
 // :645-654 with the pooled level in place of the grid); d = 0 is the
 // candidate's exact, penalised score.
+template <typename T>
 __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev, int d,
                                                         const ScanWork* __restrict__ scans,
                                                         const AngleEntry* __restrict__ angles,
@@ -160,7 +169,7 @@ __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev
       const AngleEntry ae = angles[S.angle_off + a];
       const double x = S.x0 + j0 * L.step_cells;  // :569
       const double y = S.y0 + k0 * L.step_cells;  // :572
-      const int32_t* __restrict__ g = lev.g + (int64_t)S.grid_index * lev.stride;
+      const T* __restrict__ g = (const T*)lev.g + (int64_t)S.grid_index * lev.stride;
       int64_t sum = 0;
       auto cell = [&](int b) -> int32_t {
         const double2 p = beams[b];
@@ -182,6 +191,7 @@ __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev
         sum += (int64_t)(((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7])));
       }
       for (; b < n_used; ++b) sum += cell(b);
+      sum <<= lev.qs;  // the quantised levels' unit
       const double acc = (double)(sum + (int64_t)n_used * L.outside_i) * L.int_scale;
       if (d == 0) {
         v = penalized(L, S, acc, x, y, ae.angle);
@@ -208,7 +218,9 @@ __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev
 // phase-split cells. Writes every top node and its bound in list order
 // ((window, angle, K, J), J fastest) and one best per block.
 constexpr int kTopKT = 16;
-__global__ __launch_bounds__(kPB) void pyr_top_bound_kernel(LevelWork L, PyrGrid lev, int d, int32_t nj,
+constexpr int kTB = 64;  // one wave per block: a window's blocks, XCD-remapped, share one XCD's L2
+template <typename T>
+__global__ __launch_bounds__(kTB) void pyr_top_bound_kernel(LevelWork L, PyrGrid lev, int d, int32_t nj,
                                                             int32_t ktiles, int32_t kt, int32_t col_blocks,
                                                             const ScanWork* __restrict__ scans,
                                                             const AngleEntry* __restrict__ angles,
@@ -217,13 +229,14 @@ __global__ __launch_bounds__(kPB) void pyr_top_bound_kernel(LevelWork L, PyrGrid
                                                             double* __restrict__ vals,
                                                             PyrPartial* __restrict__ partials) {
   extern __shared__ double2 beams[];
-  for (int b = threadIdx.x; b < n_used; b += kPB) beams[b] = pts[(int64_t)b * step];
+  for (int b = threadIdx.x; b < n_used; b += kTB) beams[b] = pts[(int64_t)b * step];
   __syncthreads();
   const int per_window = col_blocks * ktiles;
-  const int w = blockIdx.x / per_window;
-  const int r = blockIdx.x - w * per_window;
+  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int w = bid / per_window;
+  const int r = bid - w * per_window;
   const int cb = r / ktiles, ktile = r - cb * ktiles;
-  const int col = cb * kPB + threadIdx.x;
+  const int col = cb * kTB + threadIdx.x;
   const bool valid = col < L.n_angles * nj;
   const int a = valid ? col / nj : 0;
   const int J = valid ? col - a * nj : 0;
@@ -235,7 +248,7 @@ __global__ __launch_bounds__(kPB) void pyr_top_bound_kernel(LevelWork L, PyrGrid
   double y[kTopKT];
 #pragma unroll
   for (int kk = 0; kk < kTopKT; ++kk) y[kk] = S.y0 + ((K0 + kk) << d) * L.step_cells;  // :572
-  const int32_t* __restrict__ g = lev.g + (int64_t)S.grid_index * lev.stride;
+  const T* __restrict__ g = (const T*)lev.g + (int64_t)S.grid_index * lev.stride;
   const int sh = lev.shift, W = lev.width, H = lev.height, pitch = lev.pitch, lg = lev.lg, qc = lev.q;
   const int pm = (1 << lg) - 1;
   int64_t sum[kTopKT];
@@ -253,7 +266,7 @@ __global__ __launch_bounds__(kPB) void pyr_top_bound_kernel(LevelWork L, PyrGrid
     for (int kk = 0; kk < kTopKT; ++kk) {
       const int gy = (int)((ly + y[kk]) + 0.5) + sh;
       const bool in = inx && (unsigned)gy < (unsigned)H && kk < krem;
-      const int32_t v = g[in ? (int64_t)gy * pitch + cx : 0];
+      const int32_t v = (int32_t)g[in ? (int64_t)gy * pitch + cx : 0];
       c[kk] = in ? v : 0;
     }
 #pragma unroll
@@ -267,7 +280,7 @@ __global__ __launch_bounds__(kPB) void pyr_top_bound_kernel(LevelWork L, PyrGrid
   for (int kk = 0; kk < kTopKT; ++kk) {
     if (valid && kk < krem) {
       const int K = K0 + kk;
-      const double acc = (double)(sum[kk] + (int64_t)n_used * L.outside_i) * L.int_scale;
+      const double acc = (double)((sum[kk] << lev.qs) + (int64_t)n_used * L.outside_i) * L.int_scale;
       const double raw = acc / S.divisor;
       const double v = (L.use_penalty && raw < 0.0) ? raw * 0.45 : raw;
       const int64_t idx = (wbase + K) * nj + J;
@@ -282,7 +295,7 @@ __global__ __launch_bounds__(kPB) void pyr_top_bound_kernel(LevelWork L, PyrGrid
       }
     }
   }
-  block_best(bv, bf, bn, partials + blockIdx.x);
+  block_best<kTB>(bv, bf, bn, partials + bid);
 }
 
 // merge (one block): fold the best partial into the incumbent. Otherwise
@@ -404,8 +417,12 @@ hipError_t launch_pyr_pool(const PyrGrid& src, const PyrGrid& dst, int d, int32_
   const int t1 = d == 1 ? 1 : (1 << (d - 1));
   const int t2 = d == 1 ? 2 : 0;
   const int ntaps = d == 1 ? 3 : 2;
-  hipLaunchKernelGGL(pyr_pool_kernel, dim3(blocks_for(total, 256)), dim3(256), 0, stream, src, dst, t1, t2, ntaps,
-                     total);
+  if (src.qs == 0)
+    hipLaunchKernelGGL(pyr_pool_kernel<int32_t>, dim3(blocks_for(total, 256)), dim3(256), 0, stream, src, dst, t1, t2,
+                       ntaps, total);
+  else
+    hipLaunchKernelGGL(pyr_pool_kernel<int16_t>, dim3(blocks_for(total, 256)), dim3(256), 0, stream, src, dst, t1, t2,
+                       ntaps, total);
   return hipGetLastError();
 }
 
@@ -427,9 +444,14 @@ hipError_t launch_pyr_bound(const LevelWork& L, const PyrGrid& lev, int d, const
                             const uint64_t* nodes, int64_t n, const unsigned long long* n_dev, int64_t upper,
                             double* vals, PyrPartial* partials, unsigned long long* scored, hipStream_t stream) {
   if (upper <= 0) return hipSuccess;
-  hipLaunchKernelGGL(pyr_bound_kernel, dim3(pyr_blocks(upper)), dim3(kPB), (size_t)n_used * sizeof(double2), stream,
-                     L, lev, d, scans, angles, reinterpret_cast<const double2*>(pts), n_used, step, nodes, n, n_dev,
-                     vals, partials, scored);
+  if (lev.qs == 0)
+    hipLaunchKernelGGL(pyr_bound_kernel<int32_t>, dim3(pyr_blocks(upper)), dim3(kPB), (size_t)n_used * sizeof(double2),
+                       stream, L, lev, d, scans, angles, reinterpret_cast<const double2*>(pts), n_used, step, nodes, n,
+                       n_dev, vals, partials, scored);
+  else
+    hipLaunchKernelGGL(pyr_bound_kernel<int16_t>, dim3(pyr_blocks(upper)), dim3(kPB), (size_t)n_used * sizeof(double2),
+                       stream, L, lev, d, scans, angles, reinterpret_cast<const double2*>(pts), n_used, step, nodes, n,
+                       n_dev, vals, partials, scored);
   return hipGetLastError();
 }
 
@@ -443,7 +465,7 @@ hipError_t launch_pyr_final(const PyrPartial* partials, int64_t n, bool merge, i
 int pyr_top_blocks(const LevelWork& L, int32_t nj, int32_t* ktiles, int32_t* kt, int32_t* col_blocks) {
   *ktiles = (nj + kTopKT - 1) / kTopKT;
   *kt = (nj + *ktiles - 1) / *ktiles;
-  *col_blocks = (int32_t)(((int64_t)L.n_angles * nj + kPB - 1) / kPB);
+  *col_blocks = (int32_t)(((int64_t)L.n_angles * nj + kTB - 1) / kTB);
   const int64_t b = (int64_t)L.n_scans * *col_blocks * *ktiles;
   return b > INT32_MAX ? -1 : (int)b;
 }
@@ -454,9 +476,14 @@ hipError_t launch_pyr_top_bound(const LevelWork& L, const PyrGrid& lev, int d, i
   int32_t ktiles, kt, col_blocks;
   const int blocks = pyr_top_blocks(L, nj, &ktiles, &kt, &col_blocks);
   if (blocks <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pyr_top_bound_kernel, dim3(blocks), dim3(kPB), (size_t)n_used * sizeof(double2), stream, L, lev,
-                     d, nj, ktiles, kt, col_blocks, scans, angles, reinterpret_cast<const double2*>(pts), n_used,
-                     step, nodes, vals, partials);
+  if (lev.qs == 0)
+    hipLaunchKernelGGL(pyr_top_bound_kernel<int32_t>, dim3(blocks), dim3(kTB), (size_t)n_used * sizeof(double2), stream,
+                       L, lev, d, nj, ktiles, kt, col_blocks, scans, angles, reinterpret_cast<const double2*>(pts),
+                       n_used, step, nodes, vals, partials);
+  else
+    hipLaunchKernelGGL(pyr_top_bound_kernel<int16_t>, dim3(blocks), dim3(kTB), (size_t)n_used * sizeof(double2), stream,
+                       L, lev, d, nj, ktiles, kt, col_blocks, scans, angles, reinterpret_cast<const double2*>(pts),
+                       n_used, step, nodes, vals, partials);
   return hipGetLastError();
 }
 

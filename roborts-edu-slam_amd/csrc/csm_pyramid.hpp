@@ -31,14 +31,21 @@ constexpr int kPyrMaxDepth = 10;
 // Columns are stored phase-split: x' = qx * 2^lg + ph sits at column
 // ph * q + qx (q = ceil(width / 2^lg)), so the anchors of nodes J, J+1, ...
 // (2^lg cells apart) are adjacent in memory and a wave's gathers coalesce.
-// Level 0 is the fixed-point grid itself (lg = 0, shift 0: plain rows).
+// Level 0 is the fixed-point grid itself (lg = 0, shift 0: plain rows,
+// int32). Levels d >= 1 hold int16 values ceil(max / 2^qs) (qs = kPyrQuant):
+// |fixed-point value| < 2^26 (csm_set_grid), so |max / 2^qs| <= 2^14, and
+// 2^qs * ceil(max / 2^qs) >= max keeps every bound admissible while halving
+// the bytes the node gathers pull through the caches.
+constexpr int kPyrQuant = 12;
 struct PyrGrid {
-  const int32_t* g;
+  const void* g;       // int32 (qs == 0) or int16 (qs > 0) cells
   int64_t stride;
   int32_t pitch;
   int32_t shift;
   int32_t width, height;
   int32_t lg, q;
+  int32_t qs;          // 0: exact int32 level; kPyrQuant: int16 quantised level
+  int32_t pad;
 };
 
 // Search nodes: window (20 bits) | angle (12) | J (16) | K (16).

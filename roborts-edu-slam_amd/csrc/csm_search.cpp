@@ -55,7 +55,7 @@ struct PyramidSearch::Impl {
   // pooled levels 1..kPyrMaxDepth of the current fixed-point grid
   Buf level[kPyrMaxDepth + 1];
   PyrGrid lev[kPyrMaxDepth + 1]{};
-  const int32_t* key_g = nullptr;
+  const void* key_g = nullptr;
   uint64_t key_gen = 0;
   int32_t key_sx = -1, key_sy = -1, key_grids = -1, built = 0;
   // per-depth node lists, their values and counts (counts[d]: nodes[d]'s
@@ -96,8 +96,9 @@ struct PyramidSearch::Impl {
       L.q = (L.width + L.shift - 1) >> d;
       L.pitch = ((L.q << d) + 3) & ~3;
       L.stride = (int64_t)L.pitch * L.height;
-      if ((e = level[d].ensure((size_t)L.stride * (size_t)x.n_grids * sizeof(int32_t))) != hipSuccess) return e;
-      L.g = (const int32_t*)level[d].p;
+      L.qs = kPyrQuant;
+      if ((e = level[d].ensure((size_t)L.stride * (size_t)x.n_grids * sizeof(int16_t))) != hipSuccess) return e;
+      L.g = level[d].p;
       if ((e = launch_pyr_pool(lev[d - 1], L, d, x.n_grids, x.stream)) != hipSuccess) return e;
     }
     if ((e = hipStreamSynchronize(x.stream)) != hipSuccess) return e;

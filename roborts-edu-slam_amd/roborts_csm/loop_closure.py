@@ -48,6 +48,18 @@ def world_to_map(pose_world, resolution: float, offset) -> np.ndarray:
     return np.array([s * pose_world[0] + s * offset[0], s * pose_world[1] + s * offset[1], pose_world[2]])
 
 
+def worlds_to_map(pose_world, resolution: float, offsets) -> np.ndarray:
+    """world_to_map for every submap offset at once (the same expressions,
+    elementwise: s * x + s * offset_x, with s = 1 / resolution)."""
+    s = 1.0 / resolution
+    off = np.asarray(offsets, dtype=np.float64).reshape(-1, 2)
+    out = np.empty((off.shape[0], 3))
+    out[:, 0] = s * pose_world[0] + s * off[:, 0]
+    out[:, 1] = s * pose_world[1] + s * off[:, 1]
+    out[:, 2] = pose_world[2]
+    return out
+
+
 @dataclass
 class LoopClosureResult:
     score: float
@@ -80,7 +92,7 @@ class ShardedLoopClosure:
             return LoopClosureResult(-np.inf, -1, -1, 0.0, 0.0, 0.0)
         na, ns = window_dims(param)
         n_cand = na * ns * ns
-        centers = np.stack([world_to_map(pose_world, self.resolution, o) for o in self.offsets])
+        centers = worlds_to_map(pose_world, self.resolution, self.offsets)
         if self.search == "pyramid":
             b, w, self.last_stats = self.scorer.search_windows(points_cells, param, np.arange(n_loc), centers)
             return LoopClosureResult(float(b.score), int((self.lo + w) * n_cand + b.flat_index), self.lo + w,
