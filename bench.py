@@ -250,7 +250,8 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
     if args.search == "pyramid":
         st = lc.last_stats or {}
         search = {"kind": "admissible multi-resolution branch and bound (csm_search_windows)",
-                  "depth": st.get("depth"), "nodes_per_level": st.get("nodes"),
+                  "depth": st.get("depth"), "top_level_as_beam_boxes": st.get("top_box"),
+                  "nodes_per_level": st.get("nodes"),
                   "probe_leaves": st.get("probe_leaves"),
                   "nodes_scored_per_query_rank0": (sum(st.get("nodes", [])) + st.get("probe_leaves", 0)),
                   "beam_reads_per_query_rank0": st.get("beam_reads"),
@@ -354,7 +355,8 @@ def willow_bench(args, rank, world_size, dist, torch):
     search = None
     if args.search == "pyramid":
         search = {"kind": "admissible multi-resolution branch and bound (csm_search_windows)",
-                  "depth": last.get("depth"), "nodes_per_level_last_query": last.get("nodes"),
+                  "depth": last.get("depth"), "top_level_as_beam_boxes": last.get("top_box"),
+                  "nodes_per_level_last_query": last.get("nodes"),
                   "beam_reads_last_query": last.get("beam_reads"),
                   "value_note": "value counts every candidate of the window as resolved (the answer equals "
                                 "the exhaustive argmax, tests/test_gpu_search.py)"}

@@ -331,7 +331,9 @@ typedef struct csm_search_options {
                               < 0: automatic (the smallest with ceil(n_space / 2^d) <= 32) */
   int32_t probe_min_nodes; /* below the top, a level of at least this many nodes first
                               scores its best node's leaves exactly (0: 4096) */
-  int64_t node_capacity;   /* nodes per level list (0: 2^22); larger levels are split */
+  int64_t node_capacity;   /* nodes per level list (0: 2^24); larger levels are split */
+  int32_t top_kernel;      /* 0: the top level as beam boxes when eligible, 1: per-node gathers */
+  int32_t reserved;
 } csm_search_options;
 
 typedef struct csm_search_stats {
@@ -343,6 +345,8 @@ typedef struct csm_search_stats {
   int64_t beam_reads;      /* grid reads in all: (sum of nodes + probe_leaves) * B     */
   double build_ms;         /* pooled levels built by this call (0: cached)            */
   int64_t syncs;           /* node counts the host read back (level passes it waited on) */
+  int32_t top_box;         /* 1: the top level ran as beam boxes                       */
+  int32_t reserved;
 } csm_search_stats;
 
 int csm_search_windows(csm_ctx* ctx, const double* points_xy, int32_t n_points,

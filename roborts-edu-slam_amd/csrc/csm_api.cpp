@@ -2651,6 +2651,7 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
     while (((D.n_space + (1 << depth) - 1) >> depth) > 32 && depth < csm::kPyrMaxDepth) ++depth;
   }
   depth = std::min(depth, csm::kPyrMaxDepth);
+  bool box_ok = true;
   for (const WindowPlan& W : plans) {
     if (!ok) break;
     const double far = (double)(D.n_space - 1) * f;
@@ -2658,6 +2659,8 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
                                  std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
     const double R = c->pts_maxabs * (1.0 + 1e-9) + span + 2.0 + (double)(1 << depth);
     if (!(R < std::ldexp(1.0, 29))) ok = false;
+    // the top kernel's box test: every |t| < 2^24 cells (csm_pyramid.hip)
+    if (!(R < std::ldexp(1.0, 23))) box_ok = false;
   }
   BestPartial b{};
   if (!ok) {
@@ -2719,6 +2722,8 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
     in.n_used = W0.n_used;
     in.step = W0.step;
     in.depth = depth;
+    in.top_mode = options ? options->top_kernel : 0;
+    in.box_ok = box_ok ? 1 : 0;
     c->pyramid.configure(options ? options->node_capacity : 0, options ? options->probe_min_nodes : 0);
     csm::PyrStats ps;
     std::string what;
@@ -2740,6 +2745,7 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
     S.beam_reads = scored * W0.n_used;
     S.build_ms = ps.build_ms;
     S.syncs = ps.syncs;
+    S.top_box = ps.top_box;
     // one grid read per beam per scored node (the pooled levels included)
     if (c->profiling) c->account("pyramid_search", ms, (double)S.beam_reads * 4.0, (double)S.candidates);
   }

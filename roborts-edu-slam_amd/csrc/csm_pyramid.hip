@@ -298,6 +298,220 @@ __global__ __launch_bounds__(kTB) void pyr_top_bound_kernel(LevelWork L, PyrGrid
   block_best<kTB>(bv, bf, bn, partials + bid);
 }
 
+// The top level as beam boxes (csm_box.hip's argument with node steps of 2^d
+// cells). With step one cell the anchor column of node J is
+// trunc(fl(fl(lx + fl(x0 + J 2^d)) + 0.5)); whenever the beam passes the box
+// test (t_0 >= 0, fraction at least kTopBoxMargin from an integer, |t| < 2^24
+// cells: the host's box_ok) it equals trunc(t_0) + J 2^d for every J, rows
+// likewise. In the phase-split layout the anchors of J = 0, 1, ... are then
+// adjacent cells of phase (trunc(t_0) + shift) mod 2^d, so a beam's nodes of
+// one row K are nj consecutive int16 cells of the box copy (tb: level d, each
+// phase's columns padded with zeros past the grid, 2^d nj zero rows below
+// it) and one row piece per lane covers all nj x nj nodes in NL
+// buffer_load_dwordx4 per beam, instead of nj^2 / 64 dword gathers. Rejected
+// beams are summed node by node with pyr_top_bound_kernel's expressions
+// afterwards; nodes, bounds and the best per wave are written exactly as that
+// kernel writes them.
+//
+// Loads are dword-aligned: lane (K, c) loads the 16 bytes at element
+// c0a + 8c (c0 = the row's node 0, c0a = c0 rounded down to even), NP =
+// ceil((nj + 1) / 8) pieces per row. Element e then belongs to node
+// e - (c0 - c0a): the beam's parity (uniform) picks the accumulator set, even
+// (node 8c + i) or odd (node 8c + i - 1, folded across pieces through LDS at
+// the end). Measured (config 3, d = 4, nj = 21): 1.58 ms per query against
+// 2.9 ms for the gathers and 1.98 ms for an int32 copy (twice the bytes per
+// beam); L2-bound (~15 TB/s of 64-byte requests, 96 % hits).
+constexpr double kTopBoxMargin = 0x1p-20;
+
+template <int NP, int NL>
+__global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb, int d, int32_t nj,
+                                                          const ScanWork* __restrict__ scans,
+                                                          const AngleEntry* __restrict__ angles,
+                                                          const double2* __restrict__ pts, int32_t n_used,
+                                                          int32_t step, uint64_t* __restrict__ nodes,
+                                                          double* __restrict__ vals,
+                                                          PyrPartial* __restrict__ partials) {
+  constexpr int GB = NL == 1 ? 8 : 4;  // beams whose loads are issued together
+  __shared__ int32_t odd_sum[32][8 * 5 + 8];
+  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int w = bid / L.n_angles;
+  const int a = bid - w * L.n_angles;
+  const ScanWork S = scans[w];
+  const AngleEntry ae = angles[S.angle_off + a];
+  const int lane = threadIdx.x;
+  const int pitch2 = tb.pitch * 2;  // bytes per row
+  const int sh = tb.shift, lg = tb.lg, pm = (1 << lg) - 1, W = tb.width, H = tb.height, qc = tb.q;
+  const int sx = W - sh, sy = H - sh;
+  const int zero_el = H * tb.pitch;  // element offset of the zero rows (even: pitch is)
+  bool act[NL];
+  int Ks[NL], cs[NL], voff[NL];
+#pragma unroll
+  for (int s = 0; s < NL; ++s) {
+    const int i = s * 64 + lane;
+    act[s] = i < nj * NP;
+    Ks[s] = act[s] ? i / NP : 0;
+    cs[s] = act[s] ? i - Ks[s] * NP : 0;
+    voff[s] = ((Ks[s] << d) * pitch2) + 16 * cs[s];
+  }
+  const int16_t* g = (const int16_t*)tb.g + (int64_t)S.grid_index * tb.stride;
+  const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)g);
+  const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)g >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)ghi << 32) | glo), (short)0, (int)(tb.stride * 2), 0x00020000);
+  const double x_0 = S.x0 + 0 * L.step_cells;  // :569, J = 0
+  const double y_0 = S.y0 + 0 * L.step_cells;  // :572, K = 0
+  // element offset of the beam's node (0, 0) (zero_el: reads zeros)
+  auto test = [&](const double2 p, double& lx, double& ly, int& el) -> bool {
+    lx = ae.cosine * p.x - ae.sine * p.y;  // :179
+    ly = ae.sine * p.x + ae.cosine * p.y;  // :180
+    const double tx = (lx + x_0) + 0.5;
+    const double ty = (ly + y_0) + 0.5;
+    const double fx = tx - floor(tx), fy = ty - floor(ty);
+    const bool clean = tx >= 0.0 && ty >= 0.0 && fx >= kTopBoxMargin && fx <= 1.0 - kTopBoxMargin &&
+                       fy >= kTopBoxMargin && fy <= 1.0 - kTopBoxMargin;
+    const int ix0 = clean ? (int)tx : 0, iy0 = clean ? (int)ty : 0;
+    const int xs = ix0 + sh, ys = iy0 + sh;
+    el = (clean && ix0 < sx && iy0 < sy) ? ys * tb.pitch + (xs & pm) * qc + (xs >> lg) : zero_el;
+    return clean;
+  };
+  typedef int32_t v4i __attribute__((ext_vector_type(4)));
+  int32_t ae_[NL][8], ao_[NL][8];  // even / odd parity sums (|sum| <= 4096 * 2^14)
+#pragma unroll
+  for (int s = 0; s < NL; ++s)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) ae_[s][t] = ao_[s][t] = 0;
+  auto add8 = [&](int32_t (&acc)[8], const v4i v) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc[2 * t] += (int32_t)((uint32_t)v[t] << 16) >> 16;  // low half: element 2t
+      acc[2 * t + 1] += v[t] >> 16;                // high half: element 2t + 1
+    }
+  };
+  uint64_t slow = 0;
+  double2 pn = pts[(int64_t)min(lane, n_used - 1) * step];
+  for (int cb = 0; cb < n_used; cb += 64) {
+    const double2 p = pn;
+    pn = pts[(int64_t)min(cb + 64 + lane, n_used - 1) * step];
+    double lx, ly;
+    int el;
+    const bool clean = test(p, lx, ly, el);
+    const bool live = cb + lane < n_used;
+    if (!live) el = zero_el;
+    slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean) != 0) << min(cb >> 6, 63);
+    const int nb = min(64, n_used - cb);
+    for (int r = 0; r < nb; r += GB) {  // beams past nb read the zero rows
+      int so[GB];
+#pragma unroll
+      for (int u = 0; u < GB; ++u) so[u] = __builtin_amdgcn_readlane(el, r + u);
+      v4i buf[GB][NL];
+#pragma unroll
+      for (int u = 0; u < GB; ++u)
+#pragma unroll
+        for (int s = 0; s < NL; ++s)
+          buf[u][s] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff[s], (so[u] & ~1) * 2, 0);
+#pragma unroll
+      for (int u = 0; u < GB; ++u) {
+        if (so[u] & 1) {  // uniform
+#pragma unroll
+          for (int s = 0; s < NL; ++s) add8(ao_[s], buf[u][s]);
+        } else {
+#pragma unroll
+          for (int s = 0; s < NL; ++s) add8(ae_[s], buf[u][s]);
+        }
+      }
+    }
+  }
+  // odd sums to their nodes: element 8c + t of row K is node 8c + t - 1
+#pragma unroll
+  for (int s = 0; s < NL; ++s)
+    if (act[s])
+#pragma unroll
+      for (int t = 0; t < 8; ++t) odd_sum[Ks[s]][8 * cs[s] + t] = ao_[s][t];
+  __syncthreads();
+  int32_t acc[NL][8];
+#pragma unroll
+  for (int s = 0; s < NL; ++s)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int J = 8 * cs[s] + t;
+      acc[s][t] = ae_[s][t] + ((act[s] && J + 1 < 8 * NP) ? odd_sum[Ks[s]][J + 1] : 0);
+    }
+  // rejected beams, node by node (pyr_top_bound_kernel's expressions)
+  for (uint64_t m = slow; m != 0; m &= m - 1) {
+    const int c0 = (int)__builtin_ctzll(m);
+    const int c_end = c0 == 63 ? (n_used + 63) / 64 : c0 + 1;
+    for (int c = c0; c < c_end; ++c) {
+      const int cb = c * 64;
+      double lx, ly;
+      int el;
+      const bool clean = test(pts[(int64_t)min(cb + lane, n_used - 1) * step], lx, ly, el);
+      for (uint64_t rej = __builtin_amdgcn_ballot_w64(cb + lane < n_used && !clean); rej != 0; rej &= rej - 1) {
+        const int l = (int)__builtin_ctzll(rej);  // uniform: one beam for the whole wave
+        const double bx = dev::bcast_lane(lx, l);
+        const double by = dev::bcast_lane(ly, l);
+#pragma unroll
+        for (int s = 0; s < NL; ++s) {
+          const int gy = (int)((by + (S.y0 + (Ks[s] << d) * L.step_cells)) + 0.5) + sh;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int J = 8 * cs[s] + t;
+            const int gx = (int)((bx + (S.x0 + (J << d) * L.step_cells)) + 0.5) + sh;
+            const bool in = act[s] && J < nj && (unsigned)gx < (unsigned)W && (unsigned)gy < (unsigned)H;
+            const int32_t v = g[in ? (int64_t)gy * tb.pitch + (int64_t)(gx & pm) * qc + (gx >> lg) : 0];
+            acc[s][t] += in ? v : 0;
+          }
+        }
+      }
+    }
+  }
+  double bv = -1.0e300;
+  int64_t bf = INT64_MAX;
+  uint64_t bn = kPyrNoNode;
+  const int64_t wbase = ((int64_t)w * L.n_angles + a) * nj;
+#pragma unroll
+  for (int s = 0; s < NL; ++s) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int J = 8 * cs[s] + t, K = Ks[s];
+      if (act[s] && J < nj) {
+        const double acc_d = (double)(((int64_t)acc[s][t] << tb.qs) + (int64_t)n_used * L.outside_i) * L.int_scale;
+        const double raw = acc_d / S.divisor;
+        const double v = (L.use_penalty && raw < 0.0) ? raw * 0.45 : raw;
+        const int64_t idx = (wbase + K) * nj + J;
+        const uint64_t nd = pyr_node((uint32_t)w, (uint32_t)a, (uint32_t)J, (uint32_t)K);
+        nodes[idx] = nd;
+        vals[idx] = v;
+        const int64_t gflat = (int64_t)w * L.n_cand + ((int64_t)a * L.n_space + (J << d)) * L.n_space + (K << d);
+        if (better(v, gflat, bv, bf)) {
+          bv = v;
+          bf = gflat;
+          bn = nd;
+        }
+      }
+    }
+  }
+  block_best<64>(bv, bf, bn, partials + bid);
+}
+
+// tb (padded phase-split int16) from level d: every stored cell written,
+// zero outside the level.
+__global__ __launch_bounds__(256) void pyr_widen_kernel(PyrGrid src, PyrGrid dst, int64_t total) {
+  const int16_t* __restrict__ sg = (const int16_t*)src.g;
+  int16_t* __restrict__ dg = (int16_t*)const_cast<void*>(dst.g);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t gidx = i / dst.stride;
+    const int64_t r = i - gidx * dst.stride;
+    const int ys = (int)(r / dst.pitch), c = (int)(r - (int64_t)ys * dst.pitch);
+    const int ph = c / dst.q, qx = c - ph * dst.q;
+    const int xs = (qx << dst.lg) + ph;
+    int16_t v = 0;
+    if (ph < (1 << dst.lg) && xs < dst.width && ys < dst.height)
+      v = sg[gidx * src.stride + (int64_t)ys * src.pitch + pyr_col(src, xs)];
+    dg[i] = v;
+  }
+}
+
 // merge (one block): fold the best partial into the incumbent. Otherwise
 // block i picks the best of the i-th of gridDim.x equal segments of the
 // partials (different windows / angle ranges: diverse probe roots) when it
@@ -485,6 +699,41 @@ hipError_t launch_pyr_top_bound(const LevelWork& L, const PyrGrid& lev, int d, i
                        L, lev, d, nj, ktiles, kt, col_blocks, scans, angles, reinterpret_cast<const double2*>(pts),
                        n_used, step, nodes, vals, partials);
   return hipGetLastError();
+}
+
+int pyr_topbox_pieces(int32_t nj) { return (nj >= 1 && nj <= 32) ? (nj + 8) / 8 : 0; }
+
+hipError_t launch_pyr_widen(const PyrGrid& src, const PyrGrid& dst, int32_t n_grids, hipStream_t stream) {
+  if (src.qs == 0 || src.lg != dst.lg || dst.qs != src.qs) return hipErrorInvalidValue;
+  const int64_t total = dst.stride * n_grids;
+  hipLaunchKernelGGL(pyr_widen_kernel, dim3(blocks_for(total, 256)), dim3(256), 0, stream, src, dst, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32_t nj, const ScanWork* scans,
+                             const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
+                             uint64_t* nodes, double* vals, PyrPartial* partials, hipStream_t stream) {
+  const int np = pyr_topbox_pieces(nj);
+  const int64_t blocks = (int64_t)L.n_scans * L.n_angles;
+  if (np == 0 || blocks <= 0 || blocks > INT32_MAX || n_used < 1 || n_used > 4096 || tb.qs == 0 ||
+      tb.stride * 2 >= INT32_MAX || tb.pitch % 2 != 0)
+    return hipErrorInvalidValue;
+  const int nl = (nj * np + 63) / 64;
+  const double2* p = reinterpret_cast<const double2*>(pts);
+#define CSM_TOPBOX(NP, NL)                                                                                       \
+  if (np == NP && nl == NL) {                                                                                  \
+    hipLaunchKernelGGL((pyr_topbox_kernel<NP, NL>), dim3((unsigned)blocks), dim3(64), 0, stream, L, tb, d, nj, \
+                       scans, angles, p, n_used, step, nodes, vals, partials);                                  \
+    return hipGetLastError();                                                                                   \
+  }
+  CSM_TOPBOX(1, 1)
+  CSM_TOPBOX(2, 1)
+  CSM_TOPBOX(3, 1)
+  CSM_TOPBOX(3, 2)
+  CSM_TOPBOX(4, 2)
+  CSM_TOPBOX(5, 3)
+#undef CSM_TOPBOX
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_pyr_probe(int d, int n_probe, const uint64_t* probe, uint64_t* out, hipStream_t stream) {

@@ -86,6 +86,17 @@ int pyr_top_blocks(const LevelWork& L, int32_t nj, int32_t* ktiles, int32_t* kt,
 hipError_t launch_pyr_top_bound(const LevelWork& L, const PyrGrid& lev, int d, int32_t nj, const ScanWork* scans,
                                 const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
                                 uint64_t* nodes, double* vals, PyrPartial* partials, hipStream_t stream);
+// The top level as beam boxes (pyr_topbox_kernel): tb is level d in a padded
+// phase-split int16 layout (8 * pyr_topbox_pieces(nj) zero cells past each
+// phase's columns, 2^d * nj zero rows below); the host guarantees |t| < 2^24
+// cells (the box test's rounding argument). Same outputs as
+// launch_pyr_top_bound, one best per (window, angle) wave (n_scans *
+// n_angles partials).
+int pyr_topbox_pieces(int32_t nj);  // 16-byte pieces per node row (0: unsupported nj)
+hipError_t launch_pyr_widen(const PyrGrid& src, const PyrGrid& dst, int32_t n_grids, hipStream_t stream);
+hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32_t nj, const ScanWork* scans,
+                             const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
+                             uint64_t* nodes, double* vals, PyrPartial* partials, hipStream_t stream);
 // Reduce n partials. merge = true: fold the best into the incumbent *inc
 // (better score, or equal with a lower index). merge = false: probe[i] =
 // the best node of the i-th of n_probe equal segments of the partials, if it
@@ -107,6 +118,7 @@ struct PyrStats {
   int64_t probe_leaves = 0;              // candidates scored by incumbent probes
   int64_t slices = 0;                    // expand launches
   int64_t syncs = 0;                     // node counts read back by the host
+  int32_t top_box = 0;                   // 1: the top level ran as beam boxes
   double build_ms = 0.0;                 // pooled levels built (0 when cached)
 };
 
@@ -121,6 +133,8 @@ struct PyrInputs {
   const double* pts;        // device, the one scan's points
   int32_t n_used, step;
   int32_t depth;            // top depth
+  int32_t top_mode;         // 0: beam boxes when eligible, 1: per-node gathers
+  int32_t box_ok;           // every window's |t| < 2^24 cells (the box test's bound)
 };
 
 class PyramidSearch {

@@ -58,6 +58,10 @@ struct PyramidSearch::Impl {
   const void* key_g = nullptr;
   uint64_t key_gen = 0;
   int32_t key_sx = -1, key_sy = -1, key_grids = -1, built = 0;
+  // the top level's box copy (pyr_topbox_kernel): depth and pieces it was built for
+  Buf box;
+  PyrGrid boxg{};
+  int32_t box_depth = -1, box_npc = 0;
   // per-depth node lists, their values and counts (counts[d]: nodes[d]'s
   // length as the expand that filled it left it)
   Buf nodes[kPyrMaxDepth + 1], vals[kPyrMaxDepth + 1];
@@ -77,6 +81,7 @@ struct PyramidSearch::Impl {
     const int32_t sx = x.level0.width, sy = x.level0.height;
     if (key_g != x.level0.g || key_gen != x.grid_gen || key_sx != sx || key_sy != sy || key_grids != x.n_grids) {
       built = 0;
+      box_depth = -1;
       key_g = x.level0.g;
       key_gen = x.grid_gen;
       key_sx = sx;
@@ -104,6 +109,32 @@ struct PyramidSearch::Impl {
     if ((e = hipStreamSynchronize(x.stream)) != hipSuccess) return e;
     built = x.depth;
     if (st) st->build_ms = now_ms() - t0;
+    return hipSuccess;
+  }
+
+  // Level D copied into the box layout (after build(x)): columns of each
+  // phase padded by 8 * npc zeros, 2^D * nj zero rows below.
+  hipError_t build_box(const PyrInputs& x, int D, int32_t nj, int npc) {
+    if (box_depth == D && box_npc == npc &&
+        boxg.height + (nj << D) <= (int32_t)(boxg.stride / boxg.pitch))
+      return hipSuccess;
+    const PyrGrid& src = lev[D];
+    PyrGrid b = src;
+    b.q = src.q + 8 * npc;
+    b.pitch = b.q << D;
+    const int64_t rows = (int64_t)src.height + ((int64_t)nj << D);
+    b.stride = (int64_t)b.pitch * rows;
+    if (b.stride * 2 >= INT32_MAX) return hipErrorInvalidValue;
+    hipError_t e;
+    const double t0 = now_ms();
+    if ((e = box.ensure((size_t)b.stride * (size_t)x.n_grids * sizeof(int16_t))) != hipSuccess) return e;
+    b.g = box.p;
+    if ((e = launch_pyr_widen(src, b, x.n_grids, x.stream)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(x.stream)) != hipSuccess) return e;
+    boxg = b;
+    box_depth = D;
+    box_npc = npc;
+    if (st) st->build_ms += now_ms() - t0;
     return hipSuccess;
   }
 
@@ -260,7 +291,29 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
   const int top_blocks = pyr_top_blocks(x.L, (int32_t)nj, &ktiles, &kt, &col_blocks);
   const int D = x.depth;
   int64_t top_scored = 0;
-  if (D > 0 && top_blocks > 0 && n_top <= ((int64_t)1 << 28)) {
+  // the top level as beam boxes: one-cell steps are given; the box test
+  // needs |t| < 2^24 (box_ok), nj <= 32, a launch of n_scans * n_angles waves
+  const int npc = pyr_topbox_pieces((int32_t)nj);
+  const int64_t box_blocks = (int64_t)x.L.n_scans * x.L.n_angles;
+  const bool use_box = D > 0 && x.top_mode == 0 && x.box_ok && npc > 0 && box_blocks <= INT32_MAX &&
+                       n_top <= ((int64_t)1 << 28) && x.n_used >= 1 && x.n_used <= 4096;
+  if (use_box && (e = I.build_box(x, D, (int32_t)nj, npc)) == hipSuccess) {
+    if ((e = I.nodes[D].ensure((size_t)n_top * sizeof(uint64_t))) != hipSuccess ||
+        (e = I.vals[D].ensure((size_t)n_top * sizeof(double))) != hipSuccess)
+      return fail(e, "pyramid top level");
+    if ((e = I.partials.ensure((size_t)std::max<int64_t>(box_blocks, pyr_blocks(INT64_MAX / 2)) *
+                               sizeof(PyrPartial))) != hipSuccess)
+      return fail(e, "pyramid partials");
+    if ((e = launch_pyr_topbox(x.L, I.boxg, D, (int32_t)nj, x.scans, x.angles, x.pts, x.n_used, x.step,
+                               (uint64_t*)I.nodes[D].p, (double*)I.vals[D].p, (PyrPartial*)I.partials.p,
+                               x.stream)) != hipSuccess)
+      return fail(e, "pyr_topbox_kernel");
+    top_scored = n_top;
+    I.st->top_box = 1;
+    if ((e = I.descend(D, n_top, n_top, true, box_blocks)) != hipSuccess) return fail(e, "pyramid level pass");
+  } else if (use_box && e != hipErrorInvalidValue) {
+    return fail(e, "pyramid box level");
+  } else if (D > 0 && top_blocks > 0 && n_top <= ((int64_t)1 << 28)) {
     // the whole top level in one launch (column layout), then descend
     if ((e = I.nodes[D].ensure((size_t)n_top * sizeof(uint64_t))) != hipSuccess ||
         (e = I.vals[D].ensure((size_t)n_top * sizeof(double))) != hipSuccess)

@@ -389,7 +389,7 @@ class Context:
 
 
     def search_windows(self, points_cells, param, grid_index, centers_map, max_depth: int = -1,
-                       probe_min_nodes: int = 0, node_capacity: int = 0):
+                       probe_min_nodes: int = 0, node_capacity: int = 0, top_kernel: int = 0):
         """Best candidate of one scan over many windows by the admissible
         multi-resolution search (csm_search_windows) -> (CsmBest, window, stats
         dict). Same answer as reducing best_windows: max score, lowest
@@ -399,7 +399,7 @@ class Context:
         gi = np.ascontiguousarray(grid_index, dtype=np.int32)
         ctr = np.ascontiguousarray(centers_map, dtype=np.float64).reshape(-1, 3)
         assert gi.size == ctr.shape[0]
-        opt = _abi.CsmSearchOptions(int(max_depth), int(probe_min_nodes), int(node_capacity))
+        opt = _abi.CsmSearchOptions(int(max_depth), int(probe_min_nodes), int(node_capacity), int(top_kernel), 0)
         b = CsmBest()
         w = C.c_int32(-1)
         st = _abi.CsmSearchStats()
@@ -408,7 +408,7 @@ class Context:
                                             C.byref(b), C.byref(w), C.byref(st)))
         stats = dict(depth=st.depth, exhaustive=bool(st.exhaustive), candidates=st.candidates,
                      nodes=list(st.nodes), probe_leaves=st.probe_leaves, beam_reads=st.beam_reads,
-                     build_ms=st.build_ms, syncs=st.syncs)
+                     build_ms=st.build_ms, syncs=st.syncs, top_box=bool(st.top_box))
         return b, int(w.value), stats
 
 

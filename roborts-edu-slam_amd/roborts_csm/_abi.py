@@ -96,6 +96,8 @@ class CsmSearchOptions(C.Structure):
         ("max_depth", C.c_int32),
         ("probe_min_nodes", C.c_int32),
         ("node_capacity", C.c_int64),
+        ("top_kernel", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 
@@ -109,6 +111,8 @@ class CsmSearchStats(C.Structure):
         ("beam_reads", C.c_int64),
         ("build_ms", C.c_double),
         ("syncs", C.c_int64),
+        ("top_box", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 

@@ -129,7 +129,36 @@ def test_search_negative_fixed_point_and_off_grid(f1):
             c.set_outside_value(0.75)
             c.set_grid_stack(g, res, version=1)
             centers = np.array([[-20.0, 10.0, 0.3], [sx + 15.0, sy - 5.0, -1.0]])
-            _check_same(c, f1["points"], p, np.arange(2), centers, max_depth=5)
+            _, _, s1 = _check_same(c, f1["points"], p, np.arange(2), centers, max_depth=5)
+            _, _, s2 = _check_same(c, f1["points"], p, np.arange(2), centers, max_depth=5, top_kernel=1)
+            assert s1["top_box"] and not s2["top_box"] and s1["nodes"] == s2["nodes"]
+
+
+@pytest.mark.parametrize("size,depth,penalty", [(2.0, 1, False), (2.0, 2, True), (2.0, 3, False), (2.0, 6, True),
+                                                (2.35, 1, True), (2.5, 1, False), (2.75, 1, True), (3.15, 1, False),
+                                                (0.8, 1, True), (1.95, 1, False), (1.5, 1, True), (0.3, 1, False),
+                                                (2.2, 1, True)])
+def test_top_boxes_equal_gathers(f1, stack5, size, depth, penalty):
+    """The top level as beam boxes (pyr_topbox_kernel, every (pieces, loads)
+    instantiation: nj = 21, 11, 6, 1, 24, 26, 28, 32, 9, 20, 16, 4, 23) writes the same
+    bounds as the per-node gather kernel: the searches visit the same nodes
+    at every level and return the exhaustive argmax."""
+    import roborts_csm
+    from roborts_csm.loop_closure import world_to_map
+    from roborts_csm.params import CorrelationScanMatchParam
+    res = float(f1["resolution"])
+    p = CorrelationScanMatchParam(size, 0.05, 0.6, 0.0349, 0.5, 100, 0, penalty, 0)
+    with roborts_csm.Context(0) as c:
+        c.set_grid_stack(stack5, res, version=3)
+        centers = np.stack([world_to_map(f1["init_pose"], res, f1["offset"])] * stack5.shape[0])
+        centers[1, :2] += (17.0, -9.0)
+        centers[3, :2] = (-3.0, 2.5)  # hanging off the grid's low corner
+        gi = np.arange(stack5.shape[0])
+        b1, w1, s1 = _check_same(c, f1["points"], p, gi, centers, max_depth=depth)
+        b2, w2, s2 = c.search_windows(f1["points"], p, gi, centers, max_depth=depth, top_kernel=1)
+        assert s1["top_box"] and not s2["top_box"]
+        assert (w1, b1.score, b1.flat_index) == (w2, b2.score, b2.flat_index)
+        assert s1["nodes"] == s2["nodes"] and s1["probe_leaves"] == s2["probe_leaves"]
 
 
 def test_search_non_unit_step_is_exhaustive(f1, stack5):
