@@ -417,6 +417,85 @@ def willow_bench(args, rank, world_size, dist, torch):
     }
 
 
+class _AttachedBackEnd:
+    """The back end beside the front end (SlamProcessor::BackEndProcessThread,
+    slam_processor.cpp:384-426): a host thread fed the kept scans. Per new
+    vertex it adds the scan (AddRangeData) and runs the vertex's
+    ScanMatchInterface jobs (slam_processor.cpp:250-326) in one batch: the
+    near-chain link against the previous 10 kept scans (LinkNearChains,
+    range_scan_pose_graph.cpp:120-167) and, once enough scans are kept, a
+    loop-closure candidate against a chain 40-50 vertices back (TryCloseLoop,
+    :299-355). Its own device context and stream on the same GPU; ctypes
+    releases the GIL, so the front end keeps running. The pose-graph solve
+    itself is out of scope."""
+
+    def __init__(self, device: int):
+        import queue
+        import threading
+        from roborts_csm.backend import BackEndParam, ScanMatchService
+        self.svc = ScanMatchService(BackEndParam(), device=device)
+        self.q = queue.Queue()
+        self.kept = []
+        self.jobs = 0
+        self.lags = []
+        self.busy = 0.0
+        self.err = None
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    def submit(self, points_m, pose):
+        self.q.put((np.array(points_m, copy=True), np.array(pose, dtype=np.float64), time.perf_counter()))
+
+    def _run(self):
+        while True:
+            item = self.q.get()
+            if item is None:
+                self.q.task_done()
+                return
+            try:
+                pts, pose, t_enq = item
+                t = time.perf_counter()
+                rid = self.svc.AddRangeData(pts, pose)
+                self.kept.append(rid)
+                queries, chains, inits = [], [], []
+                if len(self.kept) >= 11:
+                    queries.append(pts), chains.append(self.kept[-11:-1]), inits.append(pose)
+                if len(self.kept) >= 51:
+                    queries.append(pts), chains.append(self.kept[-51:-41]), inits.append(pose)
+                if queries:
+                    self.svc.scan_match_jobs(queries, chains, inits, pose, None)
+                    self.jobs += len(queries)
+                now = time.perf_counter()
+                self.busy += now - t
+                self.lags.append(now - t_enq)
+            except Exception as e:  # reported, not raised in the thread
+                self.err = repr(e)
+            self.q.task_done()
+
+    def drain(self):
+        self.q.join()
+
+    def reset_stats(self):
+        self.drain()
+        self.jobs, self.lags, self.busy = 0, [], 0.0
+
+    def finish(self, fe_elapsed: float) -> dict:
+        self.drain()
+        self.q.put(None)
+        self.th.join()
+        lag = np.array(self.lags) * 1e3 if self.lags else np.zeros(1)
+        out = {"vertices": len(self.lags), "jobs": self.jobs, "kept_total": len(self.kept),
+               "busy_fraction_of_stream": self.busy / fe_elapsed if fe_elapsed > 0 else None,
+               "vertex_lag_ms": {"p50": float(np.median(lag)), "max": float(lag.max())},
+               "what": "per kept scan: AddRangeData + near-chain job (+ a loop-closure job 40-50 vertices back) "
+                       "on a second device context, concurrently with the front end; no PubMap check "
+                       "(pub_map=None), no pose-graph solve"}
+        if self.err:
+            out["error"] = self.err
+        self.svc.close()
+        return out
+
+
 def online_bench(args, rank, world_size, dist, torch):
     """Config 5: a 40 Hz-style 1081-beam scan stream through the
     device-resident front-end (include/csm_frontend.h: SlamProcessor::process
@@ -430,8 +509,13 @@ def online_bench(args, rank, world_size, dist, torch):
     world = worlds.make_world(2000, 2000, 0.05, seed=20261015)
     stream = worlds.make_scan_stream(world, n, seed=77 + rank)
     fe = SlamFrontEnd(FrontEndParam(), device=int(os.environ.get("LOCAL_RANK", "0")))
+    be = _AttachedBackEnd(int(os.environ.get("LOCAL_RANK", "0"))) if args.attach_backend else None
     for k in range(args.warmup):
-        fe.process(stream.points_m[k], stream.odom_poses[k])
+        r = fe.process(stream.points_m[k], stream.odom_poses[k])
+        if be is not None and r.map_updated:
+            be.submit(stream.points_m[k], r.pose)
+    if be is not None:
+        be.drain()
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     if torch.cuda.is_available():
         torch.cuda.synchronize()
@@ -440,11 +524,22 @@ def online_bench(args, rank, world_size, dist, torch):
     lat = []
     err = []
     t0 = time.perf_counter()
+    if be is not None:
+        be.reset_stats()
+    period = 1.0 / args.rate_hz if args.rate_hz > 0 else 0.0
     for k in range(args.warmup, n):
+        if period:  # paced stream: scan k arrives at t0 + (k - warmup) * period
+            wait = t0 + (k - args.warmup) * period - time.perf_counter()
+            if wait > 0:
+                time.sleep(wait)
         t = time.perf_counter()
         r = fe.process(stream.points_m[k], stream.odom_poses[k])
+        if be is not None and r.map_updated:  # a kept scan: a new vertex for the back end
+            be.submit(stream.points_m[k], r.pose)
         lat.append(time.perf_counter() - t)
         err.append(r.pose)
+    fe_elapsed = time.perf_counter() - t0
+    backend = be.finish(fe_elapsed) if be is not None else None
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     if dist is not None:
@@ -508,7 +603,9 @@ def online_bench(args, rank, world_size, dist, torch):
                    "latency_ms": {"mean": float(lat_ms.mean()), "p50": float(np.median(lat_ms)),
                                   "p99": float(np.percentile(lat_ms, 99)), "max": float(lat_ms.max())},
                    "rate_40hz_headroom": float(world_size * args.steps / elapsed / 40.0),
+                   "paced_hz": args.rate_hz or None,
                    "median_pose_error_m": float(np.median(perr)), "max_pose_error_m": float(perr.max()),
+                   "backend_attached": backend,
                    "correct_pose_and_map": {"kept_scans": int(kept.shape[0]), "ms": correct_ms,
                                             "what": "CorrectPoseAndMap: all kept poses corrected, PubMap + coarse + "
                                                     "fine rebuilt from every kept scan on the device"}},
@@ -720,6 +817,10 @@ def main():
                     help="config2: the headline front-end batch; loop_closure: config 3; willow: config 4; "
                          "online: config 5 (steps = scans); backend: f2 pose-graph jobs")
     ap.add_argument("--jobs", type=int, default=16, help="backend: ScanMatchInterface jobs per step")
+    ap.add_argument("--rate-hz", type=float, default=0.0,
+                    help="online: pace the scan stream (40 = the Hokuyo's rate; 0 = as fast as possible)")
+    ap.add_argument("--attach-backend", action="store_true",
+                    help="online: run the back end's per-vertex jobs in a thread beside the front end (config 5)")
     ap.add_argument("--window-m", type=float, default=20.0, help="willow: window edge (m)")
     ap.add_argument("--submaps", type=int, default=512, help="loop_closure: submaps in total")
     ap.add_argument("--search", choices=["pyramid", "exhaustive"], default="pyramid",
