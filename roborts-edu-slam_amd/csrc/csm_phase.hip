@@ -278,7 +278,10 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
             const uint32_t addr = cact ? esum_b + (uint32_t)(e_prev * ECELLS * 4 + lane_cell) : dummy_b;
             __attribute__((address_space(3))) int32_t* dst = (__attribute__((address_space(3))) int32_t*)(uintptr_t)addr;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) __hip_atomic_fetch_add(dst + t, part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            for (int t = 0; t < 4; ++t) {
+              __hip_atomic_fetch_add(dst + t, part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              part[t] = 0;  // inside the uniform branch: no per-group selects
+            }
           }
 #else
           // lanes past the slots always flush into their dummy cells
@@ -286,9 +289,9 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
           __attribute__((address_space(3))) int32_t* dst = (__attribute__((address_space(3))) int32_t*)(uintptr_t)addr;
 #pragma unroll
           for (int t = 0; t < 4; ++t) __hip_atomic_fetch_add(dst + t, part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
 #pragma unroll
           for (int t = 0; t < 4; ++t) part[t] = nb ? 0 : part[t];
+#endif
           e_prev = ej;
           v4i v = buf[j];
           asm volatile("" : "+v"(v));  // consume group g here, in order
