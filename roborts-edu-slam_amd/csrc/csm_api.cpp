@@ -2724,6 +2724,9 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
     in.depth = depth;
     in.top_mode = options ? options->top_kernel : 0;
     in.box_ok = box_ok ? 1 : 0;
+    in.one_scan = 1;  // the windows share the one scan: check what the implicit top level relies on
+    for (const WindowPlan& W : plans)
+      if (W.use != W0.use || W.n_used != W0.n_used || W.step != W0.step) in.one_scan = 0;
     c->pyramid.configure(options ? options->node_capacity : 0, options ? options->probe_min_nodes : 0);
     csm::PyrStats ps;
     std::string what;

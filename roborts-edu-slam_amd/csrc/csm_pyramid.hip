@@ -98,6 +98,16 @@ __global__ __launch_bounds__(256) void pyr_top_kernel(LevelWork L, int32_t nj, i
   }
 }
 
+// A node's bound from its integer sum over the beams of a quantised level
+// (units of 2^qs): the raw score if >= 0, 0.45 times it otherwise (the
+// centre penalty's floor).
+__device__ __forceinline__ double level_bound(const LevelWork& L, const ScanWork& S, int64_t sum, int qs,
+                                              int32_t n_used) {
+  const double acc = (double)((sum << qs) + (int64_t)n_used * L.outside_i) * L.int_scale;
+  const double raw = acc / S.divisor;
+  return (L.use_penalty && raw < 0.0) ? raw * 0.45 : raw;
+}
+
 template <int NT = kPB>
 __device__ __forceinline__ void block_best(double v, int64_t f, uint64_t nd, PyrPartial* __restrict__ out) {
   __shared__ double rs[NT / 64];
@@ -328,8 +338,7 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
                                                           const ScanWork* __restrict__ scans,
                                                           const AngleEntry* __restrict__ angles,
                                                           const double2* __restrict__ pts, int32_t n_used,
-                                                          int32_t step, uint64_t* __restrict__ nodes,
-                                                          double* __restrict__ vals,
+                                                          int32_t step, int32_t* __restrict__ sums,
                                                           PyrPartial* __restrict__ partials) {
   constexpr int GB = NL == 1 ? 8 : 4;  // beams whose loads are issued together
   __shared__ int32_t odd_sum[32][8 * 5 + 8];
@@ -474,13 +483,9 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
     for (int t = 0; t < 8; ++t) {
       const int J = 8 * cs[s] + t, K = Ks[s];
       if (act[s] && J < nj) {
-        const double acc_d = (double)(((int64_t)acc[s][t] << tb.qs) + (int64_t)n_used * L.outside_i) * L.int_scale;
-        const double raw = acc_d / S.divisor;
-        const double v = (L.use_penalty && raw < 0.0) ? raw * 0.45 : raw;
-        const int64_t idx = (wbase + K) * nj + J;
+        const double v = level_bound(L, S, acc[s][t], tb.qs, n_used);
+        sums[(wbase + K) * nj + J] = acc[s][t];  // the node is implicit in the index
         const uint64_t nd = pyr_node((uint32_t)w, (uint32_t)a, (uint32_t)J, (uint32_t)K);
-        nodes[idx] = nd;
-        vals[idx] = v;
         const int64_t gflat = (int64_t)w * L.n_cand + ((int64_t)a * L.n_space + (J << d)) * L.n_space + (K << d);
         if (better(v, gflat, bv, bf)) {
           bv = v;
@@ -564,6 +569,95 @@ __global__ __launch_bounds__(256) void pyr_probe_kernel(int d, int n_probe, cons
   }
 }
 
+// Wave-aggregated append of each lane's kept children (mask bit 2 dk + dj).
+__device__ __forceinline__ void append_children(int w, int a, int J, int K, uint32_t mask,
+                                                uint64_t* __restrict__ out, unsigned long long* __restrict__ count,
+                                                int64_t cap) {
+  const int lane = threadIdx.x & 63;
+  const int cnt = __builtin_popcount(mask);
+  int incl = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  const int total = __shfl(incl, 63, 64);
+  unsigned long long base = 0;
+  if (lane == 63 && total > 0) base = atomicAdd(count, (unsigned long long)total);
+  base = __shfl(base, 63, 64);
+  int64_t o = (int64_t)base + (incl - cnt);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (mask & (1u << q)) {
+      if (o < cap)
+        out[o] = pyr_node((uint32_t)w, (uint32_t)a, (uint32_t)(2 * J + (q & 1)), (uint32_t)(2 * K + (q >> 1)));
+      ++o;
+    }
+  }
+}
+
+// The incumbent as integer sums (one thread): level_bound is monotone in the
+// sum, so with every window sharing one scan (divisor, beam count: the host
+// checks) bound > score <=> sum >= thr[0] and bound >= score <=> sum >=
+// thr[1] (INT32_MAX + 1: no such sum).
+__global__ void pyr_threshold_kernel(LevelWork L, const ScanWork* __restrict__ scans, int qs, int32_t n_used,
+                                     const BestPartial* __restrict__ inc, int64_t* __restrict__ thr) {
+  const BestPartial cur = *inc;
+  const ScanWork S = scans[0];
+  for (int strict = 1; strict >= 0; --strict) {
+    int64_t lo = INT32_MIN, hi = (int64_t)INT32_MAX + 1;
+    while (lo < hi) {
+      const int64_t mid = lo + ((hi - lo) >> 1);
+      const double v = level_bound(L, S, mid, qs, n_used);
+      if (strict ? v > cur.score : v >= cur.score) hi = mid;
+      else lo = mid + 1;
+    }
+    thr[1 - strict] = lo;
+  }
+}
+
+// The children of top nodes [first, first + n) of pyr_topbox_kernel's
+// implicit list ((window, angle, K, J), J fastest), from their integer sums
+// against pyr_threshold_kernel's thresholds: the same test as
+// better(bound, lowest, incumbent) without a division per node; only the
+// few nodes at or above the incumbent decode their index.
+__global__ __launch_bounds__(256) void pyr_expand_top_kernel(LevelWork L, int d, int32_t nj,
+                                                             const int64_t* __restrict__ thr,
+                                                             const int32_t* __restrict__ sums, int64_t first,
+                                                             int64_t n, const BestPartial* __restrict__ inc,
+                                                             uint64_t* __restrict__ out,
+                                                             unsigned long long* __restrict__ count, int64_t cap) {
+  const BestPartial cur = *inc;
+  const int64_t t_gt = thr[0], t_ge = thr[1];
+  const int h = d - 1;
+  const int64_t per_angle = (int64_t)nj * nj;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = i0 + threadIdx.x;
+    int w = 0, a = 0, J = 0, K = 0;
+    uint32_t mask = 0;
+    const int64_t q = first + i;
+    const int64_t sum = i < n ? (int64_t)sums[q] : INT64_MIN;
+    if (sum >= t_ge) {
+      const int64_t wa = q / per_angle;
+      const int64_t r = q - wa * per_angle;
+      K = (int)(r / nj);
+      J = (int)(r - (int64_t)K * nj);
+      w = (int)(wa / L.n_angles);
+      a = (int)(wa - (int64_t)w * L.n_angles);
+      const int64_t lowest = (int64_t)w * L.n_cand + ((int64_t)a * L.n_space + (J << d)) * L.n_space + (K << d);
+      if (sum >= t_gt || lowest < cur.flat) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int cj = 2 * J + (c & 1), ck = 2 * K + (c >> 1);
+          if ((cj << h) < L.n_space && (ck << h) < L.n_space) mask |= 1u << c;
+        }
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(mask != 0) == 0) continue;  // uniform: the usual case
+    append_children(w, a, J, K, mask, out, count, cap);
+  }
+}
+
 // Children in the order (2J, 2K), (2J+1, 2K), (2J, 2K+1), (2J+1, 2K+1): J
 // pairs adjacent, as the next level's gathers want them.
 __global__ __launch_bounds__(256) void pyr_expand_kernel(LevelWork L, int d, const uint64_t* __restrict__ nodes,
@@ -574,7 +668,6 @@ __global__ __launch_bounds__(256) void pyr_expand_kernel(LevelWork L, int d, con
                                                          unsigned long long* __restrict__ count, int64_t cap) {
   const BestPartial cur = *inc;
   const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
-  const int lane = threadIdx.x & 63;
   const int h = d - 1;
   // whole waves step together (the append below is wave-wide)
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
@@ -594,27 +687,7 @@ __global__ __launch_bounds__(256) void pyr_expand_kernel(LevelWork L, int d, con
         }
       }
     }
-    // wave-aggregated append: one atomic per wave
-    const int cnt = __builtin_popcount(mask);
-    int incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int o = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += o;
-    }
-    const int total = __shfl(incl, 63, 64);
-    unsigned long long base = 0;
-    if (lane == 63 && total > 0) base = atomicAdd(count, (unsigned long long)total);
-    base = __shfl(base, 63, 64);
-    int64_t o = (int64_t)base + (incl - cnt);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (mask & (1u << q)) {
-        if (o < cap)
-          out[o] = pyr_node((uint32_t)w, (uint32_t)a, (uint32_t)(2 * J + (q & 1)), (uint32_t)(2 * K + (q >> 1)));
-        ++o;
-      }
-    }
+    append_children(w, a, J, K, mask, out, count, cap);  // one atomic per wave
   }
 }
 
@@ -712,7 +785,7 @@ hipError_t launch_pyr_widen(const PyrGrid& src, const PyrGrid& dst, int32_t n_gr
 
 hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32_t nj, const ScanWork* scans,
                              const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
-                             uint64_t* nodes, double* vals, PyrPartial* partials, hipStream_t stream) {
+                             int32_t* sums, PyrPartial* partials, hipStream_t stream) {
   const int np = pyr_topbox_pieces(nj);
   const int64_t blocks = (int64_t)L.n_scans * L.n_angles;
   if (np == 0 || blocks <= 0 || blocks > INT32_MAX || n_used < 1 || n_used > 4096 || tb.qs == 0 ||
@@ -723,7 +796,7 @@ hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32
 #define CSM_TOPBOX(NP, NL)                                                                                       \
   if (np == NP && nl == NL) {                                                                                  \
     hipLaunchKernelGGL((pyr_topbox_kernel<NP, NL>), dim3((unsigned)blocks), dim3(64), 0, stream, L, tb, d, nj, \
-                       scans, angles, p, n_used, step, nodes, vals, partials);                                  \
+                       scans, angles, p, n_used, step, sums, partials);                                         \
     return hipGetLastError();                                                                                   \
   }
   CSM_TOPBOX(1, 1)
@@ -734,6 +807,19 @@ hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32
   CSM_TOPBOX(5, 3)
 #undef CSM_TOPBOX
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_pyr_expand_top(const LevelWork& L, int d, int32_t nj, int qs, int32_t n_used, const ScanWork* scans,
+                                 const int32_t* sums, int64_t first, int64_t n, const BestPartial* inc,
+                                 int64_t* thr, uint64_t* out, unsigned long long* count, int64_t cap,
+                                 hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pyr_threshold_kernel, dim3(1), dim3(1), 0, stream, L, scans, qs, n_used, inc, thr);
+  // a block per 256 nodes up to 65536 blocks: the loop is one dependent load
+  // per iteration, so few iterations per thread
+  hipLaunchKernelGGL(pyr_expand_top_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, stream, L, d, nj, thr, sums,
+                     first, n, inc, out, count, cap);
+  return hipGetLastError();
 }
 
 hipError_t launch_pyr_probe(int d, int n_probe, const uint64_t* probe, uint64_t* out, hipStream_t stream) {

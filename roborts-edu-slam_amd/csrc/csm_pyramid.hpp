@@ -90,13 +90,22 @@ hipError_t launch_pyr_top_bound(const LevelWork& L, const PyrGrid& lev, int d, i
 // phase-split int16 layout (8 * pyr_topbox_pieces(nj) zero cells past each
 // phase's columns, 2^d * nj zero rows below); the host guarantees |t| < 2^24
 // cells (the box test's rounding argument). Same outputs as
-// launch_pyr_top_bound, one best per (window, angle) wave (n_scans *
-// n_angles partials).
+// launch_pyr_top_bound (the bounds as integer sums, the nodes implicit),
+// one best per (window, angle) wave (n_scans * n_angles partials).
 int pyr_topbox_pieces(int32_t nj);  // 16-byte pieces per node row (0: unsupported nj)
 hipError_t launch_pyr_widen(const PyrGrid& src, const PyrGrid& dst, int32_t n_grids, hipStream_t stream);
+// Writes each node's integer sum (level units) at its index of the implicit
+// list ((window, angle, K, J), J fastest).
 hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32_t nj, const ScanWork* scans,
                              const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
-                             uint64_t* nodes, double* vals, PyrPartial* partials, hipStream_t stream);
+                             int32_t* sums, PyrPartial* partials, hipStream_t stream);
+// launch_pyr_expand for nodes [first, first + n) of that implicit list; every
+// window must share one scan (divisor, beam count). thr: 2 int64 of device
+// scratch (the incumbent as integer sums).
+hipError_t launch_pyr_expand_top(const LevelWork& L, int d, int32_t nj, int qs, int32_t n_used, const ScanWork* scans,
+                                 const int32_t* sums, int64_t first, int64_t n, const BestPartial* inc,
+                                 int64_t* thr, uint64_t* out, unsigned long long* count, int64_t cap,
+                                 hipStream_t stream);
 // Reduce n partials. merge = true: fold the best into the incumbent *inc
 // (better score, or equal with a lower index). merge = false: probe[i] =
 // the best node of the i-th of n_probe equal segments of the partials, if it
@@ -135,6 +144,7 @@ struct PyrInputs {
   int32_t depth;            // top depth
   int32_t top_mode;         // 0: beam boxes when eligible, 1: per-node gathers
   int32_t box_ok;           // every window's |t| < 2^24 cells (the box test's bound)
+  int32_t one_scan;         // every window has the same divisor and beam count
 };
 
 class PyramidSearch {

@@ -66,6 +66,10 @@ struct PyramidSearch::Impl {
   // length as the expand that filled it left it)
   Buf nodes[kPyrMaxDepth + 1], vals[kPyrMaxDepth + 1];
   Buf partials, inc, probe_slot, probe_nodes, probe_vals, counts, scored;
+  // the beam-box top level: integer sums of the implicit node list
+  Buf top_sums, top_thr;
+  int top_implicit = -1;  // its depth while a search runs (-1: the top is a node list)
+  int32_t top_nj = 0;
   unsigned long long* h_counts = nullptr;  // pinned: counts read back, then scored
   int64_t cap = (int64_t)1 << 24;
   int probe_min = 4096;
@@ -194,6 +198,10 @@ struct PyramidSearch::Impl {
     hipError_t e;
     if ((e = hipMemsetAsync(count_dev(d - 1), 0, sizeof(unsigned long long), in.stream)) != hipSuccess) return e;
     st->slices += 1;
+    if (d == top_implicit)
+      return launch_pyr_expand_top(in.L, d, top_nj, boxg.qs, in.n_used, in.scans, (const int32_t*)top_sums.p, s, k,
+                                   (const BestPartial*)inc.p, (int64_t*)top_thr.p, (uint64_t*)nodes[d - 1].p,
+                                   count_dev(d - 1), cap, in.stream);
     return launch_pyr_expand(in.L, d, (const uint64_t*)nodes[d].p + s, (const double*)vals[d].p + s, k, n_dev, upper,
                              (const BestPartial*)inc.p, (uint64_t*)nodes[d - 1].p, count_dev(d - 1), cap, in.stream);
   }
@@ -295,22 +303,25 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
   // needs |t| < 2^24 (box_ok), nj <= 32, a launch of n_scans * n_angles waves
   const int npc = pyr_topbox_pieces((int32_t)nj);
   const int64_t box_blocks = (int64_t)x.L.n_scans * x.L.n_angles;
-  const bool use_box = D > 0 && x.top_mode == 0 && x.box_ok && npc > 0 && box_blocks <= INT32_MAX &&
+  const bool use_box = D > 0 && x.top_mode == 0 && x.box_ok && x.one_scan && npc > 0 && box_blocks <= INT32_MAX &&
                        n_top <= ((int64_t)1 << 28) && x.n_used >= 1 && x.n_used <= 4096;
   if (use_box && (e = I.build_box(x, D, (int32_t)nj, npc)) == hipSuccess) {
-    if ((e = I.nodes[D].ensure((size_t)n_top * sizeof(uint64_t))) != hipSuccess ||
-        (e = I.vals[D].ensure((size_t)n_top * sizeof(double))) != hipSuccess)
+    if ((e = I.top_sums.ensure((size_t)n_top * sizeof(int32_t))) != hipSuccess ||
+        (e = I.top_thr.ensure(2 * sizeof(int64_t))) != hipSuccess)
       return fail(e, "pyramid top level");
     if ((e = I.partials.ensure((size_t)std::max<int64_t>(box_blocks, pyr_blocks(INT64_MAX / 2)) *
                                sizeof(PyrPartial))) != hipSuccess)
       return fail(e, "pyramid partials");
     if ((e = launch_pyr_topbox(x.L, I.boxg, D, (int32_t)nj, x.scans, x.angles, x.pts, x.n_used, x.step,
-                               (uint64_t*)I.nodes[D].p, (double*)I.vals[D].p, (PyrPartial*)I.partials.p,
-                               x.stream)) != hipSuccess)
+                               (int32_t*)I.top_sums.p, (PyrPartial*)I.partials.p, x.stream)) != hipSuccess)
       return fail(e, "pyr_topbox_kernel");
     top_scored = n_top;
     I.st->top_box = 1;
-    if ((e = I.descend(D, n_top, n_top, true, box_blocks)) != hipSuccess) return fail(e, "pyramid level pass");
+    I.top_implicit = D;
+    I.top_nj = (int32_t)nj;
+    e = I.descend(D, n_top, n_top, true, box_blocks);
+    I.top_implicit = -1;
+    if (e != hipSuccess) return fail(e, "pyramid level pass");
   } else if (use_box && e != hipErrorInvalidValue) {
     return fail(e, "pyramid box level");
   } else if (D > 0 && top_blocks > 0 && n_top <= ((int64_t)1 << 28)) {
