@@ -354,19 +354,13 @@ class ThreadPool {
       n_items_ = n;
       // items are claimed in chunks: one shared counter bumped per item cost
       // more than the work itself at ~1 us per window (cache-line contention)
-      static const bool per_item = [] {  // CSM_POOL_CHUNK=1: one item per claim (A/B)
-        const char* e = std::getenv("CSM_POOL_CHUNK");
-        return e && std::atoi(e) == 1;
-      }();
-      chunk_ = per_item ? 1 : std::max(1, n / (threads * 8));
+      chunk_ = std::max(1, n / (threads * 8));
       next_.store(0);
       active_ = threads - 1;
-      active_spin_.store(threads - 1, std::memory_order_relaxed);
       epoch_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     drain(job, n);
-    spin_until([&] { return active_spin_.load(std::memory_order_acquire) == 0; });
     std::unique_lock<std::mutex> lk(mu_);
     done_cv_.wait(lk, [&] { return active_ == 0; });
     job_ = nullptr;
@@ -396,11 +390,6 @@ class ThreadPool {
       const std::function<void(int)>* job = nullptr;
       int n = 0;
       {
-        // optionally a short spin first (CSM_POOL_SPIN_US): levels follow each
-        // other every few hundred microseconds and a condition-variable wake-up
-        // sits on the critical path; measured no faster on config 2 (4.70-4.82
-        // vs 4.60-5.06 ms per step interleaved), so off by default
-        spin_until([&] { return epoch_.load(std::memory_order_acquire) != seen; });
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return stop_ || (epoch_.load() != seen && id < wanted_); });
         if (stop_) return;
@@ -411,7 +400,6 @@ class ThreadPool {
       drain(*job, n);
       {
         std::lock_guard<std::mutex> lk(mu_);
-        active_spin_.fetch_sub(1, std::memory_order_release);
         if (--active_ == 0) done_cv_.notify_one();
       }
     }
@@ -423,18 +411,6 @@ class ThreadPool {
   const std::function<void(int)>* job_ = nullptr;
   int n_items_ = 0, active_ = 0, wanted_ = 0, chunk_ = 1;
   std::atomic<uint64_t> epoch_{0};
-  std::atomic<int> active_spin_{0};
-  template <class Pred>
-  static void spin_until(Pred done) {
-    static const int spin_us = [] {
-      const char* e = std::getenv("CSM_POOL_SPIN_US");
-      return e ? std::max(0, std::atoi(e)) : 0;  // off by default: 300 us measured no faster
-    }();
-    if (spin_us == 0) return;
-    const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
-    for (int k = 0; !done(); ++k)
-      if ((k & 255) == 255 && std::chrono::steady_clock::now() > t_end) return;
-  }
   std::atomic<int> next_{0};
   bool stop_ = false;
 };
@@ -458,12 +434,6 @@ struct csm_ctx {
   // the kernels by events: a part's inputs go up while the other part's
   // kernels run, its results come down while the next kernels run.
   hipStream_t h2d = nullptr, d2h = nullptr;
-  // CSM_FINISH_STREAM=1: the device finish runs on a stream of its own, so one
-  // part's finish (latency-bound, a few blocks wide at its exact pass) can
-  // overlap the next part's scoring launch; its results go down only after it
-  // (ev_k on this stream). Opt-in: measured no faster on config 2 (5.72-6.41
-  // vs 5.78-6.19 ms/step interleaved, the host plan slows down under it).
-  hipStream_t fin_stream = nullptr;
   std::mutex mu;
   std::string err;
   float outside = 0.3f;  // kMapUnknownCellProb (slam/slam_processor.h:264)
@@ -488,24 +458,9 @@ struct csm_ctx {
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
   bool fast_finish = true;    // CSM_FINISH=exact: always the full device std::sort emulation
   int device_finish_min = 1;  // fewest windows per launch that finish on the device
-  // Windows of at least this many candidates that the fast finish flags are
-  // sorted on the host (libstdc++ std::sort, what the reference runs) instead
-  // of by the device's exact pass: a handful per launch, so the host does them
-  // while the device scores the other part, and the level's device time loses
-  // the exact pass's tail (one window's sort chain). CSM_HOST_EXACT_MIN (e.g.
-  // 4096); 0, the default: off. Measured slower on config 2: the coarse
-  // finish drops 0.188 -> 0.062 ms per launch, but the host sorts (5070
-  // candidates each) land on the pipeline's critical path, 4.70-4.82 ->
-  // 5.24-5.40 ms per step (profiles/r01/experiments/ab_host_exact.txt).
-  int64_t host_exact_min = 0;
-  hipStream_t x2h = nullptr;  // copies of the flagged windows' scores
-  HostBuf h_exact;            // ... their pinned staging
   bool column_kernel = true;  // CSM_KERNEL=v1 selects the lane-per-candidate kernels
   bool row_kernel = true;     // CSM_KERNEL=v2 (or v1) turns the row-segment kernels off
   bool row_dma = true;        // CSM_KERNEL=v3: register-staged row segments instead of LDS-DMA
-  bool tile_kernel = false;   // CSM_KERNEL=v5 opts into the beam-tile kernel (exact; measured
-                              // slower than v4 on config 2: 8.3 vs 7.0 ms, profiles/r01)
-  int tile_beams = 8;         // beams per box of the beam-tile kernel (CSM_TILE_BEAMS: 4 or 8)
   bool phase_kernel = true;   // v7 phase kernel for sub-cell window steps (CSM_KERNEL=v7 or unset)
   int phase_margin_log2 = 20; // CSM_PHASE_MARGIN_LOG2 (tests: a wider margin sends more beams to the exact path)
   bool box_kernel = true;     // v6 box kernel for one-cell window steps; any CSM_KERNEL other
@@ -595,25 +550,17 @@ struct csm_ctx {
 
   // Second set of per-launch buffers: the 3-level driver keeps two halves of
   // a batch in flight (match_levels_pipelined); swap_slot() exchanges the
-  // sets so run_windows works on whichever half is current.
-  // Optionally each part has its own kernel stream (CSM_PART_STREAMS=1), so one
-  // part's finish (a few latency-bound blocks) can overlap the next part's scoring.
+  // sets so run_windows works on whichever half is current. Every part uses
+  // the one kernel stream: a stream per part measured slower (two concurrent
+  // box-kernel launches contend for L2, 1.01 -> 1.57 ms each; profiles/r01).
   struct Slot {
     DevBuf scans, angles, scores, partials, best, fin;
     HostBuf h_scores, h_fin, h_angles, h_sw;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr, ev_in = nullptr, ev_k = nullptr;
-    // null (default): the part shares csm_ctx::stream. CSM_PART_STREAMS=1 gives each part its
-    // own stream; measured slower on config 2 (6.23 vs 5.96 ms per step: two concurrent
-    // box-kernel launches contend for L2 and the coarse launch goes 1.01 -> 1.57 ms).
-    hipStream_t stream = nullptr;
   };
   static constexpr int kMaxParts = 4;
   Slot alt[kMaxParts - 1];
   int pipeline_min = 512;    // fewest scans the 3-level driver splits into parts (CSM_PIPELINE)
-  // level_begin: windows in a Z-order of map regions (CSM_SPATIAL=1). Opt-in:
-  // measured slower, the box kernel 1.025 -> 1.14 ms per launch (each XCD's
-  // windows then hammer the same grid rows; scan order spreads them)
-  bool spatial_order = false;
   bool skip_dead_lists = true;  // live_lists (CSM_SKIP_DEAD_LISTS=0: every level fills both lists)
   int pipeline_parts = 2;    // parts in flight (CSM_PIPELINE_PARTS: 2..kMaxParts; 2 measured fastest)
   void swap_slot(int i) {    // i >= 1: exchange the current buffer set with alt[i - 1]
@@ -634,9 +581,7 @@ struct csm_ctx {
     std::swap(ev_done, a.ev_done);
     std::swap(ev_in, a.ev_in);
     std::swap(ev_k, a.ev_k);
-    if (a.stream) std::swap(stream, a.stream);
   }
-  hipEvent_t ev_fork = nullptr;  // the pipelined driver's part streams start after the main stream
   std::vector<csm_kernel_stat> stats;
   void account(const char* name, float ms, double bytes, double scorings) {
     for (auto& s : stats)
@@ -849,10 +794,8 @@ struct PendingRun {
   double alg_bytes = 0.0, scorings = 0.0, finish_bytes = 0.0;
   bool device_finish = false, timed = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, done = nullptr;
-  const int32_t* flags = nullptr;  // need-exact flags on the host (profiling, host_exact)
+  const int32_t* flags = nullptr;  // need-exact flags on the host (profiling)
   int n_flags = 0;
-  bool host_exact = false;          // flagged windows finish on the host (level_end)
-  const double* d_scores = nullptr; // their scores on the device
 };
 
 int wait_run(csm_ctx* c, const PendingRun& p) {
@@ -958,37 +901,23 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     rows_sq = csm::rows_pick_sq(D.n_space, (int)std::floor(span * (1.0 + 1e-9) + 1e-9) + 2);
     if (c->info.size_x < 4 * rows_sq) rows_sq = 0;
   }
-  // v5 beam-tile kernel: whole-cell window step, supported n_space, every
-  // endpoint within 16000 cells of the map origin (its packed row/column base)
-  bool tiles = false;
-  if (use_int && c->tile_kernel && f == 1.0 && csm::tiles_supported(D.n_space) && c->pitch >= 32 &&
-      c->pitch < 65536 && c->info.size_y < 16000) {
-    tiles = true;
-    for (const WindowPlan& W : plans) {
-      const double far = (double)(D.n_space - 1) * f;
-      const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
-                                   std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
-      if (!(c->pts_maxabs * (1.0 + 1e-9) + span + 64.0 < 16000.0)) tiles = false;
-    }
-  }
-  if (tiles) rows_sq = 0;
   // v6 box kernel: whole-cell window step (use_int bounds |t| < 2^24 cells,
   // which its rounding margin needs)
-  const bool box = !tiles && use_int && c->box_kernel && f == 1.0 && csm::box_supported(D.n_space) &&
+  const bool box = use_int && c->box_kernel && f == 1.0 && csm::box_supported(D.n_space) &&
                    c->pitch >= c->info.size_x + csm::kGridiPadCols;
   if (box) rows_sq = 0;
   // v7 phase kernel: sub-cell window step with an instantiated bucket shape
   csm::PhaseTable PT{};
-  const bool phase = !tiles && !box && use_int && c->phase_kernel && f < 1.0 &&
+  const bool phase = !box && use_int && c->phase_kernel && f < 1.0 &&
                      phase_table(f, D.n_space, c->phase_margin_log2, PT) &&
                      csm::phase_supported(D.n_space, PT.cells, PT.nq) &&
                      c->pitch >= c->info.size_x + csm::kGridiPadCols;
   if (phase) rows_sq = 0;
   const int cpl = pick_cpl(D.n_cand);
   const int64_t per_block = (int64_t)csm::kBlock * cpl;
-  const int64_t rows_groups = (rows_sq || tiles) ? 64 / D.n_space : 1;
+  const int64_t rows_groups = rows_sq ? 64 / D.n_space : 1;
   const int64_t bps = (box || phase) ? D.n_angles
-                      : (rows_sq || tiles) ? (D.n_angles + rows_groups - 1) / rows_groups
+                      : rows_sq ? (D.n_angles + rows_groups - 1) / rows_groups
                       : v2    ? col_blocks * ktiles
                               : (D.n_cand + per_block - 1) / per_block;
   if (bps * nw > INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
@@ -1058,8 +987,6 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     std::snprintf(kname, sizeof(kname), "score_box_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (phase)
     std::snprintf(kname, sizeof(kname), "score_phase_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
-  else if (tiles)
-    std::snprintf(kname, sizeof(kname), "score_tiles_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (rows_sq)
     std::snprintf(kname, sizeof(kname), "%s<%d,%d,%s>", c->row_dma ? "score_rowsd_kernel" : "score_rows_kernel",
                   D.n_space, rows_sq, best_out ? "best" : "all");
@@ -1072,7 +999,6 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
 
   const int32_t* flags_h = nullptr;
   int n_flags = 0;
-  bool host_exact = false;
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
@@ -1084,10 +1010,6 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       e = csm::launch_score_phase(L, PT, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                   (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
                                   c->stream);
-    else if (tiles)
-      e = csm::launch_score_tiles(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
-                                  c->tile_beams, c->stream);
     else if (rows_sq)
       e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr,
@@ -1123,21 +1045,14 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       A.exact_list = c->fast_finish ? A.need_exact + nw : nullptr;
       if ((e = c->h_fin.ensure(fbytes + (size_t)nw * sizeof(int32_t))) != hipSuccess)
         return c->hip_fail(e, "hipHostMalloc(finish)");
-      // the finish stream starts after the scoring kernel (ev_k, re-recorded below
-      // once the finish is queued: a wait binds to the record before it)
-      hipStream_t fs = c->fin_stream ? c->fin_stream : c->stream;
-      if (fs != c->stream &&
-          ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(fs, c->ev_k, 0)) != hipSuccess))
-        return c->hip_fail(e, "finish stream event");
-      host_exact = pend && A.need_exact && c->host_exact_min > 0 && D.n_cand >= c->host_exact_min;
       if ((e = csm::launch_finish(A, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
-                                  (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw, fs,
-                                  !host_exact)) != hipSuccess)
+                                  (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw, c->stream, true)) !=
+          hipSuccess)
         return c->hip_fail(e, "finish_kernel");
-      if (c->profiling && (e = hipEventRecord(c->ev2, fs)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+      if (c->profiling && (e = hipEventRecord(c->ev2, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
       // with profiling on, the flags come back too: how many windows needed the exact sort
-      const size_t cbytes = fbytes + (((c->profiling || host_exact) && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
-      if ((e = hipEventRecord(c->ev_k, fs)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
+      const size_t cbytes = fbytes + ((c->profiling && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
+      if ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
         return c->hip_fail(e, "kernels event");
       if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, cbytes, hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
         return c->hip_fail(e, "hipMemcpyAsync(finish)");
@@ -1158,10 +1073,6 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       e = csm::launch_score_phase(L, PT, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                   (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
                                   D.n_space, c->stream);
-    else if (tiles)
-      e = csm::launch_score_tiles(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                  (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
-                                  D.n_space, c->tile_beams, c->stream);
     else if (rows_sq)
       e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
@@ -1188,8 +1099,6 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   PendingRun& p = pend ? *pend : local;
   p.flags = flags_h;
   p.n_flags = n_flags;
-  p.host_exact = host_exact;
-  p.d_scores = (const double*)c->scores.p;
   std::snprintf(p.kname, sizeof(p.kname), "%s", kname);
   std::snprintf(p.fname, sizeof(p.fname), "finish_kernel<%lld>", (long long)D.n_cand);
   p.alg_bytes = alg_bytes;
@@ -1472,28 +1381,6 @@ int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
   const int nw = (int)R.scan_of.size();
   if (nw == 0) return CSM_OK;
   const double t0 = now_ms();
-  // Windows in a Z-order of 8 x 8 map regions (a stable counting sort):
-  // consecutive windows go to one XCD (xcd_remap), so each XCD's L2 serves a
-  // compact part of the grid. The order changes no result (level_end maps
-  // window i back to scan scan_of[i]).
-  if (c->spatial_order && nw >= 512 && !scan_grid) {
-    int cnt[65] = {0};
-    std::vector<uint8_t> key((size_t)nw);
-    for (int i = 0; i < nw; ++i) {
-      double m[3];
-      G.to_map(poses + 3 * (size_t)R.scan_of[(size_t)i], m);
-      const int rx = std::max(0, std::min(7, (int)(m[0] * 8.0 / std::max(1, c->info.size_x))));
-      const int ry = std::max(0, std::min(7, (int)(m[1] * 8.0 / std::max(1, c->info.size_y))));
-      int z = 0;
-      for (int b = 0; b < 3; ++b) z |= (((rx >> b) & 1) << (2 * b)) | (((ry >> b) & 1) << (2 * b + 1));
-      key[(size_t)i] = (uint8_t)z;
-      cnt[z + 1]++;
-    }
-    for (int z = 0; z < 64; ++z) cnt[z + 1] += cnt[z];
-    std::vector<int> sorted((size_t)nw);
-    for (int i = 0; i < nw; ++i) sorted[(size_t)cnt[key[(size_t)i]]++] = R.scan_of[(size_t)i];
-    R.scan_of.swap(sorted);
-  }
   R.plans.assign((size_t)nw, WindowPlan{});
   R.pt_off.assign((size_t)nw, 0);
   hipError_t he;
@@ -1539,31 +1426,9 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
   const Geometry G(c->info);
   if (R.dev)
     for (int i = 0; i < nw; ++i)
-      if (R.fin[i].count < 0 && !(R.pend.host_exact && R.pend.flags && R.pend.flags[i]))
+      if (R.fin[i].count < 0)
         return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
   const double f = P.search_space_resolution / G.mres;
-  // windows the fast finish flagged and left to the host: their scores come
-  // down (pinned staging, one stream sync) and std::sort orders them below
-  std::vector<int> slot_of;  // window -> staging slot (-1: the device finished it)
-  const double* xs = nullptr;
-  if (R.dev && R.pend.host_exact && R.pend.flags) {
-    slot_of.assign((size_t)nw, -1);
-    int nx = 0;
-    for (int i = 0; i < nw; ++i)
-      if (R.pend.flags[i]) slot_of[(size_t)i] = nx++;
-    if (nx > 0) {
-      const size_t wb = (size_t)D.n_cand * sizeof(double);
-      hipError_t e;
-      if ((e = c->h_exact.ensure((size_t)nx * wb)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(exact)");
-      for (int i = 0; i < nw; ++i)
-        if (slot_of[(size_t)i] >= 0 &&
-            (e = hipMemcpyAsync((char*)c->h_exact.p + (size_t)slot_of[(size_t)i] * wb, R.pend.d_scores + (size_t)i * D.n_cand,
-                                wb, hipMemcpyDeviceToHost, c->x2h)) != hipSuccess)
-          return c->hip_fail(e, "hipMemcpyAsync(exact scores)");
-      if ((e = hipStreamSynchronize(c->x2h)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(exact)");
-      xs = (const double*)c->h_exact.p;
-    }
-  }
   const int threads = (nw >= 64) ? c->host_threads : 1;
   c->parallel_for(nw, threads, [&](int i) {
     thread_local std::vector<Entry> scratch;
@@ -1572,10 +1437,7 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
                      (int64_t)D.n_space * D.n_space};
     csm::FinishOut local;
     const csm::FinishOut* o = nullptr;
-    if (R.dev && xs && slot_of[(size_t)i] >= 0) {
-      host_sort_finish(xs + (size_t)slot_of[(size_t)i] * (size_t)D.n_cand, D, C, P, G, scratch, local);
-      o = &local;
-    } else if (R.dev) {
+    if (R.dev) {
       o = R.fin + i;
     } else {
       host_sort_finish(R.scores + (size_t)i * (size_t)D.n_cand, D, C, P, G, scratch, local);
@@ -1616,11 +1478,6 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
   }
   std::vector<double> resp((size_t)n_scans, 0.0);
   LevelRun R[csm_ctx::kMaxParts];
-  hipError_t he;  // part streams start after everything already on the main stream (grid, points)
-  if ((he = hipEventRecord(c->ev_fork, c->stream)) != hipSuccess) return c->hip_fail(he, "hipEventRecord(fork)");
-  for (int h = 1; h < K; ++h)
-    if (c->alt[h - 1].stream && (he = hipStreamWaitEvent(c->alt[h - 1].stream, c->ev_fork, 0)) != hipSuccess)
-      return c->hip_fail(he, "hipStreamWaitEvent(fork)");
   auto begin = [&](int l, int h) {
     if (h > 0) c->swap_slot(h);
     const int32_t s0 = first[h];
@@ -2032,31 +1889,19 @@ int csm_create(int device, csm_ctx** out) {
     c->column_kernel = std::strcmp(env, "v1") != 0;
     c->row_kernel = std::strcmp(env, "v1") != 0 && std::strcmp(env, "v2") != 0;
     c->row_dma = std::strcmp(env, "v3") != 0;
-    c->tile_kernel = std::strcmp(env, "v5") == 0;
     c->box_kernel = std::strcmp(env, "v6") == 0 || std::strcmp(env, "v7") == 0;
     c->phase_kernel = std::strcmp(env, "v7") == 0;
   }
   if (const char* env = std::getenv("CSM_PHASE_MARGIN_LOG2"))
     c->phase_margin_log2 = std::max(2, std::min(std::atoi(env), 20));
-  if (const char* env = std::getenv("CSM_TILE_BEAMS")) c->tile_beams = std::atoi(env) == 4 ? 4 : 8;
   if (const char* env = std::getenv("CSM_PIPELINE")) {  // 0: never split the 3-level batch
     const int v = std::atoi(env);
     c->pipeline_min = v > 0 ? v : INT32_MAX;
   }
   if (const char* env = std::getenv("CSM_SKIP_DEAD_LISTS")) c->skip_dead_lists = std::atoi(env) != 0;
-  if (const char* env = std::getenv("CSM_HOST_EXACT_MIN")) c->host_exact_min = std::atoll(env);
-  if (const char* env = std::getenv("CSM_SPATIAL")) c->spatial_order = std::atoi(env) != 0;
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
   bool ev_ok = true;
-  const char* ps = std::getenv("CSM_PART_STREAMS");
-  if (ps && std::atoi(ps) != 0)
-    for (auto& a : c->alt) ev_ok = ev_ok && hipStreamCreateWithFlags(&a.stream, hipStreamNonBlocking) == hipSuccess;
-  const char* fsn = std::getenv("CSM_FINISH_STREAM");
-  if (!(ps && std::atoi(ps) != 0) && fsn && std::atoi(fsn) != 0)
-    ev_ok = ev_ok && hipStreamCreateWithFlags(&c->fin_stream, hipStreamNonBlocking) == hipSuccess;
-  ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
-  ev_ok = ev_ok && hipStreamCreateWithFlags(&c->x2h, hipStreamNonBlocking) == hipSuccess;
   for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k})
     ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
   for (auto& a : c->alt)
@@ -2079,15 +1924,8 @@ int csm_destroy(csm_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->h2d);
     (void)hipStreamSynchronize(c->d2h);
-    for (auto& a : c->alt)
-      if (a.stream) (void)hipStreamSynchronize(a.stream);
-    if (c->fin_stream) (void)hipStreamSynchronize(c->fin_stream);
-    if (c->x2h) (void)hipStreamSynchronize(c->x2h);
     csm::gridmap_drop_reader(c->stream);
-    for (auto& a : c->alt)
-      if (a.stream) csm::gridmap_drop_reader(a.stream);
     c->grid_buf.release();
-    c->h_exact.release();
     c->gridi.release();
     c->h_pack.release();
     c->d_updates.release();
@@ -2125,13 +1963,9 @@ int csm_destroy(csm_ctx* c) {
       a.h_sw.release();
       for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k})
         if (ev) (void)hipEventDestroy(ev);
-      if (a.stream) (void)hipStreamDestroy(a.stream);
     }
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k})
       if (ev) (void)hipEventDestroy(ev);
-    if (c->fin_stream) (void)hipStreamDestroy(c->fin_stream);
-    if (c->x2h) (void)hipStreamDestroy(c->x2h);
     (void)hipStreamDestroy(c->h2d);
     (void)hipStreamDestroy(c->d2h);
     (void)hipStreamDestroy(c->stream);
@@ -2356,8 +2190,6 @@ int csm_set_grid_gridmap(csm_ctx* c, csm_gridmap* map) {
     hipError_t e = hipStreamWaitEvent(c->stream, v.ready, 0);
     if (e != hipSuccess) return c->fail(CSM_ERR_HIP, hipGetErrorString(e));
     csm::gridmap_add_reader(map, c->stream);
-    for (auto& a : c->alt)
-      if (a.stream) csm::gridmap_add_reader(map, a.stream);
   }
   csm_map_info info{};
   info.resolution = v.resolution;

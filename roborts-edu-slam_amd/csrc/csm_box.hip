@@ -22,8 +22,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <cstdlib>
-#include <cstring>
 
 #include "csm_device.hpp"
 #include "csm_internal.hpp"
@@ -42,7 +40,7 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));
 // trunc(t_0) + j for every j; the same for rows.
 constexpr double kBoxMargin = 0x1p-20;
 
-// Beams per run-list segment (RUNS): the list of one segment lives in LDS.
+// Beams per run-list segment: the list of one segment lives in LDS.
 #ifndef CSM_RUN_SEG
 #define CSM_RUN_SEG 1152
 #endif
@@ -51,11 +49,14 @@ constexpr int kRunSeg = CSM_RUN_SEG;
 #define CSM_BOX_PF 6
 #endif
 constexpr int kPF = CSM_BOX_PF;  // chunks of beam points in flight while a run list is built
+// Runs in flight per wave (16 measured no better; one load per beam instead of
+// per run: 2.28 vs 1.02 ms, profiles/r01)
+constexpr int kD = 8;
 static_assert(kRunSeg % 64 == 0, "segments of whole 64-beam chunks");
 
 
 // One wave's view of its (window, angle): the beam points, the box test and
-// the per-segment run list (shared by the run-list and the grouped kernels).
+// the per-segment run list.
 struct BoxWave {
   const ScanWork& S;
   const AngleEntry& ae;
@@ -217,7 +218,7 @@ __device__ __forceinline__ void box_epilogue(const LevelWork& L, const ScanWork&
   }
 }
 
-template <int NS, int D, bool RUNS, bool BEST>
+template <int NS, int D, bool BEST>
 __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWork* __restrict__ scans,
                                                        const double2* __restrict__ pts,
                                                        const AngleEntry* __restrict__ angles,
@@ -253,135 +254,75 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   int64_t acc[4] = {0, 0, 0, 0};
   uint64_t slow = 0;
   v4i buf[D];
-  if constexpr (!RUNS) {
-    int offA = B.offsets(B.point(0), 0, slow);    // beams of the current chunk
-    int offB = B.offsets(B.point(64), 64, slow);  // and of the next one
-    double2 pn = B.point(128);                    // points of the chunk after, in flight
-    // soffset of beam cb + r, 0 <= r < 128
-    auto off_of = [&](int r) -> int {
-      return r < 64 ? __builtin_amdgcn_readlane(offA, r) : __builtin_amdgcn_readlane(offB, r - 64);
-    };
-#pragma unroll
-    for (int j = 0; j < D; ++j) buf[j] = load(off_of(j));
-    const int nchunks = (n_used + 63) / 64;
-    for (int c = 0; c < nchunks; ++c) {
-#pragma unroll
-      for (int h = 0; h < 64; h += 32) {  // 32 * (2^26 - 1) < 2^31 (ensure_int_grid)
-        int32_t part[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < 32; i += D) {
-          // the D box corners this group issues (readlanes batched: a VALU
-          // SGPR write needs 5 wait states before a VMEM instruction reads it)
-          int so[D];
-#pragma unroll
-          for (int j = 0; j < D; ++j) so[j] = off_of(h + i + j + D);
-#pragma unroll
-          for (int j = 0; j < D; ++j) {
-            v4i v = buf[j];
-            asm volatile("" : "+v"(v));  // consume beam h+i+j here, in order
-            part[0] += v.x;
-            part[1] += v.y;
-            part[2] += v.z;
-            part[3] += v.w;
-            asm volatile("" : "+v"(part[0]), "+v"(part[1]), "+v"(part[2]), "+v"(part[3]));
-            buf[j] = load(so[j]);
-            // keep the issue order: D loads in flight, not the whole chunk
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] += part[t];
-      }
-      offA = offB;
-      offB = B.offsets(pn, (c + 2) * 64, slow);
-      pn = B.point((c + 3) * 64);
+  // Run list: a run is one load whose values are added count times. Lists
+  // are built per segment of kRunSeg beams (list, padding, then one scratch
+  // slot per lane for the branch-free list writes).
+  constexpr int kScratch = kRunSeg + 64 + 2 * D;
+  __shared__ int32_t run_off[kScratch + 64];
+  __shared__ int32_t run_cnt[kScratch + 64];
+  for (int s0 = 0; s0 < n_used; s0 += kRunSeg) {
+    const int s1 = min(n_used, s0 + kRunSeg);
+    const int nruns = B.build_runs(s0, s1, run_off, run_cnt, kScratch, slow);
+    // whole groups of D, then empty runs (zero block, count 0) far enough
+    // past the list for the issue-ahead window below
+    const int npad = (nruns + D - 1) / D * D;
+    for (int i = nruns + lane; i < npad + 64 + D; i += 64) {
+      run_off[i] = zero_off;
+      run_cnt[i] = 0;
     }
-  } else {
-    // Run list: a run is one load whose values are added count times. Lists
-    // are built per segment of kRunSeg beams (list, padding, then one scratch
-    // slot per lane for the branch-free list writes).
-    constexpr int kScratch = kRunSeg + 64 + 2 * D;
-    __shared__ int32_t run_off[kScratch + 64];
-    __shared__ int32_t run_cnt[kScratch + 64];
-    for (int s0 = 0; s0 < n_used; s0 += kRunSeg) {
-      const int s1 = min(n_used, s0 + kRunSeg);
-      const int nruns = B.build_runs(s0, s1, run_off, run_cnt, kScratch, slow);
-      // whole groups of D, then empty runs (zero block, count 0) far enough
-      // past the list for the issue-ahead window below
-      const int npad = (nruns + D - 1) / D * D;
-      for (int i = nruns + lane; i < npad + 64 + D; i += 64) {
-        run_off[i] = zero_off;
-        run_cnt[i] = 0;
+    __syncthreads();
+    if (npad == 0) continue;
+    // lane i of cA: count of run rb + i; of wI: corner of run rb + D + i
+    // (loads are issued exactly D runs ahead of their use)
+    int rb = 0;
+    int cA = run_cnt[lane];
+    int wI = run_off[D + lane];
+#pragma unroll
+    for (int j = 0; j < D; ++j) buf[j] = load(run_off[j]);
+    for (int r0 = 0; r0 < npad; r0 += D) {
+      int so[D], cn[D];
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        cn[j] = __builtin_amdgcn_readlane(cA, r0 + j - rb);
+        so[j] = __builtin_amdgcn_readlane(wI, r0 + j - rb);
       }
-      __syncthreads();
-      if (npad == 0) continue;
-      // lane i of cA: count of run rb + i; of wI: corner of run rb + D + i
-      // (loads are issued exactly D runs ahead of their use)
-      int rb = 0;
-
-      int cA = run_cnt[lane];
-      int wI = run_off[D + lane];
 #pragma unroll
-      for (int j = 0; j < D; ++j) buf[j] = load(run_off[j]);
-      for (int r0 = 0; r0 < npad; r0 += D) {
-        int so[D], cn[D];
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-          cn[j] = __builtin_amdgcn_readlane(cA, r0 + j - rb);
-          so[j] = __builtin_amdgcn_readlane(wI, r0 + j - rb);
-        }
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-          v4i v = buf[j];
-          asm volatile("" : "+v"(v));  // consume run r0+j here, in order
-          acc[0] += (int64_t)cn[j] * v.x;
-          acc[1] += (int64_t)cn[j] * v.y;
-          acc[2] += (int64_t)cn[j] * v.z;
-          acc[3] += (int64_t)cn[j] * v.w;
-          asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
-          buf[j] = load(so[j]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (((r0 + D) & 63) == 0) {  // slide the register windows by 64 runs
-          rb += 64;
-          cA = run_cnt[rb + lane];
-          wI = run_off[rb + D + lane];
-        }
+      for (int j = 0; j < D; ++j) {
+        v4i v = buf[j];
+        asm volatile("" : "+v"(v));  // consume run r0+j here, in order
+        acc[0] += (int64_t)cn[j] * v.x;
+        acc[1] += (int64_t)cn[j] * v.y;
+        acc[2] += (int64_t)cn[j] * v.z;
+        acc[3] += (int64_t)cn[j] * v.w;
+        asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
+        buf[j] = load(so[j]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __syncthreads();  // the next segment rewrites the list
+      if (((r0 + D) & 63) == 0) {  // slide the register windows by 64 runs
+        rb += 64;
+        cA = run_cnt[rb + lane];
+        wI = run_off[rb + D + lane];
+      }
     }
+    __syncthreads();  // the next segment rewrites the list
   }
   slow_beams<NS>(B, L, gi, slow, k, q, acc);
   box_epilogue<NS, BEST>(L, S, ae, win, a, act, k, q, acc, out, partials);
 }
 
-template <int NS, int D, bool RUNS>
+template <int NS>
 hipError_t launch_ns(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
                      BestPartial* part, unsigned nblk, hipStream_t stream) {
   if (part)
-    hipLaunchKernelGGL((score_box_kernel<NS, D, RUNS, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out,
-                       part);
+    hipLaunchKernelGGL((score_box_kernel<NS, kD, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
   else
-    hipLaunchKernelGGL((score_box_kernel<NS, D, RUNS, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out,
-                       part);
+    hipLaunchKernelGGL((score_box_kernel<NS, kD, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
   return hipGetLastError();
 }
 
 }  // namespace
 
 bool box_supported(int ns) { return ns >= 9 && ns <= 16; }
-
-// CSM_BOX=beams: one load per beam (no run list); CSM_BOX_DEPTH=16: 16 loads
-// in flight per wave instead of 8. (Grouping runs of nearby corners into one
-// shared load measured slower: profiles/r02/experiments/ab_box_groups.txt.)
-int box_mode() {
-  static const int m = [] {
-    const char* env = std::getenv("CSM_BOX_DEPTH");
-    const char* mode = std::getenv("CSM_BOX");
-    return ((env && std::atoi(env) == 16) ? 1 : 0) | ((mode && std::strcmp(mode, "beams") == 0) ? 2 : 0);
-  }();
-  return m;
-}
 
 hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                             const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
@@ -392,32 +333,17 @@ hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const d
     return hipErrorInvalidValue;
   const double2* p = reinterpret_cast<const double2*>(d_pts);
   const unsigned n = (unsigned)nblk;
-  const int mode = box_mode();
-#define CSM_BOX_CASE(N)                                                                        \
-  case N:                                                                                      \
-    switch (mode & 3) {                                                                        \
-      case 0:                                                                                  \
-        return launch_ns<N, 8, true>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);   \
-      case 1:                                                                                  \
-        return launch_ns<N, 16, true>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);  \
-      case 2:                                                                                  \
-        return launch_ns<N, 8, false>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);  \
-      default:                                                                                 \
-        return launch_ns<N, 16, false>(L, d_scans, p, d_angles, d_out, d_partials, n, stream); \
-    }
   switch (ns) {
-    CSM_BOX_CASE(9)
-    CSM_BOX_CASE(10)
-    CSM_BOX_CASE(11)
-    CSM_BOX_CASE(12)
-    CSM_BOX_CASE(13)
-    CSM_BOX_CASE(14)
-    CSM_BOX_CASE(15)
-    CSM_BOX_CASE(16)
-    default:
-      return hipErrorInvalidValue;
+    case 9: return launch_ns<9>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 10: return launch_ns<10>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 11: return launch_ns<11>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 12: return launch_ns<12>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 13: return launch_ns<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 14: return launch_ns<14>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 15: return launch_ns<15>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 16: return launch_ns<16>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    default: return hipErrorInvalidValue;
   }
-#undef CSM_BOX_CASE
 }
 
 }  // namespace csm

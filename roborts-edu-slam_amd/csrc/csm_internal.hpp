@@ -177,13 +177,6 @@ struct TreeWork {
 hipError_t launch_score_tree(const TreeWork& T, const ScanWork* d_scans, const double* d_pts,
                              const AngleEntry* d_angles, double* d_out, hipStream_t stream);
 
-// Beam-tile kernel (v5, csm_tiles.hip): INT mode, window step exactly one
-// cell, n_space in {13, 21}; same block layout as the row-segment kernels.
-// The host also keeps every endpoint within |map coords| < 16000 cells.
-bool tiles_supported(int ns);
-hipError_t launch_score_tiles(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
-                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
-                              int tile_beams, hipStream_t stream);
 // Box kernel (v6, csm_box.hip): INT mode, window step exactly one cell,
 // n_space <= 16; one wave per (window, angle), one 16-byte row piece per lane
 // per beam. blocks_per_scan = n_angles.

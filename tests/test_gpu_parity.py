@@ -365,7 +365,7 @@ def test_kernel_variants_agree(f1, grid_kind):
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
     ctxs = []
-    for kern in ("v1", "v2", "v3", "v4", "v5", "v6", None):  # None: default (v6 box / v7 phase / v4 where eligible)
+    for kern in ("v1", "v2", "v3", "v4", "v6", None):  # None: default (v6 box / v7 phase / v4 where eligible)
         if kern:
             os.environ["CSM_KERNEL"] = kern
         try:

@@ -33,7 +33,7 @@ def _short(name: str) -> str:
             ns, sq, best = [a.strip() for a in name[i:name.index(">", i)].split(",")][:3]
             return f"{key[:-1]}<{ns},{sq},{'best' if best == 'true' else 'all'}>"
     key = "score_box_kernel<"
-    if key in name:  # <int NS, int D, bool RUNS, bool BEST>
+    if key in name:  # <int NS, int D, bool BEST>
         i = name.index(key) + len(key)
         args = [a.strip() for a in name[i:name.index(">", i)].split(",")]
         return f"score_box_kernel<{args[0]},{'best' if args[-1] == 'true' else 'all'}>"
@@ -42,11 +42,6 @@ def _short(name: str) -> str:
         i = name.index(key) + len(key)
         args = [a.strip() for a in name[i:name.index(">", i)].split(",")]
         return f"score_phase_kernel<{args[0]},{'best' if args[-1] == 'true' else 'all'}>"
-    key = "score_tiles_kernel<"
-    if key in name:  # <int NS, int T, bool BEST>
-        i = name.index(key) + len(key)
-        ns, _, best = [a.strip() for a in name[i:name.index(">", i)].split(",")]
-        return f"score_tiles_kernel<{ns},{'best' if best == 'true' else 'all'}>"
     for key in ("score_all_kernel<", "score_best_kernel<"):
         if key in name:
             i = name.index(key)
