@@ -462,6 +462,7 @@ struct csm_ctx {
   bool row_kernel = true;     // CSM_KERNEL=v2 (or v1) turns the row-segment kernels off
   bool row_dma = true;        // CSM_KERNEL=v3: register-staged row segments instead of LDS-DMA
   bool phase_kernel = true;   // v7 phase kernel for sub-cell window steps (CSM_KERNEL=v7 or unset)
+  bool tiny_kernel = true;    // v8 tiny-window kernel, spans under one cell (CSM_KERNEL=v8 or unset)
   int phase_margin_log2 = 20; // CSM_PHASE_MARGIN_LOG2 (tests: a wider margin sends more beams to the exact path)
   bool box_kernel = true;     // v6 box kernel for one-cell window steps; any CSM_KERNEL other
                               // than v6 turns it off (CSM_KERNEL=v4: the LDS-DMA row kernel)
@@ -913,10 +914,15 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                      csm::phase_supported(D.n_space, PT.cells, PT.nq) &&
                      c->pitch >= c->info.size_x + csm::kGridiPadCols;
   if (phase) rows_sq = 0;
+  // v8 tiny-window kernel: a sub-cell step whose whole span is under one cell
+  const bool tiny = !box && !phase && use_int && c->tiny_kernel && f < 1.0 && csm::tiny_supported(D.n_space, f) &&
+                    c->pitch >= c->info.size_x + csm::kGridiPadCols &&
+                    (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows) * 4 < INT32_MAX;
+  if (tiny) rows_sq = 0;
   const int cpl = pick_cpl(D.n_cand);
   const int64_t per_block = (int64_t)csm::kBlock * cpl;
   const int64_t rows_groups = rows_sq ? 64 / D.n_space : 1;
-  const int64_t bps = (box || phase) ? D.n_angles
+  const int64_t bps = (box || phase || tiny) ? D.n_angles
                       : rows_sq ? (D.n_angles + rows_groups - 1) / rows_groups
                       : v2    ? col_blocks * ktiles
                               : (D.n_cand + per_block - 1) / per_block;
@@ -987,6 +993,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     std::snprintf(kname, sizeof(kname), "score_box_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (phase)
     std::snprintf(kname, sizeof(kname), "score_phase_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
+  else if (tiny)
+    std::snprintf(kname, sizeof(kname), "score_tiny_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (rows_sq)
     std::snprintf(kname, sizeof(kname), "%s<%d,%d,%s>", c->row_dma ? "score_rowsd_kernel" : "score_rows_kernel",
                   D.n_space, rows_sq, best_out ? "best" : "all");
@@ -1010,6 +1018,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       e = csm::launch_score_phase(L, PT, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                   (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
                                   c->stream);
+    else if (tiny)
+      e = csm::launch_score_tiny(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                 (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space, c->stream);
     else if (rows_sq)
       e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr,
@@ -1073,6 +1084,10 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       e = csm::launch_score_phase(L, PT, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                   (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
                                   D.n_space, c->stream);
+    else if (tiny)
+      e = csm::launch_score_tiny(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                 (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p, D.n_space,
+                                 c->stream);
     else if (rows_sq)
       e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                  (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
@@ -1890,7 +1905,9 @@ int csm_create(int device, csm_ctx** out) {
     c->row_kernel = std::strcmp(env, "v1") != 0 && std::strcmp(env, "v2") != 0;
     c->row_dma = std::strcmp(env, "v3") != 0;
     c->box_kernel = std::strcmp(env, "v6") == 0 || std::strcmp(env, "v7") == 0;
-    c->phase_kernel = std::strcmp(env, "v7") == 0;
+    c->box_kernel = c->box_kernel || std::strcmp(env, "v8") == 0;
+    c->phase_kernel = std::strcmp(env, "v7") == 0 || std::strcmp(env, "v8") == 0;
+    c->tiny_kernel = std::strcmp(env, "v8") == 0;
   }
   if (const char* env = std::getenv("CSM_PHASE_MARGIN_LOG2"))
     c->phase_margin_log2 = std::max(2, std::min(std::atoi(env), 20));

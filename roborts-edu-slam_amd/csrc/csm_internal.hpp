@@ -177,6 +177,13 @@ struct TreeWork {
 hipError_t launch_score_tree(const TreeWork& T, const ScanWork* d_scans, const double* d_pts,
                              const AngleEntry* d_angles, double* d_out, hipStream_t stream);
 
+// Tiny-window kernel (v8, csm_tiny.hip): INT mode, 2 <= n_space <= 4 with
+// (n_space - 1) * step < 1 cell; one wave per (window, angle), lanes are
+// beams. blocks_per_scan = n_angles.
+bool tiny_supported(int ns, double f);
+hipError_t launch_score_tiny(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
+                             const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
+                             hipStream_t stream);
 // Box kernel (v6, csm_box.hip): INT mode, window step exactly one cell,
 // n_space <= 16; one wave per (window, angle), one 16-byte row piece per lane
 // per beam. blocks_per_scan = n_angles.

@@ -233,9 +233,9 @@ def test_batch_three_level_bit_exact(ctx, world2000, which):
 
 def test_headline_runs_row_segment_kernels(ctx, world2000):
     """The config-2 levels run on the box kernel (coarse: one-cell step), the
-    phase kernel (fine: 0.4-cell step) and the LDS-DMA row-segment kernel
-    (super-fine), not a fallback, and the device finish, and the result is the
-    oracle's bit for bit."""
+    phase kernel (fine: 0.4-cell step) and the tiny-window kernel (super-fine:
+    a 0.4-cell span), not a fallback, and the device finish, and the result is
+    the oracle's bit for bit."""
     from roborts_csm.params import headline_levels
     w, b = world2000
     ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
@@ -247,7 +247,7 @@ def test_headline_runs_row_segment_kernels(ctx, world2000):
     names = {k["name"] for k in ctx.kernel_stats()}
     ctx.set_profiling(False)
     for want in ("score_box_kernel<13,all>", "score_phase_kernel<11,all>",
-                 "score_rowsd_kernel<3,1,all>", "finish_kernel<5070>"):
+                 "score_tiny_kernel<3,all>", "finish_kernel<5070>"):
         assert want in names, names
     m = O.Map(w.grid, w.resolution, w.offset)
     s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(),
@@ -365,7 +365,7 @@ def test_kernel_variants_agree(f1, grid_kind):
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
     ctxs = []
-    for kern in ("v1", "v2", "v3", "v4", "v6", None):  # None: default (v6 box / v7 phase / v4 where eligible)
+    for kern in ("v1", "v2", "v3", "v4", "v6", "v7", None):  # None: default (v6 box / v7 phase / v8 tiny / v4)
         if kern:
             os.environ["CSM_KERNEL"] = kern
         try:
@@ -725,6 +725,56 @@ def test_phase_kernel_edge_beams(world2000, margin_log2):
             assert got.score == s and got.flat_index == flat
     names = {k["name"] for k in ctxs[0].kernel_stats()}
     assert "score_phase_kernel<11,all>" in names and "score_phase_kernel<11,best>" in names, names
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.parametrize("size,res", [(0.02, 0.01), (0.01, 0.01), (0.03, 0.01), (0.015, 0.005)])
+def test_tiny_kernel_edge_beams(world2000, size, res):
+    """v8 tiny-window kernel (spans under one cell: the super-fine level, 3 x 3
+    steps of 0.2 cells, and 2 x 2 / 4 x 4 / 0.1-cell variants) on its edge
+    cases: origin points on rounding boundaries, beams off the grid's low edge
+    (negative indices: the cell-by-cell path) and far past the high edges,
+    windows at inexact step sums, every beam summed (several 16-chunk folds).
+    Scores and argmax against the oracle and the v4 row kernel."""
+    import roborts_csm
+    from roborts_csm.params import SIM_YAML_LEVELS
+    w, b = world2000
+    m = O.Map(w.grid, w.resolution, w.offset)
+    pts = np.concatenate([b.points_cells[b.offsets[k]:b.offsets[k + 1]] for k in range(2)])
+    extra = np.array([[0.0, 0.0], [0.0, 0.0], [1.0, -2.0], [-1500.0, 3.0], [2.0, -1500.0],
+                      [900.0, 900.0], [-3000.0, -3000.0], [0.25, 0.0], [0.2, 0.6], [-0.4, 0.8],
+                      [0.5, 0.5], [-0.5, -0.5]])
+    pts = np.ascontiguousarray(np.concatenate([pts, extra]))
+    lv = SIM_YAML_LEVELS[2].with_(search_space_size=size, search_space_resolution=res,
+                                  use_point_size=pts.shape[0])
+    na, ns = roborts_csm.window_dims(lv)
+    assert 2 <= ns <= 4
+    half = (lv.search_space_size / w.resolution) * 0.5
+    centers = [[100.5 + half, 200.5 + half, 0.0], [100.7 + half, 200.9 + half, 1.3],
+               [100.3 + half, 200.1 + half, -0.4], [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
+               [0.2, 0.1, -2.5], [1999.6, 1999.7, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
+    ctxs = []
+    for kern in (None, "v4"):
+        if kern:
+            os.environ["CSM_KERNEL"] = kern
+        try:
+            ctxs.append(roborts_csm.Context(0))
+        finally:
+            os.environ.pop("CSM_KERNEL", None)
+    for c in ctxs:
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+    ctxs[0].set_profiling(True)
+    for cen in centers:
+        cen = np.array(cen)
+        want = O.score_window(m, pts, lv, cen, na * ns * ns)
+        for c in ctxs:
+            assert np.array_equal(c.score_window(pts, lv, cen), want), cen
+            got = c.best_window(pts, lv, cen)
+            s, flat = O.best_window(m, pts, lv, cen)
+            assert got.score == s and got.flat_index == flat
+    names = {k["name"] for k in ctxs[0].kernel_stats()}
+    assert f"score_tiny_kernel<{ns},all>" in names and f"score_tiny_kernel<{ns},best>" in names, names
     for c in ctxs:
         c.close()
 
