@@ -40,7 +40,7 @@ namespace {
 // Waves per window of the exact path. Segments are handed out level by level
 // with barriers in between (an earlier version pulled them from a spin-locked
 // LDS stack and, rarely, spun past its iteration bound).
-constexpr int kWaves = 4;
+constexpr int kWaves = kFinishWaves;
 // Partial sort (positions past what the ordered scans read stay unsorted) for
 // windows of at least this many candidates; kNearRounds: tighten the second
 // stage's limit to the 20th near-best score (20 block-wide rounds) instead of
@@ -81,7 +81,7 @@ struct WaveScratch {      // per-wave LDS scratch of the register sort
 
 static_assert(sizeof(WaveScratch) <= kFinishWaveScratch, "finish_layout wave scratch");
 
-struct Shared {           // misc block of the LDS carve (finish_layout: 128 B)
+struct Shared {           // misc block of the LDS carve (finish_layout: kFinishMisc bytes)
   int plim, top, pending, pad;
   double bx, by;
   int ndef, cnt_a, cnt_b, nan;
@@ -89,7 +89,7 @@ struct Shared {           // misc block of the LDS carve (finish_layout: 128 B)
   int wl[kWaves], wr[kWaves];  // partition_block: per-wave counts
   int fail;                    // partition_block: first rank that is not a pair
 };
-static_assert(sizeof(Shared) <= 128, "finish_layout misc block");
+static_assert(sizeof(Shared) <= kFinishMisc, "finish_layout misc block");
 
 // Block-wide reductions (all threads of the 4-wave block must call them).
 __device__ double block_max(double v, Shared* sh, int wave) {

@@ -102,7 +102,14 @@ struct FinishOut {
   double ang_score[kCovPoints];
 };
 
-constexpr int kFinishWaveScratch = 640;  // bytes of per-wave scratch (4 waves)
+constexpr int kFinishWaveScratch = 640;  // bytes of per-wave scratch
+#ifndef CSM_FINISH_WAVES
+#define CSM_FINISH_WAVES 4
+#endif
+constexpr int kFinishWaves = CSM_FINISH_WAVES;  // waves per window of the exact finish
+// misc block of the finish carve (csm_finish.hip Shared): counts, limits,
+// best (x, y), per-wave reductions
+constexpr size_t kFinishMisc = (48 + 16 * (size_t)kFinishWaves + 4 + 15) & ~(size_t)15;
 
 struct FinishLayout {
   size_t wave_scratch, defer, keys, vals, lpos, rpos, stack, total;
@@ -110,13 +117,13 @@ struct FinishLayout {
 constexpr int kFinishDefer = 64;  // segments the partial sort may set aside (12 B each)
 
 // LDS carve of the finish kernel for n candidates (16-byte aligned pieces):
-// misc | 4 wave scratches | deferred segments | keys f64[n] | vals u16[n] |
+// misc | kFinishWaves wave scratches | deferred segments | keys f64[n] | vals u16[n] |
 // lpos u16[n] | rpos u16[n] | shared segment stack.
 constexpr FinishLayout finish_layout(int64_t n) {
   FinishLayout L{};
-  size_t o = 128;  // misc (csm_finish.hip Shared): list counts, limits, best (x, y), reductions
+  size_t o = kFinishMisc;
   L.wave_scratch = o;
-  o += 4 * (size_t)kFinishWaveScratch;
+  o += (size_t)kFinishWaves * kFinishWaveScratch;
   L.defer = o;
   o += (size_t)kFinishDefer * 12;
   L.keys = o;

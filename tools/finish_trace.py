@@ -19,6 +19,9 @@ from roborts_csm.params import headline_levels  # noqa: E402
 lib = C.CDLL(os.environ["CSM_LIB"])
 lib.csm_debug_finish_trace.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 n_scans = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+# optional: which headline levels to run as the three levels (e.g. "2,2,2":
+# the super-fine window three times)
+level_sel = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else None
 world = worlds.make_world(2000, 2000, 0.05, seed=20261015)
 batch = worlds.make_scan_batch(world, n_scans, seed=1000)
 ctx = roborts_csm.Context(0)
@@ -29,11 +32,16 @@ for it in range(2):
     lib.csm_debug_finish_trace(buf, 256)  # reset
     poses = np.ascontiguousarray(batch.init_poses.copy())
     covs = np.ascontiguousarray(np.tile(np.eye(3).reshape(1, 9), (n_scans, 1)))
-    ctx.scan_matchers_loaded(headline_levels(), poses, covs)
+    lv = headline_levels()
+    ctx.scan_matchers_loaded([lv[i] for i in level_sel] if level_sel else lv, poses, covs)
 n = lib.csm_debug_finish_trace(buf, 256)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 10)[:n].astype(np.int64)
 print("windows traced:", n)
 print("   n  plim   load  count  sort  find  stage2 lists  total  (us)")
+rows = []
 for r in a:
     d = np.diff(r[:7]) / 100.0  # wall_clock64: 100 MHz
+    rows.append(list(d) + [(r[6] - r[0]) / 100.0])
     print("%5d %5d " % (r[9], r[8]) + " ".join("%6.1f" % x for x in d) + "  %6.1f" % ((r[6] - r[0]) / 100.0))
+if rows:
+    print("mean        " + " ".join("%6.1f" % x for x in np.mean(np.array(rows), axis=0)))
