@@ -216,7 +216,7 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
     offsets = np.tile(np.array(bases[0].offset), (hi - lo, 1))
     param = CorrelationScanMatchParam(16.0, 0.05, math.pi, 0.0349, 0.5, 100, 0, False, 0)
     na, ns = roborts_csm.window_dims(param)
-    ctx = roborts_csm.Context(int(os.environ.get("LOCAL_RANK", "0")))
+    ctx = roborts_csm.Context(_device())
     ctx.set_grid_stack(stack, res, version=1)
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     lc = ShardedLoopClosure(ctx, n_sub, res, offsets, rank=rank, world=world_size, device=dev,
@@ -323,7 +323,7 @@ def willow_bench(args, rank, world_size, dist, torch):
     batch = worlds.make_scan_batch(w, max(1, args.steps + args.warmup), seed=31 + rank)
     param = CorrelationScanMatchParam(args.window_m, 0.05, math.pi, 0.0349, 0.5, 1081, 0, False, 0)
     na, ns = roborts_csm.window_dims(param)
-    ctx = roborts_csm.Context(int(os.environ.get("LOCAL_RANK", "0")))
+    ctx = roborts_csm.Context(_device())
     ctx.set_grid(roborts_csm.ScanMatchMap(w.grid, w.resolution, w.offset, 0, 1))
     from roborts_csm.loop_closure import world_to_map
 
@@ -508,8 +508,8 @@ def online_bench(args, rank, world_size, dist, torch):
     n = args.warmup + args.steps
     world = worlds.make_world(2000, 2000, 0.05, seed=20261015)
     stream = worlds.make_scan_stream(world, n, seed=77 + rank)
-    fe = SlamFrontEnd(FrontEndParam(), device=int(os.environ.get("LOCAL_RANK", "0")))
-    be = _AttachedBackEnd(int(os.environ.get("LOCAL_RANK", "0"))) if args.attach_backend else None
+    fe = SlamFrontEnd(FrontEndParam(), device=_device())
+    be = _AttachedBackEnd(_device()) if args.attach_backend else None
     for k in range(args.warmup):
         r = fe.process(stream.points_m[k], stream.odom_poses[k])
         if be is not None and r.map_updated:
@@ -626,7 +626,7 @@ def backend_bench(args, rank, world_size, dist, torch):
     w = worlds_mod().make_world(1000, 1000, 0.05, seed=20261015)
     st = worlds_mod().make_scan_stream(w, n_scans, seed=55 + rank)
     prm = BackEndParam()
-    svc = ScanMatchService(prm, device=int(os.environ.get("LOCAL_RANK", "0")))
+    svc = ScanMatchService(prm, device=_device())
     for k in range(n_scans):
         svc.AddRangeData(st.points_m[k], st.true_poses[k])
     pub = OccuGridMap(w.resolution, (w.size_x, w.size_y), w.offset, 0.0, 0.5, kind=1)
@@ -798,6 +798,16 @@ def spawn_ranks(n: int) -> int:
     return next((c for c in codes if c != 0), 0)
 
 
+def _device() -> int:
+    """This rank's GPU: LOCAL_RANK, or LOCAL_RANK modulo the visible devices
+    when CSM_BENCH_SHARE_GPU=1 (rehearsing N ranks on fewer GPUs, gloo)."""
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("CSM_BENCH_SHARE_GPU") == "1":
+        import torch
+        return lr % max(1, torch.cuda.device_count())
+    return lr
+
+
 def worlds_mod():
     from roborts_csm import worlds
     return worlds
@@ -845,7 +855,7 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = _device()
     if world_size != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_size}")
     dist = None
