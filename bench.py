@@ -58,6 +58,8 @@ METRIC = "candidate-pose scorings/sec (1081-beam scan, 2000×2000 grid) at 1/2/4
 HBM_PEAK_GBS = 8000.0
 N_CU, N_SIMD, CLK_GHZ = 256, 1024, 2.4
 COUNTERS_JSON = os.path.join(ROOT, "profiles", "r02", "counters.json")
+# the loop-closure / willow legs' counters (tools/pmc_topbox.sh: the search's top-level kernel)
+COUNTERS_LC_JSON = os.path.join(ROOT, "profiles", "r02", "counters_lc.json")
 CSRC = os.path.join(ROOT, "roborts-edu-slam_amd", "csrc")
 
 
@@ -241,11 +243,14 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     total = float(n_sub) * na * ns * ns * args.steps
-    kst = [s for s in stats if not s["name"].startswith("host:")]
+    # the dominant kernel; the search's own aggregate ("pyramid_search") is
+    # not a kernel: its top-level kernel is priced instead
+    kst = [s for s in stats if not s["name"].startswith("host:") and s["name"] != "pyramid_search"]
+    kst = kst or [s for s in stats if not s["name"].startswith("host:")]
     dom = max(kst, key=lambda s: s["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
-    rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"],
-                  load_counters(args.counters_json), args.counters_json)
+    cj = COUNTERS_LC_JSON if args.counters_json == COUNTERS_JSON else args.counters_json
+    rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"], load_counters(cj), cj)
     search = None
     if args.search == "pyramid":
         st = lc.last_stats or {}
@@ -380,11 +385,14 @@ def willow_bench(args, rank, world_size, dist, torch):
         elapsed, total = float(e.item()), float(s.item())
     else:
         total = local
-    kst = [s for s in stats if not s["name"].startswith("host:")]
+    # the dominant kernel; the search's own aggregate ("pyramid_search") is
+    # not a kernel: its top-level kernel is priced instead
+    kst = [s for s in stats if not s["name"].startswith("host:") and s["name"] != "pyramid_search"]
+    kst = kst or [s for s in stats if not s["name"].startswith("host:")]
     dom = max(kst, key=lambda s: s["total_ms"])
     avg_ms = dom["total_ms"] / dom["launches"]
-    rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"],
-                  load_counters(args.counters_json), args.counters_json)
+    cj = COUNTERS_LC_JSON if args.counters_json == COUNTERS_JSON else args.counters_json
+    rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"], load_counters(cj), cj)
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu:
         import pyoracle as O

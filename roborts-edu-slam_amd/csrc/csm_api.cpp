@@ -2573,6 +2573,7 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
     in.depth = depth;
     in.top_mode = options ? options->top_kernel : 0;
     in.box_ok = box_ok ? 1 : 0;
+    in.timed = c->profiling ? 1 : 0;
     in.one_scan = 1;  // the windows share the one scan: check what the implicit top level relies on
     for (const WindowPlan& W : plans)
       if (W.use != W0.use || W.n_used != W0.n_used || W.step != W0.step) in.one_scan = 0;
@@ -2599,7 +2600,10 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
     S.syncs = ps.syncs;
     S.top_box = ps.top_box;
     // one grid read per beam per scored node (the pooled levels included)
-    if (c->profiling) c->account("pyramid_search", ms, (double)S.beam_reads * 4.0, (double)S.candidates);
+    if (c->profiling) {
+      c->account("pyramid_search", ms, (double)S.beam_reads * 4.0, (double)S.candidates);
+      if (ps.top_name[0]) c->account(ps.top_name, (float)ps.top_ms, ps.top_bytes, 0.0);
+    }
   }
   if (b.flat == INT64_MAX) return c->fail(CSM_ERR_HIP, "search found no candidate");
   const int32_t w = (int32_t)(b.flat / D.n_cand);

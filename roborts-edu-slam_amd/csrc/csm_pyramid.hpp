@@ -128,6 +128,11 @@ struct PyrStats {
   int64_t slices = 0;                    // expand launches
   int64_t syncs = 0;                     // node counts read back by the host
   int32_t top_box = 0;                   // 1: the top level ran as beam boxes
+  // PyrInputs::timed: the top-level kernel's time (HIP events around its
+  // launch), its name as csm_kernel_stats reports it, and its algorithmic
+  // bytes (one int16 pooled value per node and beam)
+  double top_ms = 0.0, top_bytes = 0.0;
+  char top_name[48] = {0};
   double build_ms = 0.0;                 // pooled levels built (0 when cached)
 };
 
@@ -145,6 +150,7 @@ struct PyrInputs {
   int32_t top_mode;         // 0: beam boxes when eligible, 1: per-node gathers
   int32_t box_ok;           // every window's |t| < 2^24 cells (the box test's bound)
   int32_t one_scan;         // every window has the same divisor and beam count
+  int32_t timed;            // time the top-level kernel (PyrStats::top_ms)
 };
 
 class PyramidSearch {

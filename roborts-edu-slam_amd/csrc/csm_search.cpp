@@ -19,6 +19,7 @@
 #include <cfloat>
 #include <chrono>
 #include <climits>
+#include <cstdio>
 #include <vector>
 
 namespace csm {
@@ -71,6 +72,7 @@ struct PyramidSearch::Impl {
   int top_implicit = -1;  // its depth while a search runs (-1: the top is a node list)
   int32_t top_nj = 0;
   unsigned long long* h_counts = nullptr;  // pinned: counts read back, then scored
+  hipEvent_t ev_top[2] = {nullptr, nullptr};  // PyrInputs::timed
   int64_t cap = (int64_t)1 << 24;
   int probe_min = 4096;
   static constexpr int kRoots = 8;  // probe roots per probe (best partials of distinct blocks)
@@ -79,6 +81,13 @@ struct PyramidSearch::Impl {
 
   ~Impl() {
     if (h_counts) (void)hipHostFree(h_counts);
+    for (hipEvent_t e : ev_top)
+      if (e) (void)hipEventDestroy(e);
+  }
+  hipError_t mark_top(int i, hipStream_t stream) {
+    hipError_t e;
+    if (!ev_top[i] && (e = hipEventCreate(&ev_top[i])) != hipSuccess) return e;
+    return hipEventRecord(ev_top[i], stream);
   }
 
   hipError_t build(const PyrInputs& x) {
@@ -312,9 +321,16 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
     if ((e = I.partials.ensure((size_t)std::max<int64_t>(box_blocks, pyr_blocks(INT64_MAX / 2)) *
                                sizeof(PyrPartial))) != hipSuccess)
       return fail(e, "pyramid partials");
+    if (x.timed && (e = I.mark_top(0, x.stream)) != hipSuccess) return fail(e, "hipEventRecord");
     if ((e = launch_pyr_topbox(x.L, I.boxg, D, (int32_t)nj, x.scans, x.angles, x.pts, x.n_used, x.step,
                                (int32_t*)I.top_sums.p, (PyrPartial*)I.partials.p, x.stream)) != hipSuccess)
       return fail(e, "pyr_topbox_kernel");
+    if (x.timed) {
+      if ((e = I.mark_top(1, x.stream)) != hipSuccess) return fail(e, "hipEventRecord");
+      std::snprintf(I.st->top_name, sizeof(I.st->top_name), "pyr_topbox_kernel<%d,%d>", npc,
+                    (int)((nj * npc + 63) / 64));
+      I.st->top_bytes = (double)n_top * (double)x.n_used * 2.0;
+    }
     top_scored = n_top;
     I.st->top_box = 1;
     I.top_implicit = D;
@@ -354,6 +370,11 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
     return fail(e, "node counters copy");
   if ((e = hipStreamSynchronize(x.stream)) != hipSuccess) return fail(e, "pyramid search");
   for (int d = 0; d <= kPyrMaxDepth; ++d) I.st->nodes[d] = (int64_t)h_scored[d];
+  if (x.timed && I.st->top_name[0]) {
+    float ms = 0.f;
+    if ((e = hipEventElapsedTime(&ms, I.ev_top[0], I.ev_top[1])) != hipSuccess) return fail(e, "hipEventElapsedTime");
+    I.st->top_ms = ms;
+  }
   I.st->nodes[D] += top_scored;
   return hipSuccess;
 }

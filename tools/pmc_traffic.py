@@ -37,6 +37,11 @@ def _short(name: str) -> str:
         i = name.index(key) + len(key)
         args = [a.strip() for a in name[i:name.index(">", i)].split(",")]
         return f"score_box_kernel<{args[0]},{'best' if args[-1] == 'true' else 'all'}>"
+    key = "pyr_topbox_kernel<"
+    if key in name:  # <int NP, int NL>
+        i = name.index(key) + len(key)
+        args = [a.strip() for a in name[i:name.index(">", i)].split(",")]
+        return f"pyr_topbox_kernel<{args[0]},{args[1]}>"
     key = "score_tiny_kernel<"
     if key in name:  # <int NS, bool BEST>
         i = name.index(key) + len(key)
