@@ -142,11 +142,12 @@ __device__ __forceinline__ void block_best(double v, int64_t f, uint64_t nd, Pyr
   }
 }
 
-// One lane per node (blocks stride over the list): the sum over the scan's
-// beams of the level-d value at the anchor candidate's cell (GetResponse
-// :645-654 with the pooled level in place of the grid); d = 0 is the
-// candidate's exact, penalised score.
-template <typename T>
+// LPN lanes per node (blocks stride over the list; a node's lanes take every
+// LPN-th beam and meet by shuffles): the sum over the scan's beams of the
+// level-d value at the anchor candidate's cell (GetResponse :645-654 with the
+// pooled level in place of the grid); d = 0 is the candidate's exact,
+// penalised score. Integer sums: the split changes nothing.
+template <typename T, int LPN>
 __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev, int d,
                                                         const ScanWork* __restrict__ scans,
                                                         const AngleEntry* __restrict__ angles,
@@ -166,7 +167,8 @@ __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev
   uint64_t bn = kPyrNoNode;
   const int sh = lev.shift, W = lev.width, H = lev.height, pitch = lev.pitch, lg = lev.lg, qc = lev.q;
   const int pm = (1 << lg) - 1;
-  for (int64_t i = (int64_t)blockIdx.x * kPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kPB) {
+  const int sub = (int)(threadIdx.x % LPN);
+  for (int64_t i = ((int64_t)blockIdx.x * kPB + threadIdx.x) / LPN; i < n; i += (int64_t)gridDim.x * (kPB / LPN)) {
     const uint64_t nd = nodes[i];
     int w, a, J, K;
     node_decode(nd, w, a, J, K);
@@ -174,13 +176,13 @@ __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev
     const bool valid = nd != kPyrNoNode && w < L.n_scans && a < L.n_angles && j0 < L.n_space && k0 < L.n_space;
     double v = -1.0e300;
     int64_t gflat = INT64_MAX;
+    int64_t sum = 0;
     if (valid) {
       const ScanWork S = scans[w];
       const AngleEntry ae = angles[S.angle_off + a];
       const double x = S.x0 + j0 * L.step_cells;  // :569
       const double y = S.y0 + k0 * L.step_cells;  // :572
       const T* __restrict__ g = (const T*)lev.g + (int64_t)S.grid_index * lev.stride;
-      int64_t sum = 0;
       auto cell = [&](int b) -> int32_t {
         const double2 p = beams[b];
         const double lx = ae.cosine * p.x - ae.sine * p.y;
@@ -192,15 +194,23 @@ __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev
         const int32_t c = g[in ? idx : 0];
         return in ? c : 0;
       };
-      int b = 0;
-      for (; b + 8 <= n_used; b += 8) {  // 8 gathers in flight per lane
+      int b = sub;
+      for (; b + 7 * LPN < n_used; b += 8 * LPN) {  // 8 gathers in flight per lane
         int32_t c[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) c[u] = cell(b + u);
+        for (int u = 0; u < 8; ++u) c[u] = cell(b + u * LPN);
         // |c| < 2^26: eight fit an int32
         sum += (int64_t)(((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7])));
       }
-      for (; b < n_used; ++b) sum += cell(b);
+      for (; b < n_used; b += LPN) sum += cell(b);
+    }
+#pragma unroll
+    for (int o = LPN / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);  // the node's lanes (all valid or none)
+    if (valid) {
+      const ScanWork S = scans[w];
+      const AngleEntry ae = angles[S.angle_off + a];
+      const double x = S.x0 + j0 * L.step_cells;  // :569
+      const double y = S.y0 + k0 * L.step_cells;  // :572
       sum <<= lev.qs;  // the quantised levels' unit
       const double acc = (double)(sum + (int64_t)n_used * L.outside_i) * L.int_scale;
       if (d == 0) {
@@ -211,7 +221,7 @@ __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev
       }
       gflat = (int64_t)w * L.n_cand + ((int64_t)a * L.n_space + j0) * L.n_space + k0;
     }
-    vals[i] = v;
+    if (sub == 0) vals[i] = v;
     if (better(v, gflat, bv, bf)) {
       bv = v;
       bf = gflat;
@@ -338,13 +348,18 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
                                                           const ScanWork* __restrict__ scans,
                                                           const AngleEntry* __restrict__ angles,
                                                           const double2* __restrict__ pts, int32_t n_used,
-                                                          int32_t step, int32_t* __restrict__ sums,
+                                                          int32_t step, int split, int32_t* __restrict__ sums,
                                                           PyrPartial* __restrict__ partials) {
   constexpr int GB = NL == 1 ? 8 : 4;  // beams whose loads are issued together
   __shared__ int32_t odd_sum[32][8 * 5 + 8];
-  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  // split > 1 (few windows): `split` waves per (window, angle), each over a
+  // contiguous range of the beams, adding their sums into `sums` (zeroed by
+  // the host); pyr_topbox_final_kernel then bounds the nodes
+  const int bid0 = dev::xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = bid0 / split, part = bid0 - (bid0 / split) * split;
   const int w = bid / L.n_angles;
   const int a = bid - w * L.n_angles;
+  const int b_lo = (int)((int64_t)n_used * part / split), b_hi = (int)((int64_t)n_used * (part + 1) / split);
   const ScanWork S = scans[w];
   const AngleEntry ae = angles[S.angle_off + a];
   const int lane = threadIdx.x;
@@ -396,18 +411,18 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
       acc[2 * t + 1] += v[t] >> 16;                // high half: element 2t + 1
     }
   };
-  uint64_t slow = 0;
-  double2 pn = pts[(int64_t)min(lane, n_used - 1) * step];
-  for (int cb = 0; cb < n_used; cb += 64) {
+  uint64_t slow = 0;  // bit c: chunk c of this wave's range holds a rejected beam
+  double2 pn = pts[(int64_t)min(b_lo + lane, n_used - 1) * step];
+  for (int cb = b_lo; cb < b_hi; cb += 64) {
     const double2 p = pn;
     pn = pts[(int64_t)min(cb + 64 + lane, n_used - 1) * step];
     double lx, ly;
     int el;
     const bool clean = test(p, lx, ly, el);
-    const bool live = cb + lane < n_used;
+    const bool live = cb + lane < b_hi;
     if (!live) el = zero_el;
-    slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean) != 0) << min(cb >> 6, 63);
-    const int nb = min(64, n_used - cb);
+    slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean) != 0) << min((cb - b_lo) >> 6, 63);
+    const int nb = min(64, b_hi - cb);
     for (int r = 0; r < nb; r += GB) {  // beams past nb read the zero rows
       int so[GB];
 #pragma unroll
@@ -448,13 +463,13 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
   // rejected beams, node by node (pyr_top_bound_kernel's expressions)
   for (uint64_t m = slow; m != 0; m &= m - 1) {
     const int c0 = (int)__builtin_ctzll(m);
-    const int c_end = c0 == 63 ? (n_used + 63) / 64 : c0 + 1;
+    const int c_end = c0 == 63 ? (b_hi - b_lo + 63) / 64 : c0 + 1;
     for (int c = c0; c < c_end; ++c) {
-      const int cb = c * 64;
+      const int cb = b_lo + c * 64;
       double lx, ly;
       int el;
       const bool clean = test(pts[(int64_t)min(cb + lane, n_used - 1) * step], lx, ly, el);
-      for (uint64_t rej = __builtin_amdgcn_ballot_w64(cb + lane < n_used && !clean); rej != 0; rej &= rej - 1) {
+      for (uint64_t rej = __builtin_amdgcn_ballot_w64(cb + lane < b_hi && !clean); rej != 0; rej &= rej - 1) {
         const int l = (int)__builtin_ctzll(rej);  // uniform: one beam for the whole wave
         const double bx = dev::bcast_lane(lx, l);
         const double by = dev::bcast_lane(ly, l);
@@ -477,6 +492,16 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
   int64_t bf = INT64_MAX;
   uint64_t bn = kPyrNoNode;
   const int64_t wbase = ((int64_t)w * L.n_angles + a) * nj;
+  if (split > 1) {  // partial sums of this beam range
+#pragma unroll
+    for (int s = 0; s < NL; ++s)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int J = 8 * cs[s] + t, K = Ks[s];
+        if (act[s] && J < nj) atomicAdd(&sums[(wbase + K) * nj + J], acc[s][t]);
+      }
+    return;
+  }
 #pragma unroll
   for (int s = 0; s < NL; ++s) {
 #pragma unroll
@@ -493,6 +518,34 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
           bn = nd;
         }
       }
+    }
+  }
+  block_best<64>(bv, bf, bn, partials + bid);
+}
+
+// After a split pyr_topbox_kernel: each (window, angle)'s node bounds from the
+// summed integers and its best (one wave per (window, angle), as the
+// unsplit kernel writes them).
+__global__ __launch_bounds__(64) void pyr_topbox_final_kernel(LevelWork L, int d, int32_t nj, int qs, int32_t n_used,
+                                                              const ScanWork* __restrict__ scans,
+                                                              const int32_t* __restrict__ sums,
+                                                              PyrPartial* __restrict__ partials) {
+  const int bid = blockIdx.x;
+  const int w = bid / L.n_angles;
+  const int a = bid - w * L.n_angles;
+  const ScanWork S = scans[w];
+  const int64_t wbase = ((int64_t)w * L.n_angles + a) * nj;
+  double bv = -1.0e300;
+  int64_t bf = INT64_MAX;
+  uint64_t bn = kPyrNoNode;
+  for (int i = threadIdx.x; i < nj * nj; i += 64) {
+    const int K = i / nj, J = i - K * nj;
+    const double v = level_bound(L, S, sums[wbase * nj + i], qs, n_used);
+    const int64_t gflat = (int64_t)w * L.n_cand + ((int64_t)a * L.n_space + (J << d)) * L.n_space + (K << d);
+    if (better(v, gflat, bv, bf)) {
+      bv = v;
+      bf = gflat;
+      bn = pyr_node((uint32_t)w, (uint32_t)a, (uint32_t)J, (uint32_t)K);
     }
   }
   block_best<64>(bv, bf, bn, partials + bid);
@@ -726,19 +779,34 @@ int pyr_blocks(int64_t upper) {
   return (int)(b < 1 ? 1 : b);
 }
 
+int pyr_bound_lanes(int32_t n_used) { return n_used >= 1024 ? 8 : n_used >= 512 ? 4 : 1; }
+
+int pyr_bound_blocks(int64_t upper, int32_t n_used) { return pyr_blocks(upper * pyr_bound_lanes(n_used)); }
+
 hipError_t launch_pyr_bound(const LevelWork& L, const PyrGrid& lev, int d, const ScanWork* scans,
                             const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
                             const uint64_t* nodes, int64_t n, const unsigned long long* n_dev, int64_t upper,
                             double* vals, PyrPartial* partials, unsigned long long* scored, hipStream_t stream) {
   if (upper <= 0) return hipSuccess;
-  if (lev.qs == 0)
-    hipLaunchKernelGGL(pyr_bound_kernel<int32_t>, dim3(pyr_blocks(upper)), dim3(kPB), (size_t)n_used * sizeof(double2),
-                       stream, L, lev, d, scans, angles, reinterpret_cast<const double2*>(pts), n_used, step, nodes, n,
-                       n_dev, vals, partials, scored);
-  else
-    hipLaunchKernelGGL(pyr_bound_kernel<int16_t>, dim3(pyr_blocks(upper)), dim3(kPB), (size_t)n_used * sizeof(double2),
-                       stream, L, lev, d, scans, angles, reinterpret_cast<const double2*>(pts), n_used, step, nodes, n,
-                       n_dev, vals, partials, scored);
+  // long scans: several lanes per node (every LPN-th beam each), so a short
+  // node list still fills the chip and each lane's gather chain is shorter
+  const int lpn = pyr_bound_lanes(n_used);
+  const unsigned blocks = (unsigned)pyr_bound_blocks(upper, n_used);
+  const size_t lds = (size_t)n_used * sizeof(double2);
+  const double2* p = reinterpret_cast<const double2*>(pts);
+#define CSM_BOUND(T, LPN)                                                                                     \
+  hipLaunchKernelGGL((pyr_bound_kernel<T, LPN>), dim3(blocks), dim3(kPB), lds, stream, L, lev, d, scans, angles, \
+                     p, n_used, step, nodes, n, n_dev, vals, partials, scored)
+  if (lev.qs == 0) {
+    if (lpn == 8) CSM_BOUND(int32_t, 8);
+    else if (lpn == 4) CSM_BOUND(int32_t, 4);
+    else CSM_BOUND(int32_t, 1);
+  } else {
+    if (lpn == 8) CSM_BOUND(int16_t, 8);
+    else if (lpn == 4) CSM_BOUND(int16_t, 4);
+    else CSM_BOUND(int16_t, 1);
+  }
+#undef CSM_BOUND
   return hipGetLastError();
 }
 
@@ -785,7 +853,7 @@ hipError_t launch_pyr_widen(const PyrGrid& src, const PyrGrid& dst, int32_t n_gr
 
 hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32_t nj, const ScanWork* scans,
                              const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
-                             int32_t* sums, PyrPartial* partials, hipStream_t stream) {
+                             int32_t* sums, PyrPartial* partials, hipStream_t stream, int* split_out) {
   const int np = pyr_topbox_pieces(nj);
   const int64_t blocks = (int64_t)L.n_scans * L.n_angles;
   if (np == 0 || blocks <= 0 || blocks > INT32_MAX || n_used < 1 || n_used > 4096 || tb.qs == 0 ||
@@ -793,11 +861,22 @@ hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32
     return hipErrorInvalidValue;
   const int nl = (nj * np + 63) / 64;
   const double2* p = reinterpret_cast<const double2*>(pts);
-#define CSM_TOPBOX(NP, NL)                                                                                       \
-  if (np == NP && nl == NL) {                                                                                  \
-    hipLaunchKernelGGL((pyr_topbox_kernel<NP, NL>), dim3((unsigned)blocks), dim3(64), 0, stream, L, tb, d, nj, \
-                       scans, angles, p, n_used, step, sums, partials);                                         \
-    return hipGetLastError();                                                                                   \
+  // few (window, angle) pairs: split each one's beams over up to 16 waves (at
+  // least 128 beams each) so the launch fills the chip
+  int split = 1;
+  while (split < 16 && blocks * split < 4096 && n_used / (2 * split) >= 128) split *= 2;
+  if (split_out) *split_out = split;
+  hipError_t e;
+  if (split > 1 &&
+      (e = hipMemsetAsync(sums, 0, (size_t)blocks * (size_t)nj * (size_t)nj * sizeof(int32_t), stream)) != hipSuccess)
+    return e;
+  const unsigned grid = (unsigned)(blocks * split);
+  bool launched = false;
+#define CSM_TOPBOX(NP, NL)                                                                                         \
+  if (!launched && np == NP && nl == NL) {                                                                       \
+    hipLaunchKernelGGL((pyr_topbox_kernel<NP, NL>), dim3(grid), dim3(64), 0, stream, L, tb, d, nj, scans, angles, \
+                       p, n_used, step, split, sums, partials);                                                   \
+    launched = true;                                                                                              \
   }
   CSM_TOPBOX(1, 1)
   CSM_TOPBOX(2, 1)
@@ -806,7 +885,12 @@ hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32
   CSM_TOPBOX(4, 2)
   CSM_TOPBOX(5, 3)
 #undef CSM_TOPBOX
-  return hipErrorInvalidValue;
+  if (!launched) return hipErrorInvalidValue;
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (split > 1)
+    hipLaunchKernelGGL(pyr_topbox_final_kernel, dim3((unsigned)blocks), dim3(64), 0, stream, L, d, nj, tb.qs, n_used,
+                       scans, sums, partials);
+  return hipGetLastError();
 }
 
 hipError_t launch_pyr_expand_top(const LevelWork& L, int d, int32_t nj, int qs, int32_t n_used, const ScanWork* scans,

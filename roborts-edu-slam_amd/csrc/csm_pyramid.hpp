@@ -72,8 +72,12 @@ hipError_t launch_pyr_top(const LevelWork& L, int32_t nj, int64_t first, int64_t
 // Node counts: n_dev (device, may be null) overrides n; `upper` (>= the
 // count) sizes the grid, whose blocks stride over the list.
 int pyr_blocks(int64_t upper);
+// Lanes per node of the bound kernel (long scans split their beams) and its
+// block count: the number of partials a bound launch writes (<= pyr_blocks's cap).
+int pyr_bound_lanes(int32_t n_used);
+int pyr_bound_blocks(int64_t upper, int32_t n_used);
 // Bounds (d >= 1) or exact scores (d = 0) of the nodes; one best per block
-// into partials (pyr_blocks(upper) entries); *scored (nullable) += the count. The windows share one scan: its
+// into partials (pyr_bound_blocks(upper, n_used) entries); *scored (nullable) += the count. The windows share one scan: its
 // n_used beams (stride step from pts) are staged in LDS.
 hipError_t launch_pyr_bound(const LevelWork& L, const PyrGrid& lev, int d, const ScanWork* scans,
                             const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
@@ -96,9 +100,11 @@ int pyr_topbox_pieces(int32_t nj);  // 16-byte pieces per node row (0: unsupport
 hipError_t launch_pyr_widen(const PyrGrid& src, const PyrGrid& dst, int32_t n_grids, hipStream_t stream);
 // Writes each node's integer sum (level units) at its index of the implicit
 // list ((window, angle, K, J), J fastest).
+// With few (window, angle) pairs each one's beams are split over several
+// waves (*split_out, nullable: how many), their sums added, then bounded.
 hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32_t nj, const ScanWork* scans,
                              const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
-                             int32_t* sums, PyrPartial* partials, hipStream_t stream);
+                             int32_t* sums, PyrPartial* partials, hipStream_t stream, int* split_out = nullptr);
 // launch_pyr_expand for nodes [first, first + n) of that implicit list; every
 // window must share one scan (divisor, beam count). thr: 2 int64 of device
 // scratch (the incumbent as integer sums).

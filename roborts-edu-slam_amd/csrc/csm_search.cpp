@@ -195,7 +195,7 @@ struct PyramidSearch::Impl {
                               (const uint64_t*)probe_nodes.p, np, nullptr, np, (double*)probe_vals.p,
                               (PyrPartial*)partials.p, nullptr, in.stream)) != hipSuccess)
       return e;
-    if ((e = launch_pyr_final((const PyrPartial*)partials.p, pyr_blocks(np), true, 0, (BestPartial*)inc.p, nullptr,
+    if ((e = launch_pyr_final((const PyrPartial*)partials.p, pyr_bound_blocks(np, in.n_used), true, 0, (BestPartial*)inc.p, nullptr,
                               in.stream)) != hipSuccess)
       return e;
     st->probe_leaves += np;
@@ -232,7 +232,7 @@ struct PyramidSearch::Impl {
     hipError_t e;
     const unsigned long long* nd = n >= 0 ? nullptr : count_dev(d);
     if ((e = bound(d, (const uint64_t*)nodes[d].p, (double*)vals[d].p, n, nd, upper)) != hipSuccess) return e;
-    return descend(d, n, upper, top, pyr_blocks(upper));
+    return descend(d, n, upper, top, pyr_bound_blocks(upper, in.n_used));
   }
 
   // nodes[d] and vals[d] are in place, the block bests in partials.

@@ -161,6 +161,29 @@ def test_top_boxes_equal_gathers(f1, stack5, size, depth, penalty):
         assert s1["nodes"] == s2["nodes"] and s1["probe_leaves"] == s2["probe_leaves"]
 
 
+@pytest.mark.parametrize("depth,penalty", [(1, False), (2, True), (3, False), (4, True)])
+def test_search_long_scans(config3, depth, penalty):
+    """Every beam of 1081-beam scans summed: the level passes split each node's
+    beams over 8 lanes (pyr_bound_lanes) and, with one or two windows, the top
+    level's beams over several waves per angle. Same answer as the exhaustive
+    device argmax, at several depths, on three submaps and on one."""
+    import roborts_csm
+    from roborts_csm.loop_closure import world_to_map
+    from roborts_csm.params import CorrelationScanMatchParam
+    bases, batch = config3
+    pts = batch.points_cells[batch.offsets[0]:batch.offsets[1]]
+    assert pts.shape[0] >= 1024
+    res = bases[0].resolution
+    p = CorrelationScanMatchParam(3.0, 0.05, 0.8, 0.0349, 0.5, pts.shape[0], 0, penalty, 0)
+    stack = np.stack([b.grid for b in bases])
+    centers = np.stack([world_to_map(batch.init_poses[0], res, b.offset) for b in bases])
+    with roborts_csm.Context(0) as c:
+        c.set_grid_stack(stack, res, version=1)
+        for gi in (np.arange(3), np.array([1])):
+            _, _, st = _check_same(c, pts, p, gi, centers[gi], max_depth=depth)
+            assert st["top_box"] and not st["exhaustive"]
+
+
 def test_search_non_unit_step_is_exhaustive(f1, stack5):
     """A window step other than one cell is outside the pooled search: the
     call falls back to the exhaustive device search, same result."""
@@ -271,6 +294,14 @@ def test_config4_willow_20m():
         b, win, st = c.search_windows(pts, p, [0], center.reshape(1, 3))
         assert win == 0 and b.score == got.score and b.flat_index == got.flat_index
         assert (b.x, b.y, b.angle) == (got.x, got.y, got.angle)
+        # one window: the top level's beams are split over several waves per
+        # angle, their sums added; the same answer and top level as the
+        # per-node gathers (the levels below may differ: the probe roots are
+        # the best of segments of each kernel's own block partials)
+        b2, _, st2 = c.search_windows(pts, p, [0], center.reshape(1, 3), top_kernel=1)
+        assert st["top_box"] and not st2["top_box"]
+        assert st["nodes"][st["depth"]] == st2["nodes"][st2["depth"]]
+        assert (b2.score, b2.flat_index) == (b.score, b.flat_index)
         O.set_threads(16)
         try:
             s2, f2 = O.best_window(O.Map(w.grid, w.resolution, w.offset), pts, p, center)
