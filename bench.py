@@ -904,10 +904,13 @@ def main():
     poses0 = np.ascontiguousarray(batch.init_poses)
     covs0 = np.ascontiguousarray(np.tile(np.eye(3).reshape(1, 9), (args.scans, 1)))
 
+    poses_w, covs_w = np.empty_like(poses0), np.empty_like(covs0)  # reset in place each step
+
     def step():
-        poses, covs = poses0.copy(), covs0.copy()
-        ctx.scan_matchers_loaded(levels, poses, covs)
-        return poses
+        np.copyto(poses_w, poses0)
+        np.copyto(covs_w, covs0)
+        ctx.scan_matchers_loaded(levels, poses_w, covs_w)
+        return poses_w
 
     def barrier():
         if dist is not None:
