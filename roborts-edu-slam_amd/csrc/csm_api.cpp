@@ -434,6 +434,12 @@ struct csm_ctx {
   // the kernels by events: a part's inputs go up while the other part's
   // kernels run, its results come down while the next kernels run.
   hipStream_t h2d = nullptr, d2h = nullptr;
+  // The exact finish pass (a few latency-bound blocks per launch: the flagged
+  // windows' sort chains) runs here, after the fast pass (ev_fast), so it
+  // overlaps the other part's scoring on `stream`; the part's results go down
+  // after it (ev_k on this stream). CSM_EXACT_STREAM=0: everything on `stream`.
+  hipStream_t x_stream = nullptr;
+  hipEvent_t ev_fast = nullptr;
   std::mutex mu;
   std::string err;
   float outside = 0.3f;  // kMapUnknownCellProb (slam/slam_processor.h:264)
@@ -558,6 +564,7 @@ struct csm_ctx {
     DevBuf scans, angles, scores, partials, best, fin;
     HostBuf h_scores, h_fin, h_angles, h_sw;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr, ev_in = nullptr, ev_k = nullptr;
+    hipEvent_t ev_fast = nullptr;
   };
   static constexpr int kMaxParts = 4;
   Slot alt[kMaxParts - 1];
@@ -582,6 +589,7 @@ struct csm_ctx {
     std::swap(ev_done, a.ev_done);
     std::swap(ev_in, a.ev_in);
     std::swap(ev_k, a.ev_k);
+    std::swap(ev_fast, a.ev_fast);
   }
   std::vector<csm_kernel_stat> stats;
   void account(const char* name, float ms, double bytes, double scorings) {
@@ -1056,14 +1064,16 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       A.exact_list = c->fast_finish ? A.need_exact + nw : nullptr;
       if ((e = c->h_fin.ensure(fbytes + (size_t)nw * sizeof(int32_t))) != hipSuccess)
         return c->hip_fail(e, "hipHostMalloc(finish)");
+      // the exact pass on x_stream (when there is one and the fast pass runs first)
+      hipStream_t fs = (c->x_stream && A.need_exact) ? c->x_stream : c->stream;
       if ((e = csm::launch_finish(A, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
-                                  (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw, c->stream, true)) !=
-          hipSuccess)
+                                  (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw, c->stream, fs,
+                                  c->ev_fast)) != hipSuccess)
         return c->hip_fail(e, "finish_kernel");
-      if (c->profiling && (e = hipEventRecord(c->ev2, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+      if (c->profiling && (e = hipEventRecord(c->ev2, fs)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
       // with profiling on, the flags come back too: how many windows needed the exact sort
       const size_t cbytes = fbytes + ((c->profiling && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
-      if ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
+      if ((e = hipEventRecord(c->ev_k, fs)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
         return c->hip_fail(e, "kernels event");
       if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, cbytes, hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
         return c->hip_fail(e, "hipMemcpyAsync(finish)");
@@ -1919,11 +1929,14 @@ int csm_create(int device, csm_ctx** out) {
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
   bool ev_ok = true;
-  for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k})
+  for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k, &c->ev_fast})
     ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
   for (auto& a : c->alt)
-    for (hipEvent_t* ev : {&a.ev_done, &a.ev_in, &a.ev_k})
+    for (hipEvent_t* ev : {&a.ev_done, &a.ev_in, &a.ev_k, &a.ev_fast})
       ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
+  const char* xs = std::getenv("CSM_EXACT_STREAM");
+  if (!(xs && std::atoi(xs) == 0))
+    ev_ok = ev_ok && hipStreamCreateWithFlags(&c->x_stream, hipStreamNonBlocking) == hipSuccess;
   if (!ev_ok) {
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1941,6 +1954,7 @@ int csm_destroy(csm_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->h2d);
     (void)hipStreamSynchronize(c->d2h);
+    if (c->x_stream) (void)hipStreamSynchronize(c->x_stream);
     csm::gridmap_drop_reader(c->stream);
     c->grid_buf.release();
     c->gridi.release();
@@ -1978,11 +1992,12 @@ int csm_destroy(csm_ctx* c) {
       a.h_fin.release();
       a.h_angles.release();
       a.h_sw.release();
-      for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k})
+      for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k, a.ev_fast})
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k})
+    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k, c->ev_fast})
       if (ev) (void)hipEventDestroy(ev);
+    if (c->x_stream) (void)hipStreamDestroy(c->x_stream);
     (void)hipStreamDestroy(c->h2d);
     (void)hipStreamDestroy(c->d2h);
     (void)hipStreamDestroy(c->stream);

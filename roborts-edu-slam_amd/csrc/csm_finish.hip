@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
 
 hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const AngleEntry* d_angles,
                          const double* d_scores, FinishOut* d_out, int32_t n_windows, hipStream_t stream,
-                         bool exact_on_device) {
+                         hipStream_t exact_stream, hipEvent_t ev_fast) {
   const size_t lds = finish_lds_bytes(A.n_cand);
   if (A.n_cand <= 0 || A.n_cand > kFinishMaxCand || lds > 160 * 1024 || n_windows <= 0) return hipErrorInvalidValue;
   static bool attr_set = false;
@@ -1143,11 +1143,17 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (!exact_on_device && A.need_exact && !A.order_out) return hipSuccess;  // flagged windows: the host
+  hipStream_t xs = stream;
+  if (exact_stream && exact_stream != stream && A.need_exact && !A.order_out && ev_fast) {
+    hipError_t e;
+    if ((e = hipEventRecord(ev_fast, stream)) != hipSuccess || (e = hipStreamWaitEvent(exact_stream, ev_fast, 0)) != hipSuccess)
+      return e;
+    xs = exact_stream;
+  }
   FinishArgs B = A;
   if (A.order_out) B.need_exact = nullptr;  // the permutation hook always sorts
   if (!listed) B.exact_list = nullptr;
-  hipLaunchKernelGGL(finish_kernel, dim3(listed ? std::min(n_windows, 512) : n_windows), dim3(64 * kWaves), lds, stream, B, d_scans,
+  hipLaunchKernelGGL(finish_kernel, dim3(listed ? std::min(n_windows, 512) : n_windows), dim3(64 * kWaves), lds, xs, B, d_scans,
                      d_angles, d_scores, d_out);
   return hipGetLastError();
 }

@@ -143,9 +143,12 @@ constexpr size_t finish_lds_bytes(int64_t n) { return finish_layout(n).total; }
 
 // exact_on_device = false: only the fast pass runs; the windows it flags
 // (need_exact) are left for the host's std::sort (csm_api.cpp level_end).
+// The fast pass (when A.need_exact) and the exact pass on `stream`; with
+// exact_stream (and ev_fast, an event to record) the exact pass runs there,
+// after the fast pass.
 hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const AngleEntry* d_angles,
                          const double* d_scores, FinishOut* d_out, int32_t n_windows,
-                         hipStream_t stream, bool exact_on_device = true);
+                         hipStream_t stream, hipStream_t exact_stream = nullptr, hipEvent_t ev_fast = nullptr);
 
 // Launchers (csm_kernels.hip). All enqueue on `stream` and return hipError_t.
 hipError_t launch_score_all(const LevelWork& L, const ScanWork* d_scans,
