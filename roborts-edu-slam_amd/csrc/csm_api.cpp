@@ -936,6 +936,13 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const bool box = use_int && c->box_kernel && f == 1.0 && csm::box_supported(D.n_space) &&
                    c->pitch >= c->info.size_x + csm::kGridiPadCols;
   if (box) rows_sq = 0;
+  // v6 over 16 x 16 tiles: the argmax of a one-cell-step window wider than 16
+  // (loop-closure windows), in place of the column kernel's dword gathers
+  const int tile_n = (D.n_space + 15) / 16;
+  const bool box_tiled = !box && best_out && use_int && c->box_kernel && f == 1.0 && D.n_space > 16 &&
+                         c->pitch >= c->info.size_x + csm::kGridiPadCols &&
+                         (int64_t)nw * tile_n * tile_n * D.n_angles <= INT32_MAX;
+  if (box_tiled) rows_sq = 0;
   // v7 phase kernel: sub-cell window step with an instantiated bucket shape
   csm::PhaseTable PT{};
   const bool phase = !box && use_int && c->phase_kernel && f < 1.0 &&
@@ -951,7 +958,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const int cpl = pick_cpl(D.n_cand);
   const int64_t per_block = (int64_t)csm::kBlock * cpl;
   const int64_t rows_groups = rows_sq ? 64 / D.n_space : 1;
-  const int64_t bps = (box || phase || tiny) ? D.n_angles
+  const int64_t bps = box_tiled ? (int64_t)tile_n * tile_n * D.n_angles
+                      : (box || phase || tiny) ? D.n_angles
                       : rows_sq ? (D.n_angles + rows_groups - 1) / rows_groups
                       : v2    ? col_blocks * ktiles
                               : (D.n_cand + per_block - 1) / per_block;
@@ -981,8 +989,10 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   L.n_angles = D.n_angles;
   L.n_space = D.n_space;
   L.n_cand = D.n_cand;
-  L.blocks_per_scan = (int32_t)bps;
+  L.blocks_per_scan = box_tiled ? D.n_angles : (int32_t)bps;  // per (window, tile) when tiled
   L.n_scans = nw;
+  L.tile_n = box_tiled ? tile_n : 0;
+  L.tile_ns = D.n_space;
   L.step_cells = P.search_space_resolution / G.mres;
   L.use_penalty = P.use_center_penalty ? 1 : 0;
   L.dist_gain = (P.type == CSM_COARSE) ? 0.4 : 0.2;  // :759-761
@@ -1020,6 +1030,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   char kname[48];
   if (box)
     std::snprintf(kname, sizeof(kname), "score_box_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
+  else if (box_tiled)
+    std::snprintf(kname, sizeof(kname), "score_box_kernel<16,best,tiles>");
   else if (phase)
     std::snprintf(kname, sizeof(kname), "score_phase_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (tiny)
@@ -1107,10 +1119,10 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     const size_t pbytes = (size_t)nw * (size_t)bps * sizeof(BestPartial);
     if ((e = c->partials.ensure(pbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(partials)");
     if ((e = c->best.ensure((size_t)nw * sizeof(BestPartial))) != hipSuccess) return c->hip_fail(e, "hipMalloc(best)");
-    if (box)
+    if (box || box_tiled)
       e = csm::launch_score_box(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                 (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
-                                D.n_space, c->stream);
+                                box_tiled ? 16 : D.n_space, c->stream);
     else if (phase)
       e = csm::launch_score_phase(L, PT, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                   (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,

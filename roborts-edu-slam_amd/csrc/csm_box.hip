@@ -19,6 +19,15 @@
 // within the margin of a rounding boundary) read the zero
 // block and are summed afterwards cell by cell with the reference's own
 // expressions, so the scores are the reference's bit for bit in every case.
+//
+// Tiled mode (L.tile_n > 0, best only): a one-cell-step window wider than 16
+// (the loop-closure windows, 321^2 and 401^2) is covered by 16 x 16 tiles at
+// offsets (ox, oy) = (min(16 ti, n - 16), min(16 tj, n - 16)), one wave per
+// (window, tile, angle): the last tile of an axis is shifted back to the edge
+// (overlapping candidates score identically). Candidate (j, k) of a tile is the
+// window's (ox + j, oy + k), formed as x0 + (ox + j) * f like the reference's
+// x_j, and its flat index is the window's, so the per-window reduction keeps
+// the lowest index among equal scores across tiles.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -62,7 +71,7 @@ struct BoxWave {
   const AngleEntry& ae;
   const double2* __restrict__ P;
   int step, n_used, lane, sx, sy, pitch4, zero_off;
-  double x_0, y_0;
+  double x_0, y_0;  // x_ox, y_oy: the tile's first candidate
 
   // The box test of one beam point; on success (ix0, iy0) is the box corner.
   __device__ __forceinline__ bool box_test(const double2 p, double& lx, double& ly, int& ix0, int& iy0) const {
@@ -146,7 +155,7 @@ struct BoxWave {
 // lane's candidates (j = 4q .. 4q+3, row k).
 template <int NS>
 __device__ __forceinline__ void slow_beams(const BoxWave& B, const LevelWork& L, const int32_t* gi, uint64_t slow,
-                                           int k, int q, int64_t (&acc)[4]) {
+                                           int k, int q, int ox, int oy, int64_t (&acc)[4]) {
   const double f = L.step_cells;
   for (uint64_t m = slow; m != 0; m &= m - 1) {
     const int c0 = (int)__builtin_ctzll(m);
@@ -160,13 +169,13 @@ __device__ __forceinline__ void slow_beams(const BoxWave& B, const LevelWork& L,
         const int l = (int)__builtin_ctzll(rej);  // uniform: one beam for the whole wave
         const double bx = dev::bcast_lane(lx, l);
         const double by = dev::bcast_lane(ly, l);
-        const int gy = (int)((by + (B.S.y0 + k * f)) + 0.5);
+        const int gy = (int)((by + (B.S.y0 + (oy + k) * f)) + 0.5);
         const bool iny = (unsigned)gy < (unsigned)B.sy;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int j = 4 * q + t;
           if (j < NS) {
-            const int gx = (int)((bx + (B.S.x0 + j * f)) + 0.5);
+            const int gx = (int)((bx + (B.S.x0 + (ox + j) * f)) + 0.5);
             const bool in = iny && (unsigned)gx < (unsigned)B.sx;
             acc[t] += gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)B.sy * L.pitch];
           }
@@ -180,20 +189,21 @@ __device__ __forceinline__ void slow_beams(const BoxWave& B, const LevelWork& L,
 // sums: written out, or reduced to the wave's best.
 template <int NS, bool BEST>
 __device__ __forceinline__ void box_epilogue(const LevelWork& L, const ScanWork& S, const AngleEntry& ae, int win,
-                                             int a, bool act, int k, int q, const int64_t (&acc)[4],
-                                             double* __restrict__ out, BestPartial* __restrict__ partials) {
+                                             int a, bool act, int k, int q, int ox, int oy, int nsf,
+                                             const int64_t (&acc)[4], double* __restrict__ out,
+                                             BestPartial* __restrict__ partials) {
   const double f = L.step_cells;
   double bs = -1.0e300;
   int64_t bf = INT64_MAX;
-  const double yk = S.y0 + k * f;  // :572
+  const double yk = S.y0 + (oy + k) * f;  // :572
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int j = 4 * q + t;
     if (act && j < NS) {
       const double accd = (double)(acc[t] + (int64_t)S.n_used * L.outside_i) * L.int_scale;
-      const double xj = S.x0 + j * f;  // :569
+      const double xj = S.x0 + (ox + j) * f;  // :569
       const double score = dev::penalized(L, S, accd, xj, yk, ae.angle);
-      const int64_t flat = ((int64_t)a * NS + j) * NS + k;
+      const int64_t flat = ((int64_t)a * nsf + ox + j) * nsf + oy + k;
       if (BEST) {
         if (dev::better(score, flat, bs, bf)) {
           bs = score;
@@ -228,8 +238,18 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   static_assert(NS * NQ <= 64, "one box row piece per lane");
   static_assert(64 % D == 0 && 32 % D == 0, "loads in flight divide the fold block");
   const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
-  const int win = bid / L.n_angles;
-  const int a = bid - win * L.n_angles;
+  const int wt = bid / L.n_angles;  // window (untiled) or (window, tile)
+  const int a = bid - wt * L.n_angles;
+  int win = wt, ox = 0, oy = 0, nsf = NS;
+  if (L.tile_n > 0) {
+    const int tpw = L.tile_n * L.tile_n;
+    win = wt / tpw;
+    const int t = wt - win * tpw;
+    const int ti = t / L.tile_n;
+    nsf = L.tile_ns;
+    ox = min(ti * NS, nsf - NS);
+    oy = min((t - ti * L.tile_n) * NS, nsf - NS);
+  }
   const ScanWork S = scans[win];
   const AngleEntry ae = angles[S.angle_off + a];
   const int lane = threadIdx.x;
@@ -239,8 +259,8 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   const int q = act ? lane - k * NQ : lane % NQ;
   const int pitch4 = L.pitch * 4;
   const BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, pitch4,
-                  L.size_y * pitch4 /* first of the zero rows */, S.x0 + 0 * L.step_cells /* :569, j = 0 */,
-                  S.y0 + 0 * L.step_cells /* :572, k = 0 */};
+                  L.size_y * pitch4 /* first of the zero rows */, S.x0 + ox * L.step_cells /* :569, j = ox */,
+                  S.y0 + oy * L.step_cells /* :572, k = oy */};
   const int n_used = S.n_used;
   const int zero_off = B.zero_off;
   const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
@@ -306,8 +326,8 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
     }
     __syncthreads();  // the next segment rewrites the list
   }
-  slow_beams<NS>(B, L, gi, slow, k, q, acc);
-  box_epilogue<NS, BEST>(L, S, ae, win, a, act, k, q, acc, out, partials);
+  slow_beams<NS>(B, L, gi, slow, k, q, ox, oy, acc);
+  box_epilogue<NS, BEST>(L, S, ae, wt, a, act, k, q, ox, oy, nsf, acc, out, partials);
 }
 
 template <int NS>
@@ -327,9 +347,14 @@ bool box_supported(int ns) { return ns >= 9 && ns <= 16; }
 hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                             const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
                             hipStream_t stream) {
-  const int64_t nblk = (int64_t)L.n_scans * L.n_angles;
+  // tiled: n_scans windows of tile_ns, tile_n^2 tiles of ns each (best only)
+  const int64_t tiles = L.tile_n > 0 ? (int64_t)L.tile_n * L.tile_n : 1;
+  const int64_t nblk = (int64_t)L.n_scans * tiles * L.n_angles;
   if (nblk <= 0 || nblk > INT32_MAX || !L.int_mode || L.step_cells != 1.0 || L.blocks_per_scan != L.n_angles ||
       L.pitch < L.size_x + kGridiPadCols || L.pitch % 4 != 0)
+    return hipErrorInvalidValue;
+  if (L.tile_n > 0 && (!d_partials || ns != 16 || L.tile_ns < ns || (int64_t)(L.tile_n - 1) * ns >= L.tile_ns ||
+                       (int64_t)L.tile_n * ns < L.tile_ns))
     return hipErrorInvalidValue;
   const double2* p = reinterpret_cast<const double2*>(d_pts);
   const unsigned n = (unsigned)nblk;

@@ -58,6 +58,8 @@ struct LevelWork {
   int32_t pitch;           // gridi row pitch in cells (gridi_pitch(size_x))
   int64_t gridi_stride;    // int32 cells between consecutive gridi grids (pitch * (size_y +
                            // kGridiPadRows): each grid ends with zero rows)
+  int32_t tile_n;          // box kernel over a large window: tiles per axis (0: untiled)
+  int32_t tile_ns;         // ... and the window's own n_space (candidate indices are its)
 };
 
 // Argmax partial: best score of a block and its flat candidate index.

@@ -430,6 +430,53 @@ def test_box_kernel_edge_beams(world2000):
         c.close()
 
 
+@pytest.mark.parametrize("size,penalty", [(0.8, True), (0.85, False), (1.55, True), (1.6, False), (3.0, True)])
+def test_box_tiles_large_windows(world2000, size, penalty):
+    """One-cell-step windows wider than 16 (loop closure): the box kernel over
+    16 x 16 tiles (the last one shifted back to the edge) against the column
+    kernel (CSM_KERNEL=v2) and the oracle: score and flat index bit for bit,
+    with beams on rounding boundaries (the cell-by-cell path at tile offsets),
+    windows hanging off the grid and the centre penalty on and off."""
+    import roborts_csm
+    from roborts_csm.params import CorrelationScanMatchParam
+    w, b = world2000
+    m = O.Map(w.grid, w.resolution, w.offset)
+    pts = b.points_cells[b.offsets[1]:b.offsets[2]]
+    extra = np.array([[0.0, 0.0], [0.0, 0.0], [1.0, -2.0], [-1500.0, 3.0], [900.0, 900.0], [0.25, 0.0]])
+    pts = np.ascontiguousarray(np.concatenate([pts, extra]))
+    p = CorrelationScanMatchParam(size, 0.05, 0.3, 0.0349, 0.5, pts.shape[0], 0, penalty, 0)
+    na, ns = roborts_csm.window_dims(p)
+    assert ns > 16
+    half = (size / w.resolution) * 0.5
+    assert float(100.5 + half - half) + 0.5 == 101.0  # origin points on a rounding boundary
+    centers = [[100.5 + half, 200.5 + half, 0.0], [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
+               [6.2, 3.1, -2.5], [1995.0, 1990.0, 1.0]]
+    ctxs = []
+    for kern in (None, "v2"):
+        if kern:
+            os.environ["CSM_KERNEL"] = kern
+        try:
+            ctxs.append(roborts_csm.Context(0))
+        finally:
+            os.environ.pop("CSM_KERNEL", None)
+    try:
+        for c in ctxs:
+            c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+        ctxs[0].set_profiling(True)
+        cen = np.array(centers)
+        got = [c.best_windows(pts, p, np.zeros(len(centers), dtype=np.int32), cen) for c in ctxs]
+        for i in range(len(centers)):
+            s, flat = O.best_window(m, pts, p, cen[i])
+            for g in got:
+                assert g[0][i] == s and g[1][i] == flat, (i, g[0][i], s, g[1][i], flat)
+        names = {k["name"] for k in ctxs[0].kernel_stats()}
+        assert "score_box_kernel<16,best,tiles>" in names, names
+        assert not any(n.startswith("score_box_kernel") for n in {k["name"] for k in ctxs[1].kernel_stats()})
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 def test_fixed_point_path_out_of_grid(ctx):
     """Exactly-summable grid (the fixed-point kernel) with endpoints far
     outside it: the hardware range check must read the outside value."""
