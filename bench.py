@@ -824,8 +824,10 @@ def worlds_mod():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    # config 2 defaults to 30 timed steps after 5 warmups (~0.2 s): with 5 steps
+    # one host stall of a few ms on a shared box moved ms_per_step by up to 60 %
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 30 for config2, else 5)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 5 for config2, else 2)")
     ap.add_argument("--scans", type=int, default=4096, help="scans per GPU per step")
     ap.add_argument("--levels", choices=["headline", "sim"], default="headline",
                     help="headline: every beam summed (B=1081); sim: reference YAML U=100 (B=109)")
@@ -857,6 +859,10 @@ def main():
     ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
                     help="torch.distributed backend (auto: nccl = RCCL on a GPU box, gloo on CPU)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 30 if args.workload == "config2" else 5
+    if args.warmup is None:
+        args.warmup = 5 if args.workload == "config2" else 2
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
