@@ -481,6 +481,7 @@ struct csm_ctx {
   int32_t key_sx = -1, key_sy = -1;
 
   DevBuf pts, scans, angles, scores, partials, best, fin;
+  DevBuf best_tiles;  // tiled box mode: one best per (window, tile) between the two reductions
   HostBuf h_scores, h_fin, h_angles, h_sw;
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
   bool fast_finish = true;    // CSM_FINISH=exact: always the full device std::sort emulation
@@ -1145,9 +1146,20 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                                  c->stream);
     if (e != hipSuccess) return c->hip_fail(e, "score kernel (best)");
     if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
-    if ((e = csm::launch_reduce_best((const BestPartial*)c->partials.p, (int32_t)bps, nw,
-                                     (BestPartial*)c->best.p, c->stream)) != hipSuccess)
+    if (box_tiled) {  // (window, tile) over its angles, then window over its tiles: one
+                      // block per window over ~10^5 partials took 0.13 ms on willow
+      const int32_t tpw = tile_n * tile_n;
+      if ((e = c->best_tiles.ensure((size_t)nw * tpw * sizeof(BestPartial))) != hipSuccess)
+        return c->hip_fail(e, "hipMalloc(tile bests)");
+      if ((e = csm::launch_reduce_best((const BestPartial*)c->partials.p, D.n_angles, nw * tpw,
+                                       (BestPartial*)c->best_tiles.p, c->stream)) != hipSuccess ||
+          (e = csm::launch_reduce_best((const BestPartial*)c->best_tiles.p, tpw, nw, (BestPartial*)c->best.p,
+                                       c->stream)) != hipSuccess)
+        return c->hip_fail(e, "reduce_best_kernel");
+    } else if ((e = csm::launch_reduce_best((const BestPartial*)c->partials.p, (int32_t)bps, nw,
+                                            (BestPartial*)c->best.p, c->stream)) != hipSuccess) {
       return c->hip_fail(e, "reduce_best_kernel");
+    }
     if ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
       return c->hip_fail(e, "kernels event");
     if ((e = hipMemcpyAsync(best_out, c->best.p, (size_t)nw * sizeof(BestPartial), hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
