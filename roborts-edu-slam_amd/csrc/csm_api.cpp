@@ -482,6 +482,7 @@ struct csm_ctx {
 
   DevBuf pts, scans, angles, scores, partials, best, fin;
   DevBuf best_tiles;  // tiled box mode: one best per (window, tile) between the two reductions
+  HostBuf h_search;   // csm_search_windows: pinned staging of the points and angle table
   HostBuf h_scores, h_fin, h_angles, h_sw;
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
   bool fast_finish = true;    // CSM_FINISH=exact: always the full device std::sort emulation
@@ -1243,7 +1244,7 @@ bool plan_windows_shared(const csm_param& P, const Dims& D, const Geometry& G, i
   return true;
 }
 
-int upload_points(csm_ctx* c, const double* pts, int64_t n_total) {
+int upload_points(csm_ctx* c, const double* pts, int64_t n_total, void* pinned = nullptr) {
   c->loaded_n = -1;  // the point buffer is shared with csm_load_scans
   double m = 0.0;    // max |x| + |y| over the points: bounds every rotated endpoint
   for (int64_t i = 0; i < n_total; ++i) {
@@ -1254,6 +1255,11 @@ int upload_points(csm_ctx* c, const double* pts, int64_t n_total) {
   const size_t bytes = (size_t)std::max<int64_t>(n_total, 1) * 2 * sizeof(double);
   hipError_t e;
   if ((e = c->pts.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(points)");
+  // pinned: the caller's staging copy (a pageable source makes the copy wait for the device)
+  if (pinned && n_total > 0) {
+    std::memcpy(pinned, pts, (size_t)n_total * 2 * sizeof(double));
+    pts = (const double*)pinned;
+  }
   if (n_total > 0 &&
       (e = hipMemcpyAsync(c->pts.p, pts, (size_t)n_total * 2 * sizeof(double), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
     return c->hip_fail(e, "hipMemcpyAsync(points)");
@@ -2552,7 +2558,15 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
   std::vector<AngleEntry> angles;
   if (!plan_windows_shared(*param, D, G, n_points, n_windows, centers_map, angles, plans))
     return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
-  if ((st = upload_points(c, pts, n_points)) != CSM_OK) return st;
+  // the points, then the angle table, staged in pinned memory (the last call
+  // on this context has synchronised, so the staging buffer is free)
+  const size_t pts_bytes = ((size_t)n_points * 2 * sizeof(double) + 255) & ~(size_t)255;
+  hipError_t e0;
+  if ((e0 = c->h_search.ensure(pts_bytes + angles.size() * sizeof(AngleEntry))) != hipSuccess)
+    return c->hip_fail(e0, "hipHostMalloc(search staging)");
+  AngleEntry* h_ang = (AngleEntry*)((char*)c->h_search.p + pts_bytes);
+  std::memcpy(h_ang, angles.data(), angles.size() * sizeof(AngleEntry));
+  if ((st = upload_points(c, pts, n_points, c->h_search.p)) != CSM_OK) return st;
   if ((st = ensure_int_grid(c)) != CSM_OK) return st;
   csm_search_stats S{};
   S.candidates = (int64_t)n_windows * D.n_cand;
@@ -2612,7 +2626,7 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
     if ((e = c->angles.ensure(angles.size() * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
     if ((e = hipMemcpyAsync(c->scans.p, sw, (size_t)nw * sizeof(ScanWork), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
       return c->hip_fail(e, "hipMemcpyAsync(scans)");
-    if ((e = hipMemcpyAsync(c->angles.p, angles.data(), angles.size() * sizeof(AngleEntry), hipMemcpyHostToDevice,
+    if ((e = hipMemcpyAsync(c->angles.p, h_ang, angles.size() * sizeof(AngleEntry), hipMemcpyHostToDevice,
                             c->stream)) != hipSuccess)
       return c->hip_fail(e, "hipMemcpyAsync(angles)");
     csm::PyrInputs in{};

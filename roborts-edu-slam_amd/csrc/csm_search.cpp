@@ -71,7 +71,10 @@ struct PyramidSearch::Impl {
   Buf top_sums, top_thr;
   int top_implicit = -1;  // its depth while a search runs (-1: the top is a node list)
   int32_t top_nj = 0;
-  unsigned long long* h_counts = nullptr;  // pinned: counts read back, then scored
+  // pinned: counts read back, then scored, then the incumbent's initial value
+  // and the answer (pageable copies wait for the device: ~20-70 us each)
+  unsigned long long* h_counts = nullptr;
+  BestPartial* h_inc() const { return (BestPartial*)(h_counts + 2 * (kPyrMaxDepth + 1)); }
   hipEvent_t ev_top[2] = {nullptr, nullptr};  // PyrInputs::timed
   int64_t cap = (int64_t)1 << 24;
   int probe_min = 4096;
@@ -165,7 +168,8 @@ struct PyramidSearch::Impl {
     if ((e = probe_vals.ensure((size_t)np * sizeof(double))) != hipSuccess) return e;
     if ((e = counts.ensure((kPyrMaxDepth + 1) * sizeof(unsigned long long))) != hipSuccess) return e;
     if ((e = scored.ensure((kPyrMaxDepth + 1) * sizeof(unsigned long long))) != hipSuccess) return e;
-    if (!h_counts && (e = hipHostMalloc((void**)&h_counts, 2 * (kPyrMaxDepth + 1) * sizeof(unsigned long long),
+    if (!h_counts && (e = hipHostMalloc((void**)&h_counts,
+                                        2 * (kPyrMaxDepth + 1) * sizeof(unsigned long long) + 2 * sizeof(BestPartial),
                                         hipHostMallocDefault)) != hipSuccess)
       return e;
     return hipSuccess;
@@ -299,8 +303,8 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
   const int64_t nj = ((int64_t)x.L.n_space + (1 << x.depth) - 1) >> x.depth;
   const int64_t n_top = (int64_t)x.L.n_scans * x.L.n_angles * nj * nj;
   if ((e = I.ensure_lists(x.depth)) != hipSuccess) return fail(e, "pyramid node lists");
-  const BestPartial init{-DBL_MAX, INT64_MAX};
-  if ((e = hipMemcpyAsync(I.inc.p, &init, sizeof(init), hipMemcpyHostToDevice, x.stream)) != hipSuccess)
+  I.h_inc()[0] = BestPartial{-DBL_MAX, INT64_MAX};  // the last search synchronised: the slot is free
+  if ((e = hipMemcpyAsync(I.inc.p, I.h_inc(), sizeof(BestPartial), hipMemcpyHostToDevice, x.stream)) != hipSuccess)
     return fail(e, "incumbent");
   if ((e = hipMemsetAsync(I.scored.p, 0, (kPyrMaxDepth + 1) * sizeof(unsigned long long), x.stream)) != hipSuccess)
     return fail(e, "node counters");
@@ -362,13 +366,14 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
       if ((e = I.level_pass(D, m, m, true)) != hipSuccess) return fail(e, "pyramid level pass");
     }
   }
-  if ((e = hipMemcpyAsync(best, I.inc.p, sizeof(BestPartial), hipMemcpyDeviceToHost, x.stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(I.h_inc() + 1, I.inc.p, sizeof(BestPartial), hipMemcpyDeviceToHost, x.stream)) != hipSuccess)
     return fail(e, "incumbent copy");
   unsigned long long* h_scored = I.h_counts + kPyrMaxDepth + 1;
   if ((e = hipMemcpyAsync(h_scored, I.scored.p, (kPyrMaxDepth + 1) * sizeof(unsigned long long),
                           hipMemcpyDeviceToHost, x.stream)) != hipSuccess)
     return fail(e, "node counters copy");
   if ((e = hipStreamSynchronize(x.stream)) != hipSuccess) return fail(e, "pyramid search");
+  *best = I.h_inc()[1];
   for (int d = 0; d <= kPyrMaxDepth; ++d) I.st->nodes[d] = (int64_t)h_scored[d];
   if (x.timed && I.st->top_name[0]) {
     float ms = 0.f;
