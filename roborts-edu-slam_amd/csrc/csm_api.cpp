@@ -483,6 +483,9 @@ struct csm_ctx {
   DevBuf pts, scans, angles, scores, partials, best, fin;
   DevBuf best_tiles;  // tiled box mode: one best per (window, tile) between the two reductions
   HostBuf h_search;   // csm_search_windows: pinned staging of the points and angle table
+  HostBuf h_pts;      // upload_points: pinned staging of a scan's points (and small host arrays)
+  hipEvent_t ev_pts = nullptr;  // the last copy out of h_pts
+  bool ev_pts_used = false;
   HostBuf h_scores, h_fin, h_angles, h_sw;
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
   bool fast_finish = true;    // CSM_FINISH=exact: always the full device std::sort emulation
@@ -1255,14 +1258,27 @@ int upload_points(csm_ctx* c, const double* pts, int64_t n_total, void* pinned =
   const size_t bytes = (size_t)std::max<int64_t>(n_total, 1) * 2 * sizeof(double);
   hipError_t e;
   if ((e = c->pts.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(points)");
-  // pinned: the caller's staging copy (a pageable source makes the copy wait for the device)
+  // through pinned memory: a pageable source makes the copy wait for the device
+  // (~20-70 us per call); small uploads (a scan, a few scans) use the context's
+  // staging buffer once its last copy has finished, large ones copy directly
+  const size_t nbytes = (size_t)n_total * 2 * sizeof(double);
+  bool own = false;
+  if (!pinned && n_total > 0 && nbytes <= ((size_t)4 << 20)) {
+    if (c->ev_pts_used && (e = hipEventSynchronize(c->ev_pts)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize(points)");
+    if ((e = c->h_pts.ensure(nbytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(points)");
+    pinned = c->h_pts.p;
+    own = true;
+  }
   if (pinned && n_total > 0) {
-    std::memcpy(pinned, pts, (size_t)n_total * 2 * sizeof(double));
+    std::memcpy(pinned, pts, nbytes);
     pts = (const double*)pinned;
   }
-  if (n_total > 0 &&
-      (e = hipMemcpyAsync(c->pts.p, pts, (size_t)n_total * 2 * sizeof(double), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+  if (n_total > 0 && (e = hipMemcpyAsync(c->pts.p, pts, nbytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
     return c->hip_fail(e, "hipMemcpyAsync(points)");
+  if (own) {
+    if ((e = hipEventRecord(c->ev_pts, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord(points)");
+    c->ev_pts_used = true;
+  }
   return CSM_OK;
 }
 
@@ -1990,7 +2006,7 @@ int csm_create(int device, csm_ctx** out) {
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
   bool ev_ok = true;
-  for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k, &c->ev_fast})
+  for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k, &c->ev_fast, &c->ev_pts})
     ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
   for (auto& a : c->alt)
     for (hipEvent_t* ev : {&a.ev_done, &a.ev_in, &a.ev_k, &a.ev_fast})
@@ -2020,6 +2036,8 @@ int csm_destroy(csm_ctx* c) {
     c->grid_buf.release();
     c->gridi.release();
     c->h_pack.release();
+    c->h_pts.release();
+    c->h_search.release();
     c->d_updates.release();
     for (auto& pg : c->parked) {
       pg.grid_buf.release();
@@ -2056,7 +2074,7 @@ int csm_destroy(csm_ctx* c) {
       for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k, a.ev_fast})
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k, c->ev_fast})
+    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k, c->ev_fast, c->ev_pts})
       if (ev) (void)hipEventDestroy(ev);
     if (c->x_stream) (void)hipStreamDestroy(c->x_stream);
     (void)hipStreamDestroy(c->h2d);
