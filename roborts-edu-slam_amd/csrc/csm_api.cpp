@@ -109,12 +109,13 @@ struct DevBuf {
 struct HostBuf {  // pinned staging for device->host score copies
   void* p = nullptr;
   size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
+  // flags: hipHostMallocCoherent for buffers kernels write straight into
+  hipError_t ensure(size_t bytes, unsigned flags = hipHostMallocDefault) {
     if (bytes <= cap) return hipSuccess;
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, bytes, flags);
     if (e == hipSuccess) cap = bytes;
     return e;
   }
@@ -498,6 +499,17 @@ struct csm_ctx {
   int phase_margin_log2 = 20; // CSM_PHASE_MARGIN_LOG2 (tests: a wider margin sends more beams to the exact path)
   bool box_kernel = true;     // v6 box kernel for one-cell window steps; any CSM_KERNEL other
                               // than v6 turns it off (CSM_KERNEL=v4: the LDS-DMA row kernel)
+  // Few-window launches (run_windows_small): the split kernel's slab and
+  // arrival counters, the device copy of the windows and the finish's scratch
+  // (ScanWork[nw] | AngleEntry[..] | need[nw] | list[nw + 1] | done counter),
+  // the windows' staging and the FinishOut the finish writes straight into
+  // coherent pinned memory, followed by the flag the exact pass sets last.
+  DevBuf split_slab, split_arrive, small_dev;
+  HostBuf h_small_in, h_small_out;
+  uint32_t flag_seq = 0;
+  bool small_path = true;      // CSM_SMALL=0: few-window launches take the throughput kernels
+  int small_max_windows = 32;  // CSM_SMALL_WINDOWS
+  int split_target_blocks = 512;  // CSM_SPLIT_TARGET: blocks a split launch aims for
   HostBuf h_pack;  // pinned staging of packed grid rows / cell updates (grid uploads)
   DevBuf d_updates;  // csm_update_grid_cells entries on the device
 
@@ -510,6 +522,7 @@ struct csm_ctx {
     bool has_grid = false;
     const float* d_grid = nullptr;
     DevBuf grid_buf, gridi;
+    const int32_t* d_gridi = nullptr;
     const void* key_cells = nullptr;
     int64_t key_stride = 0, key_version = -1;
     int32_t key_sx = -1, key_sy = -1;
@@ -528,6 +541,7 @@ struct csm_ctx {
     std::swap(d_grid, g.d_grid);
     std::swap(grid_buf, g.grid_buf);
     std::swap(gridi, g.gridi);
+    std::swap(d_gridi, g.d_gridi);
     std::swap(key_cells, g.key_cells);
     std::swap(key_stride, g.key_stride);
     std::swap(key_version, g.key_version);
@@ -555,6 +569,7 @@ struct csm_ctx {
 
   // exact fixed-point copy of the grid (ensure_int_grid)
   DevBuf gridi, gstats;
+  const int32_t* d_gridi = nullptr;  // the current fixed-point grid: gridi, or a map's mirror (borrowed)
   // Changes whenever the current fixed-point grid may have (rebuilt, cells or
   // rows refreshed, another grid swapped in): keys the pooled levels of the
   // multi-resolution search.
@@ -703,6 +718,7 @@ int ensure_int_grid(csm_ctx* c) {
       return c->hip_fail(e, "fixed_point_kernel");
   // other parts' streams read gridi next (match_levels_pipelined)
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(gridi)");
+  c->d_gridi = (const int32_t*)c->gridi.p;
   c->pitch = pitch;
   c->int_exp = E;
   c->int_max_abs = vmax;
@@ -831,11 +847,42 @@ struct PendingRun {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, done = nullptr;
   const int32_t* flags = nullptr;  // need-exact flags on the host (profiling)
   int n_flags = 0;
+  // few-window launches: the finish writes FinishOut here (host memory) and
+  // stores flag_value at host_flag when the whole level is done
+  const csm::FinishOut* fin_host = nullptr;
+  const int32_t* host_flag = nullptr;
+  int32_t flag_value = 0;
 };
+
+// Spin on the host flag the exact pass stores last (a launch + flag round
+// trip measured 6 us on the GPU box against 12 us through an event,
+// tools/ubench/roundtrip.hip). Every 256 spins the stream's event is
+// polled: a launch that failed, or that completed without the flag, is an
+// error instead of a hang.
+int wait_flag(csm_ctx* c, const PendingRun& p) {
+  for (uint32_t spin = 1;; ++spin) {
+    if (__atomic_load_n(p.host_flag, __ATOMIC_ACQUIRE) == p.flag_value) return CSM_OK;
+    if ((spin & 255) == 0) {
+      const hipError_t e = hipEventQuery(p.done);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(p.host_flag, __ATOMIC_ACQUIRE) == p.flag_value) return CSM_OK;
+        return c->fail(CSM_ERR_HIP, "finish: the level completed without its host signal");
+      }
+      if (e != hipErrorNotReady) return c->hip_fail(e, "hipEventQuery(level)");
+    }
+    __builtin_ia32_pause();
+  }
+}
 
 int wait_run(csm_ctx* c, const PendingRun& p) {
   hipError_t e;
-  if ((e = hipEventSynchronize(p.done)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize");
+  if (p.host_flag) {
+    const int st = wait_flag(c, p);
+    if (st != CSM_OK) return st;
+    if (p.timed && (e = hipEventSynchronize(p.done)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize");
+  } else if ((e = hipEventSynchronize(p.done)) != hipSuccess) {
+    return c->hip_fail(e, "hipEventSynchronize");
+  }
   if (p.timed) {
     float ms = 0.f;
     if ((e = hipEventElapsedTime(&ms, p.ev0, p.ev1)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
@@ -896,6 +943,215 @@ bool phase_table(double f, int ns, int margin_log2, csm::PhaseTable& T) {
   return T.nq > 0;
 }
 
+
+// Exact fixed-point accumulation for these windows: grid eligible, beams
+// bounded, no offset wrap (every endpoint within 2^30 bytes of a row).
+bool int_mode_ok(const csm_ctx* c, const Dims& D, double f, const std::vector<WindowPlan>& plans) {
+  if (!c->int_ok) return false;
+  for (const WindowPlan& W : plans) {
+    const double far = (double)(D.n_space - 1) * f;
+    const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
+                                 std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
+    const double R = c->pts_maxabs * (1.0 + 1e-9) + span + 2.0;
+    if (!(R * 4.0 * (double)c->pitch < std::ldexp(1.0, 30))) return false;
+    if ((double)W.n_used * c->int_max_abs * std::ldexp(1.0, c->int_exp) > std::ldexp(1.0, 53)) return false;
+  }
+  return true;
+}
+
+void fill_scan_work(const Dims& D, const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
+                    const std::vector<int32_t>& grid_index, ScanWork* sw) {
+  for (size_t i = 0; i < plans.size(); ++i) {
+    const WindowPlan& W = plans[i];
+    ScanWork& s = sw[i];
+    s.pts_off = pt_offsets[i];
+    s.angle_off = W.angle_off;
+    s.out_off = (int64_t)i * D.n_cand;
+    s.n_used = W.n_used;
+    s.step = W.step;
+    s.divisor = (double)(W.use - 0);
+    s.x0 = W.x0;
+    s.y0 = W.y0;
+    s.cx = W.center[0];
+    s.cy = W.center[1];
+    s.ct = W.center[2];
+    s.reserved = 0;
+    s.grid_index = grid_index.empty() ? 0 : grid_index[i];
+  }
+}
+
+LevelWork make_level_work(const csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G, int nw,
+                          bool use_int) {
+  LevelWork L{};
+  L.n_angles = D.n_angles;
+  L.n_space = D.n_space;
+  L.n_cand = D.n_cand;
+  L.blocks_per_scan = D.n_angles;
+  L.n_scans = nw;
+  L.tile_ns = D.n_space;
+  L.step_cells = P.search_space_resolution / G.mres;
+  L.use_penalty = P.use_center_penalty ? 1 : 0;
+  L.dist_gain = (P.type == CSM_COARSE) ? 0.4 : 0.2;  // :759-761
+  L.size = P.search_space_size;
+  L.mres = G.mres;
+  L.grid = c->d_grid;
+  L.grid_stride = (int64_t)c->info.size_x * c->info.size_y;
+  L.size_x = c->info.size_x;
+  L.size_y = c->info.size_y;
+  L.outside = c->outside;
+  L.int_mode = use_int ? 1 : 0;
+  L.gridi = c->d_gridi;
+  L.int_scale = std::ldexp(1.0, -c->int_exp);
+  L.outside_i = c->outside_i;
+  L.pitch = c->pitch;
+  L.gridi_stride = (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows);
+  return L;
+}
+
+// The reference's calling pattern, one scan and one level at a time
+// (ScanMatchers::ScanMatch, scan_matchers.h:238-256), leaves the throughput
+// kernels' one wave per (window, angle) on a few dozen waves; few windows go
+// through the split kernel and a 16-wave fast finish instead.
+bool small_launch(const csm_ctx* c, const Dims& D, int nw) {
+  return c->small_path && c->fast_finish && nw <= c->small_max_windows && D.n_cand <= csm::kFinishMaxCand &&
+         D.n_cand * (int64_t)nw <= INT32_MAX && csm::finish_lds_bytes(D.n_cand) <= 160 * 1024;
+}
+
+// Few-window launch: the split kernel (csm_split.hip) scores, the fast and
+// exact finishes write each window's FinishOut straight into coherent pinned
+// host memory, and the exact pass stores a fresh flag value last (wait_run
+// spins on it). Everything on the context's stream; a single window with a
+// small angle table travels in the kernel arguments, otherwise one H2D copy.
+int run_windows_small(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
+                      const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
+                      const AngleEntry* angles, size_t n_angle_entries, const std::vector<int32_t>& grid_index,
+                      bool device_finish, PendingRun* pend, int skip_lists) {
+  const int nw = (int)plans.size();
+  hipError_t e;
+  // device carve: done counter (fixed place: zero between launches) | scans |
+  // angles | need | list
+  const size_t o_done = 0, o_scans = 64;
+  const size_t o_ang = ((o_scans + (size_t)nw * sizeof(ScanWork)) + 15) & ~(size_t)15;
+  const size_t o_need = (o_ang + n_angle_entries * sizeof(AngleEntry) + 15) & ~(size_t)15;
+  const size_t o_list = o_need + (size_t)nw * 4;
+  const size_t dev_bytes = o_list + (size_t)(nw + 1) * 4;
+  if (dev_bytes > c->small_dev.cap) {
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(small)");
+    if ((e = c->small_dev.ensure(dev_bytes * 2)) != hipSuccess) return c->hip_fail(e, "hipMalloc(small)");
+    if ((e = hipMemsetAsync(c->small_dev.p, 0, c->small_dev.cap, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemsetAsync(small)");
+  }
+  char* dv = (char*)c->small_dev.p;
+  ScanWork* d_scans = (ScanWork*)(dv + o_scans);
+  AngleEntry* d_angles = (AngleEntry*)(dv + o_ang);
+  int32_t* d_need = (int32_t*)(dv + o_need);
+  int32_t* d_list = (int32_t*)(dv + o_list);
+  int32_t* d_done = (int32_t*)(dv + o_done);
+  // host side: the windows' staging (laid out as the device carve from
+  // o_scans on), and FinishOut[nw] + the flag (coherent)
+  const size_t in_bytes = o_ang - o_scans + n_angle_entries * sizeof(AngleEntry);
+  const size_t out_flag = ((size_t)nw * sizeof(csm::FinishOut) + 63) & ~(size_t)63;
+  if ((e = c->h_small_in.ensure(in_bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(small in)");
+  if (out_flag + 64 > c->h_small_out.cap) {
+    if ((e = c->h_small_out.ensure(std::max<size_t>(out_flag + 64, 64 * 1024), hipHostMallocCoherent)) != hipSuccess)
+      return c->hip_fail(e, "hipHostMalloc(small out)");
+    std::memset(c->h_small_out.p, 0, c->h_small_out.cap);
+  }
+  csm::FinishOut* h_out = (csm::FinishOut*)c->h_small_out.p;
+  int32_t* h_flag = (int32_t*)((char*)c->h_small_out.p + out_flag);
+  ScanWork* sw = (ScanWork*)c->h_small_in.p;
+  fill_scan_work(D, plans, pt_offsets, grid_index, sw);
+  LevelWork L = make_level_work(c, P, D, G, nw, true);
+
+  // splits: enough blocks to spread the level over the chip, at least
+  // ceil(beams / kSplitMaxBeams) (int32 sums), at most one per 4 beams
+  int max_used = 1;
+  for (const WindowPlan& W : plans) max_used = std::max(max_used, W.n_used);
+  const int64_t chunks = (D.n_cand + csm::kSplitThreads - 1) / csm::kSplitThreads;
+  const int min_splits = (max_used + csm::kSplitMaxBeams - 1) / csm::kSplitMaxBeams;
+  const int64_t want = (c->split_target_blocks + (int64_t)nw * chunks - 1) / ((int64_t)nw * chunks);
+  const int splits = (int)std::max<int64_t>(min_splits, std::min<int64_t>(want, std::max(1, max_used / 4)));
+  const size_t slab_bytes = (size_t)nw * (size_t)chunks * (size_t)splits * csm::kSplitThreads * sizeof(int32_t);
+  const size_t arrive_bytes = (size_t)nw * (size_t)chunks * sizeof(int32_t);
+  if ((e = c->split_slab.ensure(slab_bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(split slab)");
+  if (arrive_bytes > c->split_arrive.cap) {  // counters start at zero; each launch leaves them at zero
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(split)");
+    if ((e = c->split_arrive.ensure(arrive_bytes * 2)) != hipSuccess) return c->hip_fail(e, "hipMalloc(split arrive)");
+    if ((e = hipMemsetAsync(c->split_arrive.p, 0, c->split_arrive.cap, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemsetAsync(split arrive)");
+  }
+  csm::SplitWork W{};
+  W.splits = splits;
+  W.chunks = (int32_t)chunks;
+  W.slab = (int32_t*)c->split_slab.p;
+  W.arrive = (int32_t*)c->split_arrive.p;
+  W.clear_word = d_list;
+  W.inline_window = (nw == 1 && D.n_angles <= csm::kSplitArgAngles && n_angle_entries == (size_t)D.n_angles) ? 1 : 0;
+  if (W.inline_window) {
+    W.sw = sw[0];
+    W.sw.angle_off = 0;  // the copy block 0 stores for the finish starts the angle rows
+    std::memcpy(W.ang, angles, (size_t)D.n_angles * sizeof(AngleEntry));
+    W.scans_out = d_scans;
+    W.angles_out = d_angles;
+  } else {
+    std::memcpy((char*)c->h_small_in.p + (o_ang - o_scans), angles, n_angle_entries * sizeof(AngleEntry));
+    if ((e = hipMemcpyAsync(d_scans, c->h_small_in.p, in_bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(small windows)");
+  }
+  const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
+  if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
+  if (c->profiling && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+  if ((e = csm::launch_score_split(L, W, d_scans, (const double*)c->pts.p, d_angles, (double*)c->scores.p,
+                                   c->stream)) != hipSuccess)
+    return c->hip_fail(e, "score_split_kernel");
+  if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+  PendingRun local;
+  PendingRun& p = pend ? *pend : local;
+  p = PendingRun{};
+  std::snprintf(p.kname, sizeof(p.kname), "score_split_kernel<%d,%d>", D.n_space, splits);
+  double beams = 0.0;
+  for (const WindowPlan& Wp : plans) beams += (double)Wp.n_used;
+  p.alg_bytes = beams * (double)D.n_cand * 4.0;
+  p.scorings = (double)nw * (double)D.n_cand;
+  p.timed = c->profiling;
+  p.ev0 = c->ev0;
+  p.ev1 = c->ev1;
+  p.ev2 = c->ev2;
+  p.done = c->ev_done;
+  if (!device_finish) {  // every score to the host (csm_score_window, host std::sort)
+    if ((e = c->h_scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scores)");
+    if ((e = hipMemcpyAsync(c->h_scores.p, c->scores.p, bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(scores)");
+    if ((e = hipEventRecord(c->ev_done, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+    if (pend) return CSM_OK;
+    return wait_run(c, p);
+  }
+  csm::FinishArgs A{};
+  A.n_cand = D.n_cand;
+  A.n_space = D.n_space;
+  A.step_cells = L.step_cells;
+  A.lin_tol = P.search_space_resolution / G.mres;
+  A.skip_lists = skip_lists;
+  A.need_exact = d_need;
+  A.exact_list = d_list;
+  A.done_ctr = d_done;
+  A.host_flag = h_flag;
+  A.flag_value = (int32_t)(++c->flag_seq & 0x7FFFFFFF);
+  if (A.flag_value == 0) A.flag_value = (int32_t)(++c->flag_seq & 0x7FFFFFFF);
+  if ((e = csm::launch_finish(A, d_scans, d_angles, (const double*)c->scores.p, h_out, nw, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "finish_kernel");
+  if (c->profiling && (e = hipEventRecord(c->ev2, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+  std::snprintf(p.fname, sizeof(p.fname), "finish_kernel<%lld>", (long long)D.n_cand);
+  p.finish_bytes = (double)nw * (double)D.n_cand * 8.0;
+  p.device_finish = true;
+  p.fin_host = h_out;
+  p.host_flag = h_flag;
+  p.flag_value = A.flag_value;
+  if ((e = hipEventRecord(c->ev_done, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+  if (pend) return CSM_OK;
+  return wait_run(c, p);
+}
+
 // With pend == nullptr the call returns once results are on the host; with
 // pend it returns as soon as the work is enqueued (join with wait_run).
 int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
@@ -914,18 +1170,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const int64_t n_cols = (int64_t)D.n_angles * D.n_space;
   const int64_t col_blocks = (n_cols + 63) / 64;
   const bool v2 = c->column_kernel && n_cols < INT32_MAX;
-  // exact fixed-point accumulation: grid eligible, beams bounded, no offset wrap
-  bool use_int = v2 && c->int_ok;
   const double f = P.search_space_resolution / G.mres;
-  for (const WindowPlan& W : plans) {
-    if (!use_int) break;
-    const double far = (double)(D.n_space - 1) * f;
-    const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
-                                 std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
-    const double R = c->pts_maxabs * (1.0 + 1e-9) + span + 2.0;
-    if (!(R * 4.0 * (double)c->pitch < std::ldexp(1.0, 30))) use_int = false;
-    if ((double)W.n_used * c->int_max_abs * std::ldexp(1.0, c->int_exp) > std::ldexp(1.0, 53)) use_int = false;
-  }
+  const bool use_int = v2 && int_mode_ok(c, D, f, plans);
+  if (mode != Finish::kBest && use_int && small_launch(c, D, nw))
+    return run_windows_small(c, P, D, G, plans, pt_offsets, angles, n_angle_entries, grid_index,
+                             mode == Finish::kDevice, pend, skip_lists);
   // v3 row-segment kernel: fixed-point grid and an instantiation whose row
   // segment covers the x-span of a group, (n_space-1)*f cells (+2 for the
   // truncations); the kernel re-checks and recomputes exactly if exceeded
@@ -973,50 +1222,13 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   hipError_t e;
   if ((e = c->h_sw.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scans)");
   ScanWork* sw = (ScanWork*)c->h_sw.p;  // pinned staging
-  for (int i = 0; i < nw; ++i) {
-    const WindowPlan& W = plans[(size_t)i];
-    ScanWork& s = sw[i];
-    s.pts_off = pt_offsets[(size_t)i];
-    s.angle_off = W.angle_off;
-    s.out_off = (int64_t)i * D.n_cand;
-    s.n_used = W.n_used;
-    s.step = W.step;
-    s.divisor = (double)(W.use - 0);
-    s.x0 = W.x0;
-    s.y0 = W.y0;
-    s.cx = W.center[0];
-    s.cy = W.center[1];
-    s.ct = W.center[2];
-    s.reserved = 0;
-    s.grid_index = grid_index.empty() ? 0 : grid_index[(size_t)i];
-  }
-  LevelWork L{};
-  L.n_angles = D.n_angles;
-  L.n_space = D.n_space;
-  L.n_cand = D.n_cand;
+  fill_scan_work(D, plans, pt_offsets, grid_index, sw);
+  LevelWork L = make_level_work(c, P, D, G, nw, use_int);
   L.blocks_per_scan = box_tiled ? D.n_angles : (int32_t)bps;  // per (window, tile) when tiled
-  L.n_scans = nw;
   L.tile_n = box_tiled ? tile_n : 0;
-  L.tile_ns = D.n_space;
-  L.step_cells = P.search_space_resolution / G.mres;
-  L.use_penalty = P.use_center_penalty ? 1 : 0;
-  L.dist_gain = (P.type == CSM_COARSE) ? 0.4 : 0.2;  // :759-761
-  L.size = P.search_space_size;
-  L.mres = G.mres;
-  L.grid = c->d_grid;
-  L.grid_stride = (int64_t)c->info.size_x * c->info.size_y;
-  L.size_x = c->info.size_x;
-  L.size_y = c->info.size_y;
-  L.outside = c->outside;
-  L.int_mode = use_int ? 1 : 0;
-  L.gridi = (const int32_t*)c->gridi.p;
-  L.int_scale = std::ldexp(1.0, -c->int_exp);
-  L.outside_i = c->outside_i;
   L.n_cols = (int32_t)n_cols;
   L.ktiles = ktiles;
   L.col_blocks = (int32_t)col_blocks;
-  L.pitch = c->pitch;
-  L.gridi_stride = (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows);
 
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
   if ((e = c->angles.ensure(n_angle_entries * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
@@ -1171,6 +1383,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   }
   PendingRun local;
   PendingRun& p = pend ? *pend : local;
+  p = PendingRun{};
   p.flags = flags_h;
   p.n_flags = n_flags;
   std::snprintf(p.kname, sizeof(p.kname), "%s", kname);
@@ -1499,7 +1712,7 @@ int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
   st = run_windows(c, P, D, G, R.plans, R.pt_off, angles, n_ang_total, R.grid, nullptr,
                    R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend, skip_lists);
   if (st != CSM_OK) return st;
-  R.fin = (const csm::FinishOut*)c->h_fin.p;
+  R.fin = R.pend.fin_host ? R.pend.fin_host : (const csm::FinishOut*)c->h_fin.p;
   R.scores = (const double*)c->h_scores.p;
   if (c->profiling) {  // per level (window size), and in all
     char nm[48];
@@ -1572,6 +1785,14 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
                            int n_levels, double* poses, double* covs, double* sum,
                            const int32_t* scan_grid = nullptr) {
   const int K = std::max(2, std::min(c->pipeline_parts, csm_ctx::kMaxParts));
+  // parts in flight share no few-window buffers: every part takes the
+  // throughput kernels (a part is hundreds of windows at the default split)
+  struct SmallOff {
+    csm_ctx* c;
+    bool was;
+    ~SmallOff() { c->small_path = was; }
+  } small_off{c, c->small_path};
+  c->small_path = false;
   int32_t first[csm_ctx::kMaxParts], count[csm_ctx::kMaxParts];
   for (int h = 0; h < K; ++h) {
     first[h] = (int32_t)((int64_t)n_scans * h / K);
@@ -2003,6 +2224,9 @@ int csm_create(int device, csm_ctx** out) {
     c->pipeline_min = v > 0 ? v : INT32_MAX;
   }
   if (const char* env = std::getenv("CSM_SKIP_DEAD_LISTS")) c->skip_dead_lists = std::atoi(env) != 0;
+  if (const char* env = std::getenv("CSM_SMALL")) c->small_path = std::atoi(env) != 0;
+  if (const char* env = std::getenv("CSM_SMALL_WINDOWS")) c->small_max_windows = std::max(1, std::atoi(env));
+  if (const char* env = std::getenv("CSM_SPLIT_TARGET")) c->split_target_blocks = std::max(1, std::atoi(env));
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
   bool ev_ok = true;
@@ -2044,6 +2268,11 @@ int csm_destroy(csm_ctx* c) {
       pg.gridi.release();
     }
     c->gstats.release();
+    c->split_slab.release();
+    c->split_arrive.release();
+    c->small_dev.release();
+    c->h_small_in.release();
+    c->h_small_out.release();
     c->pts.release();
     c->scans.release();
     c->angles.release();
@@ -2662,7 +2891,7 @@ int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const cs
     L.outside_i = c->outside_i;
     L.int_mode = 1;
     L.int_scale = std::ldexp(1.0, -c->int_exp);
-    in.level0 = csm::PyrGrid{(const int32_t*)c->gridi.p,
+    in.level0 = csm::PyrGrid{c->d_gridi,
                              (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows), c->pitch, 0,
                              c->info.size_x, c->info.size_y, 0, c->info.size_x, 0, 0};
     in.n_grids = c->n_grids;

@@ -841,6 +841,19 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
       finish_window(A, scans, angles, scores, out, A.exact_list[1 + i], smem);
       __syncthreads();  // the next window reuses the LDS carve
     }
+    if (A.host_flag) {  // every block's FinishOut stores land, then the last block signals the host
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(A.done_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == (int)gridDim.x - 1) {
+          __hip_atomic_store(A.done_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(A.host_flag, A.flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
     return;
   }
   const int w = blockIdx.x;
@@ -865,11 +878,16 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
 //      (<= kFastNearCap) and ranked the same way for the angular list.
 // A repeat where order decides, a NaN or an oversized set flags the window
 // for finish_kernel's exact std::sort emulation, which runs next and skips
-// every other window. One 256-thread block per window, ~8 barriers.
-constexpr int kFastThreads = 256;
+// every other window. One block of T threads per window; each thread holds
+// its V = ceil(n / T) scores in registers (loaded once, all in flight: the
+// passes re-reading the scores from L2 were latency-bound, one round trip per
+// 256 candidates per pass), and the window's angle rows sit in LDS for the
+// sequential FindBest sums. T = 1024 for launches of few windows (the
+// reference's single-scan levels), 256 otherwise.
 constexpr int kFastCap = 512;      // compacted candidates of step 2
 constexpr int kFastNearCap = 512;  // compacted near-best candidates of step 3
 constexpr int kFastLevels = 8;     // thresholds best - {0.01, 0.02, ..., 0.64}, then everything > bound
+constexpr int kFastAngles = 256;   // angle rows staged in LDS (more: read from memory)
 
 __device__ __forceinline__ double wave_max_d(double v) {
   for (int o = 32; o > 0; o >>= 1) {
@@ -879,17 +897,20 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
-__global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A, const ScanWork* __restrict__ scans,
-                                                                   const AngleEntry* __restrict__ angles,
-                                                                   const double* __restrict__ scores,
-                                                                   FinishOut* __restrict__ out) {
+template <int T, int V>
+__global__ __launch_bounds__(T) void finish_fast_kernel(FinishArgs A, const ScanWork* __restrict__ scans,
+                                                        const AngleEntry* __restrict__ angles,
+                                                        const double* __restrict__ scores,
+                                                        FinishOut* __restrict__ out) {
+  constexpr int NW = T / 64;
   __shared__ double ck[kFastCap];   // step 2 candidates (value, index), then ...
   __shared__ int ci[kFastCap];
   __shared__ double sk[kFastCap];   // ... sorted by value (rank order)
   __shared__ int si[kFastCap];
   __shared__ double nk[kFastNearCap];
   __shared__ int ni[kFastNearCap];
-  __shared__ double red[4];
+  __shared__ double acs[kFastAngles], asn[kFastAngles];
+  __shared__ double red[NW];
   __shared__ int cnt_s[kFastLevels];
   __shared__ int nC_s, nN_s, flag_s;
   __shared__ double sbx, sby;
@@ -902,6 +923,25 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     *need = 1;
     if (A.exact_list) A.exact_list[1 + atomicAdd(A.exact_list, 1)] = w;
   };
+  // the scores, every load in flight (index clamped, value masked after)
+  double v[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int i = tid + k * T;
+    const double x = sc[min(i, n - 1)];
+    v[k] = i < n ? x : -INFINITY;
+  }
+  const ScanWork S = scans[w];
+  const int ns = A.n_space;
+  const int nss = ns * ns;
+  {
+    const int na = min(n / nss, kFastAngles);
+    for (int t = tid; t < na; t += T) {
+      const AngleEntry ae = angles[S.angle_off + t];
+      acs[t] = ae.cosine;
+      asn[t] = ae.sine;
+    }
+  }
   if (tid < kFastLevels) cnt_s[tid] = 0;
   if (tid == 0) {
     nC_s = 0;
@@ -912,16 +952,18 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
   // 1. best = the front of the sorted candidates (:607); NaN anywhere: exact path
   double m = -INFINITY;
   bool nan = false;
-  for (int i = tid; i < n; i += kFastThreads) {
-    const double v = sc[i];
-    nan |= (v != v);
-    m = (v > m) ? v : m;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    nan |= (v[k] != v[k]);
+    m = (v[k] > m) ? v[k] : m;
   }
   m = wave_max_d(m);
   if (lane == 0) red[wave] = m;
   if (__ballot(nan) != 0 && lane == 0) flag_s = 1;
   __syncthreads();
-  const double best = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  double best = red[0];
+#pragma unroll
+  for (int q = 1; q < NW; ++q) best = fmax(best, red[q]);
   if (flag_s || n <= 0) {
     if (tid == 0) flag();
     return;
@@ -937,19 +979,21 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
       if (d >= -dl) return k;
     return kFastLevels - 1;
   };
+  int lv[V];
   {
     int c[kFastLevels];
 #pragma unroll
     for (int k = 0; k < kFastLevels; ++k) c[k] = 0;
-    for (int i = tid; i < n; i += kFastThreads) {
-      const int lv = level_of(sc[i]);
 #pragma unroll
-      for (int k = 0; k < kFastLevels; ++k) c[k] += (lv == k) ? 1 : 0;
+    for (int k = 0; k < V; ++k) {
+      lv[k] = level_of(v[k]);  // -INFINITY padding: no level
+#pragma unroll
+      for (int q = 0; q < kFastLevels; ++q) c[q] += (lv[k] == q) ? 1 : 0;
     }
 #pragma unroll
-    for (int k = 0; k < kFastLevels; ++k) {
-      const int t = wave_sum_i(c[k]);
-      if (lane == 0 && t) atomicAdd(&cnt_s[k], t);
+    for (int q = 0; q < kFastLevels; ++q) {
+      const int t = wave_sum_i(c[q]);
+      if (lane == 0 && t) atomicAdd(&cnt_s[q], t);
     }
   }
   __syncthreads();
@@ -970,35 +1014,37 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     if (tid == 0) flag();
     return;
   }
-  for (int i0 = tid - lane; i0 < n; i0 += kFastThreads) {
-    const int i = i0 + lane;
-    const double s = i < n ? sc[i] : -INFINITY;
-    const bool in = i < n && level_of(s) <= L;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int i = tid + k * T;
+    const bool in = lv[k] <= L;  // padding never qualifies
     const uint64_t mm = __ballot(in);
-    int base = 0;
-    if (lane == 0 && mm) base = atomicAdd(&nC_s, popc(mm));
-    base = uni(base);
-    if (in) {
-      const int p = base + popc(mm & below_mask(lane));
-      ck[p] = s;
-      ci[p] = i;
+    if (mm) {  // wave-uniform
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&nC_s, popc(mm));
+      base = uni(base);
+      if (in) {
+        const int p = base + popc(mm & below_mask(lane));
+        ck[p] = v[k];
+        ci[p] = i;
+      }
     }
   }
   __syncthreads();
   // rank = elements greater; any equal value where the order decides: exact
   // path (the prefix, the positional 20 and the value just past them)
-  for (int t = tid; t < nC; t += kFastThreads) {
-    const double v = ck[t];
+  for (int t = tid; t < nC; t += T) {
+    const double x = ck[t];
     int r = 0, eq = 0;
     for (int j = 0; j < nC; ++j) {
       const double u = ck[j];
-      r += (u > v) ? 1 : 0;
-      eq += (u == v) ? 1 : 0;
+      r += (u > x) ? 1 : 0;
+      eq += (u == x) ? 1 : 0;
     }
-    const double d = v - best;
+    const double d = x - best;
     const bool inF = d < 0.0 ? d >= -1e-2 : d <= 1e-2;  // DoubleEqual(s, best, 1e-2)
     if (eq > 1 && (inF || (want_pos && r <= kCovPoints))) flag_s = 1;
-    sk[r] = v;  // distinct ranks whenever nothing is flagged
+    sk[r] = x;  // distinct ranks whenever nothing is flagged
     si[r] = ci[t];
   }
   __syncthreads();
@@ -1006,9 +1052,6 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     if (tid == 0) flag();
     return;
   }
-  const ScanWork S = scans[w];
-  const int ns = A.n_space;
-  const int nss = ns * ns;
   const double f = A.step_cells;
   auto cx = [&](int idx) { return S.x0 + ((idx / ns) % ns) * f; };
   auto cy = [&](int idx) { return S.y0 + (idx % ns) * f; };
@@ -1021,11 +1064,13 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
       const double d = s - best;
       if (!(d < 0.0 ? d >= -1e-2 : d <= 1e-2)) break;
       const int idx = si[r];
-      const AngleEntry ae = angles[S.angle_off + idx / nss];
+      const int a = idx / nss;
+      const double ca = a < kFastAngles ? acs[a] : angles[S.angle_off + a].cosine;
+      const double sa = a < kFastAngles ? asn[a] : angles[S.angle_off + a].sine;
       ax += cx(idx) * s;
       ay += cy(idx) * s;
-      thx += ae.cosine * s;
-      thy += ae.sine * s;
+      thx += ca * s;
+      thy += sa * s;
       ssum += s;
       count++;
     }
@@ -1045,13 +1090,12 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     }
     o->best_x = sbx;
     o->best_y = sby;
-    // positional list (:915-928): the sorted prefix with score > bound, <= 20
-    const int np = want_pos ? min(nC, kCovPoints) : 0;
-    for (int r = 0; r < np; ++r) {
-      o->pos_idx[r] = si[r];
-      o->pos_score[r] = sk[r];
-    }
-    o->n_pos = np;
+    o->n_pos = want_pos ? min(nC, kCovPoints) : 0;
+  }
+  // positional list (:915-928): the sorted prefix with score > bound, <= 20
+  if (want_pos && tid < min(nC, kCovPoints)) {
+    o->pos_idx[tid] = si[tid];
+    o->pos_score[tid] = sk[tid];
   }
   __syncthreads();
   // 3. angular list (:990-1003): near the best, score >= bound
@@ -1063,28 +1107,28 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     return;
   }
   const double bx = sbx, by = sby, tol = A.lin_tol;
-  for (int i0 = tid - lane; i0 < n; i0 += kFastThreads) {
-    const int i = i0 + lane;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int i = tid + k * T;
+    const double s = v[k];
     bool in = false;
-    double s = 0.0;
-    if (i < n) {
-      s = sc[i];
-      if (s >= bound) {
-        const double dx = cx(i) - bx, dy = cy(i) - by;
-        const bool ex = dx < 0.0 ? dx >= -fabs(tol) : dx <= fabs(tol);
-        const bool ey = dy < 0.0 ? dy >= -fabs(tol) : dy <= fabs(tol);
-        in = ex && ey;
-      }
+    if (s >= bound) {  // padding (-inf) never qualifies
+      const double dx = cx(i) - bx, dy = cy(i) - by;
+      const bool ex = dx < 0.0 ? dx >= -fabs(tol) : dx <= fabs(tol);
+      const bool ey = dy < 0.0 ? dy >= -fabs(tol) : dy <= fabs(tol);
+      in = ex && ey;
     }
     const uint64_t mm = __ballot(in);
-    int base = 0;
-    if (lane == 0 && mm) base = atomicAdd(&nN_s, popc(mm));
-    base = uni(base);
-    if (in) {
-      const int p = base + popc(mm & below_mask(lane));
-      if (p < kFastNearCap) {
-        nk[p] = s;
-        ni[p] = i;
+    if (mm) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&nN_s, popc(mm));
+      base = uni(base);
+      if (in) {
+        const int p = base + popc(mm & below_mask(lane));
+        if (p < kFastNearCap) {
+          nk[p] = s;
+          ni[p] = i;
+        }
       }
     }
   }
@@ -1094,18 +1138,18 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     if (tid == 0) flag();
     return;
   }
-  for (int t = tid; t < nN; t += kFastThreads) {
-    const double v = nk[t];
+  for (int t = tid; t < nN; t += T) {
+    const double x = nk[t];
     int r = 0, eq = 0;
     for (int j = 0; j < nN; ++j) {
       const double u = nk[j];
-      r += (u > v) ? 1 : 0;
-      eq += (u == v) ? 1 : 0;
+      r += (u > x) ? 1 : 0;
+      eq += (u == x) ? 1 : 0;
     }
     if (eq > 1 && r <= kCovPoints) flag_s = 1;
     if (r < kCovPoints) {
       o->ang_idx[r] = ni[t];
-      o->ang_score[r] = v;
+      o->ang_score[r] = x;
     }
   }
   __syncthreads();
@@ -1114,6 +1158,34 @@ __global__ __launch_bounds__(kFastThreads) void finish_fast_kernel(FinishArgs A,
     if (flag_s) flag();
     else *need = 0;
   }
+}
+
+// Scores per thread of the fast finish's instantiations: the smallest V with
+// V * T >= n (n <= kFinishMaxCand = 10240).
+template <int T, int V>
+hipError_t launch_fast_tv(const FinishArgs& A, const ScanWork* s, const AngleEntry* a, const double* sc,
+                          FinishOut* o, int32_t nw, hipStream_t stream) {
+  hipLaunchKernelGGL((finish_fast_kernel<T, V>), dim3(nw), dim3(T), 0, stream, A, s, a, sc, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_fast(const FinishArgs& A, const ScanWork* s, const AngleEntry* a, const double* sc, FinishOut* o,
+                       int32_t nw, hipStream_t stream) {
+  const int64_t n = A.n_cand;
+  if (nw <= kFinishWideWindows) {  // few windows: 16 waves per window
+    if (n <= 1024) return launch_fast_tv<1024, 1>(A, s, a, sc, o, nw, stream);
+    if (n <= 2048) return launch_fast_tv<1024, 2>(A, s, a, sc, o, nw, stream);
+    if (n <= 4096) return launch_fast_tv<1024, 4>(A, s, a, sc, o, nw, stream);
+    if (n <= 6144) return launch_fast_tv<1024, 6>(A, s, a, sc, o, nw, stream);
+    return launch_fast_tv<1024, 10>(A, s, a, sc, o, nw, stream);
+  }
+  if (n <= 256) return launch_fast_tv<256, 1>(A, s, a, sc, o, nw, stream);
+  if (n <= 512) return launch_fast_tv<256, 2>(A, s, a, sc, o, nw, stream);
+  if (n <= 1024) return launch_fast_tv<256, 4>(A, s, a, sc, o, nw, stream);
+  if (n <= 1536) return launch_fast_tv<256, 6>(A, s, a, sc, o, nw, stream);
+  if (n <= 2560) return launch_fast_tv<256, 10>(A, s, a, sc, o, nw, stream);
+  if (n <= 5120) return launch_fast_tv<256, 20>(A, s, a, sc, o, nw, stream);
+  return launch_fast_tv<256, 40>(A, s, a, sc, o, nw, stream);
 }
 
 hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const AngleEntry* d_angles,
@@ -1133,14 +1205,12 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
     attr_set = true;
   }
   const bool listed = A.need_exact && A.exact_list && !A.order_out;
-  if (listed) {
+  if (listed && !A.host_flag) {  // with a host signal the scoring launch zeroed the count
     hipError_t e = hipMemsetAsync(A.exact_list, 0, sizeof(int32_t), stream);
     if (e != hipSuccess) return e;
   }
   if (A.need_exact && !A.order_out) {  // fast pass first; the exact pass only where it flagged
-    hipLaunchKernelGGL(finish_fast_kernel, dim3(n_windows), dim3(kFastThreads), 0, stream, A, d_scans,
-                       d_angles, d_scores, d_out);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_fast(A, d_scans, d_angles, d_scores, d_out, n_windows, stream);
     if (e != hipSuccess) return e;
   }
   hipStream_t xs = stream;

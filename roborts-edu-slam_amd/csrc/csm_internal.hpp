@@ -87,7 +87,16 @@ struct FinishArgs {
   int32_t* order_out;  // optional: the sorted permutation, n_cand per window
   int32_t* need_exact; // per window: 1 = the fast finish saw a tie that matters (device scratch)
   int32_t* exact_list; // [0] = count, then the flagged windows (device scratch, n_windows + 1)
+  // Host signal (nullable, listed exact pass only): the pass's last block to
+  // finish stores flag_value at host_flag with system scope once every
+  // FinishOut is written (done_ctr: a device counter, zero between launches).
+  int32_t* done_ctr;
+  int32_t* host_flag;
+  int32_t flag_value;
+  int32_t pad;
 };
+// Fast finishes of at most this many windows run 1024 threads per window.
+constexpr int kFinishWideWindows = 64;
 
 // What the host needs to complete BasedCorrelationScanMatch::ScanMatch for
 // one window after the device sorted its candidates.
@@ -143,6 +152,8 @@ constexpr FinishLayout finish_layout(int64_t n) {
 }
 constexpr size_t finish_lds_bytes(int64_t n) { return finish_layout(n).total; }
 
+// A.host_flag (the few-window path): the caller's scoring launch zeroed
+// exact_list[0] already; the exact pass then signals the host when done.
 // exact_on_device = false: only the fast pass runs; the windows it flags
 // (need_exact) are left for the host's std::sort (csm_api.cpp level_end).
 // The fast pass (when A.need_exact) and the exact pass on `stream`; with
@@ -218,6 +229,28 @@ bool phase_supported(int ns, int cells, int nq);
 hipError_t launch_score_phase(const LevelWork& L, const PhaseTable& T, const ScanWork* d_scans, const double* d_pts,
                               const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
                               hipStream_t stream);
+// Split kernel (csm_split.hip): launches of few windows, INT mode, any window
+// step. Lane = candidate, 256-candidate chunks, a window's beams split over
+// `splits` blocks per chunk (<= kSplitMaxBeams each), int32 partial sums
+// handed to the chunk's last block through a slab.
+constexpr int kSplitThreads = 256;
+constexpr int kSplitMaxBeams = 32;   // 32 * 2^26 <= 2^31: a split's int32 sum cannot overflow
+constexpr int kSplitArgAngles = 64;  // angle rows a single window carries in the kernel arguments
+struct SplitWork {
+  int32_t splits;         // beam splits per chunk
+  int32_t chunks;         // ceil(n_cand / kSplitThreads) per window
+  int32_t inline_window;  // 1: one window, its ScanWork and angle rows in `sw` / `ang`
+  int32_t pad;
+  int32_t* slab;          // n_scans * chunks * splits * kSplitThreads int32 partial sums
+  int32_t* arrive;        // n_scans * chunks arrival counters: zero before and after a launch
+  int32_t* clear_word;    // zeroed by block 0 (nullable): the finish's flagged-window count
+  ScanWork* scans_out;    // inline window: block 0 stores it here for the finish ...
+  AngleEntry* angles_out; // ... and its angle rows here
+  ScanWork sw;
+  AngleEntry ang[kSplitArgAngles];
+};
+hipError_t launch_score_split(const LevelWork& L, const SplitWork& W, const ScanWork* d_scans, const double* d_pts,
+                              const AngleEntry* d_angles, double* d_out, hipStream_t stream);
 // gridi layout: row pitch = round4(size_x + kGridiPadCols) cells, size_y +
 // kGridiPadRows rows; every cell outside [0,size_x) x [0,size_y) is zero, so a
 // 16 x 16 box whose corner lies on the grid never leaves the buffer.

@@ -35,6 +35,29 @@ def _map(grid, res, off, update_index=0, version=0):
     return roborts_csm.ScanMatchMap(grid, float(res), tuple(off), update_index, version)
 
 
+def _variant_ctx(kern, **env):
+    """A context of one kernel family. kern: a CSM_KERNEL value, None for the
+    default throughput kernels (box / phase / tiny), "split" for the
+    few-window path (tests/test_gpu_small.py), which single-window calls take
+    by default; every other variant turns it off (CSM_SMALL=0)."""
+    import roborts_csm
+    env = dict(env)
+    if kern != "split":
+        env["CSM_SMALL"] = "0"
+        if kern:
+            env["CSM_KERNEL"] = kern
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return roborts_csm.Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 @pytest.fixture(scope="module")
 def f1(golden_dir):
     return np.load(os.path.join(golden_dir, "f1_config1.npz"))
@@ -239,7 +262,7 @@ def test_headline_runs_row_segment_kernels(ctx, world2000):
     from roborts_csm.params import headline_levels
     w, b = world2000
     ctx.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
-    n = 24
+    n = 48  # above the few-window path's 32 (tests/test_gpu_small.py)
     poses = np.ascontiguousarray(b.init_poses[:n].copy())
     covs = np.tile(np.eye(3).reshape(1, 9), (n, 1))
     ctx.set_profiling(True)
@@ -364,14 +387,8 @@ def test_kernel_variants_agree(f1, grid_kind):
     else:
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
-    ctxs = []
-    for kern in ("v1", "v2", "v3", "v4", "v6", "v7", None):  # None: default (v6 box / v7 phase / v8 tiny / v4)
-        if kern:
-            os.environ["CSM_KERNEL"] = kern
-        try:
-            ctxs.append(roborts_csm.Context(0))
-        finally:
-            os.environ.pop("CSM_KERNEL", None)
+    # None: default throughput kernels (v6 box / v7 phase / v8 tiny / v4); split: few-window path
+    ctxs = [_variant_ctx(k) for k in ("v1", "v2", "v3", "v4", "v6", "v7", None, "split")]
     params = [_param(f1["param"])] + list(SIM_YAML_LEVELS) + [l.with_(use_point_size=1081) for l in SIM_YAML_LEVELS]
     params += [l.with_(use_point_size=1081) for l in PARAM_CONFIG_LEVELS]
     for c in ctxs:
@@ -405,14 +422,7 @@ def test_box_kernel_edge_beams(world2000):
     centers = [[c0, 200.5 + half, 0.0], [c0, 200.5 + half, 1.3],
                [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
                [6.2, 3.1, -2.5], [1995.0, 1990.0, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
-    ctxs = []
-    for kern in (None, "v4"):
-        if kern:
-            os.environ["CSM_KERNEL"] = kern
-        try:
-            ctxs.append(roborts_csm.Context(0))
-        finally:
-            os.environ.pop("CSM_KERNEL", None)
+    ctxs = [_variant_ctx(k) for k in (None, "v4", "split")]
     for c in ctxs:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
     ctxs[0].set_profiling(True)
@@ -748,17 +758,8 @@ def test_phase_kernel_edge_beams(world2000, margin_log2):
                [100.3 + half, 200.1 + half, -0.4],
                [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
                [1.2, 0.1, -2.5], [1998.0, 1990.0, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
-    ctxs = []
-    for kern in (None, "v4"):
-        if kern:
-            os.environ["CSM_KERNEL"] = kern
-        if margin_log2:
-            os.environ["CSM_PHASE_MARGIN_LOG2"] = margin_log2
-        try:
-            ctxs.append(roborts_csm.Context(0))
-        finally:
-            os.environ.pop("CSM_KERNEL", None)
-            os.environ.pop("CSM_PHASE_MARGIN_LOG2", None)
+    env = {"CSM_PHASE_MARGIN_LOG2": margin_log2} if margin_log2 else {}
+    ctxs = [_variant_ctx(k, **env) for k in (None, "v4", "split")]
     for c in ctxs:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
     ctxs[0].set_profiling(True)
@@ -801,14 +802,7 @@ def test_tiny_kernel_edge_beams(world2000, size, res):
     centers = [[100.5 + half, 200.5 + half, 0.0], [100.7 + half, 200.9 + half, 1.3],
                [100.3 + half, 200.1 + half, -0.4], [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
                [0.2, 0.1, -2.5], [1999.6, 1999.7, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
-    ctxs = []
-    for kern in (None, "v4"):
-        if kern:
-            os.environ["CSM_KERNEL"] = kern
-        try:
-            ctxs.append(roborts_csm.Context(0))
-        finally:
-            os.environ.pop("CSM_KERNEL", None)
+    ctxs = [_variant_ctx(k) for k in (None, "v4", "split")]
     for c in ctxs:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
     ctxs[0].set_profiling(True)
@@ -837,7 +831,7 @@ def test_phase_kernel_batch_segments(world2000):
     scans = [np.ascontiguousarray(np.concatenate([b.points_cells[b.offsets[k]:b.offsets[k + 1]]] * r))
              for k, r in ((0, 3), (1, 1), (2, 2))]
     scans.append(rng.uniform(-60, 60, size=(7, 2)))
-    c = roborts_csm.Context(0)
+    c = _variant_ctx(None)
     try:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
         for pts in scans:
