@@ -685,6 +685,7 @@ int ensure_int_grid(csm_ctx* c) {
   if (c->int_checked) return CSM_OK;
   c->int_checked = true;
   c->int_ok = false;
+  if (c->profiling) c->account("grid:analyze", 0.f, 0.0, 0.0);  // a whole-grid analysis + conversion
   const int64_t n = (int64_t)c->info.size_x * c->info.size_y * c->n_grids;
   hipError_t e;
   if ((e = c->gstats.ensure(sizeof(csm::GridStats) * (1 + csm::kAnalyzeBlocks))) != hipSuccess) return c->hip_fail(e, "hipMalloc(stats)");
@@ -2498,9 +2499,8 @@ int csm_update_grid_cells(csm_ctx* c, const void* cells, int64_t stride, const c
   return CSM_OK;
 }
 
-int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) {
-  if (!c || !info) return CSM_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
+namespace {
+int set_grid_device_locked(csm_ctx* c, const float* dev, const csm_map_info* info) {
   if (!dev || info->size_x <= 0 || info->size_y <= 0 || !(info->resolution > 0.0))
     return c->fail(CSM_ERR_INVALID_ARG, "invalid device grid");
   if ((int64_t)info->size_x * info->size_y >= ((int64_t)1 << 31))
@@ -2515,22 +2515,36 @@ int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) 
   c->key_version = -1;
   return CSM_OK;
 }
+}  // namespace
+
+int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) {
+  if (!c || !info) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return set_grid_device_locked(c, dev, info);
+}
 
 int csm_set_grid_gridmap(csm_ctx* c, csm_gridmap* map) {
   if (!c || !map) return CSM_ERR_INVALID_ARG;
-  csm::GridMapView v{};
-  int st = csm::gridmap_view(map, &v);
-  if (st != CSM_OK) return st;
-  if (v.device != c->device) return c->fail(CSM_ERR_INVALID_ARG, "map lives on another device");
+  float outside;
   {
     std::lock_guard<std::mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    // the matcher's kernels run after the map's last update, and the map's
-    // next update after the matcher's reads (csm::gridmap_add_reader)
-    hipError_t e = hipStreamWaitEvent(c->stream, v.ready, 0);
-    if (e != hipSuccess) return c->fail(CSM_ERR_HIP, hipGetErrorString(e));
-    csm::gridmap_add_reader(map, c->stream);
+    outside = c->outside;
   }
+  // the map's fixed-point mirror (kept by the map kernels from the cells each
+  // update writes): no whole-grid analysis and conversion per borrow
+  csm::GridMapFixed fx{};
+  int st = csm::gridmap_fixed_point(map, outside, &fx);
+  if (st != CSM_OK) return st;
+  csm::GridMapView v{};
+  if ((st = csm::gridmap_view(map, &v)) != CSM_OK) return st;
+  if (v.device != c->device) return c->fail(CSM_ERR_INVALID_ARG, "map lives on another device");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  // the matcher's kernels run after the map's last update, and the map's
+  // next update after the matcher's reads (csm::gridmap_add_reader)
+  hipError_t e = hipStreamWaitEvent(c->stream, v.ready, 0);
+  if (e != hipSuccess) return c->fail(CSM_ERR_HIP, hipGetErrorString(e));
+  csm::gridmap_add_reader(map, c->stream);
   csm_map_info info{};
   info.resolution = v.resolution;
   info.offset_x = v.offset_x;
@@ -2538,7 +2552,19 @@ int csm_set_grid_gridmap(csm_ctx* c, csm_gridmap* map) {
   info.size_x = v.size_x;
   info.size_y = v.size_y;
   info.update_index = v.map_update_index;
-  return csm_set_grid_device(c, v.prob, &info);
+  if ((st = set_grid_device_locked(c, v.prob, &info)) != CSM_OK) return st;
+  if (fx.ok && fx.outside == c->outside) {  // ensure_int_grid's state, borrowed
+    c->int_checked = true;
+    c->int_ok = true;
+    c->d_gridi = fx.fpm;
+    c->pitch = fx.pitch;
+    c->int_exp = fx.exp;
+    c->int_max_abs = fx.max_abs;
+    c->outside_i = (int32_t)((double)c->outside * std::ldexp(1.0, fx.exp));
+    c->grid_gen = ++c->gen_clock;
+    if (c->profiling) c->account("grid:mirror", 0.f, 0.0, 0.0);
+  }
+  return CSM_OK;
 }
 
 int csm_scan_match_batch(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,

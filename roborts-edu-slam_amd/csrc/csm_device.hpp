@@ -62,5 +62,27 @@ __device__ __forceinline__ double bcast_lane(double v, int l) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
+// CSM_TRACE_SMALL builds: wall-clock stamps (100 MHz) of the few-window
+// kernels' phases, min over blocks for slot 0 and max for the others
+// (tools/small_trace.py reads them through csm_debug_small_trace).
+#ifdef CSM_TRACE_SMALL
+static __device__ unsigned long long g_small_trace[64];  // one per translation unit
+#define CSM_TS_MIN(slot)                                                   \
+  do {                                                                     \
+    if (threadIdx.x == 0) atomicMin(&::csm::dev::g_small_trace[slot], wall_clock64()); \
+  } while (0)
+#define CSM_TS_MAX(slot)                                                   \
+  do {                                                                     \
+    if (threadIdx.x == 0) atomicMax(&::csm::dev::g_small_trace[slot], wall_clock64()); \
+  } while (0)
+#else
+#define CSM_TS_MIN(slot) \
+  do {                   \
+  } while (0)
+#define CSM_TS_MAX(slot) \
+  do {                   \
+  } while (0)
+#endif
+
 }  // namespace dev
 }  // namespace csm

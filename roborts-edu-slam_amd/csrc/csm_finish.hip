@@ -29,6 +29,7 @@
 // its leaves, then written back once.
 #include <hip/hip_runtime.h>
 
+#include "csm_device.hpp"
 #include "csm_internal.hpp"
 
 #pragma clang fp contract(off)
@@ -841,7 +842,8 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
       finish_window(A, scans, angles, scores, out, A.exact_list[1 + i], smem);
       __syncthreads();  // the next window reuses the LDS carve
     }
-    if (A.host_flag) {  // every block's FinishOut stores land, then the last block signals the host
+    if (A.host_flag && cnt > 0) {  // (nothing flagged: the fast pass signalled the host)
+      // every block's FinishOut stores land, then the last block signals the host
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -897,11 +899,50 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
+// Host signal of the few-window path (A.host_flag): every block's FinishOut
+// stores land (each wave waits, one system-scope release per block), the
+// blocks count in; the last one, if no window was flagged for the exact pass,
+// stores the flag value itself -- the exact launch behind it then returns at
+// once and is off the host's critical path.
+// (Measured: without the per-block system release the host read stale
+// FinishOut fields: the stores to pinned host memory can sit in the XCD's L2.)
+__device__ __forceinline__ void fast_signal(const FinishArgs& A) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the host reads FinishOut
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(A.done_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (int)gridDim.x - 1) {
+      __hip_atomic_store(A.done_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // flag() counts with device-scope atomics before each block's add
+      if (__hip_atomic_load(A.exact_list, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        __hip_atomic_store(A.host_flag, A.flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+template <int T, int V>
+__device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const ScanWork* __restrict__ scans,
+                                                 const AngleEntry* __restrict__ angles,
+                                                 const double* __restrict__ scores, FinishOut* __restrict__ out);
+
 template <int T, int V>
 __global__ __launch_bounds__(T) void finish_fast_kernel(FinishArgs A, const ScanWork* __restrict__ scans,
                                                         const AngleEntry* __restrict__ angles,
                                                         const double* __restrict__ scores,
                                                         FinishOut* __restrict__ out) {
+  CSM_TS_MIN(16);
+  finish_fast_body<T, V>(A, scans, angles, scores, out);
+  CSM_TS_MAX(24);  // body done
+  if (A.host_flag) fast_signal(A);
+  CSM_TS_MAX(25);  // signalled
+}
+
+template <int T, int V>
+__device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const ScanWork* __restrict__ scans,
+                                                 const AngleEntry* __restrict__ angles,
+                                                 const double* __restrict__ scores, FinishOut* __restrict__ out) {
   constexpr int NW = T / 64;
   __shared__ double ck[kFastCap];   // step 2 candidates (value, index), then ...
   __shared__ int ci[kFastCap];
@@ -934,6 +975,7 @@ __global__ __launch_bounds__(T) void finish_fast_kernel(FinishArgs A, const Scan
   const ScanWork S = scans[w];
   const int ns = A.n_space;
   const int nss = ns * ns;
+  CSM_TS_MAX(17);  // score loads issued
   {
     const int na = min(n / nss, kFastAngles);
     for (int t = tid; t < na; t += T) {
@@ -964,6 +1006,7 @@ __global__ __launch_bounds__(T) void finish_fast_kernel(FinishArgs A, const Scan
   double best = red[0];
 #pragma unroll
   for (int q = 1; q < NW; ++q) best = fmax(best, red[q]);
+  CSM_TS_MAX(18);  // max reduced
   if (flag_s || n <= 0) {
     if (tid == 0) flag();
     return;
@@ -981,22 +1024,26 @@ __global__ __launch_bounds__(T) void finish_fast_kernel(FinishArgs A, const Scan
   };
   int lv[V];
   {
+    // per-wave counts from ballots (scalar popcounts; shuffle reductions were
+    // a chain of LDS-permute latencies per level)
     int c[kFastLevels];
 #pragma unroll
-    for (int k = 0; k < kFastLevels; ++k) c[k] = 0;
+    for (int q = 0; q < kFastLevels; ++q) c[q] = 0;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       lv[k] = level_of(v[k]);  // -INFINITY padding: no level
 #pragma unroll
-      for (int q = 0; q < kFastLevels; ++q) c[q] += (lv[k] == q) ? 1 : 0;
+      for (int q = 0; q < kFastLevels; ++q) c[q] += popc(__ballot(lv[k] == q));
     }
+    if (lane < kFastLevels) {
+      int t = 0;
 #pragma unroll
-    for (int q = 0; q < kFastLevels; ++q) {
-      const int t = wave_sum_i(c[q]);
-      if (lane == 0 && t) atomicAdd(&cnt_s[q], t);
+      for (int q = 0; q < kFastLevels; ++q) t = (lane == q) ? c[q] : t;
+      if (t) atomicAdd(&cnt_s[lane], t);
     }
   }
   __syncthreads();
+  CSM_TS_MAX(19);  // level counts
   // 2. the smallest level whose cumulative count reaches 20 (or all > bound);
   // without the positional list, level 0 (exactly FindBest's prefix set)
   const bool want_pos = !(A.skip_lists & 1), want_ang = !(A.skip_lists & 2);
@@ -1048,6 +1095,7 @@ __global__ __launch_bounds__(T) void finish_fast_kernel(FinishArgs A, const Scan
     si[r] = ci[t];
   }
   __syncthreads();
+  CSM_TS_MAX(20);  // compacted and ranked
   if (flag_s) {
     if (tid == 0) flag();
     return;
@@ -1098,6 +1146,7 @@ __global__ __launch_bounds__(T) void finish_fast_kernel(FinishArgs A, const Scan
     o->pos_score[tid] = sk[tid];
   }
   __syncthreads();
+  CSM_TS_MAX(21);  // prefix sums and positional list
   // 3. angular list (:990-1003): near the best, score >= bound
   if (!want_ang) {
     if (tid == 0) {
@@ -1229,6 +1278,16 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
 }
 
 }  // namespace csm
+
+#ifdef CSM_TRACE_SMALL
+// Trace readout of the fast finish's stamps (slots 16-25; tools/small_trace.py).
+extern "C" int csm_debug_fast_trace(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(csm::dev::g_small_trace), 64 * 8) != hipSuccess) return -1;
+  unsigned long long init[64] = {0};
+  init[0] = init[16] = ~0ull;
+  return hipMemcpyToSymbol(HIP_SYMBOL(csm::dev::g_small_trace), init, 64 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef CSM_FINISH_TRACE
 // Trace readout for tools/finish_trace.py: copies and resets the stamps.

@@ -27,6 +27,7 @@
 
 #include "csm_gridmap.h"
 #include "csm_gridmap_internal.hpp"
+#include "csm_internal.hpp"
 #include "host_math.hpp"
 
 namespace {
@@ -121,6 +122,20 @@ struct csm_gridmap {
   uint32_t seq = 0;  // scans drawn with lines (line event keys)
 
   DBuf prob, pass, hit, uidx, touched, fkey, oseq, ends, ktab, count;
+  // Fixed-point mirror of prob for the scan matcher (gridmap_fixed_point):
+  // kept equal to (prob - fpm_outside) * 2^fpm_exp by every kernel that writes
+  // prob while fpm_valid; a growth or an incompatible value drops it.
+  DBuf fpm;
+  bool fpm_valid = false;
+  float fpm_outside = 0.f;
+  int fpm_exp = 0;
+  int32_t fpm_pitch = 0;
+  // A superset of the values the cells can hold, known while every write is
+  // a host-known value (fresh cells, resets, blur splats of the kernel table);
+  // lost for good once an occupied or line update computes values on the device.
+  bool vals_known = true;
+  int vals_min_g = INT32_MAX;  // every nonzero value is a multiple of 2^vals_min_g
+  float vals_max = 0.f;        // max |value|
   void* h_ends = nullptr;
   size_t h_cap = 0;
   bool ktab_dirty = true;
@@ -145,9 +160,47 @@ struct csm_gridmap {
     C.row = row;
     C.size_x = size_x;
     C.size_y = size_y;
+    C.fpm = fpm_valid ? fpm.as<int32_t>() : nullptr;
+    C.fpm_pitch = fpm_pitch;
+    C.fpm_outside = fpm_outside;
+    C.fpm_scale = std::ldexp(1.0, fpm_exp);
     return C;
   }
+  // (max |v| + |outside|) * 2^E below 2^26: the matcher's int32 chunk sums
+  bool fpm_fits(int min_g, float vmax, float outside, int E) const {
+    return (min_g == INT32_MAX || min_g >= -E) && ((double)vmax + std::fabs((double)outside)) * std::ldexp(1.0, E) <
+                                                      std::ldexp(1.0, 26);
+  }
+  // A value the cells may now hold (before the kernel that writes it).
+  void note_value(float v);
+  void note_unknown() {
+    vals_known = false;
+    fpm_valid = false;
+  }
 };
+
+namespace {
+// Smallest power of two a float is an integer multiple of (INT32_MAX for 0).
+int float_granularity(float v) {
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  u &= 0x7FFFFFFFu;
+  if (u == 0) return INT32_MAX;
+  const uint32_t e = u >> 23, mant = u & 0x7FFFFFu;
+  const uint32_t mm = (e == 0) ? mant : (mant | 0x800000u);
+  return ((e == 0) ? -149 : (int)e - 150) + __builtin_ctz(mm);
+}
+}  // namespace
+
+void csm_gridmap::note_value(float v) {
+  if (!std::isfinite(v)) {
+    note_unknown();
+    return;
+  }
+  vals_min_g = std::min(vals_min_g, float_granularity(v));
+  vals_max = std::max(vals_max, std::fabs(v));
+  if (fpm_valid && !fpm_fits(vals_min_g, vals_max, fpm_outside, fpm_exp)) fpm_valid = false;
+}
 
 namespace {
 
@@ -208,6 +261,9 @@ int upload_ktab(csm_gridmap* m) {
   // SetGridProbability(cell, kernel_value[k] * cell_occu_prob_offset_): the
   // double product narrowed to the float parameter (occu_grid_map.h:567).
   for (int k = 0; k < k2; ++k) t[(size_t)k] = (float)(m->kernel[(size_t)k] * m->occu_offset);
+  m->note_value(1.0f);  // the splat's centre
+  for (float v : t)
+    if (v <= 1.0f) m->note_value(v);  // the values blur_splat_kernel writes
   GM_HIP(hipStreamSynchronize(m->stream));
   GM_HIP(m->ktab.ensure((size_t)(k2 > 0 ? k2 : 1) * 4));
   if (k2 > 0) GM_HIP(hipMemcpy(m->ktab.p, t.data(), (size_t)k2 * 4, hipMemcpyHostToDevice));
@@ -259,6 +315,13 @@ int extend_size(csm_gridmap* m) {
   N.row = nsx;
   N.size_x = nsx;
   N.size_y = nsy;
+  N.fpm = nullptr;  // the mirror is rebuilt at the new size on the matcher's next request
+  N.fpm_pitch = 0;
+  N.fpm_outside = 0.f;
+  N.fpm_scale = 1.0;
+  m->fpm_valid = false;
+  m->note_value(m->default_prob);  // fresh cells (fresh_kernel)
+  m->note_value(kDefaultCellProb);
   GM_HIP(csm::gm_launch_fresh(N, n, m->default_prob, m->stream));
   GM_HIP(csm::gm_launch_extend_copy(m->cells(), N, gx, gy, m->stream));
   GM_HIP(hipStreamSynchronize(m->stream));
@@ -373,6 +436,7 @@ int update_by_range(csm_gridmap* m, const double* pts, int n, const double origi
   } else {
     if ((st = flush_pending(m)) != CSM_OK) return st;
     if ((st = upload_ends(m, ends)) != CSM_OK) return st;
+    m->note_unknown();  // cell values computed on the device from here on
     if (mode == kOccupied) {
       GM_HIP(csm::gm_launch_occupied(m->ends.as<GmEnd>(), (int)ends.size(), m->cells(), m->ops, tol, m->stream));
     } else {
@@ -432,6 +496,42 @@ void gridmap_add_reader(csm_gridmap* m, hipStream_t s) {
 void gridmap_drop_reader(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_readers_mu);
   for (auto& kv : g_readers) kv.second.erase(std::remove(kv.second.begin(), kv.second.end(), s), kv.second.end());
+}
+
+int gridmap_fixed_point(csm_gridmap* m, float outside, GridMapFixed* f) {
+  if (!m || !f) return CSM_ERR_INVALID_ARG;
+  *f = GridMapFixed{};
+  std::lock_guard<std::mutex> lk(m->mu);
+  DeviceGuard g(m->device);
+  int st;
+  if ((st = flush_pending(m)) != CSM_OK) return st;  // pending splats first (they keep a valid mirror)
+  if (!m->vals_known || m->kind != kGmProbability || !std::isfinite(outside)) return CSM_OK;
+  // E: every value and `outside` multiples of 2^-E (ensure_int_grid's rule, on
+  // the host-known value set instead of a scan of the cells)
+  const int min_g = std::min(m->vals_min_g, float_granularity(outside));
+  const int E = (min_g == INT32_MAX) ? 0 : std::max(0, -min_g);
+  if (E > 60 || !m->fpm_fits(min_g, m->vals_max, outside, E)) return CSM_OK;
+  const int32_t pitch = gridi_pitch(m->size_x);
+  const int64_t ni = (int64_t)pitch * (m->size_y + kGridiPadRows);
+  if (ni * 4 > 0x7F000000LL) return CSM_OK;
+  if (!(m->fpm_valid && m->fpm_outside == outside && m->fpm_exp == E && m->fpm_pitch == pitch)) {
+    if ((size_t)ni * 4 > m->fpm.cap) GM_HIP(hipStreamSynchronize(m->stream));  // the old buffer may still be read
+    GM_HIP(m->fpm.ensure((size_t)ni * 4));
+    GM_HIP(launch_fixed_point(m->prob.as<float>(), m->size_x, m->size_y, pitch, outside, E, m->fpm.as<int32_t>(),
+                              m->stream, true));
+    m->fpm_valid = true;
+    m->fpm_outside = outside;
+    m->fpm_exp = E;
+    m->fpm_pitch = pitch;
+    GM_HIP(hipEventRecord(m->ready, m->stream));
+  }
+  f->ok = true;
+  f->fpm = m->fpm.as<int32_t>();
+  f->pitch = pitch;
+  f->exp = E;
+  f->max_abs = std::max((double)m->vals_max, std::fabs((double)outside));
+  f->outside = outside;
+  return CSM_OK;
 }
 
 int gridmap_view(csm_gridmap* m, GridMapView* v) {
@@ -498,6 +598,8 @@ int csm_gridmap_create(int device, int32_t kind, double resolution, int32_t size
       }
   }
   const int64_t n = (int64_t)size_x * size_y;
+  m->note_value(default_cell_prob);  // fresh_kernel: element 0, then kDefaultCellProb
+  m->note_value(kDefaultCellProb);
   int st = alloc_cells(m, n, m->prob, m->pass, m->hit, m->uidx, m->touched);
   if (st == CSM_OK && (csm::gm_launch_fresh(m->cells(), n, default_cell_prob, m->stream) != hipSuccess ||
                        m->count.ensure(64) != hipSuccess || hipEventRecord(m->staged, m->stream) != hipSuccess ||
@@ -517,7 +619,7 @@ int csm_gridmap_destroy(csm_gridmap* m) {
     DeviceGuard g(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
     for (DBuf* b : {&m->prob, &m->pass, &m->hit, &m->uidx, &m->touched, &m->fkey, &m->oseq, &m->ends, &m->ktab,
-                    &m->count})
+                    &m->count, &m->fpm})
       b->release();
     if (m->h_ends) (void)hipHostFree(m->h_ends);
     {
@@ -581,6 +683,7 @@ int csm_gridmap_reset(csm_gridmap* m) {
   int st;
   if ((st = flush_pending(m)) != CSM_OK) return st;
   // Reset (grid_map_base.h:95-103) leaves map_update_point_ as it is.
+  m->note_value(m->default_prob);
   GM_HIP(csm::gm_launch_reset(m->cells(), m->ncells(), m->default_prob, false, false, m->stream));
   return finish(m);
 }
@@ -631,6 +734,7 @@ int csm_gridmap_init_with_range_vec(csm_gridmap* m, int32_t n_scans, const doubl
     return m->fail(st, "update mode not supported (full update with blur, or blur on CountCell)");
   if ((st = flush_pending(m)) != CSM_OK) return st;
   // speedup: ResetValueSpeedup(map_update_point_); else Reset(); then the list is cleared
+  m->note_value(m->default_prob);
   GM_HIP(csm::gm_launch_reset(m->cells(), m->ncells(), m->default_prob, speedup != 0, true, m->stream));
   m->cur_update_index = 0;
   m->cur_mark_occu = -1;

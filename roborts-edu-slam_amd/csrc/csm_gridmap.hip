@@ -71,6 +71,18 @@ __device__ __forceinline__ void cell_unset_free(const GmCells& C, const GmOps& P
 __device__ __forceinline__ void raise_prob(float* prob, int64_t i, float p) {
   if (prob[i] < p) atomicMax(reinterpret_cast<unsigned int*>(prob + i), __float_as_uint(p));
 }
+// The fixed-point mirror (GmCells::fpm) of a cell: the fixed_point_kernel's
+// expression (csm_kernels.hip). The map is monotone in the value, so raising
+// the mirror to the max of the raises keeps it equal to the raised cell.
+__device__ __forceinline__ int32_t fixed_of(const GmCells& C, float p) {
+  return (int32_t)(((double)p - (double)C.fpm_outside) * C.fpm_scale);
+}
+__device__ __forceinline__ void raise_mirror(const GmCells& C, int64_t x, int64_t y, float p) {
+  if (!C.fpm) return;
+  int32_t* a = C.fpm + y * C.fpm_pitch + x;
+  const int32_t q = fixed_of(C, p);
+  if (*a < q) atomicMax(a, q);
+}
 
 // LineVisitor::ErgodLineBresenhami (occu_grid_map.h:125-188) in closed form:
 // after the reference's swaps, iteration t visits x0 + t and has taken
@@ -122,11 +134,17 @@ __global__ __launch_bounds__(kThreads) void blur_splat_kernel(const GmEnd* __res
   if (!in_map(C, e.x, e.y, tol)) return;  // CellUpdate :476-478
   const int64_t ci = (int64_t)e.y * C.row + e.x;
   if (!(C.uidx[ci] < e.occu_idx)) return;  // :534
-  if (k == 0) raise_prob(C.prob, ci, 1.0f);  // SetGridProbability(center, 1.0f) :544
+  if (k == 0) {  // SetGridProbability(center, 1.0f) :544
+    raise_prob(C.prob, ci, 1.0f);
+    raise_mirror(C, e.x, e.y, 1.0f);
+  }
   const int i = k % ks - hk, j = k / ks - hk;  // kernel_index = (i+hk) + ks*(j+hk) :563
   const int64_t c = (int64_t)(e.y + j) * C.row + (e.x + i);
   const float p = ktab[k];  // (float)(kernel_value * cell_occu_prob_offset_) :567
-  if (p <= 1.0f) raise_prob(C.prob, c, p);
+  if (p <= 1.0f) {
+    raise_prob(C.prob, c, p);
+    raise_mirror(C, e.x + i, e.y + j, p);
+  }
   C.touched[c] = 1;  // map_update_point_.push_back :571
 }
 
@@ -264,6 +282,10 @@ __global__ __launch_bounds__(kThreads) void reset_kernel(GmCells C, int64_t n, f
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
     if (only_touched && !C.touched[i]) continue;
     C.prob[i] = v;
+    if (C.fpm) {
+      const int64_t y = i / C.row;
+      C.fpm[y * C.fpm_pitch + (i - y * C.row)] = fixed_of(C, v);
+    }
     if (C.pass) {
       C.pass[i] = 0.0f;
       C.hit[i] = 0.0f;

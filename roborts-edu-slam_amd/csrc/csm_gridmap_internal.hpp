@@ -20,6 +20,13 @@ struct GmCells {
   uint8_t* touched;  // map_update_point_ as a set of linear indices
   int32_t row;       // size_x_ (row length of GetCell)
   int32_t size_x, size_y;
+  // Fixed-point mirror of prob the scan matcher reads (nullable): cell (x, y)
+  // at fpm[y * fpm_pitch + x] holds (prob - fpm_outside) * fpm_scale, exact
+  // (csm_internal.hpp gridi layout). Kernels that write prob keep it equal.
+  int32_t* fpm;
+  int32_t fpm_pitch;
+  float fpm_outside;
+  double fpm_scale;
 };
 
 // Cell-function parameters (grid_map_cell.h).
@@ -48,6 +55,20 @@ hipError_t gm_launch_lines(const GmEnd* ends, int n, int sx, int sy, const GmCel
 hipError_t gm_launch_feedback(const GmEnd* ends, int n, int sx, int sy, const GmCells& C, const GmOps& P,
                               int use_blur, double occu_offset, int64_t min_d2, int* count, hipStream_t s);
 
+// The map's fixed-point mirror for a matcher whose off-grid value is
+// `outside` (gridmap_fixed_point): ok = false when the map's values are not
+// known to be exactly summable in fixed point (a line or occupied update on
+// the device wrote values the host cannot bound), and the matcher converts
+// the grid itself.
+struct GridMapFixed {
+  bool ok;
+  const int32_t* fpm;
+  int32_t pitch;
+  int32_t exp;        // E: values are multiples of 2^-E
+  double max_abs;     // max |value| (and |outside|) the map can hold
+  float outside;
+};
+
 // What the scan matcher needs to borrow a map's probabilities.
 struct GridMapView {
   const float* prob;
@@ -62,6 +83,8 @@ struct GridMapView {
 struct csm_gridmap;
 namespace csm {
 int gridmap_view(csm_gridmap* m, GridMapView* v);
+// Builds (or keeps) the mirror for `outside`; the map's `ready` event covers it.
+int gridmap_fixed_point(csm_gridmap* m, float outside, GridMapFixed* f);
 // A matcher stream reads the map: the map's next updates wait for the work
 // enqueued on it so far. drop_reader: the stream is going away.
 void gridmap_add_reader(csm_gridmap* m, hipStream_t s);

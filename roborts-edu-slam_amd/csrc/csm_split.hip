@@ -16,8 +16,8 @@
 // step size, and gathers (value - outside) * 2^E from the fixed-point grid
 // (out-of-grid cells fail the buffer range check and read 0 = `outside`).
 // The int32 partial sums go to a slab; the last block of a chunk to arrive
-// (agent-scope release/acquire around one counter, cdna_hip_programming.md
-// "in-launch split-K reduction") adds the splits in int64 and writes the
+// (one agent-scope counter, write-through slab stores and loads) adds the
+// splits in int64 and writes the
 // penalised scores (:659, :718-745). Integer sums are exact, so the split
 // changes nothing: scores equal the reference's bit for bit.
 //
@@ -45,6 +45,7 @@ __global__ __launch_bounds__(kT) void score_split_kernel(LevelWork L, SplitWork 
                                                          double* __restrict__ out) {
   __shared__ int32_t sh_last[1];
   const int tid = threadIdx.x;
+  CSM_TS_MIN(0);
   if (blockIdx.x == 0) {
     if (W.clear_word && tid == 0) *W.clear_word = 0;
     if (W.inline_window) {
@@ -60,15 +61,20 @@ __global__ __launch_bounds__(kT) void score_split_kernel(LevelWork L, SplitWork 
   const ScanWork S = W.inline_window ? W.sw : scans[win];
   const AngleEntry* __restrict__ ang = W.inline_window ? W.ang : angles + S.angle_off;
 
+  // Lanes run x-fastest inside a row of the window (item i = (a * n + k) * n
+  // + j), not in flat order: at a 5-cell step the flat order (y fastest)
+  // sends every lane of a gather to its own row, the x order lets ~13 lanes
+  // share 2-3 cache lines. The candidate's flat index is (a * n + j) * n + k.
   const int ns = L.n_space;
   const int nss = ns * ns;
-  const int q = chunk * kT + tid;
-  const bool valid = q < L.n_cand;
-  const int qc = valid ? q : 0;
-  const int a = qc / nss;
-  const int r = qc - a * nss;
-  const int j = r / ns;
-  const int k = r - j * ns;
+  const int i = chunk * kT + tid;
+  const bool valid = i < L.n_cand;
+  const int ic = valid ? i : 0;
+  const int a = ic / nss;
+  const int r = ic - a * nss;
+  const int k = r / ns;
+  const int j = r - k * ns;
+  const int q = (a * ns + j) * ns + k;
   const AngleEntry ae = ang[a];
   const double f = L.step_cells;
   const double x = S.x0 + j * f;  // :569
@@ -107,32 +113,49 @@ __global__ __launch_bounds__(kT) void score_split_kernel(LevelWork L, SplitWork 
     for (int u = 0; u < kUnroll; ++u) acc += v[u];
   }
 
-  // slab hand-off: plain stores, release, one ticket per chunk
+  CSM_TS_MAX(1);  // gathers issued and summed
+  // Slab hand-off without fences (MI355X_MICROARCH.md, hand-offs with sc1
+  // loads in place of the acquire, first row): every slab store and load is
+  // an agent-scope (sc1, write-through / L1-bypassing) access, every storing
+  // wave waits for its stores, one lane per block adds to the chunk's counter
+  // behind a barrier, and the block whose add returned splits - 1 reads the
+  // slab after that add has returned (the barrier passes it on). A release /
+  // acquire fence pair here cost ~3.4 us on the level's critical path.
   const int64_t cidx = (int64_t)win * W.chunks + chunk;
   int32_t* slab = W.slab + cidx * W.splits * kT;
-  slab[split * kT + tid] = acc;
+  const uint32_t slo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)slab);
+  const uint32_t shi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)slab >> 32));
+  const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)shi << 32) | slo), (short)0, W.splits * kT * 4, 0x00020000);
+  constexpr int kSc1 = 16;  // cache policy sc1: write-through stores, L1-bypassing loads
+  __builtin_amdgcn_raw_buffer_store_b32(acc, srsrc, (split * kT + tid) * 4, 0, kSc1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int ticket = __hip_atomic_fetch_add(W.arrive + cidx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh_last[0] = ticket == W.splits - 1;
   }
   __syncthreads();
+  CSM_TS_MAX(2);  // tickets drawn
   if (!sh_last[0]) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    W.arrive[cidx] = 0;  // ready for the next launch (kernel boundary orders it)
-  }
-  __syncthreads();
+  if (tid == 0)  // ready for the next launch (the kernel boundary orders it)
+    __hip_atomic_store(W.arrive + cidx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // every split's partial in flight at once (sc1 loads), then the int64 sum
   int64_t sum = 0;
-  for (int s = 0; s < W.splits; ++s) sum += slab[s * kT + tid];
+  for (int s0 = 0; s0 < W.splits; s0 += kUnroll) {
+    int32_t v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+      v[u] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, s0 + u < W.splits ? ((s0 + u) * kT + tid) * 4 : -(1 << 30), 0,
+                                                  kSc1);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) sum += v[u];
+  }
   if (valid) {
     const double accd = (double)(sum + (int64_t)S.n_used * L.outside_i) * L.int_scale;
     out[S.out_off + q] = dev::penalized(L, S, accd, x, y, ae.angle);
   }
+  CSM_TS_MAX(3);  // chunk reduced, scores written
 }
 
 }  // namespace
@@ -152,3 +175,14 @@ hipError_t launch_score_split(const LevelWork& L, const SplitWork& W, const Scan
 }
 
 }  // namespace csm
+
+#ifdef CSM_TRACE_SMALL
+// Trace readout for tools/small_trace.py: copies the stamps, then resets them
+// (slot 0 and 16 to the maximum for the min stamps, the rest to 0).
+extern "C" int csm_debug_small_trace(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(csm::dev::g_small_trace), 64 * 8) != hipSuccess) return -1;
+  unsigned long long init[64] = {0};
+  init[0] = init[16] = ~0ull;
+  return hipMemcpyToSymbol(HIP_SYMBOL(csm::dev::g_small_trace), init, 64 * 8) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -127,3 +127,54 @@ def test_map_update_after_set_grid_is_ordered():
             om = O.Map(prob, st.resolution, (st.offset_x, st.offset_y), st.map_update_index)
             s2, pose2, cov2 = O.scan_matchers(om, scans[k], SIM_YAML_LEVELS, init, np.eye(3))
             assert s == s2 and np.array_equal(pose, pose2) and np.array_equal(cov, cov2), k
+
+
+def test_matcher_uses_map_mirror_exactly():
+    """The map keeps a fixed-point mirror of its cells (every kernel that
+    writes prob writes it too), so csm_set_grid_gridmap no longer analyses and
+    converts the whole grid per scan. Through blur updates, a growth, a blur
+    offset change (new splat values), the back end's reset speed-up and a
+    full reset, every borrow uses the mirror and every score of three windows
+    equals the oracle's on the downloaded cells; a map that took a line update
+    (device-computed values) falls back to the whole-grid conversion, still
+    exact."""
+    import pyoracle as O
+    import roborts_csm
+    from roborts_csm.gridmap import OccuGridMap, set_matcher_grid
+    from roborts_csm.params import SIM_YAML_LEVELS
+    scans, poses = _fine_map_stream(8)
+    res = 0.01
+    off = (-(poses[0][0] - 0.5 * 700 * res), -(poses[0][1] - 0.5 * 700 * res))
+
+    def check(ctx, m, k, want_mirror):
+        ctx.set_profiling(True)
+        set_matcher_grid(ctx, m)
+        st = m.state()
+        prob = m.cells()[0]
+        om = O.Map(prob, st.resolution, (st.offset_x, st.offset_y), st.map_update_index)
+        c = O.world_to_map(om, poses[k] + np.array([0.02, -0.01, 0.01]))
+        for lv in SIM_YAML_LEVELS:
+            got = ctx.score_window(scans[k], lv, c)
+            assert np.array_equal(got, O.score_window(om, scans[k], lv, c, got.size)), (k, lv)
+        names = {s["name"] for s in ctx.kernel_stats()}
+        ctx.set_profiling(False)
+        assert ("grid:mirror" in names) == want_mirror and ("grid:analyze" in names) != want_mirror, names
+
+    with roborts_csm.Context(0) as ctx:
+        m = OccuGridMap(res, (700, 700), off, 0.03, 0.3)
+        m.set_options(True, True, 0.88, 0.2)
+        for k in range(3):  # blur splats; the 700-cell map grows under the 10 m scans
+            m.UpdateMapByRange(scans[k], poses[k], use_blur=True)
+            check(ctx, m, k + 1, True)
+        m.set_options(True, True, 0.72, 0.2)  # new splat values
+        m.UpdateMapByRange(scans[4], poses[4], use_blur=True)
+        check(ctx, m, 5, True)
+        m.InitMapWithRangeVec([scans[5], scans[6]], [poses[5], poses[6]], use_blur=True, use_reset_speedup=True)
+        check(ctx, m, 7, True)
+        m.Reset()
+        check(ctx, m, 7, True)
+        lines = OccuGridMap(res, (700, 700), off, 0.0, 0.3)
+        lines.set_options(True, False, 0.88, 0.2)
+        drawn = [lines.UpdateMapByRange(scans[k], poses[k]) for k in range(3)]  # the first grows the map
+        assert any(drawn)
+        check(ctx, lines, 3, False)

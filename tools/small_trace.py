@@ -1,0 +1,60 @@
+"""Phase stamps of the few-window kernels (CSM_TRACE_SMALL build:
+`make VARIANT=trace EXTRA=-DCSM_TRACE_SMALL`, loaded with CSM_LIB): per level
+of single-scan matches on a 1 cm map, microseconds from the split kernel's
+first block start."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "roborts-edu-slam_amd"))
+import roborts_csm  # noqa: E402
+from roborts_csm import _abi, worlds  # noqa: E402
+from roborts_csm.params import SIM_YAML_LEVELS  # noqa: E402
+
+
+def main():
+    lib = roborts_csm._lib
+    buf = (C.c_ulonglong * 64)()
+    rd = {"split": lib.csm_debug_small_trace, "fast": lib.csm_debug_fast_trace}
+    w = worlds.make_world(3000, 3000, 0.01, seed=31)
+    b = worlds.make_scan_batch(w, 16, seed=5)
+    names = {"split": {1: "gathers", 2: "tickets", 3: "reduced"},
+             "fast": {16: "start", 17: "loads", 18: "max", 19: "counts", 20: "ranked", 21: "prefix", 24: "body",
+                      25: "signal"}}
+    res = {lv: [] for lv in range(3)}
+    with roborts_csm.Context(0) as ctx:
+        ctx.set_grid(roborts_csm.ScanMatchMap(w.grid, 0.01, tuple(w.offset), 0, 1))
+        for f in rd.values():
+            f(buf)
+        for i in range(60):
+            k = i % 16
+            pts = b.points_cells[b.offsets[k]:b.offsets[k + 1]]
+            pose = np.array(b.init_poses[k])
+            for lv in range(3):
+                cov = np.eye(3).reshape(9).copy()
+                ctx.scan_match(pts, SIM_YAML_LEVELS[lv], pose, cov)
+                st = {}
+                for nm, f in rd.items():
+                    f(buf)
+                    st[nm] = list(buf)
+                t0 = st["split"][0]
+                row = {}
+                for nm in names:
+                    for slot, lab in names[nm].items():
+                        v = st[nm][slot]
+                        row[f"{nm}:{lab}"] = (v - t0) / 100.0 if v not in (0, 2 ** 64 - 1) else None
+                if i >= 10:
+                    res[lv].append(row)
+    out = {}
+    for lv, rows in res.items():
+        keys = rows[0].keys()
+        out[f"level{lv}"] = {k: float(np.median([r[k] for r in rows if r[k] is not None]))
+                             for k in keys if any(r[k] is not None for r in rows)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
