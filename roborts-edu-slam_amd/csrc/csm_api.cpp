@@ -511,6 +511,12 @@ struct csm_ctx {
   int small_max_windows = 32;  // CSM_SMALL_WINDOWS
   int split_target_blocks = 512;  // CSM_SPLIT_TARGET: blocks a split launch aims for
   HostBuf h_pack;  // pinned staging of packed grid rows / cell updates (grid uploads)
+  hipEvent_t ev_pack = nullptr;  // the last copy out of h_pack (cell updates return before it ends)
+  bool ev_pack_used = false;
+  // the points last uploaded (upload_points skips an identical upload: the
+  // reference's ScanMatchers calls each level with the same range data)
+  std::vector<double> pts_host;
+  bool pts_cached = false;
   DevBuf d_updates;  // csm_update_grid_cells entries on the device
 
   // Resident grids of other host maps. csm_set_grid keys a grid on the host
@@ -591,6 +597,7 @@ struct csm_ctx {
 
   // per-kernel HIP-event timing (csm_set_profiling / csm_kernel_stats)
   bool profiling = false;
+  bool stats_dump = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   hipEvent_t ev_done = nullptr;  // end of a launch's work (async runs)
   hipEvent_t ev_in = nullptr;    // a launch's inputs are on the device
@@ -1463,6 +1470,11 @@ bool plan_windows_shared(const csm_param& P, const Dims& D, const Geometry& G, i
 
 int upload_points(csm_ctx* c, const double* pts, int64_t n_total, void* pinned = nullptr) {
   c->loaded_n = -1;  // the point buffer is shared with csm_load_scans
+  const size_t nb = (size_t)std::max<int64_t>(n_total, 0) * 2 * sizeof(double);
+  if (c->pts_cached && n_total > 0 && c->pts_host.size() * sizeof(double) == nb &&
+      std::memcmp(c->pts_host.data(), pts, nb) == 0)
+    return CSM_OK;  // the device buffer holds these points (and pts_maxabs is theirs)
+  c->pts_cached = false;
   double m = 0.0;    // max |x| + |y| over the points: bounds every rotated endpoint
   for (int64_t i = 0; i < n_total; ++i) {
     const double a = std::fabs(pts[2 * i]) + std::fabs(pts[2 * i + 1]);
@@ -1492,6 +1504,10 @@ int upload_points(csm_ctx* c, const double* pts, int64_t n_total, void* pinned =
   if (own) {
     if ((e = hipEventRecord(c->ev_pts, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord(points)");
     c->ev_pts_used = true;
+  }
+  if (n_total > 0 && nbytes <= ((size_t)4 << 20)) {
+    c->pts_host.assign(pts, pts + 2 * n_total);
+    c->pts_cached = true;
   }
   return CSM_OK;
 }
@@ -2226,12 +2242,15 @@ int csm_create(int device, csm_ctx** out) {
   }
   if (const char* env = std::getenv("CSM_SKIP_DEAD_LISTS")) c->skip_dead_lists = std::atoi(env) != 0;
   if (const char* env = std::getenv("CSM_SMALL")) c->small_path = std::atoi(env) != 0;
+  // CSM_STATS_DUMP=1: profiling on from the start, the per-kernel stats printed
+  // to stderr by csm_destroy (C++ callers without a stats hook, tests/cpp)
+  if (const char* env = std::getenv("CSM_STATS_DUMP")) c->stats_dump = std::atoi(env) != 0;
   if (const char* env = std::getenv("CSM_SMALL_WINDOWS")) c->small_max_windows = std::max(1, std::atoi(env));
   if (const char* env = std::getenv("CSM_SPLIT_TARGET")) c->split_target_blocks = std::max(1, std::atoi(env));
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
   bool ev_ok = true;
-  for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k, &c->ev_fast, &c->ev_pts})
+  for (hipEvent_t* ev : {&c->ev_done, &c->ev_in, &c->ev_k, &c->ev_fast, &c->ev_pts, &c->ev_pack})
     ev_ok = ev_ok && hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
   for (auto& a : c->alt)
     for (hipEvent_t* ev : {&a.ev_done, &a.ev_in, &a.ev_k, &a.ev_fast})
@@ -2245,11 +2264,16 @@ int csm_create(int device, csm_ctx** out) {
     return CSM_ERR_HIP;
   }
   *out = c;
+  if (c->stats_dump) csm_set_profiling(c, 1);
   return CSM_OK;
 }
 
 int csm_destroy(csm_ctx* c) {
   if (!c) return CSM_OK;
+  if (c->stats_dump)
+    for (const auto& st : c->stats)
+      std::fprintf(stderr, "csm stats: %-40s launches %8lld  avg_us %10.3f  total_ms %10.3f\n", st.name,
+                   (long long)st.launches, st.launches ? st.total_ms / st.launches * 1e3 : 0.0, st.total_ms);
   {
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
@@ -2304,7 +2328,7 @@ int csm_destroy(csm_ctx* c) {
       for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k, a.ev_fast})
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k, c->ev_fast, c->ev_pts})
+    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k, c->ev_fast, c->ev_pts, c->ev_pack})
       if (ev) (void)hipEventDestroy(ev);
     if (c->x_stream) (void)hipStreamDestroy(c->x_stream);
     (void)hipStreamDestroy(c->h2d);
@@ -2355,6 +2379,7 @@ int check_grid_args(csm_ctx* c, const void* cells, int64_t stride, const csm_map
 int upload_grid(csm_ctx* c, const void* cells, int64_t stride, const csm_map_info* info, int64_t version) {
   const size_t ncell = (size_t)info->size_x * (size_t)info->size_y;
   hipError_t e;
+  if (c->ev_pack_used && (e = hipEventSynchronize(c->ev_pack)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize(pack)");
   if ((e = c->grid_buf.ensure(ncell * sizeof(float))) != hipSuccess) return c->hip_fail(e, "hipMalloc(grid)");
   if ((e = c->h_pack.ensure(ncell * sizeof(float))) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(grid)");
   pack_rows(c, cells, stride, info->size_x, 0, info->size_y, (float*)c->h_pack.p);
@@ -2418,6 +2443,7 @@ int csm_update_grid_rows(csm_ctx* c, const void* cells, int64_t stride, const cs
   const int32_t sx = info->size_x;
   const size_t n = (size_t)(row_end - row_begin) * (size_t)sx;
   hipError_t e;
+  if (c->ev_pack_used && (e = hipEventSynchronize(c->ev_pack)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize(pack)");
   if ((e = c->h_pack.ensure(n * sizeof(float))) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(rows)");
   const PackStats ps = pack_rows(c, cells, stride, sx, row_begin, row_end, (float*)c->h_pack.p);
   float* dst = (float*)c->grid_buf.p + (int64_t)row_begin * sx;
@@ -2447,16 +2473,22 @@ int csm_update_grid_cells(csm_ctx* c, const void* cells, int64_t stride, const c
   if (!same_geometry(c, cells, stride, info)) return upload_grid(c, cells, stride, info, version);
   const int64_t ncell = (int64_t)info->size_x * info->size_y;
   hipError_t e;
+  if (c->ev_pack_used && (e = hipEventSynchronize(c->ev_pack)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize(pack)");
   if ((e = c->h_pack.ensure((size_t)std::max<int64_t>(n_indices, 1) * sizeof(csm::CellUpdate))) != hipSuccess)
     return c->hip_fail(e, "hipHostMalloc(cell updates)");
   csm::CellUpdate* u = (csm::CellUpdate*)c->h_pack.p;
+  const double t_pack0 = now_ms();
   const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(c->host_threads * 4, n_indices / 4096 + 1));
   std::vector<PackStats> part((size_t)chunks);
   std::atomic<bool> bad{false};
   c->parallel_for(chunks, c->host_threads, [&](int t) {
     const int64_t i0 = n_indices * t / chunks, i1 = n_indices * (t + 1) / chunks;
     PackStats ps;
+    constexpr int64_t kAhead = 24;  // random reads of a large host map: keep misses in flight
+    for (int64_t i = i0; i < std::min(i1, i0 + kAhead); ++i)
+      __builtin_prefetch((const char*)cells + (int64_t)cell_indices[i] * stride);
     for (int64_t i = i0; i < i1; ++i) {
+      if (i + kAhead < i1) __builtin_prefetch((const char*)cells + (int64_t)cell_indices[i + kAhead] * stride);
       const int32_t k = cell_indices[i];
       if (k < 0 || k >= ncell) {
         bad = true;
@@ -2474,6 +2506,7 @@ int csm_update_grid_cells(csm_ctx* c, const void* cells, int64_t stride, const c
     part[(size_t)t] = ps;
   });
   if (bad) return c->fail(CSM_ERR_INVALID_ARG, "cell index outside the grid");
+  if (c->profiling) c->account("host:cells_pack", (float)(now_ms() - t_pack0), 0.0, (double)n_indices);
   c->info = *info;
   c->key_version = version;
   if (n_indices == 0) return CSM_OK;
@@ -2493,7 +2526,10 @@ int csm_update_grid_cells(csm_ctx* c, const void* cells, int64_t stride, const c
                                     info->size_x, fixed ? (int32_t*)c->gridi.p : nullptr, c->pitch, c->outside,
                                     c->int_exp, c->stream)) != hipSuccess)
     return c->hip_fail(e, "update_cells_kernel");
-  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(cells)");
+  // no wait here: the matches that read the cells follow on the same stream;
+  // the next writer of h_pack waits for this copy (ev_pack)
+  if ((e = hipEventRecord(c->ev_pack, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord(pack)");
+  c->ev_pack_used = true;
   c->grid_gen = ++c->gen_clock;
   if (c->profiling) c->account("grid:cells", 0.f, (double)bytes, 0.0);
   return CSM_OK;
