@@ -510,6 +510,7 @@ struct csm_ctx {
   bool small_path = true;      // CSM_SMALL=0: few-window launches take the throughput kernels
   int small_max_windows = 32;  // CSM_SMALL_WINDOWS
   int split_target_blocks = 512;  // CSM_SPLIT_TARGET: blocks a split launch aims for
+  int fast_wide_windows = 0;      // CSM_FAST_WIDE: fast finishes of <= this many windows on 1024 threads (0: 64; -1: never)
   HostBuf h_pack;  // pinned staging of packed grid rows / cell updates (grid uploads)
   hipEvent_t ev_pack = nullptr;  // the last copy out of h_pack (cell updates return before it ends)
   bool ev_pack_used = false;
@@ -1144,6 +1145,7 @@ int run_windows_small(csm_ctx* c, const csm_param& P, const Dims& D, const Geome
   A.exact_list = d_list;
   A.done_ctr = d_done;
   A.host_flag = h_flag;
+  A.wide_windows = c->fast_wide_windows;
   A.flag_value = (int32_t)(++c->flag_seq & 0x7FFFFFFF);
   if (A.flag_value == 0) A.flag_value = (int32_t)(++c->flag_seq & 0x7FFFFFFF);
   if ((e = csm::launch_finish(A, d_scans, d_angles, (const double*)c->scores.p, h_out, nw, c->stream)) != hipSuccess)
@@ -2247,6 +2249,7 @@ int csm_create(int device, csm_ctx** out) {
   if (const char* env = std::getenv("CSM_STATS_DUMP")) c->stats_dump = std::atoi(env) != 0;
   if (const char* env = std::getenv("CSM_SMALL_WINDOWS")) c->small_max_windows = std::max(1, std::atoi(env));
   if (const char* env = std::getenv("CSM_SPLIT_TARGET")) c->split_target_blocks = std::max(1, std::atoi(env));
+  if (const char* env = std::getenv("CSM_FAST_WIDE")) c->fast_wide_windows = std::atoi(env);
   if (const char* env = std::getenv("CSM_PIPELINE_PARTS"))
     c->pipeline_parts = std::max(2, std::min(std::atoi(env), csm_ctx::kMaxParts));
   bool ev_ok = true;

@@ -955,6 +955,11 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   __shared__ int cnt_s[kFastLevels];
   __shared__ int nC_s, nN_s, flag_s;
   __shared__ double sbx, sby;
+  // FinishOut is assembled in LDS and stored once at the end (34 16-byte
+  // stores): written field by field it was dozens of scattered stores, to
+  // pinned host memory on the few-window path, each barrier after them
+  // waiting for their completions.
+  __shared__ __attribute__((aligned(16))) FinishOut so;
   const int w = blockIdx.x;
   const int n = (int)A.n_cand;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1014,13 +1019,15 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   const double lo = best - 0.1;
   const double bound = (0.5 < lo) ? 0.5 : lo;  // std::min(best - 0.1, 0.5) (:912,:986)
   // level k < 7: s > bound and s - best >= -0.01 * 2^k; level 7: s > bound
-  auto level_of = [&](double s) {  // smallest level holding s (kFastLevels: none)
-    if (!(s > bound)) return kFastLevels;
+  // smallest level holding s (kFastLevels: none), branch-free: d >= -dl holds
+  // from the first level on (dl doubles), so the level counts the failures
+  auto level_of = [&](double s) {
     const double d = s - best;
     double dl = 0.01;
-    for (int k = 0; k < kFastLevels - 1; ++k, dl *= 2.0)
-      if (d >= -dl) return k;
-    return kFastLevels - 1;
+    int lv = 0;
+#pragma unroll
+    for (int k = 0; k < kFastLevels - 1; ++k, dl *= 2.0) lv += (d < -dl) ? 1 : 0;
+    return (s > bound) ? lv : kFastLevels;
   };
   int lv[V];
   {
@@ -1103,7 +1110,14 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   const double f = A.step_cells;
   auto cx = [&](int idx) { return S.x0 + ((idx / ns) % ns) * f; };
   auto cy = [&](int idx) { return S.y0 + (idx % ns) * f; };
-  FinishOut* o = out + w;
+  FinishOut* const o = &so;
+  auto emit = [&]() {  // all threads: the LDS FinishOut to out[w]
+    static_assert(sizeof(FinishOut) % 16 == 0, "FinishOut in 16-byte pieces");
+    constexpr int kPieces = (int)(sizeof(FinishOut) / 16);
+    __syncthreads();
+    if (tid < kPieces)
+      reinterpret_cast<int4*>(out + w)[tid] = reinterpret_cast<const int4*>(&so)[tid];
+  };
   if (tid == 0) {  // :676-707, the same sequential sums as finish_kernel
     double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;
     int count = 0;
@@ -1149,10 +1163,9 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   CSM_TS_MAX(21);  // prefix sums and positional list
   // 3. angular list (:990-1003): near the best, score >= bound
   if (!want_ang) {
-    if (tid == 0) {
-      o->n_ang = 0;
-      *need = 0;
-    }
+    if (tid == 0) o->n_ang = 0;
+    emit();
+    if (tid == 0) *need = 0;
     return;
   }
   const double bx = sbx, by = sby, tol = A.lin_tol;
@@ -1182,6 +1195,7 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
     }
   }
   __syncthreads();
+  CSM_TS_MAX(22);  // near-best compacted
   const int nN = nN_s;
   if (nN > kFastNearCap) {
     if (tid == 0) flag();
@@ -1202,11 +1216,14 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    o->n_ang = min(nN, kCovPoints);
-    if (flag_s) flag();
-    else *need = 0;
+  CSM_TS_MAX(23);  // near-best ranked
+  if (tid == 0) o->n_ang = min(nN, kCovPoints);
+  if (flag_s) {  // (flag_s is read after the barrier above: uniform)
+    if (tid == 0) flag();
+    return;
   }
+  emit();
+  if (tid == 0) *need = 0;
 }
 
 // Scores per thread of the fast finish's instantiations: the smallest V with
@@ -1221,7 +1238,7 @@ hipError_t launch_fast_tv(const FinishArgs& A, const ScanWork* s, const AngleEnt
 hipError_t launch_fast(const FinishArgs& A, const ScanWork* s, const AngleEntry* a, const double* sc, FinishOut* o,
                        int32_t nw, hipStream_t stream) {
   const int64_t n = A.n_cand;
-  if (nw <= kFinishWideWindows) {  // few windows: 16 waves per window
+  if (nw <= (A.wide_windows ? A.wide_windows : kFinishWideWindows)) {  // few windows: 16 waves per window
     if (n <= 1024) return launch_fast_tv<1024, 1>(A, s, a, sc, o, nw, stream);
     if (n <= 2048) return launch_fast_tv<1024, 2>(A, s, a, sc, o, nw, stream);
     if (n <= 4096) return launch_fast_tv<1024, 4>(A, s, a, sc, o, nw, stream);

@@ -93,9 +93,10 @@ struct FinishArgs {
   int32_t* done_ctr;
   int32_t* host_flag;
   int32_t flag_value;
-  int32_t pad;
+  // fast finishes of at most this many windows run 1024 threads per window
+  // (256 otherwise); 0 selects kFinishWideWindows
+  int32_t wide_windows;
 };
-// Fast finishes of at most this many windows run 1024 threads per window.
 constexpr int kFinishWideWindows = 64;
 
 // What the host needs to complete BasedCorrelationScanMatch::ScanMatch for

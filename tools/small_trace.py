@@ -23,7 +23,7 @@ def main():
     b = worlds.make_scan_batch(w, 16, seed=5)
     names = {"split": {1: "gathers", 2: "tickets", 3: "reduced"},
              "fast": {16: "start", 17: "loads", 18: "max", 19: "counts", 20: "ranked", 21: "prefix", 24: "body",
-                      25: "signal"}}
+                      22: "near", 23: "nrank", 25: "signal"}}
     res = {lv: [] for lv in range(3)}
     with roborts_csm.Context(0) as ctx:
         ctx.set_grid(roborts_csm.ScanMatchMap(w.grid, 0.01, tuple(w.offset), 0, 1))
