@@ -290,6 +290,58 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
     }
 
 
+def loop_closure_capi_bench(args):
+    """Config 3 through the C-ABI TryCloseLoop would call from C++
+    (include/csm_loop_closure.h; range_scan_pose_graph.cpp:299-355): ONE
+    process drives args.gpus devices, csm_loop_closure_create makes a matcher
+    context and an RCCL communicator per device (ncclCommInitAll), the 512
+    submaps are sharded over them, and each query ends in the MAX / MIN / SUM
+    all-reduces. n_devices is what the library reports in the result."""
+    import roborts_csm
+    from roborts_csm import worlds
+    from roborts_csm.loop_closure import DeviceLoopClosure
+    from roborts_csm.params import CorrelationScanMatchParam
+    n_sub, side, res = args.submaps, 800, 0.05
+    bases = [worlds.make_world(side, side, res, seed=20261015 + k) for k in range(8)]
+    stack = np.empty((n_sub, side, side), dtype=np.float32)
+    for s in range(n_sub):  # the torch-sharded bench's submaps, all in one host stack
+        stack[s] = np.roll(bases[s % 8].grid, ((s // 8) * 7, (s // 8) * 11), axis=(0, 1))
+    batch = worlds.make_scan_batch(bases[0], 1, seed=7)
+    pts = batch.points_cells[batch.offsets[0]:batch.offsets[1]]
+    pose = batch.init_poses[0]
+    offsets = np.tile(np.array(bases[0].offset), (n_sub, 1))
+    param = CorrelationScanMatchParam(16.0, 0.05, math.pi, 0.0349, 0.5, 100, 0, False, 0)
+    na, ns = roborts_csm.window_dims(param)
+    lc = DeviceLoopClosure(list(range(args.gpus)))
+    try:
+        lc.set_submaps(stack, res, offsets, version=1)
+        for _ in range(args.warmup):
+            r = lc.match(pts, param, pose, search=args.search)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            r = lc.match(pts, param, pose, search=args.search)
+        elapsed = time.perf_counter() - t0
+        n_dev = lc.last_n_devices
+    finally:
+        lc.close()
+    total = float(n_sub) * na * ns * ns * args.steps
+    return {
+        "metric": METRIC, "value": total / elapsed, "unit": "scorings/s", "n_gpus": args.gpus,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (8 seeded 800x800 wall maps, shifted into 512 submaps; one ray-cast query)",
+        "config": {"workload": f"config3 via the C-ABI (csm_loop_closure_*): 1 query x {n_sub} submaps 800x800 "
+                               f"@5cm, +-8 m / +-pi window ({na}x{ns}^2 candidates per submap), B=109",
+                   "search": args.search, "lc": "capi",
+                   "parallelism": f"one process, submaps sharded over {n_dev} devices, in-process RCCL "
+                                  f"communicator (ncclCommInitAll), MAX/MIN/SUM all-reduce",
+                   "n_devices": n_dev},
+        "roofline": None,
+        "result": {"score": r.score, "submap": r.submap, "global_index": r.global_index},
+        "cpu_baseline": None,
+    }
+
+
 def lc_cpu_baseline(bases, pts, param, pose, seconds, per_submap):
     """Config-3 CPU leg: the oracle's argmax over whole submap windows (the
     reference's GetResponse loop over 181 x 321^2 candidates), all host
@@ -847,6 +899,10 @@ def main():
                     help="loop_closure / willow: the admissible multi-resolution search (csm_search_windows) "
                          "or every candidate scored (csm_best_windows); both give the same answer")
     ap.add_argument("--depth", type=int, default=-1, help="pyramid search: top level (-1: automatic)")
+    ap.add_argument("--lc", choices=["torch", "capi"], default="torch",
+                    help="loop_closure: torch = one rank per GPU, the exchange over torch.distributed (RCCL); "
+                         "capi = ONE process over --gpus devices through csm_loop_closure_* (in-process "
+                         "RCCL communicator), what TryCloseLoop calls from C++")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true",
@@ -863,6 +919,12 @@ def main():
         args.steps = 30 if args.workload == "config2" else 5
     if args.warmup is None:
         args.warmup = 5 if args.workload == "config2" else 2
+
+    if args.workload == "loop_closure" and args.lc == "capi":  # one process, every device
+        out = loop_closure_capi_bench(args)
+        out["world"] = {"world_size": 1, "backend": "rccl (in-process communicator)"}
+        print(json.dumps(out))
+        return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))

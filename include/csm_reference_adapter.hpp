@@ -21,6 +21,13 @@
 //    ProbabilityCell stride; the library keeps up to four maps resident,
 //    keyed on that pointer, so the front end's fine map and the back end's
 //    maps (ScanMatchInterface) do not evict each other.
+//  * A map that also exposes GetCellGeneration() (an integer the reference
+//    side bumps whenever the cell buffer is allocated: AllocateGridCell and
+//    ExtendSize, grid_map_base.h:152-166,186-254) is keyed on (cell pointer,
+//    size, generation): a freed buffer reused at the same address by another
+//    map is then never refreshed incrementally against the old map's device
+//    copy. Without it the key is (cell pointer, size), and a reuse at the same
+//    address and size is detected only through the update list and reset count.
 //  * When the map also exposes GetUpdatePoints() (the reference's
 //    map_update_point_, occu_grid_map.h:589: every cell UpdateMapByRange
 //    writes is appended, :509,528,571) and GetResetCount() (bumped by
@@ -110,6 +117,19 @@ template <class M>
 struct has_update_points<M, typename voider<decltype(std::declval<const M&>().GetUpdatePoints()),
                                             decltype(std::declval<const M&>().GetResetCount())>::type>
     : std::true_type {};
+template <class M, class = void>
+struct has_cell_generation : std::false_type {};
+template <class M>
+struct has_cell_generation<M, typename voider<decltype(std::declval<const M&>().GetCellGeneration())>::type>
+    : std::true_type {};
+template <class M>
+int64_t cell_generation(const M& m, std::true_type) {
+  return static_cast<int64_t>(m.GetCellGeneration());
+}
+template <class M>
+int64_t cell_generation(const M&, std::false_type) {
+  return -1;
+}
 }  // namespace detail
 
 // Drop-in for roborts_slam::BasedCorrelationScanMatch.
@@ -154,6 +174,7 @@ class BasedCorrelationScanMatchGpu {
   struct MapState {
     int32_t size_x = -1, size_y = -1;
     int64_t reset_count = -1;
+    int64_t generation = -1;  // GetCellGeneration(), or -1 without the accessor
     size_t points_seen = 0;
     int32_t update_index = -1;
   };
@@ -192,9 +213,10 @@ class BasedCorrelationScanMatchGpu {
     const void* cells = static_cast<const void*>(map.GetCellData());
     const std::vector<int>& pts = map.GetUpdatePoints();
     const int64_t resets = static_cast<int64_t>(map.GetResetCount());
+    const int64_t gen = detail::cell_generation(map, detail::has_cell_generation<MapT>());
     MapState& s = maps_[cells];
     int st;
-    if (s.size_x == info.size_x && s.size_y == info.size_y && s.reset_count == resets &&
+    if (s.size_x == info.size_x && s.size_y == info.size_y && s.reset_count == resets && s.generation == gen &&
         pts.size() >= s.points_seen) {
       if (s.update_index == info.update_index && pts.size() == s.points_seen) {
         last_refresh_ = 0;
@@ -216,6 +238,7 @@ class BasedCorrelationScanMatchGpu {
     s.size_x = info.size_x;
     s.size_y = info.size_y;
     s.reset_count = resets;
+    s.generation = gen;
     s.points_seen = pts.size();
     s.update_index = info.update_index;
     if (maps_.size() > 8) {  // forget maps that are gone (ExtendSize frees the old buffer)

@@ -484,6 +484,8 @@ struct csm_ctx {
   DevBuf pts, scans, angles, scores, partials, best, fin;
   DevBuf best_tiles;  // tiled box mode: one best per (window, tile) between the two reductions
   HostBuf h_search;   // csm_search_windows: pinned staging of the points and angle table
+  bool staging_dirty = false;  // a search failed with copies out of its staging possibly in flight
+  csm_gridmap* reader_map = nullptr;  // the map csm_set_grid_gridmap borrowed (its updates wait for this stream)
   HostBuf h_pts;      // upload_points: pinned staging of a scan's points (and small host arrays)
   hipEvent_t ev_pts = nullptr;  // the last copy out of h_pts
   bool ev_pts_used = false;
@@ -737,10 +739,19 @@ int ensure_int_grid(csm_ctx* c) {
   return CSM_OK;
 }
 
+// The context stops reading a borrowed map: its later updates no longer wait
+// for everything on this stream, only for the reads enqueued until now.
+void release_map_reader(csm_ctx* c) {
+  if (!c->reader_map) return;
+  csm::gridmap_release_reader(c->reader_map, c->stream);
+  c->reader_map = nullptr;
+}
+
 // Make the grid keyed on `cells` current: it is current already, or parked
 // (swapped in), or new (the current host-map grid is parked first, evicting
 // the least recently used slot). Returns true when the grid was found.
 bool select_grid(csm_ctx* c, const void* cells) {
+  release_map_reader(c);
   c->cur_use = ++c->grid_clock;
   if (c->owns_host_grid() && c->key_cells == cells) return true;
   for (auto& g : c->parked)
@@ -1986,8 +1997,18 @@ int check_offsets(csm_ctx* c, int32_t n_scans, const int64_t* offsets) {
   return CSM_OK;
 }
 
+// Selects the context's device for a call and restores the caller's device
+// on return (a host process calling in keeps its own current device).
 struct DeviceGuard {
-  explicit DeviceGuard(int d) { (void)hipSetDevice(d); }
+  int prev = -1;
+  explicit DeviceGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
 };
 
 // ---- Gauss-Newton scan matcher ------------------------------------------------
@@ -2198,7 +2219,9 @@ int csm_create(int device, csm_ctx** out) {
   *out = nullptr;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return CSM_ERR_HIP;
-  if (hipSetDevice(device) != hipSuccess) return CSM_ERR_HIP;
+  DeviceGuard dg(device);  // the caller's device is restored on return
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != device) return CSM_ERR_HIP;
   csm_ctx* c = new (std::nothrow) csm_ctx();
   if (!c) return CSM_ERR_ALLOC;
   c->device = device;
@@ -2559,6 +2582,7 @@ int set_grid_device_locked(csm_ctx* c, const float* dev, const csm_map_info* inf
 int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) {
   if (!c || !info) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
+  release_map_reader(c);
   return set_grid_device_locked(c, dev, info);
 }
 
@@ -2583,7 +2607,9 @@ int csm_set_grid_gridmap(csm_ctx* c, csm_gridmap* map) {
   // next update after the matcher's reads (csm::gridmap_add_reader)
   hipError_t e = hipStreamWaitEvent(c->stream, v.ready, 0);
   if (e != hipSuccess) return c->fail(CSM_ERR_HIP, hipGetErrorString(e));
+  if (c->reader_map != map) release_map_reader(c);
   csm::gridmap_add_reader(map, c->stream);
+  c->reader_map = map;
   csm_map_info info{};
   info.resolution = v.resolution;
   info.offset_x = v.offset_x;
@@ -2847,12 +2873,34 @@ int search_exhaustive(csm_ctx* c, const csm_param& P, const Dims& D, const Geome
 
 }  // namespace
 
+static int search_windows_locked(csm_ctx* c, const double* pts, int32_t n_points, const csm_param* param,
+                                 int32_t n_windows, const int32_t* grid_index, const double* centers_map,
+                                 const csm_search_options* options, csm_best* best, int32_t* best_window,
+                                 csm_search_stats* stats);
+
+// The search stages its points, angle table and incumbent in pinned buffers
+// that the next call rewrites; a call that fails after enqueuing a copy out of
+// them leaves the stream marked, and the next call drains it first.
 int csm_search_windows(csm_ctx* c, const double* pts, int32_t n_points, const csm_param* param, int32_t n_windows,
                        const int32_t* grid_index, const double* centers_map, const csm_search_options* options,
                        csm_best* best, int32_t* best_window, csm_search_stats* stats) {
   if (!c || !param || !centers_map || !best || !best_window || n_windows <= 0) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (c->staging_dirty) {
+    (void)hipStreamSynchronize(c->stream);
+    c->staging_dirty = false;
+  }
+  const int st = search_windows_locked(c, pts, n_points, param, n_windows, grid_index, centers_map, options, best,
+                                       best_window, stats);
+  c->staging_dirty = st != CSM_OK;
+  return st;
+}
+
+static int search_windows_locked(csm_ctx* c, const double* pts, int32_t n_points, const csm_param* param,
+                                 int32_t n_windows, const int32_t* grid_index, const double* centers_map,
+                                 const csm_search_options* options, csm_best* best, int32_t* best_window,
+                                 csm_search_stats* stats) {
   Dims D;
   int st = window_dims(*param, D);
   if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
@@ -3021,6 +3069,7 @@ int csm_set_grid_stack(csm_ctx* c, const float* cells, int32_t n_grids, const cs
   if (!c || !info || !cells || n_grids <= 0) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  release_map_reader(c);
   if (info->size_x <= 0 || info->size_y <= 0 || !(info->resolution > 0.0))
     return c->fail(CSM_ERR_INVALID_ARG, "grid size and resolution must be positive");
   const int64_t ncell = (int64_t)info->size_x * info->size_y;
@@ -3200,6 +3249,7 @@ int csm_set_grid_stack_gridmaps(csm_ctx* c, csm_gridmap* const* maps, int32_t n_
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  release_map_reader(c);
   park_current(c);
   const csm::GridMapView& a = v[0];
   int32_t min_index = a.map_update_index;
@@ -3216,11 +3266,11 @@ int csm_set_grid_stack_gridmaps(csm_ctx* c, csm_gridmap* const* maps, int32_t n_
   if ((e = c->grid_buf.ensure((size_t)ncell * (size_t)n_maps * sizeof(float))) != hipSuccess)
     return c->hip_fail(e, "hipMalloc(grid stack)");
   for (int32_t i = 0; i < n_maps; ++i) {  // after each map's last update, on the matcher's stream
-    csm::gridmap_add_reader(maps[i], c->stream);  // and the map's next update after the copy
     if ((e = hipStreamWaitEvent(c->stream, v[(size_t)i].ready, 0)) != hipSuccess ||
         (e = hipMemcpyAsync((float*)c->grid_buf.p + (size_t)i * (size_t)ncell, v[(size_t)i].prob,
                             (size_t)ncell * sizeof(float), hipMemcpyDeviceToDevice, c->stream)) != hipSuccess)
       return c->hip_fail(e, "hipMemcpyAsync(map stack)");
+    csm::gridmap_add_read_fence(maps[i], c->stream);  // the map's next update after the copy (only)
   }
   c->info.resolution = a.resolution;
   c->info.offset_x = a.offset_x;

@@ -474,16 +474,43 @@ namespace {
 // cells a pending match or copy still reads.
 std::mutex g_readers_mu;
 std::map<const csm_gridmap*, std::vector<hipStream_t>> g_readers;
+// One-shot read fences: events recorded on a reader stream once its reads of
+// the map were all enqueued (a stack copy, or a matcher that moved on to
+// another grid). An update waits for each once; completed ones are dropped.
+std::map<const csm_gridmap*, std::vector<hipEvent_t>> g_fences;
 
 int wait_readers(csm_gridmap* m) {
   std::lock_guard<std::mutex> lk(g_readers_mu);
   auto it = g_readers.find(m);
-  if (it == g_readers.end()) return CSM_OK;
-  for (hipStream_t s : it->second) {
-    GM_HIP(hipEventRecord(m->read_done, s));
-    GM_HIP(hipStreamWaitEvent(m->stream, m->read_done, 0));
+  if (it != g_readers.end())
+    for (hipStream_t s : it->second) {
+      GM_HIP(hipEventRecord(m->read_done, s));
+      GM_HIP(hipStreamWaitEvent(m->stream, m->read_done, 0));
+    }
+  auto f = g_fences.find(m);
+  if (f != g_fences.end()) {
+    std::vector<hipEvent_t> keep;
+    for (hipEvent_t ev : f->second) {
+      if (hipEventQuery(ev) == hipSuccess) {  // done (and waited for by an earlier update, or now moot)
+        (void)hipEventDestroy(ev);
+        continue;
+      }
+      GM_HIP(hipStreamWaitEvent(m->stream, ev, 0));
+      keep.push_back(ev);
+    }
+    f->second.swap(keep);
   }
   return CSM_OK;
+}
+
+void add_fence_locked(const csm_gridmap* m, hipStream_t s) {
+  hipEvent_t ev = nullptr;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+  if (hipEventRecord(ev, s) != hipSuccess) {
+    (void)hipEventDestroy(ev);
+    return;
+  }
+  g_fences[m].push_back(ev);
 }
 }  // namespace
 
@@ -495,7 +522,25 @@ void gridmap_add_reader(csm_gridmap* m, hipStream_t s) {
 }
 void gridmap_drop_reader(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_readers_mu);
-  for (auto& kv : g_readers) kv.second.erase(std::remove(kv.second.begin(), kv.second.end(), s), kv.second.end());
+  for (auto& kv : g_readers) {
+    auto& v = kv.second;
+    if (std::find(v.begin(), v.end(), s) == v.end()) continue;
+    add_fence_locked(kv.first, s);  // the reads already enqueued still order the map's next update
+    v.erase(std::remove(v.begin(), v.end(), s), v.end());
+  }
+}
+void gridmap_release_reader(csm_gridmap* m, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_readers_mu);
+  auto it = g_readers.find(m);
+  if (it == g_readers.end()) return;
+  auto& v = it->second;
+  if (std::find(v.begin(), v.end(), s) == v.end()) return;
+  add_fence_locked(m, s);
+  v.erase(std::remove(v.begin(), v.end(), s), v.end());
+}
+void gridmap_add_read_fence(csm_gridmap* m, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_readers_mu);
+  add_fence_locked(m, s);
 }
 
 int gridmap_fixed_point(csm_gridmap* m, float outside, GridMapFixed* f) {
@@ -625,6 +670,11 @@ int csm_gridmap_destroy(csm_gridmap* m) {
     {
       std::lock_guard<std::mutex> lk(g_readers_mu);
       g_readers.erase(m);
+      auto f = g_fences.find(m);
+      if (f != g_fences.end()) {
+        for (hipEvent_t ev : f->second) (void)hipEventDestroy(ev);
+        g_fences.erase(f);
+      }
     }
     if (m->ready) (void)hipEventDestroy(m->ready);
     if (m->staged) (void)hipEventDestroy(m->staged);

@@ -88,6 +88,12 @@ int gridmap_fixed_point(csm_gridmap* m, float outside, GridMapFixed* f);
 // A matcher stream reads the map: the map's next updates wait for the work
 // enqueued on it so far. drop_reader: the stream is going away.
 void gridmap_add_reader(csm_gridmap* m, hipStream_t s);
+// The stream stops reading the map (its context moved to another grid): the
+// reads enqueued so far become a one-shot fence the next update waits for.
+void gridmap_release_reader(csm_gridmap* m, hipStream_t s);
+// A one-shot fence: the reads enqueued on s so far (a device-to-device copy).
+void gridmap_add_read_fence(csm_gridmap* m, hipStream_t s);
+// The stream goes away: every map it reads keeps a fence of its reads.
 void gridmap_drop_reader(hipStream_t s);
 
 }  // namespace csm

@@ -65,6 +65,18 @@ Rccl& rccl() {
   static Rccl r;
   return r;
 }
+
+// The caller's current device is restored on every return: a host process
+// (PyTorch, a ROS node) calling in must not be left on another GPU.
+struct DeviceRestore {
+  int prev = -1;
+  DeviceRestore() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceRestore() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 std::mutex& rccl_mu() {
   static std::mutex m;
   return m;
@@ -90,6 +102,9 @@ struct csm_loop_closure {
   std::vector<csm::LcExchange*> xbuf;  // device, one per device
   csm::LcExchange* h_x = nullptr;      // pinned host staging, one per device
   int32_t n_submaps = 0;
+  // A failure after the exchange's first collective was enqueued leaves the
+  // communicators out of step: the handle refuses further matches.
+  bool broken = false;
   double resolution = 0.0;
   std::vector<double> offsets;
   std::vector<int32_t> lo, hi;
@@ -112,6 +127,7 @@ extern "C" {
 
 int csm_loop_closure_destroy(csm_loop_closure* lc) {
   if (!lc) return CSM_ERR_INVALID_ARG;
+  DeviceRestore restore;
   for (size_t r = 0; r < lc->comms.size(); ++r)
     if (lc->comms[r]) (void)rccl().CommDestroy(lc->comms[r]);
   for (size_t r = 0; r < lc->devices.size(); ++r) {
@@ -129,6 +145,7 @@ int csm_loop_closure_destroy(csm_loop_closure* lc) {
 int csm_loop_closure_create(int32_t n_devices, const int32_t* devices, csm_loop_closure** out) {
   if (!out || n_devices <= 0) return CSM_ERR_INVALID_ARG;
   *out = nullptr;
+  DeviceRestore restore;
   csm_loop_closure* lc = new csm_loop_closure();
   for (int r = 0; r < n_devices; ++r) lc->devices.push_back(devices ? devices[r] : r);
   int st;
@@ -180,21 +197,27 @@ int csm_loop_closure_set_submaps(csm_loop_closure* lc, const float* cells, int32
                                  const double* offsets, int64_t version) {
   if (!lc || !cells || !info || !offsets || n_submaps <= 0) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(lc->mu);
+  DeviceRestore restore;
   const int G = (int)lc->devices.size();
   const int64_t per = (int64_t)info->size_x * info->size_y;
-  lc->lo.assign((size_t)G, 0);
-  lc->hi.assign((size_t)G, 0);
+  // the new shard ranges are committed only once every shard is resident: a
+  // failed upload leaves no submaps (match then fails with CSM_ERR_NO_GRID)
+  // instead of a mix of old and new stacks under the old ranges
+  std::vector<int32_t> lo((size_t)G, 0), hi((size_t)G, 0);
+  lc->n_submaps = 0;
   for (int r = 0; r < G; ++r) {
-    shard_range(n_submaps, r, G, &lc->lo[(size_t)r], &lc->hi[(size_t)r]);
-    const int32_t n = lc->hi[(size_t)r] - lc->lo[(size_t)r];
+    shard_range(n_submaps, r, G, &lo[(size_t)r], &hi[(size_t)r]);
+    const int32_t n = hi[(size_t)r] - lo[(size_t)r];
     if (n == 0) continue;
-    int st = csm_set_grid_stack(lc->ctx[(size_t)r], cells + lc->lo[(size_t)r] * per, n, info, version);
+    int st = csm_set_grid_stack(lc->ctx[(size_t)r], cells + lo[(size_t)r] * per, n, info, version);
     if (st != CSM_OK) return lc->fail(st, std::string("device ") + std::to_string(lc->devices[(size_t)r]) + ": " +
                                               csm_last_error(lc->ctx[(size_t)r]));
   }
-  lc->n_submaps = n_submaps;
+  lc->lo.swap(lo);
+  lc->hi.swap(hi);
   lc->resolution = info->resolution;
   lc->offsets.assign(offsets, offsets + 2 * (size_t)n_submaps);
+  lc->n_submaps = n_submaps;
   return CSM_OK;
 }
 
@@ -203,6 +226,8 @@ int csm_loop_closure_match(csm_loop_closure* lc, const double* pts, int32_t n_po
   if (!lc || !pts || !param || !pose_world || !res) return CSM_ERR_INVALID_ARG;
   if (search != CSM_LC_PYRAMID && search != CSM_LC_EXHAUSTIVE) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(lc->mu);
+  DeviceRestore restore;
+  if (lc->broken) return lc->fail(CSM_ERR_HIP, "an earlier exchange failed part-way: the communicators are out of step");
   if (lc->n_submaps == 0) return lc->fail(CSM_ERR_NO_GRID, "no submaps set");
   int32_t na = 0, ns = 0;
   if (csm_window_dims(param, &na, &ns) != CSM_OK) return lc->fail(CSM_ERR_INVALID_ARG, "invalid window parameters");
@@ -292,35 +317,44 @@ int csm_loop_closure_match(csm_loop_closure* lc, const double* pts, int32_t n_po
     if ((nr = R.GroupEnd()) != ncclSuccess) return lc->nccl_fail(nr, "ncclGroupEnd");
     return CSM_OK;
   };
+  // From the first collective on, a failure on one device leaves collectives
+  // in flight on the others: every stream is drained (best effort; the staging
+  // h_x stays untouched until then) and the handle refuses later matches.
+  auto abandon = [&](int st) {
+    lc->broken = true;
+    for (int r = 0; r < G; ++r)
+      if (hipSetDevice(lc->devices[(size_t)r]) == hipSuccess) (void)hipStreamSynchronize(lc->streams[(size_t)r]);
+    return st;
+  };
   int st;
   if ((st = all_reduce(offsetof(csm::LcExchange, score), offsetof(csm::LcExchange, score_max), 1, ncclFloat64,
                        ncclMax)) != CSM_OK)
-    return st;
+    return abandon(st);
   for (int r = 0; r < G; ++r) {
     if ((e = hipSetDevice(lc->devices[(size_t)r])) != hipSuccess ||
         (e = csm::launch_lc_pick(lc->xbuf[(size_t)r], lc->streams[(size_t)r])) != hipSuccess)
-      return lc->hip_fail(e, "lc_pick_kernel");
+      return abandon(lc->hip_fail(e, "lc_pick_kernel"));
   }
   if ((st = all_reduce(offsetof(csm::LcExchange, idx), offsetof(csm::LcExchange, idx_min), 1, ncclInt64, ncclMin)) !=
       CSM_OK)
-    return st;
+    return abandon(st);
   for (int r = 0; r < G; ++r) {
     if ((e = hipSetDevice(lc->devices[(size_t)r])) != hipSuccess ||
         (e = csm::launch_lc_row(lc->xbuf[(size_t)r], lc->streams[(size_t)r])) != hipSuccess)
-      return lc->hip_fail(e, "lc_row_kernel");
+      return abandon(lc->hip_fail(e, "lc_row_kernel"));
   }
   if ((st = all_reduce(offsetof(csm::LcExchange, row), offsetof(csm::LcExchange, row_sum), 4, ncclFloat64,
                        ncclSum)) != CSM_OK)
-    return st;
+    return abandon(st);
   csm::LcExchange* out = &lc->h_x[0];
   if ((e = hipSetDevice(lc->devices[0])) != hipSuccess ||
       (e = hipMemcpyAsync(out, lc->xbuf[0], sizeof(csm::LcExchange), hipMemcpyDeviceToHost, lc->streams[0])) !=
           hipSuccess)
-    return lc->hip_fail(e, "hipMemcpyAsync(exchange result)");
+    return abandon(lc->hip_fail(e, "hipMemcpyAsync(exchange result)"));
   for (int r = 0; r < G; ++r) {
     if ((e = hipSetDevice(lc->devices[(size_t)r])) != hipSuccess ||
         (e = hipStreamSynchronize(lc->streams[(size_t)r])) != hipSuccess)
-      return lc->hip_fail(e, "exchange");
+      return abandon(lc->hip_fail(e, "exchange"));
   }
   res->n_devices = G;
   res->score = out->score_max;

@@ -176,6 +176,7 @@ class DeviceLoopClosure:
                                                      C.byref(p), pose.ctypes.data_as(C.POINTER(C.c_double)),
                                                      0 if search == "pyramid" else 1, C.byref(r)))
         self.last_pose_world = np.array(r.pose_world[:])
+        self.last_n_devices = int(r.n_devices)
         return LoopClosureResult(r.score, r.global_index, r.submap, r.x, r.y, r.angle)
 
     def close(self):

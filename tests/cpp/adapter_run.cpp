@@ -75,6 +75,7 @@ struct Map {
   int index = 0;
   std::vector<int> update_points;
   int64_t resets = 0;
+  int64_t generation = 0;  // bumped whenever the cell buffer is (re)allocated
   int GetSizeX() const { return sx; }
   int GetSizeY() const { return sy; }
   double GetCellLength() const { return res; }
@@ -82,6 +83,7 @@ struct Map {
   const ProbabilityCell* GetCellData() const { return cells.data(); }
   const std::vector<int>& GetUpdatePoints() const { return update_points; }
   int64_t GetResetCount() const { return resets; }
+  int64_t GetCellGeneration() const { return generation; }
   float& prob(int x, int y) { return cells[(size_t)y * sx + x].prob_value_; }
 };
 // The same map without the incremental-refresh accessors (whole-grid uploads).
@@ -209,6 +211,21 @@ void extend(Map& m, int pad) {
   m.ox += pad * m.res;
   m.oy += pad * m.res;
   m.update_points.clear();
+  m.generation++;
+}
+// A map freed and another allocated at the same address and size: fresh
+// walls, an update list at least as long as the old map's, the same reset
+// count -- only the generation tells them apart.
+void reuse_buffer(Map& m) {
+  const size_t listed = m.update_points.size();
+  const ProbabilityCell* before = m.cells.data();
+  Map fresh = make_map(m.sx, m.res);
+  std::copy(fresh.cells.begin(), fresh.cells.end(), m.cells.begin());  // same buffer, new contents
+  if (m.cells.data() != before) std::abort();
+  m.update_points.clear();
+  for (size_t i = 0; i < listed + 7; ++i) m.update_points.push_back((int)(urand() * (double)m.cells.size()));
+  m.index = 0;
+  m.generation++;
 }
 
 oracle_map_c omap(const Map& m) {
@@ -243,6 +260,7 @@ int check(int n_scans) {
   for (int s = 0; s < n_scans; ++s) {
     if (s % 5 == 4) reset(*map);
     if (s == 7) extend(*map, 40);
+    if (s == 11 || s == 17) reuse_buffer(*map);
     if (s > 0) mutate(*map, 3000 + (int)(urand() * 20000));
     const double wx = (urand() - 0.5) * 20.0, wy = (urand() - 0.5) * 20.0, wth = (urand() - 0.5) * 6.0;
     auto range = std::make_shared<Range>(make_scan(*map, wx, wy, wth));

@@ -85,3 +85,86 @@ def test_capi_loop_closure_world_pose(submaps):
         assert list(lc.last_pose_world) == want
     finally:
         lc.close()
+
+
+def test_capi_failed_set_submaps_leaves_no_submaps(submaps):
+    """A set_submaps that fails part-way commits nothing: the next match
+    fails with CSM_ERR_NO_GRID instead of searching a mix of old and new
+    shards under the old ranges (csm_loop_closure.cpp)."""
+    import ctypes as C
+
+    from roborts_csm import CsmError
+    from roborts_csm._abi import CSM_ERR_NO_GRID, CsmMapInfo
+    from roborts_csm.loop_closure import DeviceLoopClosure
+    from roborts_csm.params import CorrelationScanMatchParam
+    f1, grids, offsets = submaps
+    res = float(f1["resolution"])
+    p = CorrelationScanMatchParam(1.0, 0.05, 0.3, 0.0349, 0.5, 100, 0, False, 0)
+    lc = DeviceLoopClosure(_devices())
+    try:
+        lc.set_submaps(grids, res, offsets, version=1)
+        lc.match(f1["points"], p, f1["init_pose"])
+        bad = CsmMapInfo(res, 0.0, 0.0, -5, grids.shape[1], 0, 0)  # every shard's upload fails
+        g = np.ascontiguousarray(grids)
+        off = np.ascontiguousarray(offsets)
+        st = lc._lib.csm_loop_closure_set_submaps(lc._h, g.ctypes.data_as(C.c_void_p), 2 * g.shape[0], C.byref(bad),
+                                                  off.ctypes.data_as(C.POINTER(C.c_double)), 2)
+        assert st != 0
+        with pytest.raises(CsmError) as ei:
+            lc.match(f1["points"], p, f1["init_pose"])
+        assert ei.value.status == CSM_ERR_NO_GRID
+        lc.set_submaps(grids, res, offsets, version=3)  # a good call restores service
+        assert lc.match(f1["points"], p, f1["init_pose"]).submap >= 0
+    finally:
+        lc.close()
+
+
+def test_calls_restore_the_callers_device(submaps):
+    """Every C-ABI call selects its context's device and hands the caller's
+    current device back (a host process must not be left on
+    another GPU)."""
+    import ctypes as C
+
+    import roborts_csm
+    from roborts_csm.loop_closure import DeviceLoopClosure
+    from roborts_csm.params import CorrelationScanMatchParam
+    hip = C.CDLL("libamdhip64.so")
+    n = C.c_int(0)
+    hip.hipGetDeviceCount(C.byref(n))
+    last = n.value - 1
+    cur = C.c_int(-1)
+    hip.hipSetDevice(last)
+    f1, grids, offsets = submaps
+    p = CorrelationScanMatchParam(1.0, 0.05, 0.3, 0.0349, 0.5, 100, 0, False, 0)
+    with roborts_csm.Context(0) as ctx:
+        ctx.set_grid(roborts_csm.ScanMatchMap(f1["grid"], float(f1["resolution"]), tuple(f1["offset"])), force=True)
+        pose = np.array(f1["init_pose"], dtype=np.float64)
+        ctx.scan_match(f1["points"], p, pose, np.eye(3).reshape(9).copy())
+        hip.hipGetDevice(C.byref(cur))
+        assert cur.value == last
+    lc = DeviceLoopClosure([0])
+    try:
+        lc.set_submaps(grids, float(f1["resolution"]), offsets, version=1)
+        lc.match(f1["points"], p, f1["init_pose"])
+        hip.hipGetDevice(C.byref(cur))
+        assert cur.value == last
+    finally:
+        lc.close()
+        hip.hipSetDevice(0)
+
+
+def test_bench_lc_capi_mode_runs():
+    """bench.py --workload loop_closure --lc capi: one process through
+    csm_loop_closure_* (in-process RCCL communicator over every visible
+    device), the result line reports the library's n_devices."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--workload", "loop_closure", "--lc", "capi",
+                        "--gpus", "1", "--submaps", "16", "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["config"]["lc"] == "capi" and d["config"]["n_devices"] == 1 and d["value"] > 0
+    assert d["result"]["submap"] >= 0
