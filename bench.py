@@ -190,6 +190,38 @@ def roofline(kernel: str, avg_ms: float, algorithmic_bytes: float, counters, cou
     return out
 
 
+COUNTERS_SMALL_JSON = os.path.join(ROOT, "profiles", "r03", "counters_small.json")
+
+
+def split_roofline(stats, counters_path: str = COUNTERS_SMALL_JSON):
+    """Roofline of the few-window path's dominant kernel from HIP-event stats
+    (csm_kernel_stats): the split kernel's launches of every level pooled (one
+    kernel, rocprof cannot tell the levels apart), PMC counters per launch
+    from counters_path (tools/pmc_roofline.sh --workload online)."""
+    agg = {}
+    for s in stats:  # the scoring kernels (the hot path); the finish is bookkeeping
+        if not s["name"].startswith("score_") or not s["launches"]:
+            continue
+        base = s["name"].split("<")[0]
+        a = agg.setdefault(base, {"launches": 0, "total_ms": 0.0, "bytes": 0.0})
+        a["launches"] += s["launches"]
+        a["total_ms"] += s["total_ms"]
+        a["bytes"] += s["algorithmic_bytes"]
+    if not agg:
+        return None
+    name, a = max(agg.items(), key=lambda kv: kv[1]["total_ms"])
+    rl = roofline(name, a["total_ms"] / a["launches"], a["bytes"] / a["launches"], load_counters(counters_path),
+                  counters_path)
+    rl["launches_pooled"] = a["launches"]
+    if rl.get("bound") is None and rl["algorithmic_bytes_per_launch"]:
+        # without counters: the algorithmic rate against HBM (an upper bound on the
+        # bytes the kernel could have fetched)
+        ach = rl["algorithmic_GBs"]
+        rl.update({"bound": "hbm (algorithmic)", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": ach / HBM_PEAK_GBS})
+    return rl
+
+
 def _window_cands(p) -> int:
     import roborts_csm
     na, ns = roborts_csm.window_dims(p)
@@ -489,11 +521,15 @@ class _AttachedBackEnd:
     releases the GIL, so the front end keeps running. The pose-graph solve
     itself is out of scope."""
 
-    def __init__(self, device: int):
+    def __init__(self, device: int, pub_map=None):
         import queue
         import threading
         from roborts_csm.backend import BackEndParam, ScanMatchService
         self.svc = ScanMatchService(BackEndParam(), device=device)
+        # the front end's PubMap (MapCheckPenalize with logistic in every job,
+        # slam_processor.cpp:312-317): its checks and the front end's updates
+        # run in order on the map's own stream, under the map's lock
+        self.pub_map = pub_map
         self.q = queue.Queue()
         self.kept = []
         self.jobs = 0
@@ -523,7 +559,7 @@ class _AttachedBackEnd:
                 if len(self.kept) >= 51:
                     queries.append(pts), chains.append(self.kept[-51:-41]), inits.append(pose)
                 if queries:
-                    self.svc.scan_match_jobs(queries, chains, inits, pose, None)
+                    self.svc.scan_match_jobs(queries, chains, inits, pose, self.pub_map)
                     self.jobs += len(queries)
                 now = time.perf_counter()
                 self.busy += now - t
@@ -548,8 +584,8 @@ class _AttachedBackEnd:
                "busy_fraction_of_stream": self.busy / fe_elapsed if fe_elapsed > 0 else None,
                "vertex_lag_ms": {"p50": float(np.median(lag)), "max": float(lag.max())},
                "what": "per kept scan: AddRangeData + near-chain job (+ a loop-closure job 40-50 vertices back) "
-                       "on a second device context, concurrently with the front end; no PubMap check "
-                       "(pub_map=None), no pose-graph solve"}
+                       "on a second device context, concurrently with the front end; every job ends with the "
+                       "logistic MapCheckPenalize on the front end's PubMap; no pose-graph solve"}
         if self.err:
             out["error"] = self.err
         self.svc.close()
@@ -566,11 +602,16 @@ def online_bench(args, rank, world_size, dist, torch):
     from roborts_csm import worlds
     from roborts_csm.frontend import CsmFrontendResult, FrontEndParam, SlamFrontEnd
     n = args.warmup + args.steps
+    n_prof = 60  # profiled scans after the timed ones (HIP events perturb latency)
     world = worlds.make_world(2000, 2000, 0.05, seed=20261015)
-    stream = worlds.make_scan_stream(world, n, seed=77 + rank)
+    stream = worlds.make_scan_stream(world, n + n_prof, seed=77 + rank)
     fe = SlamFrontEnd(FrontEndParam(), device=_device())
-    be = _AttachedBackEnd(_device()) if args.attach_backend else None
-    for k in range(args.warmup):
+    be = None
+    if args.attach_backend:
+        fe.process(stream.points_m[0], stream.odom_poses[0])  # the first scan creates the maps (CreateAllMap)
+        be = _AttachedBackEnd(_device(), pub_map=fe.map(0))  # CSM_PUB_MAP
+        be.submit(stream.points_m[0], fe.kept_poses()[0])
+    for k in range(1 if be is not None else 0, args.warmup):
         r = fe.process(stream.points_m[k], stream.odom_poses[k])
         if be is not None and r.map_updated:
             be.submit(stream.points_m[k], r.pose)
@@ -610,6 +651,13 @@ def online_bench(args, rank, world_size, dist, torch):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     lat_ms = np.array(lat) * 1e3
+    mctx = fe.matcher()
+    mctx.set_profiling(True)
+    for k in range(n, n + n_prof):
+        fe.process(stream.points_m[k], stream.odom_poses[k])
+    rl = split_roofline(mctx.kernel_stats())
+    mctx.set_profiling(False)
+    mctx.close()
     # SlamProcessor::CorrectPoseAndMap (slam_processor.cpp:329-370) after the
     # drive: every kept scan's pose nudged as a pose-graph solve would, all
     # three maps rebuilt on the device from every kept scan
@@ -632,17 +680,33 @@ def online_bench(args, rank, world_size, dist, torch):
     if rank == 0 and world_size == 1 and not args.no_cpu:
         import pyoracle as O
         ofe = O.FrontEnd(FrontEndParam().to_c())
+        obe, okept = None, []
+        if be is not None:  # the back end's jobs too, on the same thread after each kept scan
+            from roborts_csm.backend import BackEndParam, make_jobs
+            obe = O.BackEnd(BackEndParam().to_c())
         tc = time.perf_counter()
         m = 0
         while m < n and (m < args.warmup + 2 or time.perf_counter() - tc < args.cpu_seconds):
             if m == args.warmup:
                 tc2 = time.perf_counter()
-            ofe.process(stream.points_m[m], stream.odom_poses[m], CsmFrontendResult())
+            res = CsmFrontendResult()
+            ofe.process(stream.points_m[m], stream.odom_poses[m], res)
+            if obe is not None and res.map_updated:
+                okept.append(obe.add_scan(stream.points_m[m], np.array(res.pose[:])))
+                qs, cs, ps = [], [], []
+                if len(okept) >= 11:
+                    qs.append(stream.points_m[m]), cs.append(okept[-11:-1]), ps.append(np.array(res.pose[:]))
+                if len(okept) >= 51:
+                    qs.append(stream.points_m[m]), cs.append(okept[-51:-41]), ps.append(np.array(res.pose[:]))
+                if qs:
+                    obe.scan_match(make_jobs(qs, cs, ps), len(qs), np.array(res.pose[:]), ofe.map(0))
             m += 1
         dtc = time.perf_counter() - tc2
+        what = "front end" + (" + the back end's per-vertex jobs (near-chain link, loop-closure candidate, "
+                              "logistic PubMap check)" if obe is not None else "")
         cpu = {"value": (m - args.warmup) / dtc, "unit": "scans/s", "cores": 1, "kind": "port",
                "sample": f"scans {args.warmup}..{m - 1} of the same stream through the oracle's restatement "
-                         f"of the front-end (oracle/map_oracle.cpp), single-threaded, {dtc:.1f} s on {_cpu_model()}"}
+                         f"of the {what} (oracle/map_oracle.cpp), single-threaded, {dtc:.1f} s on {_cpu_model()}"}
         if m == n:  # the oracle kept the same scans: time its CorrectPoseAndMap too
             tco = time.perf_counter()
             try:
@@ -669,7 +733,7 @@ def online_bench(args, rank, world_size, dist, torch):
                    "correct_pose_and_map": {"kept_scans": int(kept.shape[0]), "ms": correct_ms,
                                             "what": "CorrectPoseAndMap: all kept poses corrected, PubMap + coarse + "
                                                     "fine rebuilt from every kept scan on the device"}},
-        "roofline": None, "cpu_baseline": cpu,
+        "roofline": rl, "cpu_baseline": cpu,
     }
 
 
@@ -775,9 +839,18 @@ def adapter_bench(args, rank, world_size, dist, torch):
     exe = os.path.join(ROOT, "tests", "cpp", "build", "adapter_run")
     if not os.path.exists(exe):
         raise SystemExit("tests/cpp/build/adapter_run missing: run __graft_entry__.build()")
-    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("LOCAL_RANK", "0")) if world_size > 1 else None
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("LOCAL_RANK", "0")) if world_size > 1 else dict(os.environ)
+    # latency run first; then a run with per-kernel HIP-event stats (CSM_STATS_DUMP) for the roofline
     r = subprocess.run([exe, "bench", str(max(args.steps, 3) + 1), "3000"], capture_output=True, text=True,
                        timeout=600, env=env)
+    rs = subprocess.run([exe, "bench", "21", "3000"], capture_output=True, text=True, timeout=600,
+                        env=dict(env, CSM_STATS_DUMP="1"))
+    stats = []
+    for line in rs.stderr.splitlines():
+        if line.startswith("csm stats:"):
+            f = line[len("csm stats:"):].split()
+            stats.append({"name": f[0], "launches": int(f[2]), "total_ms": float(f[6]),
+                          "algorithmic_bytes": float(f[8]), "scorings": 0.0})
     if r.returncode != 0:
         raise SystemExit(f"adapter_run failed ({r.returncode}): {r.stdout[-2000:]} {r.stderr[-2000:]}")
     a = json.loads(r.stdout.strip().splitlines()[-1])
@@ -791,8 +864,9 @@ def adapter_bench(args, rank, world_size, dist, torch):
         "config": {"workload": "adapter: BasedCorrelationScanMatchGpu x 3 levels per scan (sim YAML, U=100)",
                    "incremental_ms_p50": lat, "whole_upload_ms_p50": a["adapter_whole_upload_ms_p50"],
                    "host_map_mutation_ms_p50": a["host_map_mutation_ms_p50"],
+                   "first_level_incl_refresh_ms_p50": a.get("adapter_first_level_ms_p50"),
                    "parallelism": f"replicas x{world_size}"},
-        "roofline": None,
+        "roofline": split_roofline(stats),
         "cpu_baseline": {"value": 1e3 / a["oracle_cpu_ms_p50"], "unit": "scans/s", "cores": 1, "kind": "port",
                          "sample": f"the same {a['scans'] - 1} scans x 3 levels through oracle_scan_match "
                                    f"(single-threaded restatement of the reference) on {_cpu_model()}"},

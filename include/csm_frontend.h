@@ -94,6 +94,10 @@ int csm_frontend_process(csm_frontend* fe, const double* points_xy, int32_t n_po
 /* Borrow one of the front-end's maps (owned by the front-end; null before the
  * first scan). */
 int csm_frontend_map(csm_frontend* fe, int32_t which, csm_gridmap** map);
+/* The front end's scan-matcher context (borrowed; owned and destroyed by the
+ * front end): for profiling and kernel statistics (csm_set_profiling,
+ * csm_kernel_stats) of the matches csm_frontend_process runs. */
+int csm_frontend_matcher(csm_frontend* fe, csm_ctx** ctx);
 
 /* SlamProcessor::CorrectPoseAndMap (slam/slam_processor.cpp:329-370): the
  * pose-graph back end's corrected world poses for kept scans ids[0..n)

@@ -2298,8 +2298,9 @@ int csm_destroy(csm_ctx* c) {
   if (!c) return CSM_OK;
   if (c->stats_dump)
     for (const auto& st : c->stats)
-      std::fprintf(stderr, "csm stats: %-40s launches %8lld  avg_us %10.3f  total_ms %10.3f\n", st.name,
-                   (long long)st.launches, st.launches ? st.total_ms / st.launches * 1e3 : 0.0, st.total_ms);
+      std::fprintf(stderr, "csm stats: %-40s launches %8lld  avg_us %10.3f  total_ms %10.3f  alg_bytes %.6g\n",
+                   st.name, (long long)st.launches, st.launches ? st.total_ms / st.launches * 1e3 : 0.0, st.total_ms,
+                   st.algorithmic_bytes);
   {
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);

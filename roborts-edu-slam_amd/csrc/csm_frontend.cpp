@@ -281,6 +281,12 @@ int csm_frontend_process(csm_frontend* f, const double* pts, int32_t n, const do
   return CSM_OK;
 }
 
+int csm_frontend_matcher(csm_frontend* f, csm_ctx** ctx) {
+  if (!f || !ctx) return CSM_ERR_INVALID_ARG;
+  *ctx = f->ctx;
+  return CSM_OK;
+}
+
 int csm_frontend_correct_pose_and_map(csm_frontend* f, int32_t n, const int32_t* ids, const double* poses) {
   if (!f || n < 0 || (n > 0 && (!ids || !poses))) return CSM_ERR_INVALID_ARG;
   const csm_frontend_param& p = f->p;

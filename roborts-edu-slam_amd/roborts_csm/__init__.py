@@ -144,7 +144,22 @@ class Context:
         self.device = device
         self._grid_ref = None
 
+    @classmethod
+    def borrow(cls, handle, owner) -> "Context":
+        """A view of a context another object owns (csm_frontend_matcher):
+        close() does not destroy it; `owner` is kept alive meanwhile."""
+        c = cls.__new__(cls)
+        c._h = handle
+        c.device = None
+        c._grid_ref = None
+        c._owner = owner
+        return c
+
     def close(self):
+        if getattr(self, "_owner", None) is not None:  # borrowed
+            self._h = None
+            self._owner = None
+            return
         if getattr(self, "_h", None) is not None and self._h.value:
             _lib.csm_destroy(self._h)
             self._h = None

@@ -40,7 +40,7 @@ EXPORTED = (
     "csm_gridmap_device_prob", "csm_set_grid_gridmap", "csm_set_grid_stack_gridmaps",
     # include/csm_frontend.h
     "csm_frontend_create", "csm_frontend_destroy", "csm_frontend_last_error", "csm_frontend_process",
-    "csm_frontend_map", "csm_frontend_correct_pose_and_map", "csm_frontend_kept_scans",
+    "csm_frontend_map", "csm_frontend_correct_pose_and_map", "csm_frontend_kept_scans", "csm_frontend_matcher",
     # include/csm_loop_closure.h
     "csm_loop_closure_create", "csm_loop_closure_destroy", "csm_loop_closure_last_error",
     "csm_loop_closure_set_submaps", "csm_loop_closure_match",
@@ -243,6 +243,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_frontend_last_error": (C.c_char_p, [C.c_void_p]),
         "csm_frontend_process": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, C.c_void_p]),
         "csm_frontend_map": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
+        "csm_frontend_matcher": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
         "csm_frontend_correct_pose_and_map": (C.c_int, [C.c_void_p, C.c_int32, _i32p, _dp]),
         "csm_frontend_kept_scans": (C.c_int, [C.c_void_p, _i32p, _dp]),
         "csm_load_scans_grids": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, _i32p]),

@@ -165,6 +165,16 @@ class SlamFrontEnd:
             raise RuntimeError("front-end map not available (no scan processed yet?)")
         return _BorrowedMap(h, self)
 
+    def matcher(self):
+        """The front end's scan-matcher context (borrowed): set_profiling /
+        kernel_stats of the matches process() runs."""
+        from . import Context
+        h = C.c_void_p()
+        st = _lib.csm_frontend_matcher(self._h, C.byref(h))
+        if st != 0:
+            raise RuntimeError(f"csm_frontend_matcher failed ({st})")
+        return Context.borrow(h, self)
+
     def correct_pose_and_map(self, ids, poses) -> None:
         """SlamProcessor::CorrectPoseAndMap (slam/slam_processor.cpp:329-370):
         corrected world poses for kept scans `ids`, then the three maps are

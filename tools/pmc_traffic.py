@@ -57,7 +57,7 @@ def _short(name: str) -> str:
             i = name.index(key)
             return name[i:name.index(">", i) + 1]
     for key in ("finish_fast_kernel", "finish_kernel", "analyze_grid_kernel", "fixed_point_kernel",
-                "reduce_best_kernel", "score_tree_kernel"):
+                "reduce_best_kernel", "score_tree_kernel", "score_split_kernel"):
         if key in name:
             return key
     return name[:64]
