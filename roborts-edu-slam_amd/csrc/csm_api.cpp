@@ -360,6 +360,8 @@ class ThreadPool {
     // more than the work itself at ~1 us per window (cache-line contention)
     const int chunk = std::max(1, n / (threads * 8));
     uint32_t ep;
+    start_ns_ = now_ns();
+    first_join_ns_.store(0, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> lk(mu_);
       job_ = &job;
@@ -371,7 +373,7 @@ class ThreadPool {
       epoch_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
-    drain(job, n, chunk, ep);
+    const int mine = drain(job, n, chunk, ep, false);
     // chunks claimed by workers may still be running; they are short
     for (int spins = 0; done_.load(std::memory_order_acquire) < n; ++spins) {
       if (spins < 4096)
@@ -379,16 +381,33 @@ class ThreadPool {
       else
         std::this_thread::yield();
     }
+    last_caller_share_ = (double)mine / n;
+    const int64_t j = first_join_ns_.load(std::memory_order_relaxed);
+    last_join_us_ = j ? (double)(j - start_ns_) * 1e-3 : -1.0;
   }
+  // the last job: the caller's share of the items, and when the first worker
+  // joined it (us after the notify; -1: none did) — profiling only
+  double last_caller_share() const { return last_caller_share_; }
+  double last_join_us() const { return last_join_us_; }
 
  private:
-  void drain(const std::function<void(int)>& job, int n, int chunk, uint32_t ep) {
+  static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
+  int drain(const std::function<void(int)>& job, int n, int chunk, uint32_t ep, bool worker) {
     uint64_t c = claim_.load(std::memory_order_acquire);
+    int ran = 0;
     for (;;) {
-      if ((uint32_t)(c >> 32) != ep || (int64_t)(c & 0xffffffffu) >= n) return;
+      if ((uint32_t)(c >> 32) != ep || (int64_t)(c & 0xffffffffu) >= n) return ran;
       if (!claim_.compare_exchange_weak(c, c + (uint64_t)chunk, std::memory_order_acq_rel)) continue;
+      if (worker && ran == 0) {
+        int64_t zero = 0;
+        first_join_ns_.compare_exchange_strong(zero, now_ns(), std::memory_order_relaxed);
+      }
       const int i0 = (int)(c & 0xffffffffu), i1 = std::min(n, i0 + chunk);
       for (int i = i0; i < i1; ++i) job(i);
+      ran += i1 - i0;
       done_.fetch_add(i1 - i0, std::memory_order_release);
       c = claim_.load(std::memory_order_acquire);
     }
@@ -422,7 +441,7 @@ class ThreadPool {
         n = n_items_;
         chunk = chunk_;
       }
-      drain(*job, n, chunk, (uint32_t)seen);
+      drain(*job, n, chunk, (uint32_t)seen, true);
     }
   }
   int n_threads_, spin_us_;
@@ -435,6 +454,9 @@ class ThreadPool {
   std::atomic<uint64_t> claim_{0};
   std::atomic<int> done_{0};
   bool stop_ = false;
+  int64_t start_ns_ = 0;
+  std::atomic<int64_t> first_join_ns_{0};
+  double last_caller_share_ = 0.0, last_join_us_ = -1.0;
 };
 
 double now_ms() {
@@ -448,6 +470,26 @@ int pick_cpl(int64_t n_cand) {
 }
 
 }  // namespace
+
+// A launch left in flight by run_windows(..., pend): what wait_run needs to
+// join it and account its kernels.
+struct PendingRun {
+  char kname[48] = {0};
+  char fname[48] = {0};
+  double alg_bytes = 0.0, scorings = 0.0, finish_bytes = 0.0;
+  bool device_finish = false, timed = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, done = nullptr;
+  const int32_t* flags = nullptr;  // need-exact flags on the host (profiling)
+  int n_flags = 0;
+  // few-window launches: the finish writes FinishOut here (host memory) and
+  // stores flag_value at host_flag when the whole level is done
+  const csm::FinishOut* fin_host = nullptr;
+  const int32_t* host_flag = nullptr;
+  int32_t flag_value = 0;
+  // profiling with a host signal: read the launch's events later
+  // (flush_deferred) instead of waiting for its last kernel to retire
+  bool defer_timing = false;
+};
 
 struct csm_ctx {
   int device = 0;
@@ -490,6 +532,14 @@ struct csm_ctx {
   hipEvent_t ev_pts = nullptr;  // the last copy out of h_pts
   bool ev_pts_used = false;
   HostBuf h_scores, h_fin, h_angles, h_sw;
+  HostBuf h_angles_next;  // the next level's angle rows while this level's are still read (level_end_begin)
+  // Host-signal device finish of the throughput path (CSM_HOST_SIGNAL=0: off):
+  // the finish writes FinishOut straight into coherent pinned memory and the
+  // pass that ends last stores a flag there (no D2H copy, no event round trip).
+  // fin_sig: done counter | need[nw] | list[nw + 1]; h_fin_sig: FinishOut[nw] | flag.
+  bool host_signal = true;
+  DevBuf fin_sig;
+  HostBuf h_fin_sig;
   bool device_finish = true;  // CSM_FINISH=host forces the host std::sort path
   bool fast_finish = true;    // CSM_FINISH=exact: always the full device std::sort emulation
   int device_finish_min = 1;  // fewest windows per launch that finish on the device
@@ -613,7 +663,8 @@ struct csm_ctx {
   // box-kernel launches contend for L2, 1.01 -> 1.57 ms each; profiles/r01).
   struct Slot {
     DevBuf scans, angles, scores, partials, best, fin;
-    HostBuf h_scores, h_fin, h_angles, h_sw;
+    HostBuf h_scores, h_fin, h_angles, h_sw, h_angles_next, h_fin_sig;
+    DevBuf fin_sig;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr, ev_in = nullptr, ev_k = nullptr;
     hipEvent_t ev_fast = nullptr;
   };
@@ -622,6 +673,7 @@ struct csm_ctx {
   int pipeline_min = 512;    // fewest scans the 3-level driver splits into parts (CSM_PIPELINE)
   bool skip_dead_lists = true;  // live_lists (CSM_SKIP_DEAD_LISTS=0: every level fills both lists)
   int pipeline_parts = 2;    // parts in flight (CSM_PIPELINE_PARTS: 2..kMaxParts; 2 measured fastest)
+  int first_windows = 64;    // level_begin_split: windows the first part's first launch takes (CSM_FIRST_WINDOWS; 0: one launch)
   void swap_slot(int i) {    // i >= 1: exchange the current buffer set with alt[i - 1]
     Slot& a = alt[i - 1];
     std::swap(scans, a.scans);
@@ -633,6 +685,9 @@ struct csm_ctx {
     std::swap(h_scores, a.h_scores);
     std::swap(h_fin, a.h_fin);
     std::swap(h_angles, a.h_angles);
+    std::swap(h_angles_next, a.h_angles_next);
+    std::swap(h_fin_sig, a.h_fin_sig);
+    std::swap(fin_sig, a.fin_sig);
     std::swap(h_sw, a.h_sw);
     std::swap(ev0, a.ev0);
     std::swap(ev1, a.ev1);
@@ -642,6 +697,15 @@ struct csm_ctx {
     std::swap(ev_k, a.ev_k);
     std::swap(ev_fast, a.ev_fast);
   }
+  // profiling: the pool's last job, as "pool:<what>" (total_ms = the first
+  // worker's join latency, algorithmic_bytes = the caller's share of the items)
+  void account_pool(const char* what) {
+    if (!profiling || !pool) return;
+    char nm[48];
+    std::snprintf(nm, sizeof(nm), "pool:%s", what);
+    account(nm, (float)(std::max(0.0, pool->last_join_us()) * 1e-3), pool->last_caller_share(), 0.0);
+  }
+  std::vector<PendingRun> deferred;  // signalled launches whose timings are read later (flush_deferred)
   std::vector<csm_kernel_stat> stats;
   void account(const char* name, float ms, double bytes, double scorings) {
     for (auto& s : stats)
@@ -857,22 +921,6 @@ void note_new_values(csm_ctx* c, const PackStats& ps) {
 // null, every score is copied back into ctx->h_scores (window-major).
 enum class Finish { kScoresToHost, kDevice, kBest };
 
-// A launch left in flight by run_windows(..., pend): what wait_run needs to
-// join it and account its kernels.
-struct PendingRun {
-  char kname[48] = {0};
-  char fname[48] = {0};
-  double alg_bytes = 0.0, scorings = 0.0, finish_bytes = 0.0;
-  bool device_finish = false, timed = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, done = nullptr;
-  const int32_t* flags = nullptr;  // need-exact flags on the host (profiling)
-  int n_flags = 0;
-  // few-window launches: the finish writes FinishOut here (host memory) and
-  // stores flag_value at host_flag when the whole level is done
-  const csm::FinishOut* fin_host = nullptr;
-  const int32_t* host_flag = nullptr;
-  int32_t flag_value = 0;
-};
 
 // Spin on the host flag the exact pass stores last (a launch + flag round
 // trip measured 6 us on the GPU box against 12 us through an event,
@@ -894,15 +942,42 @@ int wait_flag(csm_ctx* c, const PendingRun& p) {
   }
 }
 
+int account_run(csm_ctx* c, const PendingRun& p);
+
 int wait_run(csm_ctx* c, const PendingRun& p) {
   hipError_t e;
   if (p.host_flag) {
     const int st = wait_flag(c, p);
     if (st != CSM_OK) return st;
+    if (p.timed && p.defer_timing) {
+      c->deferred.push_back(p);
+      return CSM_OK;
+    }
     if (p.timed && (e = hipEventSynchronize(p.done)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize");
   } else if ((e = hipEventSynchronize(p.done)) != hipSuccess) {
     return c->hip_fail(e, "hipEventSynchronize");
   }
+  return account_run(c, p);
+}
+
+// The timings of signalled launches, once their events have retired (before
+// a launch records the events again, and before the stats are read).
+int flush_deferred(csm_ctx* c) {
+  int st = CSM_OK;
+  for (const PendingRun& p : c->deferred) {
+    const hipError_t e = hipEventSynchronize(p.done);
+    if (e != hipSuccess) {
+      st = c->hip_fail(e, "hipEventSynchronize(deferred)");
+      break;
+    }
+    if ((st = account_run(c, p)) != CSM_OK) break;
+  }
+  c->deferred.clear();
+  return st;
+}
+
+int account_run(csm_ctx* c, const PendingRun& p) {
+  hipError_t e;
   if (p.timed) {
     float ms = 0.f;
     if ((e = hipEventElapsedTime(&ms, p.ev0, p.ev1)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
@@ -966,9 +1041,11 @@ bool phase_table(double f, int ns, int margin_log2, csm::PhaseTable& T) {
 
 // Exact fixed-point accumulation for these windows: grid eligible, beams
 // bounded, no offset wrap (every endpoint within 2^30 bytes of a row).
-bool int_mode_ok(const csm_ctx* c, const Dims& D, double f, const std::vector<WindowPlan>& plans) {
+bool int_mode_ok(const csm_ctx* c, const Dims& D, double f, const std::vector<WindowPlan>& plans, size_t i0 = 0,
+                 size_t i1 = SIZE_MAX) {
   if (!c->int_ok) return false;
-  for (const WindowPlan& W : plans) {
+  for (size_t i = i0; i < std::min(i1, plans.size()); ++i) {
+    const WindowPlan& W = plans[i];
     const double far = (double)(D.n_space - 1) * f;
     const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
                                  std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
@@ -980,8 +1057,8 @@ bool int_mode_ok(const csm_ctx* c, const Dims& D, double f, const std::vector<Wi
 }
 
 void fill_scan_work(const Dims& D, const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
-                    const std::vector<int32_t>& grid_index, ScanWork* sw) {
-  for (size_t i = 0; i < plans.size(); ++i) {
+                    const std::vector<int32_t>& grid_index, ScanWork* sw, size_t i0 = 0, size_t i1 = SIZE_MAX) {
+  for (size_t i = i0; i < std::min(i1, plans.size()); ++i) {
     const WindowPlan& W = plans[i];
     ScanWork& s = sw[i];
     s.pts_off = pt_offsets[i];
@@ -1175,14 +1252,36 @@ int run_windows_small(csm_ctx* c, const csm_param& P, const Dims& D, const Geome
 
 // With pend == nullptr the call returns once results are on the host; with
 // pend it returns as soon as the work is enqueued (join with wait_run).
+// Part of a level's launch (the 3-level driver's chunked first plan): score
+// windows [w0, w1) only, or only finish every window once all are scored.
+// A part needs the device finish and window i's angle rows at i * n_angles.
+struct WinSpan {
+  int w0 = 0, w1 = -1;  // w1 < 0: every window
+  bool score = true, finish = true;
+};
+
 int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
                 const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
                 const AngleEntry* angles, size_t n_angle_entries,
                 const std::vector<int32_t>& grid_index, BestPartial* best_out,
-                Finish mode = Finish::kScoresToHost, PendingRun* pend = nullptr, int skip_lists = 0) {
+                Finish mode = Finish::kScoresToHost, PendingRun* pend = nullptr, int skip_lists = 0,
+                WinSpan sp = WinSpan{}) {
   if (best_out) mode = Finish::kBest;
   const int nw = (int)plans.size();
   if (nw == 0) return CSM_OK;
+  const int w0 = sp.w1 < 0 ? 0 : sp.w0, w1 = sp.w1 < 0 ? nw : sp.w1;
+  const int nr = w1 - w0;  // windows scored by this call
+  const bool whole = w0 == 0 && w1 == nw && sp.score && sp.finish;
+  if (!c->deferred.empty()) {  // the events below are recorded again
+    const int fst = flush_deferred(c);
+    if (fst != CSM_OK) return fst;
+  }
+  if (!whole) {
+    bool ok = mode == Finish::kDevice && (sp.score || sp.finish) && 0 <= w0 && w0 < w1 && w1 <= nw &&
+              n_angle_entries == (size_t)nw * (size_t)D.n_angles;
+    for (int w = w0; ok && w < w1; ++w) ok = plans[(size_t)w].angle_off == (int64_t)w * D.n_angles;
+    if (!ok) return c->fail(CSM_ERR_INVALID_ARG, "run_windows: bad window span");
+  }
   int st;
   if ((st = ensure_int_grid(c)) != CSM_OK) return st;
   // v2 column kernel: KT rows per lane, tiles balanced so at most a few rows idle
@@ -1192,8 +1291,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const int64_t col_blocks = (n_cols + 63) / 64;
   const bool v2 = c->column_kernel && n_cols < INT32_MAX;
   const double f = P.search_space_resolution / G.mres;
-  const bool use_int = v2 && int_mode_ok(c, D, f, plans);
-  if (mode != Finish::kBest && use_int && small_launch(c, D, nw))
+  const bool use_int = v2 && int_mode_ok(c, D, f, plans, (size_t)w0, (size_t)w1);
+  if (whole && mode != Finish::kBest && use_int && small_launch(c, D, nw))
     return run_windows_small(c, P, D, G, plans, pt_offsets, angles, n_angle_entries, grid_index,
                              mode == Finish::kDevice, pend, skip_lists);
   // v3 row-segment kernel: fixed-point grid and an instantiation whose row
@@ -1238,27 +1337,51 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                       : rows_sq ? (D.n_angles + rows_groups - 1) / rows_groups
                       : v2    ? col_blocks * ktiles
                               : (D.n_cand + per_block - 1) / per_block;
-  if (bps * nw > INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
+  if (bps * nr > INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
 
   hipError_t e;
   if ((e = c->h_sw.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scans)");
   ScanWork* sw = (ScanWork*)c->h_sw.p;  // pinned staging
-  fill_scan_work(D, plans, pt_offsets, grid_index, sw);
-  LevelWork L = make_level_work(c, P, D, G, nw, use_int);
+  if (sp.score) fill_scan_work(D, plans, pt_offsets, grid_index, sw, (size_t)w0, (size_t)w1);
+  LevelWork L = make_level_work(c, P, D, G, nr, use_int);
   L.blocks_per_scan = box_tiled ? D.n_angles : (int32_t)bps;  // per (window, tile) when tiled
   L.tile_n = box_tiled ? tile_n : 0;
   L.n_cols = (int32_t)n_cols;
   L.ktiles = ktiles;
   L.col_blocks = (int32_t)col_blocks;
 
+  // Host-signal finish (the device finish with its fast pass): FinishOut goes
+  // straight to coherent pinned memory and the pass that ends last sets a flag
+  // the host spins on; the scoring kernel clears the flagged-window count.
+  const bool sig = c->host_signal && mode == Finish::kDevice && c->fast_finish;
+  int32_t *d_done = nullptr, *d_need = nullptr, *d_list = nullptr;
+  if (sig) {
+    const size_t o_need = 64, o_list = o_need + (size_t)nw * 4, dbytes = o_list + (size_t)(nw + 1) * 4;
+    if (dbytes > c->fin_sig.cap) {  // the done counter starts at zero; each launch leaves it at zero
+      if ((e = c->fin_sig.ensure(dbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(finish signal)");
+      if ((e = hipMemsetAsync(c->fin_sig.p, 0, c->fin_sig.cap, c->stream)) != hipSuccess)
+        return c->hip_fail(e, "hipMemsetAsync(finish signal)");
+    }
+    d_done = (int32_t*)c->fin_sig.p;
+    d_need = (int32_t*)((char*)c->fin_sig.p + o_need);
+    d_list = (int32_t*)((char*)c->fin_sig.p + o_list);
+    L.clear_word = d_list;
+  }
+
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
   if ((e = c->angles.ensure(n_angle_entries * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
-  if ((e = hipMemcpyAsync(c->scans.p, sw, (size_t)nw * sizeof(ScanWork), hipMemcpyHostToDevice, c->h2d)) != hipSuccess)
-    return c->hip_fail(e, "hipMemcpyAsync(scans)");
-  if ((e = hipMemcpyAsync(c->angles.p, angles, n_angle_entries * sizeof(AngleEntry), hipMemcpyHostToDevice, c->h2d)) != hipSuccess)
-    return c->hip_fail(e, "hipMemcpyAsync(angles)");
-  if ((e = hipEventRecord(c->ev_in, c->h2d)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->ev_in, 0)) != hipSuccess)
-    return c->hip_fail(e, "inputs event");
+  if (sp.score) {  // this call's windows and angle rows
+    const size_t a0 = whole ? 0 : (size_t)w0 * D.n_angles;
+    const size_t na = whole ? n_angle_entries : (size_t)nr * D.n_angles;
+    if ((e = hipMemcpyAsync((ScanWork*)c->scans.p + w0, sw + w0, (size_t)nr * sizeof(ScanWork), hipMemcpyHostToDevice,
+                            c->h2d)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(scans)");
+    if ((e = hipMemcpyAsync((AngleEntry*)c->angles.p + a0, angles + a0, na * sizeof(AngleEntry), hipMemcpyHostToDevice,
+                            c->h2d)) != hipSuccess)
+      return c->hip_fail(e, "hipMemcpyAsync(angles)");
+    if ((e = hipEventRecord(c->ev_in, c->h2d)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->ev_in, 0)) != hipSuccess)
+      return c->hip_fail(e, "inputs event");
+  }
 
   // algorithmic traffic: one fp32 grid read per summed beam per candidate
   double beams = 0.0;
@@ -1282,43 +1405,91 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                   best_out ? "best" : "all");
   else
     std::snprintf(kname, sizeof(kname), "%s<%d>", best_out ? "score_best_kernel" : "score_all_kernel", cpl);
-  if (c->profiling && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+  // a signalled launch lets the host go on before its exact pass (on
+  // x_stream) has retired: this slot's next scoring waits for it, so the
+  // count it clears is no longer read
+  if (sig && sp.score && (e = hipStreamWaitEvent(c->stream, c->ev_done, 0)) != hipSuccess)
+    return c->hip_fail(e, "hipStreamWaitEvent(previous finish)");
+  if (c->profiling && sp.score && w0 == 0 && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipEventRecord");
 
   const int32_t* flags_h = nullptr;
   int n_flags = 0;
+  csm::FinishOut* sig_out = nullptr;
+  int32_t* sig_flag = nullptr;
+  int32_t sig_value = 0;
+  hipStream_t done_stream = c->d2h;
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
-    if (box)
-      e = csm::launch_score_box(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+    const ScanWork* d_sw = (const ScanWork*)c->scans.p + w0;
+    if (!sp.score)
+      e = hipSuccess;  // scored by earlier calls
+    else if (box)
+      e = csm::launch_score_box(L, d_sw, (const double*)c->pts.p,
                                 (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
                                 c->stream);
     else if (phase)
-      e = csm::launch_score_phase(L, PT, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                  (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
-                                  c->stream);
+      e = csm::launch_score_phase(L, PT, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
+                                  (double*)c->scores.p, nullptr, D.n_space, c->stream);
     else if (tiny)
-      e = csm::launch_score_tiny(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                 (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space, c->stream);
+      e = csm::launch_score_tiny(L, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
+                                 (double*)c->scores.p, nullptr, D.n_space, c->stream);
     else if (rows_sq)
-      e = csm::launch_score_rows(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                 (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr,
-                                 D.n_space, rows_sq, c->row_dma, c->stream);
+      e = csm::launch_score_rows(L, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
+                                 (double*)c->scores.p, nullptr, D.n_space, rows_sq, c->row_dma, c->stream);
     else if (v2)
-      e = csm::launch_score_cols(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                 (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, kt,
-                                 c->stream);
+      e = csm::launch_score_cols(L, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
+                                 (double*)c->scores.p, nullptr, kt, c->stream);
     else
-      e = csm::launch_score_all(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                (const AngleEntry*)c->angles.p, (double*)c->scores.p, cpl, c->stream);
+      e = csm::launch_score_all(L, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
+                                (double*)c->scores.p, cpl, c->stream);
     if (e != hipSuccess) return c->hip_fail(e, "score kernel");
-    if (c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+    if (sp.score && c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "hipEventRecord");
+    if (!sp.finish) return CSM_OK;  // the finish comes with the level's last call
     if (mode == Finish::kScoresToHost) {
       if ((e = c->h_scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scores)");
       if ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
         return c->hip_fail(e, "kernels event");
       if ((e = hipMemcpyAsync(c->h_scores.p, c->scores.p, bytes, hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
         return c->hip_fail(e, "hipMemcpyAsync(scores)");
+    } else if (sig) {
+      csm::FinishArgs A{};
+      A.n_cand = D.n_cand;
+      A.n_space = D.n_space;
+      A.step_cells = L.step_cells;
+      A.lin_tol = P.search_space_resolution / G.mres;
+      A.skip_lists = skip_lists;
+      A.need_exact = d_need;
+      A.exact_list = d_list;
+      A.done_ctr = d_done;
+      A.wide_windows = c->fast_wide_windows;
+      // FinishOut[nw] | need[nw] (profiling: the flags the host counts) | flag
+      const size_t out_need = ((size_t)nw * sizeof(csm::FinishOut) + 63) & ~(size_t)63;
+      const size_t out_flag = (out_need + (size_t)nw * sizeof(int32_t) + 63) & ~(size_t)63;
+      if (out_flag + 64 > c->h_fin_sig.cap) {
+        if ((e = c->h_fin_sig.ensure(std::max<size_t>(out_flag + 64, 64 * 1024), hipHostMallocCoherent)) != hipSuccess)
+          return c->hip_fail(e, "hipHostMalloc(finish signal)");
+        std::memset(c->h_fin_sig.p, 0, c->h_fin_sig.cap);
+      }
+      sig_out = (csm::FinishOut*)c->h_fin_sig.p;
+      sig_flag = (int32_t*)((char*)c->h_fin_sig.p + out_flag);
+      if (c->profiling) {  // the fast pass's flags to the host: finish:exact_windows
+        A.need_exact = (int32_t*)((char*)c->h_fin_sig.p + out_need);
+        flags_h = A.need_exact;
+        n_flags = nw;
+      }
+      A.host_flag = sig_flag;
+      A.flag_value = (int32_t)(++c->flag_seq & 0x7FFFFFFF);
+      if (A.flag_value == 0) A.flag_value = (int32_t)(++c->flag_seq & 0x7FFFFFFF);
+      sig_value = A.flag_value;
+      done_stream = c->x_stream ? c->x_stream : c->stream;
+      if ((e = csm::launch_finish(A, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
+                                  (const double*)c->scores.p, sig_out, nw, c->stream, done_stream, c->ev_fast)) !=
+          hipSuccess)
+        return c->hip_fail(e, "finish_kernel");
+      if (c->profiling && (e = hipEventRecord(c->ev2, done_stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
     } else {
       csm::FinishArgs A{};
       A.n_cand = D.n_cand;
@@ -1418,7 +1589,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   p.ev1 = c->ev1;
   p.ev2 = c->ev2;
   p.done = c->ev_done;
-  if ((e = hipEventRecord(c->ev_done, c->d2h)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+  p.fin_host = sig_out;
+  p.host_flag = sig_flag;
+  p.flag_value = sig_value;
+  p.defer_timing = sig;
+  if ((e = hipEventRecord(c->ev_done, done_stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
   if (pend) return CSM_OK;
   return wait_run(c, p);
 }
@@ -1666,11 +1841,13 @@ struct LevelRun {
   std::vector<int64_t> pt_off;
   std::vector<int32_t> grid;             // resident grid of each window (empty: grid 0)
   const AngleEntry* angles = nullptr;    // pinned buffer of the slot that ran it
+  AngleEntry* rows = nullptr;            // the same, writable while the level is planned
   const csm::FinishOut* fin = nullptr;   // ditto (device finish)
   const double* scores = nullptr;        // ditto (host finish)
   bool dev = false;
   int skip_lists = 0;  // live_lists
   PendingRun pend;
+  int tag = -1;        // 3-level driver: level * 8 + part (per-phase host timings)
 };
 
 // Which covariance lists of level l a caller of the 3-level driver can see,
@@ -1690,21 +1867,22 @@ int live_lists(const csm_param* levels, int n_levels, int l) {
   return skip;
 }
 
-int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
-                const double* poses, double* responses, int64_t* argmax_flat, LevelRun& R,
-                const int32_t* scan_grid = nullptr, int skip_lists = 0) {
+// Which scans of a level have windows, and its dimensions (no planning yet).
+// `reset`: responses (and argmaxes) of the batch start at kMinResponse.
+int level_prepare(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P, double* responses,
+                  int64_t* argmax_flat, LevelRun& R, const int32_t* scan_grid, int skip_lists, bool reset) {
   R.P = P;
   R.skip_lists = skip_lists;
   R.scan_of.clear();
   R.grid.clear();
   int st = window_dims(P, R.D);
   if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
-  const Dims& D = R.D;
-  const Geometry G(c->info);
   R.scan_of.reserve((size_t)n_scans);
   for (int s = 0; s < n_scans; ++s) {
-    responses[s] = 0.0;  // kMinResponse (:1034)
-    if (argmax_flat) argmax_flat[s] = -1;
+    if (reset) {
+      responses[s] = 0.0;  // kMinResponse (:1034)
+      if (argmax_flat) argmax_flat[s] = -1;
+    }
     const int n = (int)(offsets[s + 1] - offsets[s]);
     if (!map_ready(c) || n == 0) continue;  // :792-795
     int step, use, n_used;
@@ -1713,86 +1891,213 @@ int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
     R.scan_of.push_back(s);
     if (scan_grid) R.grid.push_back(scan_grid[s]);
   }
+  return CSM_OK;
+}
+
+// Room for the level's plans and angle rows (pinned: uploaded by DMA).
+int level_alloc(csm_ctx* c, const int64_t* offsets, LevelRun& R, HostBuf& rows) {
+  const int nw = (int)R.scan_of.size();
+  R.plans.assign((size_t)nw, WindowPlan{});
+  R.pt_off.resize((size_t)nw);
+  for (int i = 0; i < nw; ++i) R.pt_off[(size_t)i] = offsets[R.scan_of[(size_t)i]];
+  const hipError_t he = rows.ensure((size_t)nw * (size_t)R.D.n_angles * sizeof(AngleEntry));
+  if (he != hipSuccess) return c->hip_fail(he, "hipHostMalloc(angles)");
+  R.rows = (AngleEntry*)rows.p;
+  R.angles = R.rows;
+  return CSM_OK;
+}
+
+// Plan window i of a prepared level around the scan's current pose: host
+// libm cos/sin per angle (AngleSearchLookUpTable::UpdateLookUpTable :154-172).
+void level_plan_one(LevelRun& R, const Geometry& G, const int64_t* offsets, const double* poses, int i) {
+  const int s = R.scan_of[(size_t)i];
+  double center[3];
+  G.to_map(poses + 3 * s, center);
+  WindowPlan& W = R.plans[(size_t)i];
+  plan_window_into(R.P, R.D, G, (int)(offsets[s + 1] - offsets[s]), center, R.rows + (size_t)i * (size_t)R.D.n_angles, W);
+  W.angle_off = (int64_t)i * R.D.n_angles;
+}
+
+// Device finish for the front-end windows (and enough of them to fill the
+// chip); a handful of windows finish faster on the host's std::sort.
+bool level_device_finish(const csm_ctx* c, const Dims& D, int nw) {
+  return c->device_finish && D.n_cand <= csm::kFinishMaxCand && csm::finish_lds_bytes(D.n_cand) <= 160 * 1024 &&
+         nw >= c->device_finish_min;
+}
+
+// Enqueue a planned level, or a span of it (nothing waits).
+int level_launch(csm_ctx* c, LevelRun& R, WinSpan sp = WinSpan{}) {
+  const int nw = (int)R.scan_of.size();
+  const Dims& D = R.D;
+  const Geometry G(c->info);
+  R.dev = level_device_finish(c, D, nw);
+  const int st = run_windows(c, R.P, D, G, R.plans, R.pt_off, R.angles, (size_t)nw * (size_t)D.n_angles, R.grid,
+                             nullptr, R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend, R.skip_lists, sp);
+  if (st != CSM_OK || !sp.finish) return st;
+  R.fin = R.pend.fin_host ? R.pend.fin_host : (const csm::FinishOut*)c->h_fin.p;
+  R.scores = (const double*)c->h_scores.p;
+  return CSM_OK;
+}
+
+int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
+                const double* poses, double* responses, int64_t* argmax_flat, LevelRun& R,
+                const int32_t* scan_grid = nullptr, int skip_lists = 0) {
+  int st = level_prepare(c, n_scans, offsets, P, responses, argmax_flat, R, scan_grid, skip_lists, true);
+  if (st != CSM_OK) return st;
   const int nw = (int)R.scan_of.size();
   if (nw == 0) return CSM_OK;
   const double t0 = now_ms();
-  R.plans.assign((size_t)nw, WindowPlan{});
-  R.pt_off.assign((size_t)nw, 0);
-  hipError_t he;
-  const size_t n_ang_total = (size_t)nw * (size_t)D.n_angles;
-  if ((he = c->h_angles.ensure(n_ang_total * sizeof(AngleEntry))) != hipSuccess)
-    return c->hip_fail(he, "hipHostMalloc(angles)");
-  AngleEntry* angles = (AngleEntry*)c->h_angles.p;  // pinned: uploaded by DMA
-  R.angles = angles;
+  if ((st = level_alloc(c, offsets, R, c->h_angles)) != CSM_OK) return st;
+  const Geometry G(c->info);
   const int threads = (nw >= 64) ? c->host_threads : 1;
-  c->parallel_for(nw, threads, [&](int i) {  // host libm cos/sin per window angle
-    const int s = R.scan_of[(size_t)i];
-    double center[3];
-    G.to_map(poses + 3 * s, center);
-    plan_window_into(P, D, G, (int)(offsets[s + 1] - offsets[s]), center,
-                     angles + (size_t)i * (size_t)D.n_angles, R.plans[(size_t)i]);
-    R.plans[(size_t)i].angle_off = (int64_t)i * D.n_angles;
-    R.pt_off[(size_t)i] = offsets[s];
-  });
-  // device finish for the front-end windows (and enough of them to fill the
-  // chip); a handful of windows finish faster on the host's std::sort
-  R.dev = c->device_finish && D.n_cand <= csm::kFinishMaxCand &&
-          csm::finish_lds_bytes(D.n_cand) <= 160 * 1024 && nw >= c->device_finish_min;
+  c->parallel_for(nw, threads, [&](int i) { level_plan_one(R, G, offsets, poses, i); });
+  if (threads > 1) c->account_pool("plan");
   const double t1 = now_ms();
-  st = run_windows(c, P, D, G, R.plans, R.pt_off, angles, n_ang_total, R.grid, nullptr,
-                   R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend, skip_lists);
-  if (st != CSM_OK) return st;
-  R.fin = R.pend.fin_host ? R.pend.fin_host : (const csm::FinishOut*)c->h_fin.p;
-  R.scores = (const double*)c->h_scores.p;
+  if ((st = level_launch(c, R)) != CSM_OK) return st;
   if (c->profiling) {  // per level (window size), and in all
+    c->account("host:launch", (float)(now_ms() - t1), 0.0, 0.0);
     char nm[48];
-    std::snprintf(nm, sizeof(nm), "host:plan<%lld>", (long long)D.n_cand);
+    std::snprintf(nm, sizeof(nm), "host:plan<%lld>", (long long)R.D.n_cand);
     c->account("host:plan", (float)(t1 - t0), 0.0, 0.0);
     c->account(nm, (float)(t1 - t0), 0.0, 0.0);
   }
   return CSM_OK;
 }
 
+// level_begin with the plan in two pieces: the first `first` windows are
+// planned on the calling thread and their scoring goes out at once, the rest
+// are planned on the pool while it runs, then the finish follows for all.
+// For the 3-level driver's first part, where nothing else keeps the device
+// busy while the host plans (a call's first ~0.15 ms).
+int level_begin_split(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P, const double* poses,
+                      double* responses, LevelRun& R, const int32_t* scan_grid, int skip_lists, int first) {
+  int st = level_prepare(c, n_scans, offsets, P, responses, nullptr, R, scan_grid, skip_lists, true);
+  if (st != CSM_OK) return st;
+  const int nw = (int)R.scan_of.size();
+  if (first <= 0 || nw < 2 * first || !level_device_finish(c, R.D, nw))
+    return level_begin(c, n_scans, offsets, P, poses, responses, nullptr, R, scan_grid, skip_lists);
+  const double t0 = now_ms();
+  if ((st = level_alloc(c, offsets, R, c->h_angles)) != CSM_OK) return st;
+  const Geometry G(c->info);
+  for (int i = 0; i < first; ++i) level_plan_one(R, G, offsets, poses, i);
+  if ((st = level_launch(c, R, WinSpan{0, first, true, false})) != CSM_OK) return st;
+  c->parallel_for(nw - first, c->host_threads, [&](int i) { level_plan_one(R, G, offsets, poses, first + i); });
+  c->account_pool("plan");
+  if ((st = level_launch(c, R, WinSpan{first, nw, true, false})) != CSM_OK) return st;
+  if ((st = level_launch(c, R, WinSpan{0, nw, false, true})) != CSM_OK) return st;
+  if (c->profiling) {
+    char nm[48];
+    std::snprintf(nm, sizeof(nm), "host:plan+launch<%lld,split>", (long long)R.D.n_cand);
+    c->account(nm, (float)(now_ms() - t0), 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+// Join a level's launch and check its device finish.
+int level_join(csm_ctx* c, LevelRun& R) {
+  const int nw = (int)R.scan_of.size();
+  const double t1 = now_ms();
+  const int st = wait_run(c, R.pend);
+  if (st != CSM_OK) return st;
+  if (c->profiling) {
+    const float tw = (float)(now_ms() - t1);
+    c->account("host:wait", tw, 0.0, 0.0);
+    if (R.tag >= 0) {
+      char nm[48];
+      std::snprintf(nm, sizeof(nm), "host:wait<l%d,p%d>", R.tag / 8, R.tag % 8);
+      c->account(nm, tw, 0.0, 0.0);
+    }
+  }
+  if (R.dev)
+    for (int i = 0; i < nw; ++i)
+      if (R.fin[i].count < 0) return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
+  return CSM_OK;
+}
+
+// Complete window i of a joined level: pose, covariance and response
+// (BasedCorrelationScanMatch::ScanMatch :815-869).
+void level_complete_one(const LevelRun& R, const Geometry& G, double* poses, double* covs, double* responses,
+                        int64_t* argmax_flat, int i) {
+  thread_local std::vector<Entry> scratch;
+  const Dims& D = R.D;
+  const csm_param& P = R.P;
+  const int s = R.scan_of[(size_t)i];
+  const double f = P.search_space_resolution / G.mres;
+  const CandGeom C{R.plans[(size_t)i], R.angles + R.plans[(size_t)i].angle_off, f, D.n_space,
+                   (int64_t)D.n_space * D.n_space};
+  csm::FinishOut local;
+  const csm::FinishOut* o = nullptr;
+  if (R.dev) {
+    o = R.fin + i;
+  } else {
+    host_sort_finish(R.scores + (size_t)i * (size_t)D.n_cand, D, C, P, G, scratch, local);
+    o = &local;
+  }
+  if (argmax_flat) argmax_flat[s] = o->front_idx;
+  responses[s] = complete_window(*o, C, P, G, poses + 3 * s, covs + 9 * s, R.skip_lists);
+}
+
 int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* responses,
               int64_t* argmax_flat) {
   const int nw = (int)R.scan_of.size();
   if (nw == 0) return CSM_OK;
-  const double t1 = now_ms();
-  int st = wait_run(c, R.pend);
+  int st = level_join(c, R);
   if (st != CSM_OK) return st;
   const double t2 = now_ms();
-  const Dims& D = R.D;
-  const csm_param& P = R.P;
   const Geometry G(c->info);
-  if (R.dev)
-    for (int i = 0; i < nw; ++i)
-      if (R.fin[i].count < 0)
-        return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
-  const double f = P.search_space_resolution / G.mres;
   const int threads = (nw >= 64) ? c->host_threads : 1;
-  c->parallel_for(nw, threads, [&](int i) {
-    thread_local std::vector<Entry> scratch;
-    const int s = R.scan_of[(size_t)i];
-    const CandGeom C{R.plans[(size_t)i], R.angles + R.plans[(size_t)i].angle_off, f, D.n_space,
-                     (int64_t)D.n_space * D.n_space};
-    csm::FinishOut local;
-    const csm::FinishOut* o = nullptr;
-    if (R.dev) {
-      o = R.fin + i;
-    } else {
-      host_sort_finish(R.scores + (size_t)i * (size_t)D.n_cand, D, C, P, G, scratch, local);
-      o = &local;
-    }
-    if (argmax_flat) argmax_flat[s] = o->front_idx;
-    responses[s] = complete_window(*o, C, P, G, poses + 3 * s, covs + 9 * s, R.skip_lists);
-  });
+  c->parallel_for(nw, threads, [&](int i) { level_complete_one(R, G, poses, covs, responses, argmax_flat, i); });
+  if (threads > 1) c->account_pool("complete");
   if (c->profiling) {
     const float tc = (float)(now_ms() - t2);
     char nm[48];
-    std::snprintf(nm, sizeof(nm), "host:complete<%lld>", (long long)D.n_cand);
-    c->account("host:wait", (float)(t2 - t1), 0.0, 0.0);
+    std::snprintf(nm, sizeof(nm), "host:complete<%lld>", (long long)R.D.n_cand);
     c->account("host:complete", tc, 0.0, 0.0);
     c->account(nm, tc, 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+// level_end of R followed by level_begin of the next level N over the same
+// scans, fused: one pass of the host pool completes window i (its new pose)
+// and plans its next window right away, so the pool wakes once per level
+// transition instead of twice and the next launch goes out one pool round
+// trip earlier (the 3-level driver's critical path). `sum`
+// accumulates each scan's response (ScanMatchers::ScanMatch :252-256) before
+// the next level overwrites it. N's angle rows go to the other pinned buffer
+// of the slot: R's rows are still being read.
+int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const int64_t* offsets,
+                    const csm_param& P, double* poses, double* covs, double* responses, double* sum,
+                    const int32_t* scan_grid, int skip_lists) {
+  int st = level_prepare(c, n_scans, offsets, P, responses, nullptr, N, scan_grid, skip_lists, false);
+  if (st != CSM_OK) return st;
+  const int nw = (int)R.scan_of.size();
+  if (N.scan_of != R.scan_of || nw == 0) {  // not the same windows: one after the other
+    if ((st = level_end(c, R, poses, covs, responses, nullptr)) != CSM_OK) return st;
+    for (int s = 0; s < n_scans; ++s) sum[s] += responses[s];
+    return level_begin(c, n_scans, offsets, P, poses, responses, nullptr, N, scan_grid, skip_lists);
+  }
+  if ((st = level_join(c, R)) != CSM_OK) return st;
+  const double t2 = now_ms();
+  std::swap(c->h_angles, c->h_angles_next);
+  if ((st = level_alloc(c, offsets, N, c->h_angles)) != CSM_OK) return st;
+  const Geometry G(c->info);
+  const int threads = (nw >= 64) ? c->host_threads : 1;
+  c->parallel_for(nw, threads, [&](int i) {
+    level_complete_one(R, G, poses, covs, responses, nullptr, i);
+    const int s = R.scan_of[(size_t)i];
+    sum[s] += responses[s];
+    level_plan_one(N, G, offsets, poses, i);
+  });
+  if (threads > 1) c->account_pool("complete+plan");
+  const double t3 = now_ms();
+  if ((st = level_launch(c, N)) != CSM_OK) return st;
+  if (c->profiling) {
+    c->account("host:launch", (float)(now_ms() - t3), 0.0, 0.0);
+    c->account("host:complete+plan", (float)(t3 - t2), 0.0, 0.0);
+    char nm[48];
+    std::snprintf(nm, sizeof(nm), "host:complete+plan<l%d,p%d>", R.tag / 8, R.tag % 8);
+    if (R.tag >= 0) c->account(nm, (float)(t3 - t2), 0.0, 0.0);
   }
   return CSM_OK;
 }
@@ -1808,9 +2113,9 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
 }
 
 // ScanMatchers::ScanMatch over a resident batch (scan_matchers.h:179-289),
-// two halves in flight: while the device runs one half's level, the host
-// completes the other half's previous level and plans its next one. Scans
-// are independent, so the split changes no result.
+// parts in flight: while the device runs one part's level, the host
+// completes another part's previous level and plans its next one
+// (level_end_begin). Scans are independent, so the split changes no result.
 int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
                            int n_levels, double* poses, double* covs, double* sum,
                            const int32_t* scan_grid = nullptr) {
@@ -1829,29 +2134,38 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
     count[h] = (int32_t)((int64_t)n_scans * (h + 1) / K) - first[h];
   }
   std::vector<double> resp((size_t)n_scans, 0.0);
-  LevelRun R[csm_ctx::kMaxParts];
-  auto begin = [&](int l, int h) {
-    if (h > 0) c->swap_slot(h);
-    const int32_t s0 = first[h];
-    const int st = level_begin(c, count[h], offsets + s0, levels[l], poses + 3 * (size_t)s0,
-                               resp.data() + s0, nullptr, R[h], scan_grid ? scan_grid + s0 : nullptr,
-                               c->skip_dead_lists ? live_lists(levels, n_levels, l) : 0);
-    if (h > 0) c->swap_slot(h);
-    return st;
-  };
-  auto end = [&](int h) {
-    const int32_t s0 = first[h];
-    const int st = level_end(c, R[h], poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, nullptr);
-    for (int s = s0; s < s0 + count[h]; ++s) sum[(size_t)s] += resp[(size_t)s];
-    return st;
-  };
+  LevelRun R[2][csm_ctx::kMaxParts];  // by level parity: level l's run and level l + 1's
+  auto skip = [&](int l) { return c->skip_dead_lists ? live_lists(levels, n_levels, l) : 0; };
   int st;
-  for (int h = 0; h < K; ++h)
-    if ((st = begin(0, h)) != CSM_OK) return st;
+  for (int h = 0; h < K; ++h) {
+    const int32_t s0 = first[h];
+    R[0][h].tag = h;
+    if (h > 0) c->swap_slot(h);
+    if (h == 0)  // the device waits for this one
+      st = level_begin_split(c, count[h], offsets + s0, levels[0], poses + 3 * (size_t)s0, resp.data() + s0, R[0][h],
+                             scan_grid ? scan_grid + s0 : nullptr, skip(0), c->first_windows);
+    else
+      st = level_begin(c, count[h], offsets + s0, levels[0], poses + 3 * (size_t)s0, resp.data() + s0, nullptr,
+                       R[0][h], scan_grid ? scan_grid + s0 : nullptr, skip(0));
+    if (h > 0) c->swap_slot(h);
+    if (st != CSM_OK) return st;
+  }
   for (int l = 0; l < n_levels; ++l) {
     for (int h = 0; h < K; ++h) {
-      if ((st = end(h)) != CSM_OK) return st;
-      if (l + 1 < n_levels && (st = begin(l + 1, h)) != CSM_OK) return st;
+      const int32_t s0 = first[h];
+      LevelRun& cur = R[l & 1][h];
+      if (l + 1 < n_levels) {
+        R[(l + 1) & 1][h].tag = (l + 1) * 8 + h;
+        if (h > 0) c->swap_slot(h);
+        st = level_end_begin(c, cur, R[(l + 1) & 1][h], count[h], offsets + s0, levels[l + 1],
+                             poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, sum + s0,
+                             scan_grid ? scan_grid + s0 : nullptr, skip(l + 1));
+        if (h > 0) c->swap_slot(h);
+      } else {
+        st = level_end(c, cur, poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, nullptr);
+        for (int s = s0; s < s0 + count[h]; ++s) sum[(size_t)s] += resp[(size_t)s];
+      }
+      if (st != CSM_OK) return st;
     }
   }
   return CSM_OK;
@@ -2244,6 +2558,8 @@ int csm_create(int device, csm_ctx** out) {
   }
   c->host_threads = threads;
   if (const char* env = std::getenv("CSM_POOL_SPIN_US")) c->pool_spin_us = std::atoi(env);
+  if (const char* env = std::getenv("CSM_FIRST_WINDOWS")) c->first_windows = std::max(0, std::atoi(env));
+  if (const char* env = std::getenv("CSM_HOST_SIGNAL")) c->host_signal = std::atoi(env) != 0;
   if (const char* env = std::getenv("CSM_FINISH")) {
     c->device_finish = std::strcmp(env, "host") != 0;
     c->fast_finish = std::strcmp(env, "exact") != 0;
@@ -2335,6 +2651,9 @@ int csm_destroy(csm_ctx* c) {
     c->h_scores.release();
     c->h_fin.release();
     c->h_angles.release();
+    c->h_angles_next.release();
+    c->h_fin_sig.release();
+    c->fin_sig.release();
     c->h_sw.release();
     c->opt_off.release();
     c->opt_scans.release();
@@ -2351,6 +2670,9 @@ int csm_destroy(csm_ctx* c) {
       a.h_scores.release();
       a.h_fin.release();
       a.h_angles.release();
+      a.h_angles_next.release();
+      a.h_fin_sig.release();
+      a.fin_sig.release();
       a.h_sw.release();
       for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k, a.ev_fast})
         if (ev) (void)hipEventDestroy(ev);
@@ -2687,6 +3009,7 @@ int csm_scan_matchers_loaded(csm_ctx* c, const csm_param levels[3], int32_t use_
   if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
   const int32_t n_scans = c->loaded_n;
   if (n_scans == 0) return CSM_OK;
+  const double t_call = now_ms();
   // ScanMatchers::ScanMatch (scan_matchers.h:179-289), use_optimize = false:
   // coarse, then (use_fine) fine and super-fine, pose fed forward in place.
   std::vector<double> resp((size_t)n_scans, 0.0), sum((size_t)n_scans, 0.0);
@@ -2711,6 +3034,7 @@ int csm_scan_matchers_loaded(csm_ctx* c, const csm_param levels[3], int32_t use_
     }
   }
   for (int s = 0; s < n_scans; ++s) scores[s] = sum[(size_t)s] / n_levels;  // :281
+  if (c->profiling) c->account("host:call", (float)(now_ms() - t_call), 0.0, 0.0);
   return CSM_OK;
 }
 
@@ -2735,6 +3059,7 @@ int csm_set_profiling(csm_ctx* c, int32_t on) {
       for (hipEvent_t* ev : {&a.ev0, &a.ev1, &a.ev2})
         if ((e = hipEventCreate(ev)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
   }
+  (void)flush_deferred(c);  // timings of the earlier setting, dropped with the stats below
   c->profiling = on != 0;
   c->stats.clear();
   return CSM_OK;
@@ -2743,6 +3068,11 @@ int csm_set_profiling(csm_ctx* c, int32_t on) {
 int csm_kernel_stats(csm_ctx* c, csm_kernel_stat* out, int32_t capacity, int32_t* count) {
   if (!c || !count) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->deferred.empty()) {
+    DeviceGuard g(c->device);
+    const int st = flush_deferred(c);
+    if (st != CSM_OK) return st;
+  }
   *count = (int32_t)c->stats.size();
   for (int32_t i = 0; i < *count && i < capacity && out; ++i) out[i] = c->stats[(size_t)i];
   return CSM_OK;

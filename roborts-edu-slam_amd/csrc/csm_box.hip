@@ -238,6 +238,7 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   static_assert(NS * NQ <= 64, "one box row piece per lane");
   static_assert(64 % D == 0 && 32 % D == 0, "loads in flight divide the fold block");
   const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  dev::clear_word(L);
   const int wt = bid / L.n_angles;  // window (untiled) or (window, tile)
   const int a = bid - wt * L.n_angles;
   int win = wt, ox = 0, oy = 0, nsf = NS;

@@ -10,6 +10,11 @@ namespace dev {
 
 // XCD-aware, bijective block remap (cdna_hip_programming.md T1): blocks that
 // share a logical neighbourhood (one window) land on one XCD's L2.
+// LevelWork::clear_word: block 0, lane 0 of a scoring kernel clears it.
+__device__ __forceinline__ void clear_word(const LevelWork& L) {
+  if (L.clear_word && blockIdx.x == 0 && threadIdx.x == 0) *L.clear_word = 0;
+}
+
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7;
   const int q = nwg >> 3, r = nwg & 7;

@@ -886,6 +886,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
 // 256 candidates per pass), and the window's angle rows sit in LDS for the
 // sequential FindBest sums. T = 1024 for launches of few windows (the
 // reference's single-scan levels), 256 otherwise.
+constexpr int kSysWriteThrough = 17;  // buffer cache policy sc0 | sc1: system-coherent, written through L2
 constexpr int kFastCap = 512;      // compacted candidates of step 2
 constexpr int kFastNearCap = 512;  // compacted near-best candidates of step 3
 constexpr int kFastLevels = 8;     // thresholds best - {0.01, 0.02, ..., 0.64}, then everything > bound
@@ -899,19 +900,19 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
-// Host signal of the few-window path (A.host_flag): every block's FinishOut
-// stores land (each wave waits, one system-scope release per block), the
-// blocks count in; the last one, if no window was flagged for the exact pass,
-// stores the flag value itself -- the exact launch behind it then returns at
-// once and is off the host's critical path.
-// (Measured: without the per-block system release the host read stale
-// FinishOut fields: the stores to pinned host memory can sit in the XCD's L2.)
+// Host signal (A.host_flag): every block's FinishOut stores land (write-
+// through sc0 sc1 stores to the coherent host buffer, each wave waits for
+// them), the blocks count in; the last one, if no window was flagged for the
+// exact pass, stores the flag value itself -- the exact launch behind it then
+// returns at once and is off the host's critical path.
+// (Measured: with plain stores and no per-block system-scope release the host
+// read stale FinishOut fields -- the lines sat in the XCD's L2 -- and that
+// release, a write-back of the whole L2 per block, cost 25-50 us per
+// 1024-window launch; write-through stores leave nothing to write back.)
 __device__ __forceinline__ void fast_signal(const FinishArgs& A) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the host reads FinishOut
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t = __hip_atomic_fetch_add(A.done_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (int)gridDim.x - 1) {
       __hip_atomic_store(A.done_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1115,8 +1116,21 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
     static_assert(sizeof(FinishOut) % 16 == 0, "FinishOut in 16-byte pieces");
     constexpr int kPieces = (int)(sizeof(FinishOut) / 16);
     __syncthreads();
-    if (tid < kPieces)
-      reinterpret_cast<int4*>(out + w)[tid] = reinterpret_cast<const int4*>(&so)[tid];
+    if (tid < kPieces) {
+      const int4 piece = reinterpret_cast<const int4*>(&so)[tid];
+      if (A.host_flag) {  // host memory: write-through (sc0 sc1), nothing left dirty in the XCD's L2
+        const uint64_t base = (uint64_t)(uintptr_t)(out + w);
+        const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+        const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(((uint64_t)bhi << 32) | blo), (short)0, (int)sizeof(FinishOut), 0x00020000);
+        typedef int32_t v4i_t __attribute__((ext_vector_type(4)));
+        const v4i_t v = {piece.x, piece.y, piece.z, piece.w};
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, tid * 16, 0, kSysWriteThrough);
+      } else {
+        reinterpret_cast<int4*>(out + w)[tid] = piece;
+      }
+    }
   };
   if (tid == 0) {  // :676-707, the same sequential sums as finish_kernel
     double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;

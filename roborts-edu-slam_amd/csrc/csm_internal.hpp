@@ -60,6 +60,10 @@ struct LevelWork {
                            // kGridiPadRows): each grid ends with zero rows)
   int32_t tile_n;          // box kernel over a large window: tiles per axis (0: untiled)
   int32_t tile_ns;         // ... and the window's own n_space (candidate indices are its)
+  // The finish's flagged-window count (FinishArgs::exact_list[0]) of a
+  // host-signal launch: block 0 of the scoring kernel, which runs before the
+  // finish on the stream, stores 0 there (nullptr: nothing to clear).
+  int32_t* clear_word;
 };
 
 // Argmax partial: best score of a block and its flat candidate index.

@@ -29,6 +29,11 @@ namespace {
 
 // XCD-aware, bijective block remap (cdna_hip_programming.md T1): blocks that
 // share a logical neighbourhood (one window) land on one XCD's L2.
+// LevelWork::clear_word: block 0, lane 0 of a scoring kernel clears it.
+__device__ __forceinline__ void clear_word(const LevelWork& L) {
+  if (L.clear_word && blockIdx.x == 0 && threadIdx.x == 0) *L.clear_word = 0;
+}
+
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7;
   const int q = nwg >> 3, r = nwg & 7;
@@ -138,6 +143,7 @@ __global__ __launch_bounds__(kBlock) void score_all_kernel(
     const AngleEntry* __restrict__ angles, double* __restrict__ out) {
   __shared__ double2 lds[kChunk];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  clear_word(L);
   const int scan = bid / L.blocks_per_scan;
   const int blk = bid - scan * L.blocks_per_scan;
   const ScanWork S = scans[scan];
@@ -174,6 +180,7 @@ __global__ __launch_bounds__(64) void score_cols_kernel(
     const AngleEntry* __restrict__ angles, double* __restrict__ out,
     BestPartial* __restrict__ partials) {
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  clear_word(L);
   const int win = bid / L.blocks_per_scan;
   const int r = bid - win * L.blocks_per_scan;
   const int cb = r / L.ktiles;
@@ -362,6 +369,7 @@ __global__ __launch_bounds__(64) void score_rows_kernel(
   constexpr int GS = NS * RS + (((GT - (NS * RS) % 64) % 64) + 64) % 64;
   __shared__ __attribute__((aligned(16))) int32_t tile[G * GS + RS];  // + a sink row
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  clear_word(L);
   const int win = bid / L.blocks_per_scan;
   const int blk = bid - win * L.blocks_per_scan;
   const ScanWork S = scans[win];
@@ -556,6 +564,7 @@ __global__ __launch_bounds__(64 * BS) void score_rowsd_kernel(
   __shared__ __attribute__((aligned(16))) int32_t zblk[NS * SEG];
   __shared__ int64_t xsum[(BS - 1) * 64 * NS + 1];  // waves 1.. -> wave 0
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  clear_word(L);
   const int win = bid / L.blocks_per_scan;
   const int blk = bid - win * L.blocks_per_scan;
   const ScanWork S = scans[win];
@@ -794,6 +803,7 @@ __global__ __launch_bounds__(kBlock) void score_best_kernel(
   __shared__ double red_s[kBlock / 64];
   __shared__ int64_t red_f[kBlock / 64];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  clear_word(L);
   const int scan = bid / L.blocks_per_scan;
   const int blk = bid - scan * L.blocks_per_scan;
   const ScanWork S = scans[scan];

@@ -89,6 +89,7 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
   __shared__ int8_t oxs[NQ][kPhaseMaxSpace];
 
   const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  dev::clear_word(L);
   const int win = bid / L.n_angles;
   const int a = bid - win * L.n_angles;
   const ScanWork S = scans[win];

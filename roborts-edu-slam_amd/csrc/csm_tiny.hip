@@ -40,6 +40,7 @@ __global__ __launch_bounds__(64) void score_tiny_kernel(LevelWork L, const ScanW
   constexpr int NC = NS * NS;
   static_assert(NC <= 64, "one candidate per lane in the epilogue");
   const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  dev::clear_word(L);
   const int win = bid / L.n_angles;
   const int a = bid - win * L.n_angles;
   const ScanWork S = scans[win];

@@ -666,22 +666,24 @@ def test_willow_best_window(ctx, willow):
         assert got.score == s and got.flat_index == flat
 
 
-@pytest.mark.parametrize("finish,parts", [("device", 2), ("host", 2), ("device", 3), ("device", 4)])
-def test_pipelined_three_level_driver(world2000, finish, parts):
+@pytest.mark.parametrize("finish,parts,first", [("device", 2, "0"), ("host", 2, "0"), ("device", 3, "0"),
+                                                 ("device", 4, "0"), ("device", 2, "5"), ("device", 3, "1"),
+                                                 ("host", 2, "5")])
+def test_pipelined_three_level_driver(world2000, finish, parts, first):
     """The batch split into 2-4 parts in flight (CSM_PIPELINE threshold
-    lowered so 96 scans split): results equal the oracle's bit for bit."""
+    lowered so 96 scans split), the first part's coarse level launched in two
+    spans (CSM_FIRST_WINDOWS, level_begin_split) or in one: results equal the
+    oracle's bit for bit."""
     import roborts_csm
     from roborts_csm.params import headline_levels
     w, b = world2000
-    os.environ["CSM_PIPELINE"] = "16"
-    os.environ["CSM_PIPELINE_PARTS"] = str(parts)
-    os.environ["CSM_FINISH"] = finish
+    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": str(parts), "CSM_FINISH": finish, "CSM_FIRST_WINDOWS": first}
+    os.environ.update(env)
     try:
         c = roborts_csm.Context(0)
     finally:
-        del os.environ["CSM_PIPELINE"]
-        del os.environ["CSM_PIPELINE_PARTS"]
-        del os.environ["CSM_FINISH"]
+        for k in env:
+            del os.environ[k]
     try:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
         poses = np.ascontiguousarray(b.init_poses.copy())
@@ -697,6 +699,37 @@ def test_pipelined_three_level_driver(world2000, finish, parts):
         assert st["host:wait"] == 3 * parts  # 3 levels x parts
     finally:
         c.close()
+
+
+def test_host_signal_finish_repeated(world2000):
+    """The throughput path's host-signal finish (FinishOut written through to
+    coherent host memory, a flag instead of a D2H copy and an event) over 25
+    back-to-back 3-level batches in 2 parts: every batch equals the oracle's
+    answer bit for bit, and the copy-back path (CSM_HOST_SIGNAL=0) agrees."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    m = O.Map(w.grid, w.resolution, w.offset)
+    eye = np.tile(np.eye(3).reshape(1, 9), (b.init_poses.shape[0], 1))
+    s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells, b.offsets, headline_levels(), b.init_poses, eye.copy())
+    for sig in ("1", "0"):
+        env = {"CSM_PIPELINE": "16", "CSM_HOST_SIGNAL": sig, "CSM_FIRST_WINDOWS": "8"}
+        os.environ.update(env)
+        try:
+            c = roborts_csm.Context(0)
+        finally:
+            for k in env:
+                del os.environ[k]
+        try:
+            c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+            c.load_scans(b.points_cells, b.offsets)
+            for it in range(25 if sig == "1" else 3):
+                poses = np.ascontiguousarray(b.init_poses.copy())
+                covs = eye.copy()
+                s = c.scan_matchers_loaded(headline_levels(), poses, covs)
+                assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2), (sig, it)
+        finally:
+            c.close()
 
 
 @pytest.mark.parametrize("order,use_fine", [((0, 1, 2), True), ((0, 1, 2), False), ((1, 0, 2), True),
