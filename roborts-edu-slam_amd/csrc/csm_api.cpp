@@ -989,6 +989,10 @@ int account_run(csm_ctx* c, const PendingRun& p) {
         int exact = 0;
         for (int i = 0; i < p.n_flags; ++i) exact += p.flags[i] != 0;
         c->account("finish:exact_windows", 0.f, 0.0, (double)exact);
+        char nm[48];  // per level: "finish_kernel<n>" -> "finish:exact_windows<n>" (bytes = windows)
+        const char* lt = std::strchr(p.fname, '<');
+        std::snprintf(nm, sizeof(nm), "finish:exact_windows%s", lt ? lt : "");
+        c->account(nm, 0.f, (double)p.n_flags, (double)exact);
       }
     }
   }
@@ -1370,6 +1374,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
 
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
   if ((e = c->angles.ensure(n_angle_entries * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
+  const double tl0 = c->profiling ? now_ms() : 0.0;  // host cost of the launch, by phase
   if (sp.score) {  // this call's windows and angle rows
     const size_t a0 = whole ? 0 : (size_t)w0 * D.n_angles;
     const size_t na = whole ? n_angle_entries : (size_t)nr * D.n_angles;
@@ -1405,6 +1410,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                   best_out ? "best" : "all");
   else
     std::snprintf(kname, sizeof(kname), "%s<%d>", best_out ? "score_best_kernel" : "score_all_kernel", cpl);
+  const double tl1 = c->profiling ? now_ms() : 0.0;
   // a signalled launch lets the host go on before its exact pass (on
   // x_stream) has retired: this slot's next scoring waits for it, so the
   // count it clears is no longer read
@@ -1419,6 +1425,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   int32_t* sig_flag = nullptr;
   int32_t sig_value = 0;
   hipStream_t done_stream = c->d2h;
+  double tl2 = 0.0;
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
     if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
@@ -1447,7 +1454,12 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if (e != hipSuccess) return c->hip_fail(e, "score kernel");
     if (sp.score && c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess)
       return c->hip_fail(e, "hipEventRecord");
+    if (c->profiling) {
+      c->account("host:launch:inputs", (float)(tl1 - tl0), 0.0, 0.0);
+      c->account("host:launch:score", (float)(now_ms() - tl1), 0.0, 0.0);
+    }
     if (!sp.finish) return CSM_OK;  // the finish comes with the level's last call
+    tl2 = c->profiling ? now_ms() : 0.0;
     if (mode == Finish::kScoresToHost) {
       if ((e = c->h_scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scores)");
       if ((e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
@@ -1594,6 +1606,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   p.flag_value = sig_value;
   p.defer_timing = sig;
   if ((e = hipEventRecord(c->ev_done, done_stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+  if (c->profiling && tl2 > 0.0) c->account("host:launch:finish", (float)(now_ms() - tl2), 0.0, 0.0);
   if (pend) return CSM_OK;
   return wait_run(c, p);
 }

@@ -673,6 +673,19 @@ __device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ 
   auto cy = [&](int idx) { return S.y0 + (idx % ns) * f; };
   const double best = keys[0];
   FinishOut* o = out + w;
+  // The window's angle rows (cos, sin) in LDS for FindBest's sequential sums:
+  // one dependent global load per prefix element made the loop latency-bound
+  // (the super-fine level's prefix holds most of its 189 candidates). The
+  // partition scratch (lpos .. stack) is free until stage 2 rewrites it.
+  const int n_ang = n / nss;
+  double2* acs = reinterpret_cast<double2*>(smem + Lo.lpos);
+  const bool staged = (size_t)n_ang * sizeof(double2) <= Lo.total - Lo.lpos;
+  if (staged)
+    for (int t = threadIdx.x; t < n_ang; t += 64 * kWaves) {
+      const AngleEntry ae = angles[S.angle_off + t];
+      acs[t] = make_double2(ae.cosine, ae.sine);
+    }
+  __syncthreads();
   if (threadIdx.x == 0) {
     // FindBestCandidate (:670-710): sequential sums over the tied prefix.
     double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;
@@ -683,7 +696,8 @@ __device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ 
       const bool eq = d < 0.0 ? d >= -1e-2 : d <= 1e-2;  // DoubleEqual(s, best, 1e-2)
       if (!eq) break;
       const int idx = vals[i];
-      const AngleEntry ae = angles[S.angle_off + idx / nss];
+      const int a = idx / nss;
+      const AngleEntry ae = staged ? AngleEntry{0.0, acs[a].x, acs[a].y} : angles[S.angle_off + a];
       ax += cx(idx) * s;
       ay += cy(idx) * s;
       thx += ae.cosine * s;

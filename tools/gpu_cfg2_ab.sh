@@ -14,6 +14,9 @@ steps = d['steps']
 for k in d['kernels']:
     if k['name'].startswith('host:'):
         print('   %-34s %8.3f ms/step  %6.1f calls/step' % (k['name'], k['total_ms'] / steps, k['launches'] / steps))
+    elif k['name'].startswith('finish:exact_windows<'):
+        print('   %-34s %6.1f of %6.1f windows per launch take the exact pass' % (k['name'],
+              k['scorings'] / k['launches'], k['algorithmic_bytes'] / k['launches']))
     elif not k['name'].startswith('pool:') and k['launches']:
         print('   %-34s %8.3f ms/step  %6.1f calls/step  %7.1f us/call' % (k['name'], k['total_ms'] / steps,
               k['launches'] / steps, k['total_ms'] / k['launches'] * 1e3))
