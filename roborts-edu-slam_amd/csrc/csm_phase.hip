@@ -18,10 +18,13 @@
 //   1. classify every beam (rotation, phases, buckets, margin test), count it
 //      into its pair, scatter its box corner into the pair's list in LDS
 //      (lists padded to whole groups of SL beams);
-//   2. walk the lists: lane (slot, cell) gathers one dword of its slot's beam
-//      box, one group of SL beams per wave instruction, kD groups in flight;
-//      at a pair boundary the slots' sums fold into accum[pair][cell];
-//   3. candidate (j, k) = sum over pairs of accum[pair][ox[qy][k]][ox[qx][j]].
+//   2. walk the lists: lane (slot, box row, piece) gathers a 16-byte row
+//      piece of its slot's beam box, one group of SL beams per wave
+//      instruction, kD groups in flight; where a list entry ends the lanes'
+//      int32 partials go into the pair's int64 box sums psum[pair][cell]
+//      (LDS, kept over the whole scan: segments add into the same sums);
+//   3. once per scan, candidate (j, k) = sum over pairs of
+//      psum[pair][ox[qy][k]][ox[qx][j]].
 // Sums are exact integers over the fixed-point grid (gridi), so their order
 // is free (csm_set_grid). Rounding, as for the box kernel (csm_box.hip): the
 // computed t_j is within 2^-27 of T + j*f (T = lx + x0 + 0.5, real), so a
@@ -39,29 +42,35 @@ namespace csm {
 namespace {
 
 #ifndef CSM_PHASE_SEG
-#define CSM_PHASE_SEG 576  // 576: 0.42 ms per fine launch; 1152: 0.48 (register and LDS pressure); 384: 0.43
+#define CSM_PHASE_SEG 576  // r03: 576: 0.352 ms per fine launch, 768: 0.364, 384: 0.381, 1152: 0.415
 #endif
 constexpr int kSeg = CSM_PHASE_SEG;  // beams classified per segment (lists in LDS)
-constexpr int kEntG = 5;             // groups per list entry: 6 slots * 5 * (2^26 - 1) < 2^31
+// groups per list entry: a lane's int32 partial sums one slot over at most
+// kEntG groups, |value| < 2^26 each, before it goes into the pair's int64 sums
+constexpr int kEntG = 31;
+static_assert(kEntG * ((1LL << 26) - 1) < 2147483647LL, "a lane's int32 partial");
 constexpr int kChunks = kSeg / 64;   // 64-beam chunks per segment, classified in registers
 #ifndef CSM_PHASE_DEPTH
-#define CSM_PHASE_DEPTH 8  // 8: 0.418-0.423 ms per fine launch, 16: 0.426, 4: 0.424 (24 was a wrong build)
+// r03 (int64 pair sums, list entries read a block ahead): 4: 0.352 ms per fine
+// launch, 8: 0.357-0.359, 16: 0.396 (r02: 8: 0.418-0.423, 16: 0.426, 4: 0.424)
+#define CSM_PHASE_DEPTH 4
 #endif
 constexpr int kD = CSM_PHASE_DEPTH;  // groups of loads in flight
 static_assert(kD <= 32, "int32 partial sums fold every kD groups");
 // gentry[lane & (kD - 1)] and the group-window slides index by masking
 static_assert((kD & (kD - 1)) == 0, "CSM_PHASE_DEPTH must be a power of two");
 static_assert(kSeg % 64 == 0, "CSM_PHASE_SEG must be whole 64-beam chunks");
-// 1: flush a lane's sums only where an entry ends (a uniform branch; 0.465 ->
-// 0.427 ms per fine launch); 0: every group adds into dummy cells, branch-free
-#ifndef CSM_PHASE_BRANCH_FLUSH
-#define CSM_PHASE_BRANCH_FLUSH 1
-#endif
 
 typedef int32_t v4i __attribute__((ext_vector_type(4)));
 
+// waves per SIMD the register allocation aims for (__launch_bounds__'s
+// second argument on AMD: minimum waves per execution unit)
+#ifndef CSM_PHASE_WAVES
+#define CSM_PHASE_WAVES 4
+#endif
+
 template <int NS, int C, int NQ, bool BEST>
-__global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable T,
+__global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelWork L, PhaseTable T,
                                                          const ScanWork* __restrict__ scans,
                                                          const double2* __restrict__ pts,
                                                          const AngleEntry* __restrict__ angles,
@@ -69,23 +78,22 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
                                                          BestPartial* __restrict__ partials) {
   constexpr int NP = NQ * NQ;   // bucket pairs
   constexpr int NPC = (C + 3) / 4;  // 16-byte pieces per box row
-  constexpr int CW = 4 * NPC;   // accumulated columns per box row (those >= C are never read)
   constexpr int LPS = C * NPC;  // lanes per slot: one row piece each
   constexpr int SL = 64 / LPS;  // beams (slots) per wave instruction
+  constexpr int PC = C * C;     // int64 box sums per pair
   static_assert(LPS <= 64 && NP <= 64 && NS <= kPhaseMaxSpace && NQ <= kPhaseMaxBuckets, "layout");
-  // padded lists, whole kD blocks of groups and the issue-ahead slack
-  static_assert(SL * kEntG * ((1 << 26) - 1) < 2147483647LL, "an entry's int32 sums");
-  constexpr int kList = kSeg + NP * (SL - 1) + 2 * SL * kD + 64;
+  static_assert(2 * NP + 1 < 256, "group tags are bytes");
+  // padded lists, whole kD blocks of groups and two blocks of issue-ahead slack
+  constexpr int kList = kSeg + NP * (SL - 1) + 3 * SL * kD + 64;
   constexpr int kMaxGroups = kList / SL + 1;
-  constexpr int kMaxEnt = NP + (kSeg / SL + NP) / kEntG + 2;  // + the spare entry
-  constexpr int ECELLS = C * CW;                              // int32 sums per entry
   __shared__ int32_t list[kList];
   __shared__ int32_t cursor[NP];
-  __shared__ int32_t ngroups_s, nent_s;
-  __shared__ uint8_t gentry[kMaxGroups];  // list entry of each group
-  __shared__ int8_t ent_pair[kMaxEnt];    // bucket pair of each entry (-1: the spare)
-  __shared__ int32_t esum[kMaxEnt * ECELLS];
-  __shared__ int32_t dummy[64 * 4 + 4];   // per-lane target of the flushes between boundaries
+  __shared__ int32_t ngroups_s;
+  // group tag: 2 * pair + (entry within the pair & 1), so the tag changes
+  // exactly where an entry ends; the groups past the lists carry 2 * NP
+  // (pair NP: a dummy row of psum nobody reads)
+  __shared__ uint8_t gtag[kMaxGroups];
+  __shared__ int64_t psum[(NP + 1) * PC];  // per pair, box cell (row, column): the whole scan's sums
   __shared__ int8_t oxs[NQ][kPhaseMaxSpace];
 
   const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
@@ -120,6 +128,7 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
 
   for (int i = lane; i < NQ * kPhaseMaxSpace; i += 64) oxs[i / kPhaseMaxSpace][i % kPhaseMaxSpace] =
       T.ox[i / kPhaseMaxSpace][i % kPhaseMaxSpace];
+  for (int i = lane; i < (NP + 1) * PC; i += 64) psum[i] = 0;
 
   auto bucket = [&](double ph, bool& ok) -> int {
     int q = 0;
@@ -157,7 +166,7 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
   // per lane: its candidates' box offsets in every bucket, 4 bits each
   constexpr int NC = NS * NS;
   constexpr int R = (NC + 63) / 64;
-  __syncthreads();  // oxs
+  __syncthreads();  // oxs, psum
   uint32_t oxj[R], oyk[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
   int64_t sum[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) sum[r] = 0;
-  const int lane_cell = (cv * CW + 4 * ch) * 4;  // byte offset of this lane's 4 sums in an entry
+  const int lane_cell = cv * C + 4 * ch;  // this lane's first box cell in a pair's sums
 
   uint64_t slow = 0;  // bit c: 64-beam chunk c holds a rejected beam (bit 63: some chunk >= 63)
   for (int s0 = 0; s0 < n_used; s0 += kSeg) {
@@ -201,44 +210,32 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
     }
     __syncthreads();
     // 1b. lists: pair p gets whole groups of SL beams, its groups split into
-    // entries of at most kEntG groups (an entry's sums fit int32)
+    // entries of at most kEntG groups (a lane's partial fits int32)
     {
       const int cnt = lane < NP ? cursor[lane] : 0;
       const int g = (cnt + SL - 1) / SL;
-      const int e = (g + kEntG - 1) / kEntG;
-      int gi_ = g, ei = e;  // inclusive scans over lanes
+      int gi_ = g;  // inclusive scan over lanes
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const int tg = __shfl_up(gi_, o, 64);
-        const int te = __shfl_up(ei, o, 64);
-        if (lane >= o) {
-          gi_ += tg;
-          ei += te;
-        }
+        if (lane >= o) gi_ += tg;
       }
-      const int g0p = gi_ - g, e0p = ei - e;
+      const int g0p = gi_ - g;
       if (lane < NP) {
         cursor[lane] = g0p * SL;
-        for (int k = 0; k < g; ++k) gentry[g0p + k] = (uint8_t)(e0p + k / kEntG);
-        for (int m = 0; m < e; ++m) ent_pair[e0p + m] = (int8_t)lane;
+        for (int k = 0; k < g; ++k) gtag[g0p + k] = (uint8_t)(2 * lane + ((k / kEntG) & 1));
       }
-      if (lane == NP - 1) {
-        ngroups_s = gi_;
-        nent_s = ei;
-        ent_pair[ei] = -1;  // the spare: groups past the lists
-      }
+      if (lane == NP - 1) ngroups_s = gi_;
     }
     __syncthreads();
     const int ngroups = __builtin_amdgcn_readfirstlane(ngroups_s);
-    const int nent = __builtin_amdgcn_readfirstlane(nent_s);
     // Whole blocks of kD groups and no branch in the unrolled loop below, so
     // the compiler keeps exactly kD loads in flight across iterations.
     // Padding entries, the groups past the lists and the issue-ahead slack
-    // read the zero block; the groups past the lists go to the spare entry.
+    // read the zero block; the groups past the lists go to the dummy pair.
     const int ng_pad = (ngroups + kD - 1) / kD * kD;
-    for (int i = lane; i < (ng_pad + kD) * SL; i += 64) list[i] = zero_off;
-    for (int i = ngroups + lane; i < ng_pad + kD; i += 64) gentry[i] = (uint8_t)nent;
-    for (int i = lane; i < (nent + 1) * ECELLS; i += 64) esum[i] = 0;
+    for (int i = lane; i < (ng_pad + 2 * kD) * SL; i += 64) list[i] = zero_off;
+    for (int i = ngroups + lane; i < ng_pad + kD; i += 64) gtag[i] = (uint8_t)(2 * NP);
     __syncthreads();
     // 1c. scatter box corners into their pair's list
 #pragma unroll
@@ -248,10 +245,9 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
     // 2. gather: group g = list entries g*SL .. g*SL + SL - 1 (slot s takes
     // g*SL + s); one 16-byte row piece per lane (buffer_load_dwordx4: the TA
     // coalesces a slot's row into its cache lines, a dword gather costs an
-    // access per lane). A lane's sums of the current entry are flushed into
-    // esum when the next group starts a new entry (CSM_PHASE_BRANCH_FLUSH=0:
-    // branch-free, every group issues the four LDS adds, into the lane's
-    // dummy cells when no entry ends there).
+    // access per lane). Where an entry ends (a uniform branch), the lanes add
+    // their int32 partials into the pair's int64 box sums (ds_add_u64; the
+    // cells past the box, columns >= C, are not kept).
     if (ngroups > 0) {
       v4i buf[kD];
 #pragma unroll
@@ -260,72 +256,59 @@ __global__ __launch_bounds__(64) void score_phase_kernel(LevelWork L, PhaseTable
         __builtin_amdgcn_sched_barrier(0);
       }
       int32_t part[4] = {0, 0, 0, 0};
-      int e_prev = __builtin_amdgcn_readfirstlane((int)gentry[0]);
-      const uint32_t esum_b = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int32_t*)esum;
-      // lane l's four dummy cells at dword 4l + (l >> 4): the 64 lanes of each
-      // of the four adds hit 64 distinct banks (4l alone is a 4-way conflict)
-      const uint32_t dummy_b =
-          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int32_t*)dummy + lane * 16 + (lane >> 4) * 4;
-      int gev = gentry[lane & (kD - 1)];
+      int t_prev = __builtin_amdgcn_readfirstlane((int)gtag[0]);
+      auto flush = [&](int tag) {  // uniform tag: pair tag >> 1
+        int64_t* dst = psum + (tag >> 1) * PC + lane_cell;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (cact && 4 * ch + t < C)
+            __hip_atomic_fetch_add(dst + t, (int64_t)part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          part[t] = 0;
+        }
+      };
+      int gev = gtag[lane & (kD - 1)];
+      // the list entries (this lane's slot) whose loads a block issues are read
+      // a block ahead, so no load waits on its address's LDS read
+      int lcur[kD];
+#pragma unroll
+      for (int j = 0; j < kD; ++j) lcur[j] = list[(kD + j) * SL + slot];
       for (int g0 = 0; g0 < ng_pad; g0 += kD) {
-        const int gev_next = gentry[g0 + kD + (lane & (kD - 1))];  // next block's entries
+        const int gev_next = gtag[g0 + kD + (lane & (kD - 1))];  // next block's tags
+        int lnext[kD];
+#pragma unroll
+        for (int j = 0; j < kD; ++j) lnext[j] = list[(g0 + 2 * kD + j) * SL + slot];
 #pragma unroll
         for (int j = 0; j < kD; ++j) {
-          const int g = g0 + j;
-          const int ej = __builtin_amdgcn_readlane(gev, j);
-          const bool nb = ej != e_prev;  // uniform
-#if CSM_PHASE_BRANCH_FLUSH
-          if (nb) {  // uniform: flush only where an entry ends
-            const uint32_t addr = cact ? esum_b + (uint32_t)(e_prev * ECELLS * 4 + lane_cell) : dummy_b;
-            __attribute__((address_space(3))) int32_t* dst = (__attribute__((address_space(3))) int32_t*)(uintptr_t)addr;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              __hip_atomic_fetch_add(dst + t, part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              part[t] = 0;  // inside the uniform branch: no per-group selects
-            }
-          }
-#else
-          // lanes past the slots always flush into their dummy cells
-          const uint32_t addr = (nb && cact) ? esum_b + (uint32_t)(e_prev * ECELLS * 4 + lane_cell) : dummy_b;
-          __attribute__((address_space(3))) int32_t* dst = (__attribute__((address_space(3))) int32_t*)(uintptr_t)addr;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) __hip_atomic_fetch_add(dst + t, part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-          for (int t = 0; t < 4; ++t) part[t] = nb ? 0 : part[t];
-#endif
-          e_prev = ej;
+          const int tj = __builtin_amdgcn_readlane(gev, j);
+          if (tj != t_prev) flush(t_prev);  // uniform: only where an entry ends
+          t_prev = tj;
           v4i v = buf[j];
-          asm volatile("" : "+v"(v));  // consume group g here, in order
+          asm volatile("" : "+v"(v));  // consume group g0 + j here, in order
           part[0] += v.x;
           part[1] += v.y;
           part[2] += v.z;
           part[3] += v.w;
-          buf[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, list[(g + kD) * SL + slot] + voff, 0, 0);
+          buf[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lcur[j] + voff, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
+#pragma unroll
+        for (int j = 0; j < kD; ++j) lcur[j] = lnext[j];
         gev = gev_next;
       }
-      if (cact) {
-        __attribute__((address_space(3))) int32_t* dst =
-            (__attribute__((address_space(3))) int32_t*)(uintptr_t)(esum_b + (uint32_t)(e_prev * ECELLS * 4 + lane_cell));
-#pragma unroll
-        for (int t = 0; t < 4; ++t) __hip_atomic_fetch_add(dst + t, part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
+      flush(t_prev);
     }
-    __syncthreads();
-    // 3a. this segment's entries into the candidates: candidate (j, k) takes
-    // box cell (ox[qy][k], ox[qx][j]) of every entry of pair (qx, qy)
-    for (int e = 0; e < nent; ++e) {
-      const int pr = __builtin_amdgcn_readfirstlane((int)ent_pair[e]);
-      const int qx = pr / NQ, qy = pr - (pr / NQ) * NQ;
+    __syncthreads();  // the next segment rewrites the lists
+  }
+  // 3. the pairs' box sums into the candidates: candidate (j, k) takes box
+  // cell (ox[qy][k], ox[qx][j]) of pair (qx, qy), once for the whole scan
+  for (int pr = 0; pr < NP; ++pr) {
+    const int qx = pr / NQ, qy = pr - (pr / NQ) * NQ;
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int u = (oxj[r] >> (4 * qx)) & 15;
-        const int v = (oyk[r] >> (4 * qy)) & 15;
-        sum[r] += esum[e * ECELLS + v * CW + u];
-      }
+    for (int r = 0; r < R; ++r) {
+      const int u = (oxj[r] >> (4 * qx)) & 15;
+      const int v = (oyk[r] >> (4 * qy)) & 15;
+      sum[r] += psum[pr * PC + v * C + u];
     }
-    __syncthreads();  // the next segment rewrites the lists and entries
   }
 
   // rejected beams, cell by cell with the reference's expressions
