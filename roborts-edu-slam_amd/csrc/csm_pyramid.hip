@@ -18,6 +18,8 @@
 // floors), so the bound is the raw score if >= 0 and 0.45 times it if < 0.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "csm_device.hpp"
 #include "csm_pyramid.hpp"
 
@@ -142,12 +144,17 @@ __device__ __forceinline__ void block_best(double v, int64_t f, uint64_t nd, Pyr
   }
 }
 
-// LPN lanes per node (blocks stride over the list; a node's lanes take every
-// LPN-th beam and meet by shuffles): the sum over the scan's beams of the
+// lpn lanes per node (blocks stride over the list; a node's lanes take every
+// lpn-th beam and meet by shuffles): the sum over the scan's beams of the
 // level-d value at the anchor candidate's cell (GetResponse :645-654 with the
 // pooled level in place of the grid); d = 0 is the candidate's exact,
-// penalised score. Integer sums: the split changes nothing.
-template <typename T, int LPN>
+// penalised score. Integer sums: the split changes nothing. The list length
+// is often only known on the device (n_dev) and far below the launch's
+// upper bound (a few hundred nodes at the lower levels of a single query),
+// so every block derives lpn from it: the most lanes per node, up to a wave,
+// the grid can give every node, each lane's gather chain a fraction of the
+// beams. Blocks past the list write an empty partial and leave.
+template <typename T>
 __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev, int d,
                                                         const ScanWork* __restrict__ scans,
                                                         const AngleEntry* __restrict__ angles,
@@ -158,17 +165,24 @@ __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev
                                                         PyrPartial* __restrict__ partials,
                                                         unsigned long long* __restrict__ scored) {
   extern __shared__ double2 beams[];
+  const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
+  const int64_t threads = (int64_t)gridDim.x * kPB;
+  int lpn = 1;  // a power of two, the same in every block
+  while (lpn < 64 && n * (2 * lpn) <= threads && 2 * lpn <= n_used) lpn <<= 1;
+  if (((int64_t)blockIdx.x * kPB) / lpn >= n) {  // no node for this block (uniform)
+    if (threadIdx.x == 0) partials[blockIdx.x] = PyrPartial{-1.0e300, INT64_MAX, kPyrNoNode};
+    return;
+  }
   for (int b = threadIdx.x; b < n_used; b += kPB) beams[b] = pts[(int64_t)b * step];
   __syncthreads();
-  const int64_t n = n_dev ? (int64_t)*n_dev : n_host;
   if (scored && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(scored, (unsigned long long)n);
   double bv = -1.0e300;
   int64_t bf = INT64_MAX;
   uint64_t bn = kPyrNoNode;
   const int sh = lev.shift, W = lev.width, H = lev.height, pitch = lev.pitch, lg = lev.lg, qc = lev.q;
   const int pm = (1 << lg) - 1;
-  const int sub = (int)(threadIdx.x % LPN);
-  for (int64_t i = ((int64_t)blockIdx.x * kPB + threadIdx.x) / LPN; i < n; i += (int64_t)gridDim.x * (kPB / LPN)) {
+  const int sub = (int)(threadIdx.x & (lpn - 1));
+  for (int64_t i = ((int64_t)blockIdx.x * kPB + threadIdx.x) / lpn; i < n; i += threads / lpn) {
     const uint64_t nd = nodes[i];
     int w, a, J, K;
     node_decode(nd, w, a, J, K);
@@ -195,17 +209,16 @@ __global__ __launch_bounds__(kPB) void pyr_bound_kernel(LevelWork L, PyrGrid lev
         return in ? c : 0;
       };
       int b = sub;
-      for (; b + 7 * LPN < n_used; b += 8 * LPN) {  // 8 gathers in flight per lane
+      for (; b + 7 * lpn < n_used; b += 8 * lpn) {  // 8 gathers in flight per lane
         int32_t c[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) c[u] = cell(b + u * LPN);
+        for (int u = 0; u < 8; ++u) c[u] = cell(b + u * lpn);
         // |c| < 2^26: eight fit an int32
         sum += (int64_t)(((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7])));
       }
-      for (; b < n_used; b += LPN) sum += cell(b);
+      for (; b < n_used; b += lpn) sum += cell(b);
     }
-#pragma unroll
-    for (int o = LPN / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);  // the node's lanes (all valid or none)
+    for (int o = lpn / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);  // the node's lanes (all valid or none)
     if (valid) {
       const ScanWork S = scans[w];
       const AngleEntry ae = angles[S.angle_off + a];
@@ -349,12 +362,16 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
                                                           const AngleEntry* __restrict__ angles,
                                                           const double2* __restrict__ pts, int32_t n_used,
                                                           int32_t step, int split, int32_t* __restrict__ sums,
+                                                          int32_t* __restrict__ slab,
                                                           PyrPartial* __restrict__ partials) {
-  constexpr int GB = NL == 1 ? 8 : 4;  // beams whose loads are issued together
+#ifndef CSM_TOPBOX_GB
+#define CSM_TOPBOX_GB 4
+#endif
+  constexpr int GB = NL == 1 ? 8 : CSM_TOPBOX_GB;  // beams whose loads are issued together
   __shared__ int32_t odd_sum[32][8 * 5 + 8];
   // split > 1 (few windows): `split` waves per (window, angle), each over a
-  // contiguous range of the beams, adding their sums into `sums` (zeroed by
-  // the host); pyr_topbox_final_kernel then bounds the nodes
+  // contiguous range of the beams, storing its sums in its own slab row;
+  // pyr_topbox_final_kernel then adds the rows and bounds the nodes
   const int bid0 = dev::xcd_remap(blockIdx.x, gridDim.x);
   const int bid = bid0 / split, part = bid0 - (bid0 / split) * split;
   const int w = bid / L.n_angles;
@@ -492,13 +509,15 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
   int64_t bf = INT64_MAX;
   uint64_t bn = kPyrNoNode;
   const int64_t wbase = ((int64_t)w * L.n_angles + a) * nj;
-  if (split > 1) {  // partial sums of this beam range
+  if (split > 1) {  // partial sums of this beam range, plain stores (device-scope
+                    // atomics from every split wave cost more than the beams)
+    int32_t* row = slab + ((int64_t)bid * split + part) * nj * nj;
 #pragma unroll
     for (int s = 0; s < NL; ++s)
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int J = 8 * cs[s] + t, K = Ks[s];
-        if (act[s] && J < nj) atomicAdd(&sums[(wbase + K) * nj + J], acc[s][t]);
+        if (act[s] && J < nj) row[K * nj + J] = acc[s][t];
       }
     return;
   }
@@ -527,20 +546,25 @@ __global__ __launch_bounds__(64) void pyr_topbox_kernel(LevelWork L, PyrGrid tb,
 // summed integers and its best (one wave per (window, angle), as the
 // unsplit kernel writes them).
 __global__ __launch_bounds__(64) void pyr_topbox_final_kernel(LevelWork L, int d, int32_t nj, int qs, int32_t n_used,
-                                                              const ScanWork* __restrict__ scans,
-                                                              const int32_t* __restrict__ sums,
+                                                              const ScanWork* __restrict__ scans, int split,
+                                                              const int32_t* __restrict__ slab,
+                                                              int32_t* __restrict__ sums,
                                                               PyrPartial* __restrict__ partials) {
   const int bid = blockIdx.x;
   const int w = bid / L.n_angles;
   const int a = bid - w * L.n_angles;
   const ScanWork S = scans[w];
   const int64_t wbase = ((int64_t)w * L.n_angles + a) * nj;
+  const int32_t* rows = slab + (int64_t)bid * split * nj * nj;
   double bv = -1.0e300;
   int64_t bf = INT64_MAX;
   uint64_t bn = kPyrNoNode;
   for (int i = threadIdx.x; i < nj * nj; i += 64) {
     const int K = i / nj, J = i - K * nj;
-    const double v = level_bound(L, S, sums[wbase * nj + i], qs, n_used);
+    int32_t sum = 0;  // |sum| <= 4096 beams * 2^15: the rows add up in int32
+    for (int p = 0; p < split; ++p) sum += rows[(int64_t)p * nj * nj + i];
+    sums[wbase * nj + i] = sum;
+    const double v = level_bound(L, S, sum, qs, n_used);
     const int64_t gflat = (int64_t)w * L.n_cand + ((int64_t)a * L.n_space + (J << d)) * L.n_space + (K << d);
     if (better(v, gflat, bv, bf)) {
       bv = v;
@@ -653,10 +677,8 @@ __device__ __forceinline__ void append_children(int w, int a, int J, int K, uint
 // sum, so with every window sharing one scan (divisor, beam count: the host
 // checks) bound > score <=> sum >= thr[0] and bound >= score <=> sum >=
 // thr[1] (INT32_MAX + 1: no such sum).
-__global__ void pyr_threshold_kernel(LevelWork L, const ScanWork* __restrict__ scans, int qs, int32_t n_used,
-                                     const BestPartial* __restrict__ inc, int64_t* __restrict__ thr) {
-  const BestPartial cur = *inc;
-  const ScanWork S = scans[0];
+__device__ void incumbent_thresholds(const LevelWork& L, const ScanWork& S, int qs, int32_t n_used,
+                                     const BestPartial& cur, int64_t* thr) {
   for (int strict = 1; strict >= 0; --strict) {
     int64_t lo = INT32_MIN, hi = (int64_t)INT32_MAX + 1;
     while (lo < hi) {
@@ -671,16 +693,20 @@ __global__ void pyr_threshold_kernel(LevelWork L, const ScanWork* __restrict__ s
 
 // The children of top nodes [first, first + n) of pyr_topbox_kernel's
 // implicit list ((window, angle, K, J), J fastest), from their integer sums
-// against pyr_threshold_kernel's thresholds: the same test as
-// better(bound, lowest, incumbent) without a division per node; only the
-// few nodes at or above the incumbent decode their index.
-__global__ __launch_bounds__(256) void pyr_expand_top_kernel(LevelWork L, int d, int32_t nj,
-                                                             const int64_t* __restrict__ thr,
+// against the incumbent's thresholds (incumbent_thresholds, each block's
+// thread 0): the same test as better(bound, lowest, incumbent) without a
+// division per node; only the few nodes at or above the incumbent decode
+// their index.
+__global__ __launch_bounds__(256) void pyr_expand_top_kernel(LevelWork L, int d, int32_t nj, int qs, int32_t n_used,
+                                                             const ScanWork* __restrict__ scans,
                                                              const int32_t* __restrict__ sums, int64_t first,
                                                              int64_t n, const BestPartial* __restrict__ inc,
                                                              uint64_t* __restrict__ out,
                                                              unsigned long long* __restrict__ count, int64_t cap) {
+  __shared__ int64_t thr[2];
   const BestPartial cur = *inc;
+  if (threadIdx.x == 0) incumbent_thresholds(L, scans[0], qs, n_used, cur, thr);
+  __syncthreads();
   const int64_t t_gt = thr[0], t_ge = thr[1];
   const int h = d - 1;
   const int64_t per_angle = (int64_t)nj * nj;
@@ -744,6 +770,14 @@ __global__ __launch_bounds__(256) void pyr_expand_kernel(LevelWork L, int d, con
   }
 }
 
+// A search's device state at its start: the incumbent at "none", the node
+// counters zero (one launch in place of a copy and a memset).
+__global__ __launch_bounds__(256) void pyr_init_kernel(BestPartial* __restrict__ inc,
+                                                       unsigned long long* __restrict__ zero, int n) {
+  if (threadIdx.x == 0) *inc = BestPartial{-1.7976931348623157e308, INT64_MAX};  // {-DBL_MAX, INT64_MAX}
+  for (int i = threadIdx.x; i < n; i += blockDim.x) zero[i] = 0;
+}
+
 int blocks_for(int64_t n, int per) {
   int64_t b = (n + per - 1) / per;
   if (b > 65536) b = 65536;
@@ -779,34 +813,27 @@ int pyr_blocks(int64_t upper) {
   return (int)(b < 1 ? 1 : b);
 }
 
-int pyr_bound_lanes(int32_t n_used) { return n_used >= 1024 ? 8 : n_used >= 512 ? 4 : 1; }
-
-int pyr_bound_blocks(int64_t upper, int32_t n_used) { return pyr_blocks(upper * pyr_bound_lanes(n_used)); }
+// launch size: room for up to a wave per node of the upper bound (the kernel
+// picks the lanes per node from the actual count)
+int pyr_bound_blocks(int64_t upper, int32_t n_used) {
+  (void)n_used;
+  return pyr_blocks(upper >= INT64_MAX / 128 ? upper : upper * 64);
+}
 
 hipError_t launch_pyr_bound(const LevelWork& L, const PyrGrid& lev, int d, const ScanWork* scans,
                             const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
                             const uint64_t* nodes, int64_t n, const unsigned long long* n_dev, int64_t upper,
                             double* vals, PyrPartial* partials, unsigned long long* scored, hipStream_t stream) {
   if (upper <= 0) return hipSuccess;
-  // long scans: several lanes per node (every LPN-th beam each), so a short
-  // node list still fills the chip and each lane's gather chain is shorter
-  const int lpn = pyr_bound_lanes(n_used);
   const unsigned blocks = (unsigned)pyr_bound_blocks(upper, n_used);
   const size_t lds = (size_t)n_used * sizeof(double2);
   const double2* p = reinterpret_cast<const double2*>(pts);
-#define CSM_BOUND(T, LPN)                                                                                     \
-  hipLaunchKernelGGL((pyr_bound_kernel<T, LPN>), dim3(blocks), dim3(kPB), lds, stream, L, lev, d, scans, angles, \
-                     p, n_used, step, nodes, n, n_dev, vals, partials, scored)
-  if (lev.qs == 0) {
-    if (lpn == 8) CSM_BOUND(int32_t, 8);
-    else if (lpn == 4) CSM_BOUND(int32_t, 4);
-    else CSM_BOUND(int32_t, 1);
-  } else {
-    if (lpn == 8) CSM_BOUND(int16_t, 8);
-    else if (lpn == 4) CSM_BOUND(int16_t, 4);
-    else CSM_BOUND(int16_t, 1);
-  }
-#undef CSM_BOUND
+  if (lev.qs == 0)
+    hipLaunchKernelGGL(pyr_bound_kernel<int32_t>, dim3(blocks), dim3(kPB), lds, stream, L, lev, d, scans, angles, p,
+                       n_used, step, nodes, n, n_dev, vals, partials, scored);
+  else
+    hipLaunchKernelGGL(pyr_bound_kernel<int16_t>, dim3(blocks), dim3(kPB), lds, stream, L, lev, d, scans, angles, p,
+                       n_used, step, nodes, n, n_dev, vals, partials, scored);
   return hipGetLastError();
 }
 
@@ -851,9 +878,21 @@ hipError_t launch_pyr_widen(const PyrGrid& src, const PyrGrid& dst, int32_t n_gr
   return hipGetLastError();
 }
 
+// fewest beams a split top-level wave takes (CSM_TOPBOX_MIN_BEAMS; each
+// split wave adds its nj^2 node sums with global atomics)
+int topbox_min_beams() {
+  static const int v = [] {
+    const char* e = std::getenv("CSM_TOPBOX_MIN_BEAMS");
+    const int x = e ? std::atoi(e) : 32;
+    return x < 1 ? 1 : x;
+  }();
+  return v;
+}
+
 hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32_t nj, const ScanWork* scans,
                              const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
-                             int32_t* sums, PyrPartial* partials, hipStream_t stream, int* split_out) {
+                             int32_t* sums, int32_t* slab, PyrPartial* partials, hipStream_t stream,
+                             int* split_out) {
   const int np = pyr_topbox_pieces(nj);
   const int64_t blocks = (int64_t)L.n_scans * L.n_angles;
   if (np == 0 || blocks <= 0 || blocks > INT32_MAX || n_used < 1 || n_used > 4096 || tb.qs == 0 ||
@@ -864,18 +903,16 @@ hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32
   // few (window, angle) pairs: split each one's beams over up to 16 waves (at
   // least 128 beams each) so the launch fills the chip
   int split = 1;
-  while (split < 16 && blocks * split < 4096 && n_used / (2 * split) >= 128) split *= 2;
+  while (split < kPyrTopMaxSplit && blocks * split < 4096 && n_used / (2 * split) >= topbox_min_beams()) split *= 2;
+  if (split > 1 && !slab) split = 1;
   if (split_out) *split_out = split;
   hipError_t e;
-  if (split > 1 &&
-      (e = hipMemsetAsync(sums, 0, (size_t)blocks * (size_t)nj * (size_t)nj * sizeof(int32_t), stream)) != hipSuccess)
-    return e;
   const unsigned grid = (unsigned)(blocks * split);
   bool launched = false;
 #define CSM_TOPBOX(NP, NL)                                                                                         \
   if (!launched && np == NP && nl == NL) {                                                                       \
     hipLaunchKernelGGL((pyr_topbox_kernel<NP, NL>), dim3(grid), dim3(64), 0, stream, L, tb, d, nj, scans, angles, \
-                       p, n_used, step, split, sums, partials);                                                   \
+                       p, n_used, step, split, sums, slab, partials);                                             \
     launched = true;                                                                                              \
   }
   CSM_TOPBOX(1, 1)
@@ -889,7 +926,7 @@ hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (split > 1)
     hipLaunchKernelGGL(pyr_topbox_final_kernel, dim3((unsigned)blocks), dim3(64), 0, stream, L, d, nj, tb.qs, n_used,
-                       scans, sums, partials);
+                       scans, split, slab, sums, partials);
   return hipGetLastError();
 }
 
@@ -898,11 +935,16 @@ hipError_t launch_pyr_expand_top(const LevelWork& L, int d, int32_t nj, int qs, 
                                  int64_t* thr, uint64_t* out, unsigned long long* count, int64_t cap,
                                  hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(pyr_threshold_kernel, dim3(1), dim3(1), 0, stream, L, scans, qs, n_used, inc, thr);
+  (void)thr;
   // a block per 256 nodes up to 65536 blocks: the loop is one dependent load
   // per iteration, so few iterations per thread
-  hipLaunchKernelGGL(pyr_expand_top_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, stream, L, d, nj, thr, sums,
-                     first, n, inc, out, count, cap);
+  hipLaunchKernelGGL(pyr_expand_top_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, stream, L, d, nj, qs, n_used,
+                     scans, sums, first, n, inc, out, count, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_pyr_init(BestPartial* inc, unsigned long long* zero, int n, hipStream_t stream) {
+  hipLaunchKernelGGL(pyr_init_kernel, dim3(1), dim3(256), 0, stream, inc, zero, n);
   return hipGetLastError();
 }
 

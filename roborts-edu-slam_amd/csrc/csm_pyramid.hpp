@@ -72,10 +72,12 @@ hipError_t launch_pyr_top(const LevelWork& L, int32_t nj, int64_t first, int64_t
 // Node counts: n_dev (device, may be null) overrides n; `upper` (>= the
 // count) sizes the grid, whose blocks stride over the list.
 int pyr_blocks(int64_t upper);
-// Lanes per node of the bound kernel (long scans split their beams) and its
-// block count: the number of partials a bound launch writes (<= pyr_blocks's cap).
-int pyr_bound_lanes(int32_t n_used);
+// Block count of the bound kernel: the number of partials a bound launch
+// writes (<= pyr_blocks's cap); the kernel spreads each node over up to a
+// wave of lanes when the list is short.
 int pyr_bound_blocks(int64_t upper, int32_t n_used);
+// A search's start: *inc = {-DBL_MAX, INT64_MAX}, zero[0, n) = 0.
+hipError_t launch_pyr_init(BestPartial* inc, unsigned long long* zero, int n, hipStream_t stream);
 // Bounds (d >= 1) or exact scores (d = 0) of the nodes; one best per block
 // into partials (pyr_bound_blocks(upper, n_used) entries); *scored (nullable) += the count. The windows share one scan: its
 // n_used beams (stride step from pts) are staged in LDS.
@@ -101,10 +103,13 @@ hipError_t launch_pyr_widen(const PyrGrid& src, const PyrGrid& dst, int32_t n_gr
 // Writes each node's integer sum (level units) at its index of the implicit
 // list ((window, angle, K, J), J fastest).
 // With few (window, angle) pairs each one's beams are split over several
-// waves (*split_out, nullable: how many), their sums added, then bounded.
+// waves (*split_out, nullable: how many) whose partial sums go to `slab`
+// (kPyrTopMaxSplit ints per top node), then are added and bounded.
+constexpr int kPyrTopMaxSplit = 16;
 hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32_t nj, const ScanWork* scans,
                              const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
-                             int32_t* sums, PyrPartial* partials, hipStream_t stream, int* split_out = nullptr);
+                             int32_t* sums, int32_t* slab, PyrPartial* partials, hipStream_t stream,
+                             int* split_out = nullptr);
 // launch_pyr_expand for nodes [first, first + n) of that implicit list; every
 // window must share one scan (divisor, beam count). thr: 2 int64 of device
 // scratch (the incumbent as integer sums).

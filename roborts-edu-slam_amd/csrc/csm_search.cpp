@@ -66,17 +66,41 @@ struct PyramidSearch::Impl {
   // per-depth node lists, their values and counts (counts[d]: nodes[d]'s
   // length as the expand that filled it left it)
   Buf nodes[kPyrMaxDepth + 1], vals[kPyrMaxDepth + 1];
-  Buf partials, inc, probe_slot, probe_nodes, probe_vals, counts, scored;
+  Buf partials, probe_slot, probe_nodes, probe_vals;
+  // device state of a search, set by one init launch: the incumbent, the
+  // nodes scored per depth, and a pool of list counters (each expand appends
+  // to a fresh, already zero counter: no memset per level)
+  static constexpr int kCountPool = 64;
+  Buf state;  // BestPartial inc | scored[kPyrMaxDepth + 1] | pool[kCountPool]
+  int cslot[kPyrMaxDepth + 1] = {};  // pool slot of list d's count (slot 0: never written, zero)
+  int next_slot = 1;
+  BestPartial* inc_dev() const { return (BestPartial*)state.p; }
+  unsigned long long* scored_dev() const { return (unsigned long long*)((char*)state.p + sizeof(BestPartial)); }
+  unsigned long long* pool_dev() const { return scored_dev() + kPyrMaxDepth + 1; }
   // the beam-box top level: integer sums of the implicit node list
-  Buf top_sums, top_thr;
+  Buf top_sums, top_thr, top_slab;
   int top_implicit = -1;  // its depth while a search runs (-1: the top is a node list)
   int32_t top_nj = 0;
-  // pinned: counts read back, then scored, then the incumbent's initial value
-  // and the answer (pageable copies wait for the device: ~20-70 us each)
+  // pinned: two counts read back, then the state's incumbent and scored
+  // counts (pageable copies wait for the device: ~20-70 us each)
   unsigned long long* h_counts = nullptr;
-  BestPartial* h_inc() const { return (BestPartial*)(h_counts + 2 * (kPyrMaxDepth + 1)); }
+  BestPartial* h_inc() const { return (BestPartial*)(h_counts + 2); }
+  unsigned long long* h_scored() const { return (unsigned long long*)(h_inc() + 1); }
   hipEvent_t ev_top[2] = {nullptr, nullptr};  // PyrInputs::timed
-  int64_t cap = (int64_t)1 << 24;
+  int64_t cap = (int64_t)1 << 25;
+  // per level: the capacity of its node list, min(cap, the nodes the level
+  // has at all), and that count; a level whose children always fit its list
+  // is descended without reading a count back (no host round trip)
+  int64_t capd[kPyrMaxDepth + 1] = {};
+  int64_t possible[kPyrMaxDepth + 1] = {};
+  void set_caps(const LevelWork& L, int D) {
+    for (int d = 0; d <= D; ++d) {
+      const double nj = (double)(((int64_t)L.n_space + (1 << d) - 1) >> d);
+      const double all = (double)L.n_scans * (double)L.n_angles * nj * nj;
+      possible[d] = all >= 9.0e18 ? INT64_MAX / 8 : (int64_t)all;
+      capd[d] = std::max<int64_t>(4, std::min(cap, possible[d]));
+    }
+  }
   int probe_min = 4096;
   static constexpr int kRoots = 8;  // probe roots per probe (best partials of distinct blocks)
   PyrInputs in{};
@@ -157,38 +181,38 @@ struct PyramidSearch::Impl {
   hipError_t ensure_lists(int D) {
     hipError_t e;
     for (int d = 0; d <= D; ++d) {
-      if ((e = nodes[d].ensure((size_t)cap * sizeof(uint64_t))) != hipSuccess) return e;
-      if ((e = vals[d].ensure((size_t)cap * sizeof(double))) != hipSuccess) return e;
+      if ((e = nodes[d].ensure((size_t)capd[d] * sizeof(uint64_t))) != hipSuccess) return e;
+      if ((e = vals[d].ensure((size_t)capd[d] * sizeof(double))) != hipSuccess) return e;
     }
     const int64_t np = ((int64_t)1 << (2 * D)) * kRoots;
     if ((e = partials.ensure((size_t)pyr_blocks(INT64_MAX / 2) * sizeof(PyrPartial))) != hipSuccess) return e;
-    if ((e = inc.ensure(sizeof(BestPartial))) != hipSuccess) return e;
+    if ((e = state.ensure(sizeof(BestPartial) + (kPyrMaxDepth + 1 + kCountPool) * sizeof(unsigned long long))) !=
+        hipSuccess)
+      return e;
     if ((e = probe_slot.ensure(kRoots * sizeof(uint64_t))) != hipSuccess) return e;
     if ((e = probe_nodes.ensure((size_t)np * sizeof(uint64_t))) != hipSuccess) return e;
     if ((e = probe_vals.ensure((size_t)np * sizeof(double))) != hipSuccess) return e;
-    if ((e = counts.ensure((kPyrMaxDepth + 1) * sizeof(unsigned long long))) != hipSuccess) return e;
-    if ((e = scored.ensure((kPyrMaxDepth + 1) * sizeof(unsigned long long))) != hipSuccess) return e;
     if (!h_counts && (e = hipHostMalloc((void**)&h_counts,
-                                        2 * (kPyrMaxDepth + 1) * sizeof(unsigned long long) + 2 * sizeof(BestPartial),
+                                        (2 + kPyrMaxDepth + 1) * sizeof(unsigned long long) + sizeof(BestPartial),
                                         hipHostMallocDefault)) != hipSuccess)
       return e;
     return hipSuccess;
   }
 
-  unsigned long long* count_dev(int d) { return (unsigned long long*)counts.p + d; }
+  unsigned long long* count_dev(int d) { return pool_dev() + cslot[d]; }
 
   // nodes (n on the host, or *n_dev), at most `upper` of them
   hipError_t bound(int d, const uint64_t* list, double* out, int64_t n, const unsigned long long* n_dev,
                    int64_t upper) {
     return launch_pyr_bound(in.L, lev[d], d, in.scans, in.angles, in.pts, in.n_used, in.step, list, n, n_dev, upper,
-                            out, (PyrPartial*)partials.p, (unsigned long long*)scored.p + d, in.stream);
+                            out, (PyrPartial*)partials.p, scored_dev() + d, in.stream);
   }
 
   // Score the leaves of the best nodes of n_partials block partials exactly
   // (the incumbent only ever rises).
   hipError_t probe(int d, int64_t n_partials) {
     hipError_t e;
-    if ((e = launch_pyr_final((const PyrPartial*)partials.p, n_partials, false, kRoots, (BestPartial*)inc.p,
+    if ((e = launch_pyr_final((const PyrPartial*)partials.p, n_partials, false, kRoots, inc_dev(),
                               (uint64_t*)probe_slot.p, in.stream)) != hipSuccess)
       return e;
     if ((e = launch_pyr_probe(d, kRoots, (const uint64_t*)probe_slot.p, (uint64_t*)probe_nodes.p, in.stream)) !=
@@ -199,7 +223,7 @@ struct PyramidSearch::Impl {
                               (const uint64_t*)probe_nodes.p, np, nullptr, np, (double*)probe_vals.p,
                               (PyrPartial*)partials.p, nullptr, in.stream)) != hipSuccess)
       return e;
-    if ((e = launch_pyr_final((const PyrPartial*)partials.p, pyr_bound_blocks(np, in.n_used), true, 0, (BestPartial*)inc.p, nullptr,
+    if ((e = launch_pyr_final((const PyrPartial*)partials.p, pyr_bound_blocks(np, in.n_used), true, 0, inc_dev(), nullptr,
                               in.stream)) != hipSuccess)
       return e;
     st->probe_leaves += np;
@@ -209,20 +233,28 @@ struct PyramidSearch::Impl {
   // Children of nodes[d][s, s + k) (k on the host, or *n_dev) into nodes[d-1].
   hipError_t expand(int d, int64_t s, int64_t k, const unsigned long long* n_dev, int64_t upper) {
     hipError_t e;
-    if ((e = hipMemsetAsync(count_dev(d - 1), 0, sizeof(unsigned long long), in.stream)) != hipSuccess) return e;
+    if (next_slot < kCountPool) {
+      cslot[d - 1] = next_slot++;  // zeroed by the search's init launch
+    } else {  // pool used up (many slices): the last slot, cleared each time
+      cslot[d - 1] = kCountPool - 1;
+      if ((e = hipMemsetAsync(count_dev(d - 1), 0, sizeof(unsigned long long), in.stream)) != hipSuccess) return e;
+    }
     st->slices += 1;
     if (d == top_implicit)
       return launch_pyr_expand_top(in.L, d, top_nj, boxg.qs, in.n_used, in.scans, (const int32_t*)top_sums.p, s, k,
-                                   (const BestPartial*)inc.p, (int64_t*)top_thr.p, (uint64_t*)nodes[d - 1].p,
-                                   count_dev(d - 1), cap, in.stream);
+                                   inc_dev(), (int64_t*)top_thr.p, (uint64_t*)nodes[d - 1].p,
+                                   count_dev(d - 1), capd[d - 1], in.stream);
     return launch_pyr_expand(in.L, d, (const uint64_t*)nodes[d].p + s, (const double*)vals[d].p + s, k, n_dev, upper,
-                             (const BestPartial*)inc.p, (uint64_t*)nodes[d - 1].p, count_dev(d - 1), cap, in.stream);
+                             inc_dev(), (uint64_t*)nodes[d - 1].p, count_dev(d - 1), capd[d - 1],
+                             in.stream);
   }
 
   // counts[d - 1] and counts[d] to the host
   hipError_t read_counts(int d) {
     hipError_t e;
-    if ((e = hipMemcpyAsync(h_counts, count_dev(d - 1), 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+    if ((e = hipMemcpyAsync(h_counts, count_dev(d - 1), sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                            in.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(h_counts + 1, count_dev(d), sizeof(unsigned long long), hipMemcpyDeviceToHost,
                             in.stream)) != hipSuccess)
       return e;
     st->syncs += 1;
@@ -244,21 +276,22 @@ struct PyramidSearch::Impl {
     hipError_t e;
     const unsigned long long* nd = n >= 0 ? nullptr : count_dev(d);
     if (d == 0)
-      return launch_pyr_final((const PyrPartial*)partials.p, n_partials, true, 0, (BestPartial*)inc.p, nullptr,
+      return launch_pyr_final((const PyrPartial*)partials.p, n_partials, true, 0, inc_dev(), nullptr,
                               in.stream);
     if ((top || n >= probe_min) && (e = probe(d, n_partials)) != hipSuccess) return e;
-    if (4 * upper <= cap) {
+    const int64_t child_upper = std::min(4 * upper, possible[d - 1]);
+    if (child_upper <= capd[d - 1]) {
       if ((e = expand(d, 0, n, nd, upper)) != hipSuccess) return e;
-      return level_pass(d - 1, -1, 4 * upper, false);
+      return level_pass(d - 1, -1, child_upper, false);
     }
     // optimistic: expand everything, then look at the count
     if ((e = expand(d, 0, n, nd, upper)) != hipSuccess) return e;
     if ((e = read_counts(d)) != hipSuccess) return e;
     const int64_t m = (int64_t)h_counts[0];
     if (n < 0) n = (int64_t)h_counts[1];
-    if (m <= cap) return m > 0 ? level_pass(d - 1, m, m, false) : hipSuccess;
-    // overflow (children dropped): slices of cap / 4 parents, each descended
-    const int64_t slice = std::max<int64_t>(1, cap / 4);
+    if (m <= capd[d - 1]) return m > 0 ? level_pass(d - 1, m, m, false) : hipSuccess;
+    // overflow (children dropped): slices of capacity / 4 parents, each descended
+    const int64_t slice = std::max<int64_t>(1, capd[d - 1] / 4);
     for (int64_t s = 0; s < n; s += slice) {
       const int64_t k = std::min(slice, n - s);
       if ((e = expand(d, s, k, nullptr, k)) != hipSuccess) return e;
@@ -277,7 +310,7 @@ void PyramidSearch::release() {
 }
 
 void PyramidSearch::configure(int64_t node_capacity, int probe_min_nodes) {
-  p_->cap = node_capacity > 0 ? std::max<int64_t>(node_capacity, 4) : ((int64_t)1 << 24);
+  p_->cap = node_capacity > 0 ? std::max<int64_t>(node_capacity, 4) : ((int64_t)1 << 25);
   p_->probe_min = probe_min_nodes > 0 ? probe_min_nodes : 4096;
 }
 
@@ -302,12 +335,12 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
   if ((e = I.build(x)) != hipSuccess) return fail(e, "pyramid levels");
   const int64_t nj = ((int64_t)x.L.n_space + (1 << x.depth) - 1) >> x.depth;
   const int64_t n_top = (int64_t)x.L.n_scans * x.L.n_angles * nj * nj;
+  I.set_caps(x.L, x.depth);
   if ((e = I.ensure_lists(x.depth)) != hipSuccess) return fail(e, "pyramid node lists");
-  I.h_inc()[0] = BestPartial{-DBL_MAX, INT64_MAX};  // the last search synchronised: the slot is free
-  if ((e = hipMemcpyAsync(I.inc.p, I.h_inc(), sizeof(BestPartial), hipMemcpyHostToDevice, x.stream)) != hipSuccess)
-    return fail(e, "incumbent");
-  if ((e = hipMemsetAsync(I.scored.p, 0, (kPyrMaxDepth + 1) * sizeof(unsigned long long), x.stream)) != hipSuccess)
-    return fail(e, "node counters");
+  for (int d = 0; d <= kPyrMaxDepth; ++d) I.cslot[d] = 0;
+  I.next_slot = 1;
+  if ((e = launch_pyr_init(I.inc_dev(), I.scored_dev(), kPyrMaxDepth + 1 + Impl::kCountPool, x.stream)) != hipSuccess)
+    return fail(e, "pyr_init_kernel");
   int32_t ktiles, kt, col_blocks;
   const int top_blocks = pyr_top_blocks(x.L, (int32_t)nj, &ktiles, &kt, &col_blocks);
   const int D = x.depth;
@@ -319,15 +352,19 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
   const bool use_box = D > 0 && x.top_mode == 0 && x.box_ok && x.one_scan && npc > 0 && box_blocks <= INT32_MAX &&
                        n_top <= ((int64_t)1 << 28) && x.n_used >= 1 && x.n_used <= 4096;
   if (use_box && (e = I.build_box(x, D, (int32_t)nj, npc)) == hipSuccess) {
+    // the split waves' partial sums: only launches of few (window, angle)s split
+    const size_t slab_ints = box_blocks < 4096 ? (size_t)n_top * kPyrTopMaxSplit : 0;  // launch_pyr_topbox's rule
     if ((e = I.top_sums.ensure((size_t)n_top * sizeof(int32_t))) != hipSuccess ||
-        (e = I.top_thr.ensure(2 * sizeof(int64_t))) != hipSuccess)
+        (e = I.top_thr.ensure(2 * sizeof(int64_t))) != hipSuccess ||
+        (slab_ints && (e = I.top_slab.ensure(slab_ints * sizeof(int32_t))) != hipSuccess))
       return fail(e, "pyramid top level");
     if ((e = I.partials.ensure((size_t)std::max<int64_t>(box_blocks, pyr_blocks(INT64_MAX / 2)) *
                                sizeof(PyrPartial))) != hipSuccess)
       return fail(e, "pyramid partials");
     if (x.timed && (e = I.mark_top(0, x.stream)) != hipSuccess) return fail(e, "hipEventRecord");
     if ((e = launch_pyr_topbox(x.L, I.boxg, D, (int32_t)nj, x.scans, x.angles, x.pts, x.n_used, x.step,
-                               (int32_t*)I.top_sums.p, (PyrPartial*)I.partials.p, x.stream)) != hipSuccess)
+                               (int32_t*)I.top_sums.p, slab_ints ? (int32_t*)I.top_slab.p : nullptr,
+                               (PyrPartial*)I.partials.p, x.stream)) != hipSuccess)
       return fail(e, "pyr_topbox_kernel");
     if (x.timed) {
       if ((e = I.mark_top(1, x.stream)) != hipSuccess) return fail(e, "hipEventRecord");
@@ -359,21 +396,20 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
     top_scored = n_top;
     if ((e = I.descend(D, n_top, n_top, true, top_blocks)) != hipSuccess) return fail(e, "pyramid level pass");
   } else {
-    for (int64_t first = 0; first < n_top; first += I.cap) {
-      const int64_t m = std::min(I.cap, n_top - first);
+    for (int64_t first = 0; first < n_top; first += I.capd[D]) {
+      const int64_t m = std::min(I.capd[D], n_top - first);
       if ((e = launch_pyr_top(x.L, (int32_t)nj, first, m, (uint64_t*)I.nodes[D].p, x.stream)) != hipSuccess)
         return fail(e, "pyr_top_kernel");
       if ((e = I.level_pass(D, m, m, true)) != hipSuccess) return fail(e, "pyramid level pass");
     }
   }
-  if ((e = hipMemcpyAsync(I.h_inc() + 1, I.inc.p, sizeof(BestPartial), hipMemcpyDeviceToHost, x.stream)) != hipSuccess)
-    return fail(e, "incumbent copy");
-  unsigned long long* h_scored = I.h_counts + kPyrMaxDepth + 1;
-  if ((e = hipMemcpyAsync(h_scored, I.scored.p, (kPyrMaxDepth + 1) * sizeof(unsigned long long),
+  // the incumbent and the scored counts, one copy
+  if ((e = hipMemcpyAsync(I.h_inc(), I.state.p, sizeof(BestPartial) + (kPyrMaxDepth + 1) * sizeof(unsigned long long),
                           hipMemcpyDeviceToHost, x.stream)) != hipSuccess)
-    return fail(e, "node counters copy");
+    return fail(e, "incumbent copy");
   if ((e = hipStreamSynchronize(x.stream)) != hipSuccess) return fail(e, "pyramid search");
-  *best = I.h_inc()[1];
+  unsigned long long* h_scored = I.h_scored();
+  *best = I.h_inc()[0];
   for (int d = 0; d <= kPyrMaxDepth; ++d) I.st->nodes[d] = (int64_t)h_scored[d];
   if (x.timed && I.st->top_name[0]) {
     float ms = 0.f;
