@@ -677,8 +677,8 @@ __device__ __forceinline__ void append_children(int w, int a, int J, int K, uint
 // sum, so with every window sharing one scan (divisor, beam count: the host
 // checks) bound > score <=> sum >= thr[0] and bound >= score <=> sum >=
 // thr[1] (INT32_MAX + 1: no such sum).
-__device__ void incumbent_thresholds(const LevelWork& L, const ScanWork& S, int qs, int32_t n_used,
-                                     const BestPartial& cur, int64_t* thr) {
+__device__ __forceinline__ void incumbent_thresholds(const LevelWork& L, const ScanWork& S, int qs, int32_t n_used,
+                                                     const BestPartial& cur, int64_t* thr) {
   for (int strict = 1; strict >= 0; --strict) {
     int64_t lo = INT32_MIN, hi = (int64_t)INT32_MAX + 1;
     while (lo < hi) {
@@ -691,6 +691,13 @@ __device__ void incumbent_thresholds(const LevelWork& L, const ScanWork& S, int 
   }
 }
 
+// The same thresholds once for a launch of many blocks (config 3's top level:
+// tens of thousands of blocks would each repeat the search).
+__global__ void pyr_threshold_kernel(LevelWork L, const ScanWork* __restrict__ scans, int qs, int32_t n_used,
+                                     const BestPartial* __restrict__ inc, int64_t* __restrict__ thr) {
+  incumbent_thresholds(L, scans[0], qs, n_used, *inc, thr);
+}
+
 // The children of top nodes [first, first + n) of pyr_topbox_kernel's
 // implicit list ((window, angle, K, J), J fastest), from their integer sums
 // against the incumbent's thresholds (incumbent_thresholds, each block's
@@ -699,13 +706,21 @@ __device__ void incumbent_thresholds(const LevelWork& L, const ScanWork& S, int 
 // their index.
 __global__ __launch_bounds__(256) void pyr_expand_top_kernel(LevelWork L, int d, int32_t nj, int qs, int32_t n_used,
                                                              const ScanWork* __restrict__ scans,
+                                                             const int64_t* __restrict__ thr_dev,
                                                              const int32_t* __restrict__ sums, int64_t first,
                                                              int64_t n, const BestPartial* __restrict__ inc,
                                                              uint64_t* __restrict__ out,
                                                              unsigned long long* __restrict__ count, int64_t cap) {
   __shared__ int64_t thr[2];
   const BestPartial cur = *inc;
-  if (threadIdx.x == 0) incumbent_thresholds(L, scans[0], qs, n_used, cur, thr);
+  if (threadIdx.x == 0) {  // few blocks: each finds them (one launch less); many: pyr_threshold_kernel did
+    if (thr_dev) {
+      thr[0] = thr_dev[0];
+      thr[1] = thr_dev[1];
+    } else {
+      incumbent_thresholds(L, scans[0], qs, n_used, cur, thr);
+    }
+  }
   __syncthreads();
   const int64_t t_gt = thr[0], t_ge = thr[1];
   const int h = d - 1;
@@ -935,11 +950,13 @@ hipError_t launch_pyr_expand_top(const LevelWork& L, int d, int32_t nj, int qs, 
                                  int64_t* thr, uint64_t* out, unsigned long long* count, int64_t cap,
                                  hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  (void)thr;
   // a block per 256 nodes up to 65536 blocks: the loop is one dependent load
   // per iteration, so few iterations per thread
-  hipLaunchKernelGGL(pyr_expand_top_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, stream, L, d, nj, qs, n_used,
-                     scans, sums, first, n, inc, out, count, cap);
+  const int blocks = blocks_for(n, 256);
+  const bool shared_thr = blocks > 1024;
+  if (shared_thr) hipLaunchKernelGGL(pyr_threshold_kernel, dim3(1), dim3(1), 0, stream, L, scans, qs, n_used, inc, thr);
+  hipLaunchKernelGGL(pyr_expand_top_kernel, dim3(blocks), dim3(256), 0, stream, L, d, nj, qs, n_used, scans,
+                     shared_thr ? (const int64_t*)thr : nullptr, sums, first, n, inc, out, count, cap);
   return hipGetLastError();
 }
 
