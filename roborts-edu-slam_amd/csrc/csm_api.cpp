@@ -479,6 +479,7 @@ struct PendingRun {
   double alg_bytes = 0.0, scorings = 0.0, finish_bytes = 0.0;
   bool device_finish = false, timed = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, done = nullptr;
+  hipEvent_t ev_fast = nullptr;  // after the fast finish pass, when the exact pass runs on x_stream
   const int32_t* flags = nullptr;  // need-exact flags on the host (profiling)
   int n_flags = 0;
   // few-window launches: the finish writes FinishOut here (host memory) and
@@ -652,6 +653,7 @@ struct csm_ctx {
   bool profiling = false;
   bool stats_dump = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  hipEvent_t ev_ft = nullptr;    // profiling: the fast finish pass ended (timed; ev_fast is not)
   hipEvent_t ev_done = nullptr;  // end of a launch's work (async runs)
   hipEvent_t ev_in = nullptr;    // a launch's inputs are on the device
   hipEvent_t ev_k = nullptr;     // a launch's kernels are done
@@ -666,6 +668,7 @@ struct csm_ctx {
     HostBuf h_scores, h_fin, h_angles, h_sw, h_angles_next, h_fin_sig;
     DevBuf fin_sig;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr, ev_in = nullptr, ev_k = nullptr;
+    hipEvent_t ev_ft = nullptr;
     hipEvent_t ev_fast = nullptr;
   };
   static constexpr int kMaxParts = 4;
@@ -696,6 +699,7 @@ struct csm_ctx {
     std::swap(ev_in, a.ev_in);
     std::swap(ev_k, a.ev_k);
     std::swap(ev_fast, a.ev_fast);
+    std::swap(ev_ft, a.ev_ft);
   }
   // profiling: the pool's last job, as "pool:<what>" (total_ms = the first
   // worker's join latency, algorithmic_bytes = the caller's share of the items)
@@ -985,6 +989,19 @@ int account_run(csm_ctx* c, const PendingRun& p) {
     if (p.device_finish) {
       if ((e = hipEventElapsedTime(&ms, p.ev1, p.ev2)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
       c->account(p.fname, ms, p.finish_bytes, 0.0);
+      if (p.ev_fast) {  // the same interval in its two passes: the fast one on the kernel stream, then
+                        // the exact one on x_stream (it overlaps the other part's scoring)
+        float mf = 0.f, mx = 0.f;
+        if ((e = hipEventElapsedTime(&mf, p.ev1, p.ev_fast)) != hipSuccess ||
+            (e = hipEventElapsedTime(&mx, p.ev_fast, p.ev2)) != hipSuccess)
+          return c->hip_fail(e, "hipEventElapsedTime");
+        const char* lt = std::strchr(p.fname, '<');
+        char nm[48];
+        std::snprintf(nm, sizeof(nm), "finish:fast%s", lt ? lt : "");
+        c->account(nm, mf, 0.0, 0.0);
+        std::snprintf(nm, sizeof(nm), "finish:exact%s", lt ? lt : "");
+        c->account(nm, mx, 0.0, 0.0);
+      }
       if (p.flags) {  // "scorings" of this entry = windows that took the exact sort
         int exact = 0;
         for (int i = 0; i < p.n_flags; ++i) exact += p.flags[i] != 0;
@@ -1501,6 +1518,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                                   (const double*)c->scores.p, sig_out, nw, c->stream, done_stream, c->ev_fast)) !=
           hipSuccess)
         return c->hip_fail(e, "finish_kernel");
+      if (c->profiling && done_stream != c->stream && (e = hipEventRecord(c->ev_ft, c->stream)) != hipSuccess)
+        return c->hip_fail(e, "hipEventRecord");
       if (c->profiling && (e = hipEventRecord(c->ev2, done_stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
     } else {
       csm::FinishArgs A{};
@@ -1524,6 +1543,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                                   (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw, c->stream, fs,
                                   c->ev_fast)) != hipSuccess)
         return c->hip_fail(e, "finish_kernel");
+      if (c->profiling && fs != c->stream && (e = hipEventRecord(c->ev_ft, c->stream)) != hipSuccess)
+        return c->hip_fail(e, "hipEventRecord");
       if (c->profiling && (e = hipEventRecord(c->ev2, fs)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
       // with profiling on, the flags come back too: how many windows needed the exact sort
       const size_t cbytes = fbytes + ((c->profiling && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
@@ -1599,6 +1620,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   p.timed = c->profiling;
   p.ev0 = c->ev0;
   p.ev1 = c->ev1;
+  p.ev_fast = (c->profiling && mode == Finish::kDevice && c->fast_finish && c->x_stream) ? c->ev_ft : nullptr;
   p.ev2 = c->ev2;
   p.done = c->ev_done;
   p.fin_host = sig_out;
@@ -2687,10 +2709,11 @@ int csm_destroy(csm_ctx* c) {
       a.h_fin_sig.release();
       a.fin_sig.release();
       a.h_sw.release();
-      for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k, a.ev_fast})
+      for (hipEvent_t ev : {a.ev0, a.ev1, a.ev2, a.ev_done, a.ev_in, a.ev_k, a.ev_fast, a.ev_ft})
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_done, c->ev_in, c->ev_k, c->ev_fast, c->ev_pts, c->ev_pack})
+    for (hipEvent_t ev : {c->ev0, c->ev1, c->ev2, c->ev_ft, c->ev_done, c->ev_in, c->ev_k, c->ev_fast, c->ev_pts,
+                          c->ev_pack})
       if (ev) (void)hipEventDestroy(ev);
     if (c->x_stream) (void)hipStreamDestroy(c->x_stream);
     (void)hipStreamDestroy(c->h2d);
@@ -3066,10 +3089,10 @@ int csm_set_profiling(csm_ctx* c, int32_t on) {
   DeviceGuard g(c->device);
   hipError_t e;
   if (on && !c->ev0) {
-    for (hipEvent_t* ev : {&c->ev0, &c->ev1, &c->ev2})
+    for (hipEvent_t* ev : {&c->ev0, &c->ev1, &c->ev2, &c->ev_ft})
       if ((e = hipEventCreate(ev)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
     for (auto& a : c->alt)
-      for (hipEvent_t* ev : {&a.ev0, &a.ev1, &a.ev2})
+      for (hipEvent_t* ev : {&a.ev0, &a.ev1, &a.ev2, &a.ev_ft})
         if ((e = hipEventCreate(ev)) != hipSuccess) return c->hip_fail(e, "hipEventCreate");
   }
   (void)flush_deferred(c);  // timings of the earlier setting, dropped with the stats below
