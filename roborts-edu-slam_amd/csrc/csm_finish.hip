@@ -65,6 +65,10 @@ struct Seg {
 constexpr int kTraceWindows = 256;
 __device__ unsigned long long g_trace[kTraceWindows][10];
 __device__ int g_trace_n;
+// per stage-1 level: [2 l] = wall clock at the level's start, [2 l + 1] =
+// segments in it << 32 | the first segment's length (csm_debug_finish_levels)
+constexpr int kTraceLevels = 16;
+__device__ unsigned long long g_ltrace[kTraceWindows][2 * kTraceLevels];
 #define CSM_STAMP(i)                                          \
   do {                                                        \
     if (threadIdx.x == 0 && tr >= 0) g_trace[tr][i] = wall_clock64(); \
@@ -597,10 +601,32 @@ __device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ 
   }
   __syncthreads();
   CSM_STAMP(2);
+  // A child segment goes to the next level's list, or straight to the
+  // deferred list when it starts at or past the limit: a level then holds only
+  // the segments that are partitioned, so the partial sort's chain (one live
+  // segment per level) takes the whole block's partition_block, not one wave.
+  auto push = [&](const Seg& c) {  // one lane
+    if (c.first >= sh->plim) {
+      const int at = atomicAdd(&sh->ndef, 1);
+      if (at < kFinishDefer) deferred[at] = c;
+      else sh->pad = 1;  // cannot happen: at most one straddling segment per level
+    } else {
+      const int at = atomicAdd(&sh->pending, 1);
+      if (at < half) nxt[at] = c;
+      else sh->pad = 1;  // list overflow: cannot happen for the layout's capacity
+    }
+  };
   auto run_levels = [&]() {
     const int plim = sh->plim;
     for (int level = 0;; ++level) {
       const int ncur = sh->top;
+#ifdef CSM_FINISH_TRACE
+      if (threadIdx.x == 0 && tr >= 0 && level < kTraceLevels && plim == sh->plim) {
+        g_ltrace[tr][2 * level] = wall_clock64();
+        g_ltrace[tr][2 * level + 1] =
+            ((unsigned long long)ncur << 32) | (unsigned)(ncur > 0 ? cur[0].last - cur[0].first : 0);
+      }
+#endif
       if (ncur == 0) break;
       if (level > 64) {  // cannot happen (depth bound); reported as count = -1
         if (threadIdx.x == 0) sh->pad = 1;
@@ -611,9 +637,8 @@ __device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ 
         // one large segment: the whole block partitions it
         const int cut = partition_block(keys, vals, lpos, rpos, s0.first, s0.last, sh, wave);
         if (threadIdx.x == 0) {
-          nxt[0] = Seg{cut, s0.last, s0.depth - 1};
-          nxt[1] = Seg{s0.first, cut, s0.depth - 1};
-          sh->pending = 2;
+          push(Seg{cut, s0.last, s0.depth - 1});
+          push(Seg{s0.first, cut, s0.depth - 1});
         }
       } else
       for (int i = wave; i < ncur; i += kWaves) {
@@ -635,13 +660,8 @@ __device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ 
           __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
           const int cut = partition_lds(keys, vals, lpos, rpos, first, last);
           if (lane == 0) {
-            const int at = atomicAdd(&sh->pending, 2);
-            if (at + 2 <= half) {
-              nxt[at] = Seg{cut, last, depth - 1};
-              nxt[at + 1] = Seg{first, cut, depth - 1};
-            } else {
-              sh->pad = 1;  // list overflow: cannot happen for the layout's capacity
-            }
+            push(Seg{cut, last, depth - 1});
+            push(Seg{first, cut, depth - 1});
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -1336,6 +1356,17 @@ extern "C" int csm_debug_fast_trace(unsigned long long* out) {
 
 #ifdef CSM_FINISH_TRACE
 // Trace readout for tools/finish_trace.py: copies and resets the stamps.
+extern "C" int csm_debug_finish_levels(unsigned long long* out, int max_windows) {
+  int n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(csm::g_trace_n), sizeof(int)) != hipSuccess) return -1;
+  n = n < csm::kTraceWindows ? n : csm::kTraceWindows;
+  n = n < max_windows ? n : max_windows;
+  if (n > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(csm::g_ltrace),
+                                   (size_t)n * 2 * csm::kTraceLevels * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  return n;
+}
+
 extern "C" int csm_debug_finish_trace(unsigned long long* out, int max_windows) {
   int n = 0;
   if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(csm::g_trace_n), sizeof(int)) != hipSuccess) return -1;

@@ -34,6 +34,9 @@ for it in range(2):
     covs = np.ascontiguousarray(np.tile(np.eye(3).reshape(1, 9), (n_scans, 1)))
     lv = headline_levels()
     ctx.scan_matchers_loaded([lv[i] for i in level_sel] if level_sel else lv, poses, covs)
+lv = (C.c_ulonglong * (256 * 32))()
+lib.csm_debug_finish_levels.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+nl = lib.csm_debug_finish_levels(lv, 256)  # before the reset below (same window count)
 n = lib.csm_debug_finish_trace(buf, 256)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 10)[:n].astype(np.int64)
 print("windows traced:", n)
@@ -45,3 +48,14 @@ for r in a:
     print("%5d %5d " % (r[9], r[8]) + " ".join("%6.1f" % x for x in d) + "  %6.1f" % ((r[6] - r[0]) / 100.0))
 if rows:
     print("mean        " + " ".join("%6.1f" % x for x in np.mean(np.array(rows), axis=0)))
+
+# stage-1 levels of the first windows: (segments, first segment's length, us)
+L = np.frombuffer(lv, dtype=np.uint64).reshape(256, 32)[:max(nl, 0)].astype(np.int64)
+for r in L[:6]:
+    out = []
+    for l in range(15):
+        t0, t1 = r[2 * l], r[2 * l + 2]
+        if t0 == 0 or t1 == 0 or t1 < t0:
+            break
+        out.append("%d:%d %.1f" % (r[2 * l + 1] >> 32, r[2 * l + 1] & 0xFFFFFFFF, (t1 - t0) / 100.0))
+    print("levels:", " | ".join(out))
