@@ -897,6 +897,14 @@ def plumbing_bench(args, rank, world_size, dist, torch):
             "rank_units": units}
 
 
+def build_info() -> dict:
+    """Which library ran: the source digest compiled into it (csm_build_digest)
+    against the tree's sources (a stale prebuilt .so shows match: false)."""
+    import roborts_csm
+    lib = roborts_csm.build_digest()
+    return {"library_digest": lib, "source_digest": source_digest(), "match": lib == source_digest()}
+
+
 def world_info(dist) -> dict:
     """What actually ran: world size and backend of the process group."""
     if dist is None:
@@ -1026,6 +1034,7 @@ def main():
         out = fn(args, rank, world_size, dist, torch)
         if rank == 0:
             out["world"] = world_info(dist)
+            out["build"] = build_info()
             print(json.dumps(out))
         if dist is not None:
             dist.barrier()
@@ -1190,6 +1199,7 @@ def main():
     else:
         out["cpu_baseline"] = None
     out["world"] = world_info(dist)
+    out["build"] = build_info()
     print(json.dumps(out))
     if dist is not None:
         dist.barrier()

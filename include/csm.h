@@ -128,6 +128,9 @@ int csm_create(int device, csm_ctx** out);
 int csm_destroy(csm_ctx* ctx);
 const char* csm_last_error(const csm_ctx* ctx);
 int csm_abi_version(void);
+/* Digest of the library sources this build was compiled from
+ * (tools/source_digest.py): tells a stale prebuilt .so from the tree's code. */
+const char* csm_build_digest(void);
 /* Value read for an endpoint outside the grid. The reference reads out of
  * bounds (UB, grid_map_base.h:352-354); this ABI defines it. Default 0.3f =
  * kMapUnknownCellProb (slam/slam_processor.h:264). */

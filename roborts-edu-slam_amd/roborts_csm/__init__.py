@@ -427,6 +427,12 @@ class Context:
         return b, int(w.value), stats
 
 
+def build_digest() -> str:
+    """The source digest the loaded library was compiled from (csm_build_digest;
+    tools/source_digest.py computes the tree's)."""
+    return _lib.csm_build_digest().decode()
+
+
 def window_dims(param) -> tuple[int, int]:
     p = _as_param(param)
     na, ns = C.c_int32(), C.c_int32()

@@ -22,7 +22,7 @@ COARSE, FINE, SUPER, FAST = 0, 1, 2, 3
 
 # Every function include/csm.h declares (checked by tests/test_abi.py).
 EXPORTED = (
-    "csm_create", "csm_destroy", "csm_last_error", "csm_abi_version",
+    "csm_create", "csm_destroy", "csm_last_error", "csm_abi_version", "csm_build_digest",
     "csm_set_outside_value", "csm_set_grid", "csm_set_grid_device", "csm_update_grid_cells",
     "csm_update_grid_rows",
     "csm_window_dims", "csm_scan_match", "csm_scan_matchers",
@@ -188,6 +188,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_destroy": (C.c_int, [_ctx]),
         "csm_last_error": (C.c_char_p, [_ctx]),
         "csm_abi_version": (C.c_int, []),
+        "csm_build_digest": (C.c_char_p, []),
         "csm_set_outside_value": (C.c_int, [_ctx, C.c_float]),
         "csm_set_grid": (C.c_int, [_ctx, C.c_void_p, C.c_int64, C.POINTER(CsmMapInfo), C.c_int64]),
         "csm_set_grid_device": (C.c_int, [_ctx, C.c_void_p, C.POINTER(CsmMapInfo)]),
