@@ -57,9 +57,9 @@ METRIC = "candidate-pose scorings/sec (1081-beam scan, 2000×2000 grid) at 1/2/4
 # fp64 arithmetic: FP64 vector peak = half the FP32 rate).
 HBM_PEAK_GBS = 8000.0
 N_CU, N_SIMD, CLK_GHZ = 256, 1024, 2.4
-COUNTERS_JSON = os.path.join(ROOT, "profiles", "r02", "counters.json")
+COUNTERS_JSON = os.path.join(ROOT, "profiles", "r03", "counters.json")
 # the loop-closure / willow legs' counters (tools/pmc_topbox.sh: the search's top-level kernel)
-COUNTERS_LC_JSON = os.path.join(ROOT, "profiles", "r02", "counters_lc.json")
+COUNTERS_LC_JSON = os.path.join(ROOT, "profiles", "r03", "counters_lc.json")
 CSRC = os.path.join(ROOT, "roborts-edu-slam_amd", "csrc")
 
 
@@ -193,11 +193,13 @@ def roofline(kernel: str, avg_ms: float, algorithmic_bytes: float, counters, cou
 COUNTERS_SMALL_JSON = os.path.join(ROOT, "profiles", "r03", "counters_small.json")
 
 
-def split_roofline(stats, counters_path: str = COUNTERS_SMALL_JSON):
+def split_roofline(stats, counters_path: str | None = None):
     """Roofline of the few-window path's dominant kernel from HIP-event stats
     (csm_kernel_stats): the split kernel's launches of every level pooled (one
     kernel, rocprof cannot tell the levels apart), PMC counters per launch
     from counters_path (tools/pmc_roofline.sh --workload online)."""
+    if counters_path is None:  # CSM_COUNTERS_SMALL: counters measured for this build elsewhere
+        counters_path = os.environ.get("CSM_COUNTERS_SMALL", COUNTERS_SMALL_JSON)
     agg = {}
     for s in stats:  # the scoring kernels (the hot path); the finish is bookkeeping
         if not s["name"].startswith("score_") or not s["launches"]:
