@@ -2,7 +2,8 @@
 #   tools/gpu_r03_final.sh tests   the whole GPU suite and smoke()
 #   tools/gpu_r03_final.sh pmc     PMC passes: config 2 (counters.json), loop closure + willow (counters_lc.json)
 #   tools/gpu_r03_final.sh bench   bench lines of every workload + rocprofv3 kernel traces
-# Results land under gpurun_out/r03/ (copied into profiles/r03 afterwards).
+# Results land under gpurun_out/r03/; copy the pmc part's counters*.json into
+# profiles/r03 before the bench part (bench.py reads them from there).
 set -o pipefail
 mkdir -p gpurun_out/r03
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -30,12 +31,11 @@ json.dump(a, open('gpurun_out/r03/counters_lc.json', 'w'), indent=1)
 PY
   cp $O/pmcr/counters.json $O/counters.json; echo "pmc done" ;;
 bench)
-  # the counters measured in the pmc part (this build's) feed the rooflines
-  CJ="--counters-json $O/counters.json"
-  export CSM_COUNTERS_SMALL=$O/counters_small.json
-  timeout -k 10 600 python bench.py $CJ > $O/bench_config2.json 2> $O/bench_config2.err || exit $?
-  timeout -k 10 300 python bench.py --workload loop_closure --steps 10 --warmup 2 --counters-json $O/counters_lc.json > $O/bench_config3_loop_closure.json 2> $O/lc.err || exit $?
-  timeout -k 10 300 python bench.py --workload willow --steps 20 --warmup 3 --counters-json $O/counters_lc.json > $O/bench_config4_willow.json 2> $O/willow.err || exit $?
+  # the counters of the pmc part, copied into profiles/r03 (gpurun_out does not
+  # travel to the next box), feed the rooflines: bench.py's defaults
+  timeout -k 10 600 python bench.py > $O/bench_config2.json 2> $O/bench_config2.err || exit $?
+  timeout -k 10 300 python bench.py --workload loop_closure --steps 10 --warmup 2 > $O/bench_config3_loop_closure.json 2> $O/lc.err || exit $?
+  timeout -k 10 300 python bench.py --workload willow --steps 20 --warmup 3 > $O/bench_config4_willow.json 2> $O/willow.err || exit $?
   timeout -k 10 300 python bench.py --workload online --steps 400 --warmup 20 > $O/bench_config5_online.json 2> $O/online.err || exit $?
   timeout -k 10 300 python bench.py --workload online --attach-backend --rate-hz 40 --steps 300 --warmup 20 > $O/bench_config5_online_backend_40hz.json 2> $O/online_be.err || exit $?
   timeout -k 10 300 python bench.py --workload adapter --steps 40 > $O/bench_adapter.json 2> $O/adapter.err || exit $?

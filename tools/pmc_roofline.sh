@@ -10,6 +10,10 @@ shift || true
 ARGS=${*:-"--steps 2 --warmup 1 --no-cpu --no-latency --no-b109"}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# every scoring dispatch a whole level-part (the 3-level driver otherwise
+# scores its first part's coarse level in two spans): counters per dispatch
+# then match bench.py's per-launch HIP-event times
+export CSM_FIRST_WINDOWS=0
 run() {  # run NAME COUNTERS...
   local name=$1; shift
   timeout -s KILL 300 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -- python3 bench.py $ARGS \
