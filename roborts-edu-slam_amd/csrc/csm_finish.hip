@@ -210,7 +210,10 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 
 // ---- large segments: one wave, LDS -------------------------------------------
 // Parallel std::__unguarded_partition(first+1, last, pivot=first). lpos/rpos
-// are the window-sized scratch arrays; this segment uses [first, first+cap).
+// are the window-sized scratch arrays; this segment uses [first, last). One
+// pass ranks both stop kinds from the left: lpos[k] = the k-th left stop
+// (l_k), rposl[g] = the g-th right stop from the LEFT, so the k-th from the
+// right is r_k = rposl[totR + 1 - k] (no counting pass for totR first).
 // Every pass takes kU chunks of 64 per iteration, their LDS reads issued
 // together (one wave works a segment alone: nothing else hides the latency);
 // ranks are still assigned chunk by chunk in order.
@@ -220,23 +223,9 @@ __device__ int partition_lds(double* k, uint16_t* v, uint16_t* lpos_all, uint16_
   const int lane = lane_id();
   const int m = last - first;
   const int cap = m / 2 + 2;  // pairs <= m/2; ranks up to pairs + 1 are read
-  uint16_t* lpos = lpos_all + first - 1;  // ranks are 1-based
-  uint16_t* rpos = rpos_all + first - 1;
+  uint16_t* lpos = lpos_all + first - 1;   // ranks are 1-based
+  uint16_t* rposl = rpos_all + first - 1;  // right stops, ranked from the left
   const double P = k[first];
-  int totR = 0;
-  for (int base = first + 1; base < last; base += 64 * kU) {
-    double key[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int p = base + 64 * u + lane;
-      key[u] = p < last ? k[p] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int p = base + 64 * u + lane;
-      totR += popc(__ballot(p < last && !gt(P, key[u])));
-    }
-  }
   int cntL = 0, cntR = 0;
   for (int base = first + 1; base < last; base += 64 * kU) {
     double key[kU];
@@ -253,14 +242,14 @@ __device__ int partition_lds(double* k, uint16_t* v, uint16_t* lpos_all, uint16_
       const bool isR = ok && !gt(P, key[u]);
       const uint64_t mL = __ballot(isL), mR = __ballot(isR);
       const int rl = cntL + popc(mL & below_mask(lane)) + 1;
-      const int rr = totR - (cntR + popc(mR & below_mask(lane)));  // rank from the right
-      if (isL && rl <= cap) lpos[rl] = (uint16_t)p;
-      if (isR && rr <= cap) rpos[rr] = (uint16_t)p;
+      const int rr = cntR + popc(mR & below_mask(lane)) + 1;
+      if (isL) lpos[rl] = (uint16_t)p;
+      if (isR) rposl[rr] = (uint16_t)p;
       cntL += popc(mL);
       cntR += popc(mR);
     }
   }
-  const int totL = cntL;
+  const int totL = cntL, totR = cntR;
   const int kmax = min(min(totL, totR), cap);
   // the pairs (l_k < r_k) are a prefix of the ranks: l_k rises, r_k falls
   int npairs = 0;
@@ -271,7 +260,7 @@ __device__ int partition_lds(double* k, uint16_t* v, uint16_t* lpos_all, uint16_
     for (int u = 0; u < kU; ++u) {
       const int kk = kb + 64 * u + lane;
       lp[u] = kk <= kmax ? (int)lpos[kk] : 0;
-      rp[u] = kk <= kmax ? (int)rpos[kk] : 0;
+      rp[u] = kk <= kmax ? (int)rposl[totR + 1 - kk] : 0;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -283,7 +272,7 @@ __device__ int partition_lds(double* k, uint16_t* v, uint16_t* lpos_all, uint16_
   }
   int cut = INT32_MAX;
   if (npairs + 1 <= totL) cut = lpos[npairs + 1];
-  if (npairs >= 1) cut = min(cut, (int)rpos[npairs]);
+  if (npairs >= 1) cut = min(cut, (int)rposl[totR + 1 - npairs]);
   // the swapped positions are all distinct: the kU chunks' swaps are independent
   for (int kb = 1; kb <= npairs; kb += 64 * kU) {
     int lp[kU], rp[kU];
@@ -291,7 +280,7 @@ __device__ int partition_lds(double* k, uint16_t* v, uint16_t* lpos_all, uint16_
     for (int u = 0; u < kU; ++u) {
       const int kk = kb + 64 * u + lane;
       lp[u] = kk <= npairs ? (int)lpos[kk] : -1;
-      rp[u] = kk <= npairs ? (int)rpos[kk] : -1;
+      rp[u] = kk <= npairs ? (int)rposl[totR + 1 - kk] : -1;
     }
     double kl[kU], kr[kU];
     uint16_t vl[kU], vr[kU];
@@ -318,18 +307,17 @@ __device__ int partition_lds(double* k, uint16_t* v, uint16_t* lpos_all, uint16_
 }
 
 // The same partition by the whole 4-wave block, for a level holding one
-// large segment (the partial sort's chain down to the prefix): the waves
-// count and rank contiguous quarters (ranks offset by the earlier quarters'
-// counts, so every rank is the one the single-wave pass assigns), find the
-// first rank that is not a pair together, and share the swaps.
+// large segment (the partial sort's chain down to the prefix): each wave
+// ranks both stop kinds of a contiguous quarter from the quarter's left, into
+// the quarter's own part of the scratch (one pass); after one barrier the
+// global rank k maps to (the wave holding it, its local rank) through the
+// waves' counts. The pairs, the cut and the swaps are the single-wave pass's.
 constexpr int kCoopMin = 256;
 __device__ int partition_block(double* k, uint16_t* v, uint16_t* lpos_all, uint16_t* rpos_all, int first,
                                int last, Shared* sh, int wave) {
   const int lane = lane_id();
   const int m = last - first;
   const int cap = m / 2 + 2;
-  uint16_t* lpos = lpos_all + first - 1;
-  uint16_t* rpos = rpos_all + first - 1;
   if (threadIdx.x == 0) {
     move_median_to_first(k, v, first, first + 1, first + m / 2, last - 1);
     sh->fail = INT32_MAX;
@@ -337,36 +325,9 @@ __device__ int partition_block(double* k, uint16_t* v, uint16_t* lpos_all, uint1
   __syncthreads();
   const double P = k[first];
   const int cq = ((m - 1 + 63) / 64 + kWaves - 1) / kWaves;  // 64-chunks per quarter
-  const int q0 = min(first + 1 + wave * cq * 64, last), q1 = min(first + 1 + (wave + 1) * cq * 64, last);
-  int cL = 0, cR = 0;
-  for (int base = q0; base < q1; base += 64 * kU) {
-    double key[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int p = base + 64 * u + lane;
-      key[u] = p < q1 ? k[p] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int p = base + 64 * u + lane;
-      cL += popc(__ballot(p < q1 && !gt(key[u], P)));
-      cR += popc(__ballot(p < q1 && !gt(P, key[u])));
-    }
-  }
-  if (lane == 0) {
-    sh->wl[wave] = cL;
-    sh->wr[wave] = cR;
-  }
-  __syncthreads();
-  int cntL = 0, cntR = 0, totL = 0, totR = 0;
-  for (int w = 0; w < kWaves; ++w) {
-    totL += sh->wl[w];
-    totR += sh->wr[w];
-    if (w < wave) {
-      cntL += sh->wl[w];
-      cntR += sh->wr[w];
-    }
-  }
+  auto q_lo = [&](int w) { return min(first + 1 + w * cq * 64, last); };
+  const int q0 = q_lo(wave), q1 = q_lo(wave + 1);
+  int cL = 0, cR = 0;  // local ranks: wave w's j-th left stop at lpos_all[q0 - 1 + j]
   for (int base = q0; base < q1; base += 64 * kU) {
     double key[kU];
 #pragma unroll
@@ -381,18 +342,43 @@ __device__ int partition_block(double* k, uint16_t* v, uint16_t* lpos_all, uint1
       const bool isL = ok && !gt(key[u], P);
       const bool isR = ok && !gt(P, key[u]);
       const uint64_t mL = __ballot(isL), mR = __ballot(isR);
-      const int rl = cntL + popc(mL & below_mask(lane)) + 1;
-      const int rr = totR - (cntR + popc(mR & below_mask(lane)));
-      if (isL && rl <= cap) lpos[rl] = (uint16_t)p;
-      if (isR && rr <= cap) rpos[rr] = (uint16_t)p;
-      cntL += popc(mL);
-      cntR += popc(mR);
+      const int rl = cL + popc(mL & below_mask(lane)) + 1;
+      const int rr = cR + popc(mR & below_mask(lane)) + 1;
+      if (isL) lpos_all[q0 - 1 + rl] = (uint16_t)p;
+      if (isR) rpos_all[q0 - 1 + rr] = (uint16_t)p;
+      cL += popc(mL);
+      cR += popc(mR);
     }
   }
+  if (lane == 0) {
+    sh->wl[wave] = cL;
+    sh->wr[wave] = cR;
+  }
   __syncthreads();
+  int offL[kWaves + 1], offR[kWaves + 1];  // counts of the earlier quarters
+  offL[0] = offR[0] = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) {
+    offL[w + 1] = offL[w] + sh->wl[w];
+    offR[w + 1] = offR[w] + sh->wr[w];
+  }
+  const int totL = offL[kWaves], totR = offR[kWaves];
+  auto lpos = [&](int kk) -> int {  // l_k, kk in [1, totL]
+    int w = 0;
+#pragma unroll
+    for (int t = 1; t < kWaves; ++t) w += kk > offL[t] ? 1 : 0;
+    return lpos_all[q_lo(w) - 1 + (kk - offL[w])];
+  };
+  auto rpos = [&](int kk) -> int {  // r_k: the (totR + 1 - k)-th right stop from the left
+    const int g = totR + 1 - kk;
+    int w = 0;
+#pragma unroll
+    for (int t = 1; t < kWaves; ++t) w += g > offR[t] ? 1 : 0;
+    return rpos_all[q_lo(w) - 1 + (g - offR[w])];
+  };
   const int kmax = min(min(totL, totR), cap);
   for (int kk = 1 + (int)threadIdx.x; kk <= kmax; kk += 64 * kWaves)
-    if (!(lpos[kk] < rpos[kk])) {  // ranks past the pairs fail from here on
+    if (!(lpos(kk) < rpos(kk))) {  // ranks past the pairs fail from here on
       atomicMin(&sh->fail, kk);
       break;
     }
@@ -400,10 +386,10 @@ __device__ int partition_block(double* k, uint16_t* v, uint16_t* lpos_all, uint1
   const int f = sh->fail;
   const int npairs = f == INT32_MAX ? kmax : f - 1;
   int cut = INT32_MAX;
-  if (npairs + 1 <= totL) cut = lpos[npairs + 1];
-  if (npairs >= 1) cut = min(cut, (int)rpos[npairs]);
+  if (npairs + 1 <= totL) cut = lpos(npairs + 1);
+  if (npairs >= 1) cut = min(cut, rpos(npairs));
   __syncthreads();  // every thread read the cut before the swaps move elements
-  for (int kk = 1 + (int)threadIdx.x; kk <= npairs; kk += 64 * kWaves) swap_kv(k, v, lpos[kk], rpos[kk]);
+  for (int kk = 1 + (int)threadIdx.x; kk <= npairs; kk += 64 * kWaves) swap_kv(k, v, lpos(kk), rpos(kk));
   __syncthreads();
   return cut;
 }
