@@ -30,6 +30,10 @@ for k, v in b['kernels'].items():
 json.dump(a, open('gpurun_out/r03/counters_lc.json', 'w'), indent=1)
 PY
   cp $O/pmcr/counters.json $O/counters.json; echo "pmc done" ;;
+trace2)
+  rm -rf $O/prof_config2
+  CSM_FIRST_WINDOWS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_config2 -o run --output-format csv -- python3 bench.py --no-cpu --no-latency --no-b109 > $O/prof_config2.json 2> $O/prof_config2.err || exit $?
+  echo "trace done" ;;
 bench)
   # the counters of the pmc part, copied into profiles/r03 (gpurun_out does not
   # travel to the next box), feed the rooflines: bench.py's defaults
@@ -42,7 +46,9 @@ bench)
   timeout -k 10 300 python bench.py --workload backend > $O/bench_backend.json 2> $O/backend.err || exit $?
   timeout -k 10 300 python bench.py --workload online --attach-backend --steps 300 --warmup 20 --no-cpu > $O/bench_config5_online_backend_unpaced.json 2> $O/online_beu.err || exit $?
   rm -rf $O/prof_config2
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_config2 -o run --output-format csv -- python3 bench.py --no-cpu --no-latency --no-b109 > $O/prof_config2.json 2> $O/prof_config2.err || exit $?
+  # whole level-parts per dispatch (CSM_FIRST_WINDOWS=0), B = 1081 only: the
+  # summary's per-dispatch averages are then the bench line's per-launch times
+  CSM_FIRST_WINDOWS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_config2 -o run --output-format csv -- python3 bench.py --no-cpu --no-latency --no-b109 > $O/prof_config2.json 2> $O/prof_config2.err || exit $?
   rm -rf $O/prof_online $O/prof_adapter
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_online -o run --output-format csv -- python3 bench.py --workload online --steps 200 --warmup 20 --no-cpu > $O/prof_online.json 2> $O/prof_online.err || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_adapter -o run --output-format csv -- tests/cpp/build/adapter_run bench 41 3000 > $O/prof_adapter.json 2> $O/prof_adapter.err || exit $?
