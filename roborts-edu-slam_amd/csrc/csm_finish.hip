@@ -29,6 +29,8 @@
 // its leaves, then written back once.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+
 #include "csm_device.hpp"
 #include "csm_internal.hpp"
 
@@ -948,16 +950,43 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
                                                  const AngleEntry* __restrict__ angles,
                                                  const double* __restrict__ scores, FinishOut* __restrict__ out);
 
+#ifdef CSM_TRACE_FASTBLK
+// per block: start, end (wall clock), hw id, then the phase stamps 16-25 of its
+// window (plain stores: no same-address atomics; tools/fast_blocks.py)
+constexpr int kFastBlkTrace = 4096;
+__device__ unsigned long long g_fast_blk[kFastBlkTrace][16];
+__device__ int g_fast_cand;  // record launches of this many candidates only (0: every launch)
+#undef CSM_TS_MIN
+#undef CSM_TS_MAX
+#define CSM_TS_MIN(slot) CSM_TS_MAX(slot)
+#define CSM_TS_MAX(slot)                                                            \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < kFastBlkTrace &&                           \
+        (g_fast_cand == 0 || A.n_cand == g_fast_cand))                              \
+      g_fast_blk[blockIdx.x][(slot) - 13] = (unsigned long long)wall_clock64();     \
+  } while (0)
+#endif
+
 template <int T, int V>
 __global__ __launch_bounds__(T) void finish_fast_kernel(FinishArgs A, const ScanWork* __restrict__ scans,
                                                         const AngleEntry* __restrict__ angles,
                                                         const double* __restrict__ scores,
                                                         FinishOut* __restrict__ out) {
   CSM_TS_MIN(16);
+#ifdef CSM_TRACE_FASTBLK
+  const unsigned long long t_start = wall_clock64();
+#endif
   finish_fast_body<T, V>(A, scans, angles, scores, out);
   CSM_TS_MAX(24);  // body done
   if (A.host_flag) fast_signal(A);
   CSM_TS_MAX(25);  // signalled
+#ifdef CSM_TRACE_FASTBLK
+  if (threadIdx.x == 0 && blockIdx.x < kFastBlkTrace && (g_fast_cand == 0 || A.n_cand == g_fast_cand)) {
+    g_fast_blk[blockIdx.x][0] = t_start;
+    g_fast_blk[blockIdx.x][1] = wall_clock64();
+    g_fast_blk[blockIdx.x][2] = __smid();
+  }
+#endif
 }
 
 template <int T, int V>
@@ -1132,12 +1161,29 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   auto cx = [&](int idx) { return S.x0 + ((idx / ns) % ns) * f; };
   auto cy = [&](int idx) { return S.y0 + (idx % ns) * f; };
   FinishOut* const o = &so;
+  // Only the pieces the host reads are stored: the header, plus the lists the
+  // level keeps (skip_lists) -- 64 B per window instead of 544 B on a level
+  // whose lists are dead, the bytes that cross to host memory with a host signal.
+  static_assert(sizeof(FinishOut) == 544 && offsetof(FinishOut, pos_idx) == 64 &&
+                    offsetof(FinishOut, ang_idx) == 144 && offsetof(FinishOut, pos_score) == 224 &&
+                    offsetof(FinishOut, ang_score) == 384,
+                "FinishOut pieces: header 0-3, pos_idx 4-8, ang_idx 9-13, pos_score 14-23, ang_score 24-33");
+  const int n_pieces = 4 + (want_pos ? 15 : 0) + (want_ang ? 15 : 0);
+  auto piece_of = [&](int t) {  // t < n_pieces: the t-th stored piece
+    if (t < 4) return t;
+    t -= 4;
+    if (want_pos) {
+      if (t < 5) return 4 + t;             // pos_idx
+      if (t < 15) return 14 + (t - 5);     // pos_score
+      t -= 15;
+    }
+    return t < 5 ? 9 + t : 24 + (t - 5);  // ang_idx, ang_score
+  };
   auto emit = [&]() {  // all threads: the LDS FinishOut to out[w]
-    static_assert(sizeof(FinishOut) % 16 == 0, "FinishOut in 16-byte pieces");
-    constexpr int kPieces = (int)(sizeof(FinishOut) / 16);
     __syncthreads();
-    if (tid < kPieces) {
-      const int4 piece = reinterpret_cast<const int4*>(&so)[tid];
+    if (tid < n_pieces) {
+      const int pc = piece_of(tid);
+      const int4 piece = reinterpret_cast<const int4*>(&so)[pc];
       if (A.host_flag) {  // host memory: write-through (sc0 sc1), nothing left dirty in the XCD's L2
         const uint64_t base = (uint64_t)(uintptr_t)(out + w);
         const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base);
@@ -1146,9 +1192,9 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
             (void*)(((uint64_t)bhi << 32) | blo), (short)0, (int)sizeof(FinishOut), 0x00020000);
         typedef int32_t v4i_t __attribute__((ext_vector_type(4)));
         const v4i_t v = {piece.x, piece.y, piece.z, piece.w};
-        __builtin_amdgcn_raw_buffer_store_b128(v, r, tid * 16, 0, kSysWriteThrough);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, pc * 16, 0, kSysWriteThrough);
       } else {
-        reinterpret_cast<int4*>(out + w)[tid] = piece;
+        reinterpret_cast<int4*>(out + w)[pc] = piece;
       }
     }
   };
@@ -1337,6 +1383,18 @@ extern "C" int csm_debug_fast_trace(unsigned long long* out) {
   unsigned long long init[64] = {0};
   init[0] = init[16] = ~0ull;
   return hipMemcpyToSymbol(HIP_SYMBOL(csm::dev::g_small_trace), init, 64 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef CSM_TRACE_FASTBLK
+// Per-block (start, end, hw id, phase stamps) of the last fast-finish launch
+// (of n_cand candidates if selected; tools/fast_blocks.py).
+extern "C" int csm_debug_fast_select(int n_cand) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(csm::g_fast_cand), &n_cand, sizeof(int)) == hipSuccess ? 0 : -1;
+}
+extern "C" int csm_debug_fast_blocks(unsigned long long* out, int max_blocks) {
+  const int n = max_blocks < csm::kFastBlkTrace ? max_blocks : csm::kFastBlkTrace;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(csm::g_fast_blk), (size_t)n * 16 * 8) == hipSuccess ? n : -1;
 }
 #endif
 
