@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "csm_device.hpp"
 #include "csm_internal.hpp"
@@ -107,26 +108,27 @@ struct BoxWave {
   // runs of boxes wholly off the grid and of rejected beams are dropped (they
   // read zeros). Slots from `scratch` on take the non-run lanes' writes
   // (branch-free). Returns the run count.
+  template <int PF = kPF>
   __device__ __forceinline__ int build_runs(int s0, int s1, int32_t* run_off, int32_t* run_cnt, int scratch,
                                             uint64_t& slow) const {
     int nruns = 0;
-    // points of kPF chunks in flight: the list build is latency-bound
+    // points of PF chunks in flight: the list build is latency-bound
     // otherwise (one dependent load per 64 beams)
-    double2 pq[kPF];
+    double2 pq[PF];
 #pragma unroll
-    for (int u = 0; u < kPF; ++u) {  // issued in the order the loop consumes them
+    for (int u = 0; u < PF; ++u) {  // issued in the order the loop consumes them
       pq[u] = point(s0 + 64 * u);
       __builtin_amdgcn_sched_barrier(0);
     }
-    for (int cb0 = s0; cb0 < s1; cb0 += 64 * kPF) {
+    for (int cb0 = s0; cb0 < s1; cb0 += 64 * PF) {
 #pragma unroll
-      for (int u = 0; u < kPF; ++u) {
+      for (int u = 0; u < PF; ++u) {
         // no early exit: a chunk at or past s1 adds no run (live is false for
         // every lane), and an exit here made the compiler drain vmcnt(0) per
-        // chunk instead of keeping kPF chunks of points in flight
+        // chunk instead of keeping PF chunks of points in flight
         const int cb = cb0 + 64 * u;
         const double2 pcur = pq[u];
-        pq[u] = point(cb + 64 * kPF);
+        pq[u] = point(cb + 64 * PF);
         __builtin_amdgcn_sched_barrier(0);
         const int off = offsets(pcur, cb, slow);
         const bool live = cb + lane < s1;
@@ -331,6 +333,163 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   box_epilogue<NS, BEST>(L, S, ae, wt, a, act, k, q, ox, oy, nsf, acc, out, partials);
 }
 
+// x from the lane `ctrl` names in the same 16-lane row (DPP row_ror), 64-bit.
+template <int CTRL>
+__device__ __forceinline__ int64_t row_ror64(int64_t x) {
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)x >> 32), CTRL, 0xF, 0xF, false);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// v9 "grouped" box kernel (box rows of four 16-byte pieces: 13 <= NS <= 16).
+// The v6 kernel above gives one load instruction to one run: lanes (row k,
+// piece q), 52 of 64 busy at NS = 13, and the texture-address unit spends its
+// cycles on all 64 lanes' 16 bytes. Here one instruction serves 16 runs: lane
+// (run rr, piece q) loads row k of run rr's box, and the instruction index is
+// the row, so NS instructions cover 16 runs with every lane busy (13 per 16
+// runs instead of 16 at NS = 13, the same bytes and cache lines per run). The
+// row is uniform, so it is the scalar offset (k * pitch) and the run's corner
+// the vector offset; the per-lane count multiplies per lane. Each lane keeps
+// the integer sums of its piece for every row, NS x 4 int64, and the 16 lanes
+// of one piece add theirs up once at the end of the wave (integer sums: the
+// order is free). Loads run 8 instructions ahead across group boundaries.
+template <int NS, bool BEST>
+__global__ __launch_bounds__(64) void score_box_grouped_kernel(LevelWork L, const ScanWork* __restrict__ scans,
+                                                               const double2* __restrict__ pts,
+                                                               const AngleEntry* __restrict__ angles,
+                                                               double* __restrict__ out,
+                                                               BestPartial* __restrict__ partials) {
+  static_assert(NS >= 13 && NS <= 16, "four 16-byte pieces per box row");
+  constexpr int RG = 16;  // runs per group: lane = (run rr, piece q)
+  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  dev::clear_word(L);
+  const int wt = bid / L.n_angles;
+  const int a = bid - wt * L.n_angles;
+  int win = wt, ox = 0, oy = 0, nsf = NS;
+  if (L.tile_n > 0) {
+    const int tpw = L.tile_n * L.tile_n;
+    win = wt / tpw;
+    const int t = wt - win * tpw;
+    const int ti = t / L.tile_n;
+    nsf = L.tile_ns;
+    ox = min(ti * NS, nsf - NS);
+    oy = min((t - ti * L.tile_n) * NS, nsf - NS);
+  }
+  const ScanWork S = scans[win];
+  const AngleEntry ae = angles[S.angle_off + a];
+  const int lane = threadIdx.x;
+  const int q = lane & 3, rr = lane >> 2;
+  const int pitch4 = L.pitch * 4;
+  const BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, pitch4,
+                  L.size_y * pitch4 /* first of the zero rows */, S.x0 + ox * L.step_cells /* :569, j = ox */,
+                  S.y0 + oy * L.step_cells /* :572, k = oy */};
+  const int n_used = S.n_used;
+  const int zero_off = B.zero_off;
+  const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
+  const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
+  const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)ghi << 32) | glo), (short)0, (int)(L.gridi_stride * 4), 0x00020000);
+  auto load = [&](int voff, int row) { return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, row * pitch4, 0); };
+
+  uint64_t slow = 0;
+  constexpr int kScratch = kRunSeg + 64 + 2 * RG;
+  __shared__ int32_t run_off[kScratch + 64];
+  __shared__ int32_t run_cnt[kScratch + 64];
+  // lane (rr, q) ends with row k = rr: candidates (j = 4q .. 4q+3, k)
+  const int k = rr;
+  int64_t mine[4] = {0, 0, 0, 0};
+  // Rows [K0, K1) of every run in the list: the sums of those rows, one group
+  // of loads in flight (row k of the next group issued as row k of this one
+  // is summed), then the 16 lanes of each piece add theirs up and lane
+  // (rr = k, q) keeps row k. The rows go in two passes over the list so only
+  // half of the box's sums are live at a time (4 waves per SIMD, not 2).
+  auto pass = [&](const int K0, int npad) {
+    constexpr int KN = (NS + 1) / 2;  // rows per pass (the second pass's last row may not exist)
+    int64_t acc[KN][4];
+#pragma unroll
+    for (int kk = 0; kk < KN; ++kk)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[kk][t] = 0;
+    int voff = run_off[rr] + 16 * q;
+    int cnt = run_cnt[rr];
+    v4i b[KN];
+#pragma unroll
+    for (int kk = 0; kk < KN; ++kk)
+      if (K0 + kk < NS) b[kk] = load(voff, K0 + kk);  // (uniform test)
+    for (int g0 = 0; g0 < npad; g0 += RG) {
+      const int voff_n = run_off[g0 + RG + rr] + 16 * q;
+      const int cnt_n = run_cnt[g0 + RG + rr];
+#pragma unroll
+      for (int kk = 0; kk < KN; ++kk) {
+        if (K0 + kk < NS) {
+          v4i v = b[kk];
+          asm volatile("" : "+v"(v));  // consume row kk here, in order
+          acc[kk][0] += (int64_t)cnt * v.x;
+          acc[kk][1] += (int64_t)cnt * v.y;
+          acc[kk][2] += (int64_t)cnt * v.z;
+          acc[kk][3] += (int64_t)cnt * v.w;
+          asm volatile("" : "+v"(acc[kk][0]), "+v"(acc[kk][1]), "+v"(acc[kk][2]), "+v"(acc[kk][3]));
+          b[kk] = load(voff_n, K0 + kk);  // the next group's row
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      voff = voff_n;
+      cnt = cnt_n;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead loads past the list land
+#pragma unroll
+    for (int kk = 0; kk < KN; ++kk) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        int64_t x = acc[kk][t];
+        x += row_ror64<0x124>(x);  // row_ror:4 -- the 4 lanes of piece q in a 16-lane row
+        x += row_ror64<0x128>(x);  // row_ror:8
+        x += __shfl_xor(x, 16, 64);
+        x += __shfl_xor(x, 32, 64);
+        mine[t] += (k == K0 + kk) ? x : 0;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one row's chains at a time: few temporaries live
+    }
+  };
+  for (int s0 = 0; s0 < n_used; s0 += kRunSeg) {
+    const int nruns = B.build_runs(s0, min(n_used, s0 + kRunSeg), run_off, run_cnt, kScratch, slow);
+    // whole groups, then one group of empty runs (zero block, count 0) that
+    // the last group's look-ahead loads read
+    const int npad = (nruns + RG - 1) / RG * RG;
+    for (int i = nruns + lane; i < npad + RG; i += 64) {
+      run_off[i] = zero_off;
+      run_cnt[i] = 0;
+    }
+    __syncthreads();
+    if (npad > 0) {
+#pragma unroll 1
+      for (int k0 = 0; k0 < NS; k0 += (NS + 1) / 2) pass(k0, npad);  // one copy of the code: its sums only
+    }
+    __syncthreads();  // the next segment rewrites the list
+  }
+  slow_beams<NS>(B, L, gi, slow, k, q, ox, oy, mine);
+  box_epilogue<NS, BEST>(L, S, ae, wt, a, k < NS, k, q, ox, oy, nsf, mine, out, partials);
+}
+
+template <int NS>
+hipError_t launch_grouped(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
+                          BestPartial* part, unsigned nblk, hipStream_t stream) {
+  if (part)
+    hipLaunchKernelGGL((score_box_grouped_kernel<NS, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+  else
+    hipLaunchKernelGGL((score_box_grouped_kernel<NS, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+  return hipGetLastError();
+}
+
+int grouped_mode() {  // CSM_BOX_GROUPED=0: the v6 kernel for every box level
+  static const int m = [] {
+    const char* e = getenv("CSM_BOX_GROUPED");
+    return e ? atoi(e) : 1;
+  }();
+  return m;
+}
+
 template <int NS>
 hipError_t launch_ns(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
                      BestPartial* part, unsigned nblk, hipStream_t stream) {
@@ -364,10 +523,14 @@ hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const d
     case 10: return launch_ns<10>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
     case 11: return launch_ns<11>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
     case 12: return launch_ns<12>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 13: return launch_ns<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 14: return launch_ns<14>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 15: return launch_ns<15>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 16: return launch_ns<16>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 13: return grouped_mode() ? launch_grouped<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)
+                                   : launch_ns<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 14: return grouped_mode() ? launch_grouped<14>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)
+                                   : launch_ns<14>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 15: return grouped_mode() ? launch_grouped<15>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)
+                                   : launch_ns<15>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 16: return grouped_mode() ? launch_grouped<16>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)
+                                   : launch_ns<16>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
     default: return hipErrorInvalidValue;
   }
 }
