@@ -859,9 +859,13 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
                                                              FinishOut* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (A.exact_list) {
-    const int cnt = A.exact_list[0];
+    // {count, tag} in one load: a pass whose launch's list has been reset by
+    // the slot's next scoring launch (another tag) had nothing to do
+    const uint64_t head = __hip_atomic_load(reinterpret_cast<uint64_t*>(A.exact_list), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    const int cnt = (uint32_t)(head >> 32) == (uint32_t)A.flag_value ? (int)(uint32_t)head : 0;
     for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
-      finish_window(A, scans, angles, scores, out, A.exact_list[1 + i], smem);
+      finish_window(A, scans, angles, scores, out, A.exact_list[2 + i], smem);
       __syncthreads();  // the next window reuses the LDS carve
     }
     if (A.host_flag && cnt > 0) {  // (nothing flagged: the fast pass signalled the host)
@@ -1017,7 +1021,7 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   int32_t* need = A.need_exact + w;
   auto flag = [&]() {  // thread 0: the exact pass takes this window
     *need = 1;
-    if (A.exact_list) A.exact_list[1 + atomicAdd(A.exact_list, 1)] = w;
+    if (A.exact_list) A.exact_list[2 + atomicAdd(A.exact_list, 1)] = w;
   };
   // the scores, every load in flight (index clamped, value masked after)
   double v[V];
@@ -1352,7 +1356,7 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
   }
   const bool listed = A.need_exact && A.exact_list && !A.order_out;
   if (listed && !A.host_flag) {  // with a host signal the scoring launch zeroed the count
-    hipError_t e = hipMemsetAsync(A.exact_list, 0, sizeof(int32_t), stream);
+    hipError_t e = hipMemsetAsync(A.exact_list, 0, 2 * sizeof(int32_t), stream);  // {count 0, tag 0}
     if (e != hipSuccess) return e;
   }
   if (A.need_exact && !A.order_out) {  // fast pass first; the exact pass only where it flagged
@@ -1367,6 +1371,7 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
     xs = exact_stream;
   }
   FinishArgs B = A;
+  if (!A.host_flag) B.flag_value = 0;       // the tag the memset above left
   if (A.order_out) B.need_exact = nullptr;  // the permutation hook always sorts
   if (!listed) B.exact_list = nullptr;
   hipLaunchKernelGGL(finish_kernel, dim3(listed ? std::min(n_windows, 512) : n_windows), dim3(64 * kWaves), lds, xs, B, d_scans,

@@ -60,10 +60,14 @@ struct LevelWork {
                            // kGridiPadRows): each grid ends with zero rows)
   int32_t tile_n;          // box kernel over a large window: tiles per axis (0: untiled)
   int32_t tile_ns;         // ... and the window's own n_space (candidate indices are its)
-  // The finish's flagged-window count (FinishArgs::exact_list[0]) of a
-  // host-signal launch: block 0 of the scoring kernel, which runs before the
-  // finish on the stream, stores 0 there (nullptr: nothing to clear).
+  // The finish's flagged-window list header (FinishArgs::exact_list[0..1]) of
+  // a host-signal launch: block 0 of the scoring kernel, which runs before the
+  // finish on the stream, stores {count 0, clear_tag} there as one 8-byte word
+  // (nullptr: nothing to clear). clear_tag is the launch's flag value: an
+  // exact pass left over from the slot's previous launch (it had nothing to
+  // do, or the host could not have gone on) finds another tag and exits.
   int32_t* clear_word;
+  int32_t clear_tag;
 };
 
 // Argmax partial: best score of a block and its flat candidate index.
@@ -90,7 +94,8 @@ struct FinishArgs {
   double lin_tol;      // search_space_resolution / map_resolution (:840,:852)
   int32_t* order_out;  // optional: the sorted permutation, n_cand per window
   int32_t* need_exact; // per window: 1 = the fast finish saw a tie that matters (device scratch)
-  int32_t* exact_list; // [0] = count, then the flagged windows (device scratch, n_windows + 1)
+  int32_t* exact_list; // [0] = count, [1] = tag (flag_value), then the flagged windows (device
+                       // scratch, 8-byte aligned, n_windows + 2)
   // Host signal (nullable, listed exact pass only): the pass's last block to
   // finish stores flag_value at host_flag with system scope once every
   // FinishOut is written (done_ctr: a device counter, zero between launches).
@@ -245,10 +250,10 @@ struct SplitWork {
   int32_t splits;         // beam splits per chunk
   int32_t chunks;         // ceil(n_cand / kSplitThreads) per window
   int32_t inline_window;  // 1: one window, its ScanWork and angle rows in `sw` / `ang`
-  int32_t pad;
+  int32_t clear_tag;      // with clear_word: LevelWork::clear_tag
   int32_t* slab;          // n_scans * chunks * splits * kSplitThreads int32 partial sums
   int32_t* arrive;        // n_scans * chunks arrival counters: zero before and after a launch
-  int32_t* clear_word;    // zeroed by block 0 (nullable): the finish's flagged-window count
+  int32_t* clear_word;    // set by block 0 (nullable): LevelWork::clear_word
   ScanWork* scans_out;    // inline window: block 0 stores it here for the finish ...
   AngleEntry* angles_out; // ... and its angle rows here
   ScanWork sw;

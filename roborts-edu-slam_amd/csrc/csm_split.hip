@@ -47,7 +47,8 @@ __global__ __launch_bounds__(kT) void score_split_kernel(LevelWork L, SplitWork 
   const int tid = threadIdx.x;
   CSM_TS_MIN(0);
   if (blockIdx.x == 0) {
-    if (W.clear_word && tid == 0) *W.clear_word = 0;
+    if (W.clear_word && tid == 0)
+      *reinterpret_cast<uint64_t*>(W.clear_word) = (uint64_t)(uint32_t)W.clear_tag << 32;  // {count 0, tag}
     if (W.inline_window) {
       if (tid == 0) *W.scans_out = W.sw;
       for (int t = tid; t < L.n_angles; t += kT) W.angles_out[t] = W.ang[t];

@@ -701,6 +701,45 @@ def test_pipelined_three_level_driver(world2000, finish, parts, first):
         c.close()
 
 
+def test_host_signal_split_levels_with_ties(world2000):
+    """Host-signal finish where the exact pass has work on every level: a map
+    quantised to three values makes equal scores common, so windows of the
+    coarse level too go to the exact pass. The first part's coarse level runs
+    in two scoring spans and a finish-only call (level_begin_split); the list
+    of flagged windows carries the tag of the slot's latest scoring call, and
+    the scoring does not wait for the slot's previous exact pass (a stale one
+    finds another tag). Three batches back to back: each equals the oracle's
+    answer bit for bit."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    grid = np.round(np.asarray(w.grid, dtype=np.float32) * 2.0).astype(np.float32) / np.float32(2.0)
+    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2", "CSM_FIRST_WINDOWS": "5"}
+    os.environ.update(env)
+    try:
+        c = roborts_csm.Context(0)
+    finally:
+        for k in env:
+            del os.environ[k]
+    m = O.Map(grid, w.resolution, w.offset)
+    s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells, b.offsets, headline_levels(), b.init_poses,
+                                       np.tile(np.eye(3).reshape(1, 9), (b.init_poses.shape[0], 1)))
+    try:
+        c.set_grid(_map(grid, w.resolution, w.offset, version=1))
+        c.set_profiling(True)
+        for _ in range(3):
+            poses = np.ascontiguousarray(b.init_poses.copy())
+            covs = np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1))
+            s = c.scan_matchers_batch(b.points_cells, b.offsets, headline_levels(), poses, covs)
+            assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2)
+        st = {k["name"]: k for k in c.kernel_stats()}
+        c.set_profiling(False)
+        coarse = [k for n, k in st.items() if n.startswith("finish:exact_windows<") and "5070" in n]
+        assert coarse and coarse[0]["scorings"] > 0  # the coarse level's exact pass had windows
+    finally:
+        c.close()
+
+
 def test_host_signal_finish_repeated(world2000):
     """The throughput path's host-signal finish (FinishOut written through to
     coherent host memory, a flag instead of a D2H copy and an event) over 25
