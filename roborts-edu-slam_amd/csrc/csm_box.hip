@@ -108,8 +108,8 @@ struct BoxWave {
   // runs of boxes wholly off the grid and of rejected beams are dropped (they
   // read zeros). Slots from `scratch` on take the non-run lanes' writes
   // (branch-free). Returns the run count.
-  template <int PF = kPF>
-  __device__ __forceinline__ int build_runs(int s0, int s1, int32_t* run_off, int32_t* run_cnt, int scratch,
+  template <int PF = kPF, typename CT = int32_t>
+  __device__ __forceinline__ int build_runs(int s0, int s1, int32_t* run_off, CT* run_cnt, int scratch,
                                             uint64_t& slow) const {
     int nruns = 0;
     // points of PF chunks in flight: the list build is latency-bound
@@ -144,7 +144,7 @@ struct BoxWave {
         const int rank = __builtin_popcountll(Hm & ((1ull << lane) - 1));
         const int slot = head ? nruns + rank : scratch + lane;
         run_off[slot] = off;
-        run_cnt[slot] = next - lane;
+        run_cnt[slot] = (CT)(next - lane);  // 1..64
         nruns += __builtin_popcountll(Hm);
       }
     }
@@ -333,6 +333,12 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   box_epilogue<NS, BEST>(L, S, ae, wt, a, act, k, q, ox, oy, nsf, acc, out, partials);
 }
 
+// passes over the run list of the grouped kernel (rows per pass: ceil(NS / passes))
+#ifndef CSM_BOX_PASSES
+#define CSM_BOX_PASSES 2
+#endif
+constexpr int kBoxPasses = CSM_BOX_PASSES;
+
 // x from the lane `ctrl` names in the same 16-lane row (DPP row_ror), 64-bit.
 template <int CTRL>
 __device__ __forceinline__ int64_t row_ror64(int64_t x) {
@@ -395,7 +401,7 @@ __global__ __launch_bounds__(64) void score_box_grouped_kernel(LevelWork L, cons
   uint64_t slow = 0;
   constexpr int kScratch = kRunSeg + 64 + 2 * RG;
   __shared__ int32_t run_off[kScratch + 64];
-  __shared__ int32_t run_cnt[kScratch + 64];
+  __shared__ uint8_t run_cnt[kScratch + 64];  // run lengths 1..64 (bytes: 6.6 KB of LDS per wave, not 10.5)
   // lane (rr, q) ends with row k = rr: candidates (j = 4q .. 4q+3, k)
   const int k = rr;
   int64_t mine[4] = {0, 0, 0, 0};
@@ -405,7 +411,7 @@ __global__ __launch_bounds__(64) void score_box_grouped_kernel(LevelWork L, cons
   // (rr = k, q) keeps row k. The rows go in two passes over the list so only
   // half of the box's sums are live at a time (4 waves per SIMD, not 2).
   auto pass = [&](const int K0, int npad) {
-    constexpr int KN = (NS + 1) / 2;  // rows per pass (the second pass's last row may not exist)
+    constexpr int KN = (NS + kBoxPasses - 1) / kBoxPasses;  // rows per pass (the last pass's may run out)
     int64_t acc[KN][4];
 #pragma unroll
     for (int kk = 0; kk < KN; ++kk)
@@ -464,7 +470,7 @@ __global__ __launch_bounds__(64) void score_box_grouped_kernel(LevelWork L, cons
     __syncthreads();
     if (npad > 0) {
 #pragma unroll 1
-      for (int k0 = 0; k0 < NS; k0 += (NS + 1) / 2) pass(k0, npad);  // one copy of the code: its sums only
+      for (int k0 = 0; k0 < NS; k0 += (NS + kBoxPasses - 1) / kBoxPasses) pass(k0, npad);  // one copy of the code
     }
     __syncthreads();  // the next segment rewrites the list
   }

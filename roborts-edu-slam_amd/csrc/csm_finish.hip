@@ -998,11 +998,11 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
                                                  const AngleEntry* __restrict__ angles,
                                                  const double* __restrict__ scores, FinishOut* __restrict__ out) {
   constexpr int NW = T / 64;
-  __shared__ double ck[kFastCap];   // step 2 candidates (value, index), then ...
+  __shared__ __attribute__((aligned(16))) double ck[kFastCap + 4];  // step 2 candidates (value, index), then ...
   __shared__ int ci[kFastCap];
   __shared__ double sk[kFastCap];   // ... sorted by value (rank order)
   __shared__ int si[kFastCap];
-  __shared__ double nk[kFastNearCap];
+  __shared__ __attribute__((aligned(16))) double nk[kFastNearCap + 4];
   __shared__ int ni[kFastNearCap];
   __shared__ double acs[kFastAngles], asn[kFastAngles];
   __shared__ double red[NW];
@@ -1085,21 +1085,27 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   };
   int lv[V];
   {
-    // per-wave counts from ballots (scalar popcounts; shuffle reductions were
-    // a chain of LDS-permute latencies per level)
-    int c[kFastLevels];
-#pragma unroll
-    for (int q = 0; q < kFastLevels; ++q) c[q] = 0;
+    // per-lane counts packed 16 bits a level (levels 0-3 in c0, 4-7 in c1; a
+    // wave counts at most 64 * V < 2^16 per level), added across the wave in
+    // two 64-bit words: vector work only. (Per-level ballots and scalar
+    // popcounts kept the CU's one scalar unit busy for every wave: ~4.6 us
+    // of a coarse window's block, tools/fast_blocks.py.)
+    static_assert(64 * V < 65536, "16-bit level counts");
+    uint64_t c0 = 0, c1 = 0;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       lv[k] = level_of(v[k]);  // -INFINITY padding: no level
+      const uint64_t one = 1ull << (16 * (lv[k] & 3));
+      c0 += lv[k] < 4 ? one : 0ull;
+      c1 += (lv[k] >= 4 && lv[k] < kFastLevels) ? one : 0ull;
+    }
 #pragma unroll
-      for (int q = 0; q < kFastLevels; ++q) c[q] += popc(__ballot(lv[k] == q));
+    for (int o = 32; o > 0; o >>= 1) {
+      c0 += __shfl_xor(c0, o, 64);
+      c1 += __shfl_xor(c1, o, 64);
     }
     if (lane < kFastLevels) {
-      int t = 0;
-#pragma unroll
-      for (int q = 0; q < kFastLevels; ++q) t = (lane == q) ? c[q] : t;
+      const int t = (int)(((lane < 4 ? c0 : c1) >> (16 * (lane & 3))) & 0xFFFF);
       if (t) atomicAdd(&cnt_s[lane], t);
     }
   }
@@ -1138,16 +1144,19 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
       }
     }
   }
+  if (tid < 4 && nC + tid < kFastCap + 4) ck[nC + tid] = -INFINITY;  // the rank loop's padding (nC known)
   __syncthreads();
   // rank = elements greater; any equal value where the order decides: exact
   // path (the prefix, the positional 20 and the value just past them)
+  // (ck padded with -inf to a multiple of 4: read 4 at a time, 2 LDS loads)
   for (int t = tid; t < nC; t += T) {
     const double x = ck[t];
     int r = 0, eq = 0;
-    for (int j = 0; j < nC; ++j) {
-      const double u = ck[j];
-      r += (u > x) ? 1 : 0;
-      eq += (u == x) ? 1 : 0;
+    for (int j = 0; j < nC; j += 4) {
+      const double2 u01 = *reinterpret_cast<const double2*>(&ck[j]);
+      const double2 u23 = *reinterpret_cast<const double2*>(&ck[j + 2]);
+      r += ((u01.x > x) ? 1 : 0) + ((u01.y > x) ? 1 : 0) + ((u23.x > x) ? 1 : 0) + ((u23.y > x) ? 1 : 0);
+      eq += ((u01.x == x) ? 1 : 0) + ((u01.y == x) ? 1 : 0) + ((u23.x == x) ? 1 : 0) + ((u23.y == x) ? 1 : 0);
     }
     const double d = x - best;
     const bool inF = d < 0.0 ? d >= -1e-2 : d <= 1e-2;  // DoubleEqual(s, best, 1e-2)
@@ -1285,13 +1294,16 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
     if (tid == 0) flag();
     return;
   }
+  if (tid < 4) nk[nN + tid] = -INFINITY;  // the rank loop's padding
+  __syncthreads();
   for (int t = tid; t < nN; t += T) {
     const double x = nk[t];
     int r = 0, eq = 0;
-    for (int j = 0; j < nN; ++j) {
-      const double u = nk[j];
-      r += (u > x) ? 1 : 0;
-      eq += (u == x) ? 1 : 0;
+    for (int j = 0; j < nN; j += 4) {  // (nk padded with -inf like ck)
+      const double2 u01 = *reinterpret_cast<const double2*>(&nk[j]);
+      const double2 u23 = *reinterpret_cast<const double2*>(&nk[j + 2]);
+      r += ((u01.x > x) ? 1 : 0) + ((u01.y > x) ? 1 : 0) + ((u23.x > x) ? 1 : 0) + ((u23.y > x) ? 1 : 0);
+      eq += ((u01.x == x) ? 1 : 0) + ((u01.y == x) ? 1 : 0) + ((u23.x == x) ? 1 : 0) + ((u23.y == x) ? 1 : 0);
     }
     if (eq > 1 && r <= kCovPoints) flag_s = 1;
     if (r < kCovPoints) {
