@@ -52,6 +52,14 @@ sys.path[:0] = [os.path.join(ROOT, "roborts-edu-slam_amd"), os.path.join(ROOT, "
 import numpy as np  # noqa: E402
 
 METRIC = "candidate-pose scorings/sec (1081-beam scan, 2000×2000 grid) at 1/2/4/8 GPUs"
+# The admissible search resolves every candidate of a window without scoring
+# most of them: its lines carry this metric, never METRIC
+RESOLVED_METRIC = "candidate poses resolved/sec by the admissible search (answer = the exhaustive argmax)"
+
+
+def _metric(search):
+    """(metric, unit) of a loop-closure / willow line for its search kind."""
+    return (RESOLVED_METRIC, "candidates/s") if search == "pyramid" else (METRIC, "scorings/s")
 # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s (spec), 256 CUs x 4 SIMD-32,
 # 2400 MHz max clock; a 64-lane VALU instruction issues over 2 cycles (4 for
 # fp64 arithmetic: FP64 vector peak = half the FP32 rate).
@@ -308,8 +316,11 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu:
         cpu = lc_cpu_baseline(bases, pts, param, pose, args.cpu_seconds, na * ns * ns)
+    met, unit = _metric(args.search)
+    if search is not None:  # what the device actually scored, per second
+        search["nodes_scored_per_s_rank0"] = search["nodes_scored_per_query_rank0"] * args.steps / elapsed
     return {
-        "metric": METRIC, "value": total / elapsed, "unit": "scorings/s", "n_gpus": world_size,
+        "metric": met, "value": total / elapsed, "unit": unit, "n_gpus": world_size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (8 seeded 800x800 wall maps, shifted into 512 submaps; one ray-cast query)",
@@ -359,8 +370,9 @@ def loop_closure_capi_bench(args):
     finally:
         lc.close()
     total = float(n_sub) * na * ns * ns * args.steps
+    met, unit = _metric(args.search)
     return {
-        "metric": METRIC, "value": total / elapsed, "unit": "scorings/s", "n_gpus": args.gpus,
+        "metric": met, "value": total / elapsed, "unit": unit, "n_gpus": args.gpus,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (8 seeded 800x800 wall maps, shifted into 512 submaps; one ray-cast query)",
@@ -497,8 +509,9 @@ def willow_bench(args, rank, world_size, dist, torch):
         cpu = {"value": m * na * ns * ns / dtc, "unit": "scorings/s", "cores": th, "kind": "port",
                "sample": f"{m} of the same queries ({na}x{ns}^2 candidates, all beams), {dtc:.1f} s, oracle "
                          f"best_window with {th} threads (OpenMP over theta) on {_cpu_model()}"}
+    met, unit = _metric(args.search)
     return {
-        "metric": METRIC, "value": total / elapsed, "unit": "scorings/s", "n_gpus": world_size,
+        "metric": met, "value": total / elapsed, "unit": unit, "n_gpus": world_size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "willow-full-0.05 occupancy (tests/golden/willow_walls.npz) with the blur splat; "

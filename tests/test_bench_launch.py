@@ -31,3 +31,14 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload",
                         "plumbing"], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_search_lines_use_their_own_metric():
+    """The admissible search's lines (config 3 / willow, --search pyramid) count
+    candidates resolved, not scorings: they never carry the headline metric."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench._metric("pyramid") == (bench.RESOLVED_METRIC, "candidates/s")
+    assert bench._metric("exhaustive") == (bench.METRIC, "scorings/s")
+    assert bench.RESOLVED_METRIC != bench.METRIC
