@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <cstdlib>
 
 #include "csm_device.hpp"
 #include "csm_internal.hpp"
@@ -917,6 +918,14 @@ constexpr int kFastCap = 512;      // compacted candidates of step 2
 constexpr int kFastNearCap = 512;  // compacted near-best candidates of step 3
 constexpr int kFastLevels = 8;     // thresholds best - {0.01, 0.02, ..., 0.64}, then everything > bound
 constexpr int kFastAngles = 256;   // angle rows staged in LDS (more: read from memory)
+// <128, 11> for 1025..1408 candidates (CSM_FAST_HALF=0: <256, 6>, the A/B)
+inline bool fast_half_blocks() {
+  static const bool on = [] {
+    const char* e = std::getenv("CSM_FAST_HALF");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 
 __device__ __forceinline__ double wave_max_d(double v) {
   for (int o = 32; o > 0; o >>= 1) {
@@ -998,13 +1007,20 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
                                                  const AngleEntry* __restrict__ angles,
                                                  const double* __restrict__ scores, FinishOut* __restrict__ out) {
   constexpr int NW = T / 64;
-  __shared__ __attribute__((aligned(16))) double ck[kFastCap + 4];  // step 2 candidates (value, index), then ...
-  __shared__ int ci[kFastCap];
-  __shared__ double sk[kFastCap];   // ... sorted by value (rank order)
-  __shared__ int si[kFastCap];
-  __shared__ __attribute__((aligned(16))) double nk[kFastNearCap + 4];
-  __shared__ int ni[kFastNearCap];
-  __shared__ double acs[kFastAngles], asn[kFastAngles];
+  // LDS lists sized to what the instantiation can hold (n <= V * T): a block
+  // of the 189- and 1331-candidate levels then fits 8 to a CU, so a part's
+  // 2048 windows take one round of blocks, not two (23.2 KB of LDS a block
+  // allowed 7). The caps only decide when the exact pass takes a window.
+  constexpr int CAP = V * T < kFastCap ? V * T : kFastCap;
+  constexpr int NCAP = V * T < kFastNearCap ? V * T : kFastNearCap;
+  constexpr int ACAP = T == 128 ? 64 : (V * T < kFastAngles ? V * T : kFastAngles);
+  __shared__ __attribute__((aligned(16))) double ck[CAP + 4];  // step 2 candidates (value, index), then ...
+  __shared__ int ci[CAP];
+  __shared__ double sk[CAP];   // ... sorted by value (rank order)
+  __shared__ int si[CAP];
+  __shared__ __attribute__((aligned(16))) double nk[NCAP + 4];
+  __shared__ int ni[NCAP];
+  __shared__ double acs[ACAP], asn[ACAP];
   __shared__ double red[NW];
   __shared__ int cnt_s[kFastLevels];
   __shared__ int nC_s, nN_s, flag_s;
@@ -1036,7 +1052,7 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   const int nss = ns * ns;
   CSM_TS_MAX(17);  // score loads issued
   {
-    const int na = min(n / nss, kFastAngles);
+    const int na = min(n / nss, ACAP);
     for (int t = tid; t < na; t += T) {
       const AngleEntry ae = angles[S.angle_off + t];
       acs[t] = ae.cosine;
@@ -1124,7 +1140,7 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   }
   int nC = 0;
   for (int k = 0; k <= L; ++k) nC += cnt_s[k];
-  if (nC > kFastCap) {
+  if (nC > CAP) {
     if (tid == 0) flag();
     return;
   }
@@ -1144,7 +1160,7 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
       }
     }
   }
-  if (tid < 4 && nC + tid < kFastCap + 4) ck[nC + tid] = -INFINITY;  // the rank loop's padding (nC known)
+  if (tid < 4 && nC + tid < CAP + 4) ck[nC + tid] = -INFINITY;  // the rank loop's padding (nC known)
   __syncthreads();
   // rank = elements greater; any equal value where the order decides: exact
   // path (the prefix, the positional 20 and the value just past them)
@@ -1220,8 +1236,8 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
       if (!(d < 0.0 ? d >= -1e-2 : d <= 1e-2)) break;
       const int idx = si[r];
       const int a = idx / nss;
-      const double ca = a < kFastAngles ? acs[a] : angles[S.angle_off + a].cosine;
-      const double sa = a < kFastAngles ? asn[a] : angles[S.angle_off + a].sine;
+      const double ca = a < ACAP ? acs[a] : angles[S.angle_off + a].cosine;
+      const double sa = a < ACAP ? asn[a] : angles[S.angle_off + a].sine;
       ax += cx(idx) * s;
       ay += cy(idx) * s;
       thx += ca * s;
@@ -1280,7 +1296,7 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
       base = uni(base);
       if (in) {
         const int p = base + popc(mm & below_mask(lane));
-        if (p < kFastNearCap) {
+        if (p < NCAP) {
           nk[p] = s;
           ni[p] = i;
         }
@@ -1290,7 +1306,7 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   __syncthreads();
   CSM_TS_MAX(22);  // near-best compacted
   const int nN = nN_s;
-  if (nN > kFastNearCap) {
+  if (nN > NCAP) {
     if (tid == 0) flag();
     return;
   }
@@ -1344,6 +1360,9 @@ hipError_t launch_fast(const FinishArgs& A, const ScanWork* s, const AngleEntry*
   if (n <= 256) return launch_fast_tv<256, 1>(A, s, a, sc, o, nw, stream);
   if (n <= 512) return launch_fast_tv<256, 2>(A, s, a, sc, o, nw, stream);
   if (n <= 1024) return launch_fast_tv<256, 4>(A, s, a, sc, o, nw, stream);
+  // two waves a window (20 KB of LDS, ~80 VGPRs): 8 blocks a CU, where
+  // <256, 6> held 7 (66 VGPRs, 23.2 KB)
+  if (n <= 1408 && fast_half_blocks()) return launch_fast_tv<128, 11>(A, s, a, sc, o, nw, stream);
   if (n <= 1536) return launch_fast_tv<256, 6>(A, s, a, sc, o, nw, stream);
   if (n <= 2560) return launch_fast_tv<256, 10>(A, s, a, sc, o, nw, stream);
   if (n <= 5120) return launch_fast_tv<256, 20>(A, s, a, sc, o, nw, stream);
