@@ -5,7 +5,9 @@
 // grid on every side, the beam-subsampling rule at n = 0, 1, use, 2*use - 1,
 // 2*use and far above it, all three sim-YAML levels (coarse / fine / super-fine
 // windows, correlate_scan_matcher.h:561-745), the FAST branch and bound
-// (:274-331) and std::sort over keys with heavy ties. Any out-of-bounds read,
+// (:274-331), std::sort over keys with heavy ties, and the map oracle: both
+// cell kinds, blur on/off, auto-resize past every edge, the batch rebuild,
+// the map-check penalty and Bresenham. Any out-of-bounds read,
 // overflow or undefined shift aborts the run (halt_on_error); the result
 // checks below are only self-consistency (the parity tests compare values).
 #include <cmath>
@@ -38,6 +40,16 @@ double oracle_scan_match(const oracle_map_c*, const double*, int, const void*, d
 double oracle_scan_matchers(const oracle_map_c*, const double*, int, const void*, int, double*, double*);
 double oracle_best_window(const oracle_map_c*, const double*, int, const void*, const double*, int64_t*);
 void oracle_std_sort_order(const double*, int64_t, int64_t*);
+void* oracle_gridmap_create(int, double, int, int, double, double, double, float);
+void oracle_gridmap_destroy(void*);
+void oracle_gridmap_set_options(void*, int, int, double, double);
+int oracle_gridmap_update_by_range(void*, const double*, int, const double*, const double*, int);
+void oracle_gridmap_init_with_range_vec(void*, const double*, const int64_t*, int, const double*, const double*, int,
+                                        int);
+double oracle_gridmap_feedback_penalty(void*, const double*, int, const double*, const double*, int, double, double,
+                                       int);
+void oracle_gridmap_info(void*, int32_t*, double*);
+int oracle_bresenham(int, int, int, int, int32_t*, int);
 }
 
 namespace {
@@ -132,6 +144,47 @@ int main() {
       if (order[(size_t)i] >= 0 && order[(size_t)i] < n) seen[(size_t)order[(size_t)i]] = 1;
       if (i > 0) check(keys[(size_t)order[(size_t)i - 1]] >= keys[(size_t)order[(size_t)i]], "not descending");
     }
+  }
+  // map building (f1) and the map check (f4): both cell kinds, blur on and off,
+  // auto-resize growing the map past every edge, the sped-up batch rebuild
+  for (int kind = 0; kind < 2; ++kind)
+    for (int blur = 0; blur < 2; ++blur) {
+      void* g = oracle_gridmap_create(kind, 0.05, 120, 100, -3.0, -2.5, 0.05, 0.5f);
+      oracle_gridmap_set_options(g, 1, 0, 0.0, 0.5);
+      std::vector<double> scan(2 * 361);
+      std::vector<double> poses, origins, all;
+      std::vector<int64_t> offs{0};
+      for (int k = 0; k < 6; ++k) {
+        for (int i = 0; i < 361; ++i) {  // meters in the sensor frame; a few far beams force resizes
+          const double r = (i % 45 == 0) ? 9.0 + 2.0 * k : 1.0 + 3.0 * u(rng);
+          const double a = M_PI * i / 180.0;
+          scan[2 * (size_t)i] = r * std::cos(a);
+          scan[2 * (size_t)i + 1] = r * std::sin(a);
+        }
+        const double origin[2] = {0.1, 0.0}, pose[3] = {0.3 * k, -0.2 * k, 0.1 * k};
+        oracle_gridmap_update_by_range(g, scan.data(), 361, origin, pose, blur);
+        const double pen = oracle_gridmap_feedback_penalty(g, scan.data(), 361, origin, pose, 100, 0.3, 2.0, blur);
+        check(std::isfinite(pen), "non-finite map penalty");
+        all.insert(all.end(), scan.begin(), scan.end());
+        offs.push_back(offs.back() + 361);
+        origins.insert(origins.end(), origin, origin + 2);
+        poses.insert(poses.end(), pose, pose + 3);
+      }
+      int32_t ints[8];
+      double dbl[7];
+      oracle_gridmap_info(g, ints, dbl);
+      check(ints[0] >= 120 && ints[1] >= 100, "map shrank");
+      oracle_gridmap_destroy(g);
+      for (int speedup = 0; speedup < 2; ++speedup) {
+        void* h = oracle_gridmap_create(kind, 0.05, 400, 400, -10.0, -10.0, 0.05, 0.5f);
+        oracle_gridmap_init_with_range_vec(h, all.data(), offs.data(), 6, origins.data(), poses.data(), blur, speedup);
+        oracle_gridmap_destroy(h);
+      }
+    }
+  {
+    std::vector<int32_t> line(2 * 512);
+    const int n = oracle_bresenham(-7, 3, 250, -40, line.data(), 512);
+    check(n == 258, "bresenham length");
   }
   if (failures) return 1;
   std::printf("san_driver ok\n");
