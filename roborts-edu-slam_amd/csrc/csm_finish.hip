@@ -954,6 +954,8 @@ __device__ __forceinline__ void fast_signal(const FinishArgs& A) {
       // flag() counts with device-scope atomics before each block's add
       if (__hip_atomic_load(A.exact_list, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
         __hip_atomic_store(A.host_flag, A.flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (A.host_fast_flag)  // every header is in: settled windows complete now
+        __hip_atomic_store(A.host_fast_flag, A.flag_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -1038,6 +1040,12 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   auto flag = [&]() {  // thread 0: the exact pass takes this window
     *need = 1;
     if (A.exact_list) A.exact_list[2 + atomicAdd(A.exact_list, 1)] = w;
+    if (A.host_fast_flag) {  // header count = pending, written through to host memory
+      const uint64_t base = (uint64_t)(uintptr_t)(out + w);
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(uintptr_t)base, (short)0, (int)sizeof(FinishOut), 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(kFinishPending, r, (int)offsetof(FinishOut, count), 0, kSysWriteThrough);
+    }
   };
   // the scores, every load in flight (index clamped, value masked after)
   double v[V];

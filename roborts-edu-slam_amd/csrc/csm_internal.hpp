@@ -105,7 +105,13 @@ struct FinishArgs {
   // fast finishes of at most this many windows run 1024 threads per window
   // (256 otherwise); 0 selects kFinishWideWindows
   int32_t wide_windows;
+  // Early host signal (nullable, with host_flag): the fast pass's last block
+  // stores flag_value here once every window's FinishOut header is written --
+  // a flagged window's with count = kFinishPending -- so the host completes
+  // the settled windows while the exact pass sorts the rest.
+  int32_t* host_fast_flag;
 };
+constexpr int32_t kFinishPending = -2;  // FinishOut::count of a window the exact pass still owes
 constexpr int kFinishWideWindows = 64;
 
 // What the host needs to complete BasedCorrelationScanMatch::ScanMatch for
