@@ -33,7 +33,6 @@ any GPU call) and prints rank 0's line; under torchrun it joins the given group.
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import math
 import os
@@ -82,14 +81,96 @@ def _cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def _host_threads() -> int:
-    """The box's CPU share (OMP_NUM_THREADS is set to it there; nproc shows the
-    whole machine)."""
+def _cgroup_cpus():
+    """CPUs the cgroup's quota allows (cpu.max "quota period"), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                return max(1, int(int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
     try:
-        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
-    except ValueError:
-        n = 0
-    return max(1, min(n or (os.cpu_count() or 1), os.cpu_count() or 1, 16))
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_cpu_share() -> dict:
+    """What this process may run on: the affinity mask, the cgroup's CPU quota,
+    and nproc (os.cpu_count(): the whole machine on the GPU box)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return {"affinity": aff, "cgroup_quota_cpus": _cgroup_cpus(), "nproc": os.cpu_count(),
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
+def _host_threads() -> int:
+    """The all-cores CPU baseline's thread count: every CPU of the affinity
+    mask, capped by the cgroup's CPU quota when one is set (threads beyond the
+    quota only time-slice)."""
+    share = host_cpu_share()
+    n = share["affinity"]
+    if share["cgroup_quota_cpus"]:
+        n = min(n, share["cgroup_quota_cpus"])
+    return max(1, n)
+
+
+def kernel_accounting(stats, elapsed_s: float, steps: int) -> dict:
+    """Device time of the timed steps from the HIP-event stats, without double
+    counting: the scoring launches and the fast finish passes run back to back
+    on the kernel stream (their sum / elapsed = kernel_share_of_step <= 1); the
+    exact finish passes run on x_stream beside the other part's scoring and are
+    reported apart. "finish_kernel<n>" is the fast + exact interval, "finish:*"
+    and "span2:*" are sub-intervals, "host:*" and "pool:*" host phases: none of
+    them is added again."""
+    by = {s["name"]: s for s in stats}
+    main_ms = exact_ms = finish_ms = 0.0
+    scorings = 0.0
+    for s in stats:
+        n = s["name"]
+        if n.startswith("score_"):
+            main_ms += s["total_ms"]
+            scorings += s["scorings"]
+        elif n.startswith("finish_kernel"):
+            lt = n[len("finish_kernel"):]
+            fast, exact = by.get("finish:fast" + lt), by.get("finish:exact" + lt)
+            finish_ms += s["total_ms"]
+            if fast is not None and exact is not None:
+                main_ms += fast["total_ms"]
+                exact_ms += exact["total_ms"]
+            else:
+                main_ms += s["total_ms"]
+    return {"kernel_stream_ms_per_step": main_ms / steps,
+            "exact_finish_side_stream_ms_per_step": exact_ms / steps,
+            "finish_ms_per_step": finish_ms / steps,
+            "kernel_share_of_step": main_ms * 1e-3 / elapsed_s,
+            "kernel_scorings_per_s": scorings / (main_ms * 1e-3) if main_ms else None}
+
+
+def dominant_kernel(stats):
+    """The scoring or finish kernel with the most device time, and its average
+    launch time over the launches that went out as ONE dispatch (the first
+    part's coarse level is two dispatches, "span2:<name>", each with its own
+    ramp and tail: a rocprof dispatch mean compares with the one-span mean)."""
+    ks = [s for s in stats if s["name"].startswith(("score_", "finish_kernel"))]
+    dom = max(ks, key=lambda s: s["total_ms"])
+    two = next((s for s in stats if s["name"] == "span2:" + dom["name"]), None)
+    n1 = dom["launches"] - (two["launches"] if two else 0)
+    info = {"launches": dom["launches"], "two_span_launches": two["launches"] if two else 0}
+    if two and n1 > 0:
+        avg = (dom["total_ms"] - two["total_ms"]) / n1
+        info["avg_ms_all_launches"] = dom["total_ms"] / dom["launches"]
+        info["avg_ms_two_span_launches"] = two["total_ms"] / two["launches"]
+    else:
+        avg = dom["total_ms"] / dom["launches"]
+    return dom, avg, info
 
 
 def cpu_baseline(world, batch, levels, seconds: float, threads: int = 1, label: str = ""):
@@ -115,20 +196,20 @@ def cpu_baseline(world, batch, levels, seconds: float, threads: int = 1, label: 
     O.set_threads(1)
     per_scan = sum(_window_cands(l) for l in levels)
     how = "single-threaded" if threads == 1 else f"{threads} threads (OpenMP over theta)"
-    return {"value": n * per_scan / dt, "unit": "scorings/s", "cores": threads, "kind": "port",
-            "sample": f"{label}{n} scans x 3 levels ({n * per_scan} scorings, {dt:.1f} s) {how} "
-                      f"oracle/csm_oracle.cpp on {_cpu_model()}"}
+    out = {"value": n * per_scan / dt, "unit": "scorings/s", "cores": threads, "kind": "port",
+           "sample": f"{label}{n} scans x 3 levels ({n * per_scan} scorings, {dt:.1f} s) {how} "
+                     f"oracle/csm_oracle.cpp on {_cpu_model()}"}
+    if threads > 1:
+        out["host_cpu_share"] = host_cpu_share()
+    return out
 
 
 def source_digest() -> str:
-    """SHA-1 over the HIP/C++ sources of the library: ties counters.json (and a
-    bench line) to the build it was measured on."""
-    h = hashlib.sha1()
-    for f in sorted(os.listdir(CSRC)):
-        if f.endswith((".hip", ".cpp", ".hpp")):
-            with open(os.path.join(CSRC, f), "rb") as fh:
-                h.update(f.encode() + b"\0" + fh.read())
-    return h.hexdigest()[:12]
+    """SHA-1 over the library's sources and public headers (tools/source_digest.py):
+    ties counters.json (and a bench line) to the build it was measured on."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import source_digest as _sd
+    return _sd.digest(ROOT)
 
 
 def load_counters(path: str):
@@ -335,42 +416,72 @@ def loop_closure_bench(args, rank, world_size, dist, torch):
     }
 
 
+def _lc_config3(n_sub: int):
+    """Config 3's inputs (the torch-sharded leg's too): 512 submaps of 800x800 @5 cm,
+    shifted copies of 8 seeded wall maps, one ray-cast query scan (B = 109)."""
+    from roborts_csm import worlds
+    from roborts_csm.params import CorrelationScanMatchParam
+    side, res = 800, 0.05
+    bases = [worlds.make_world(side, side, res, seed=20261015 + k) for k in range(8)]
+    stack = np.empty((n_sub, side, side), dtype=np.float32)
+    for s in range(n_sub):
+        stack[s] = np.roll(bases[s % 8].grid, ((s // 8) * 7, (s // 8) * 11), axis=(0, 1))
+    batch = worlds.make_scan_batch(bases[0], 1, seed=7)
+    pts = batch.points_cells[batch.offsets[0]:batch.offsets[1]]
+    offsets = np.tile(np.array(bases[0].offset), (n_sub, 1))
+    param = CorrelationScanMatchParam(16.0, 0.05, math.pi, 0.0349, 0.5, 100, 0, False, 0)
+    return bases, stack, pts, batch.init_poses[0], offsets, param, res
+
+
 def loop_closure_capi_bench(args):
     """Config 3 through the C-ABI TryCloseLoop would call from C++
     (include/csm_loop_closure.h; range_scan_pose_graph.cpp:299-355): ONE
     process drives args.gpus devices, csm_loop_closure_create makes a matcher
     context and an RCCL communicator per device (ncclCommInitAll), the 512
     submaps are sharded over them, and each query ends in the MAX / MIN / SUM
-    all-reduces. n_devices is what the library reports in the result."""
+    all-reduces. n_devices is what the library reports in the result.
+    --lc-verify: the same query on ONE device holding every submap (a plain
+    matcher context, no communicator), compared field by field."""
     import roborts_csm
-    from roborts_csm import worlds
-    from roborts_csm.loop_closure import DeviceLoopClosure
-    from roborts_csm.params import CorrelationScanMatchParam
-    n_sub, side, res = args.submaps, 800, 0.05
-    bases = [worlds.make_world(side, side, res, seed=20261015 + k) for k in range(8)]
-    stack = np.empty((n_sub, side, side), dtype=np.float32)
-    for s in range(n_sub):  # the torch-sharded bench's submaps, all in one host stack
-        stack[s] = np.roll(bases[s % 8].grid, ((s // 8) * 7, (s // 8) * 11), axis=(0, 1))
-    batch = worlds.make_scan_batch(bases[0], 1, seed=7)
-    pts = batch.points_cells[batch.offsets[0]:batch.offsets[1]]
-    pose = batch.init_poses[0]
-    offsets = np.tile(np.array(bases[0].offset), (n_sub, 1))
-    param = CorrelationScanMatchParam(16.0, 0.05, math.pi, 0.0349, 0.5, 100, 0, False, 0)
+    from roborts_csm.loop_closure import DeviceLoopClosure, ShardedLoopClosure, shard_range
+    n_sub = args.submaps
+    t_setup = time.perf_counter()
+    lc = DeviceLoopClosure(list(range(args.gpus)))  # first: no device or no RCCL fails before the inputs are made
+    bases, stack, pts, pose, offsets, param, res = _lc_config3(n_sub)
     na, ns = roborts_csm.window_dims(param)
-    lc = DeviceLoopClosure(list(range(args.gpus)))
+    search_ms, exchange_ms, query_ms = [], [], []
     try:
         lc.set_submaps(stack, res, offsets, version=1)
         for _ in range(args.warmup):
             r = lc.match(pts, param, pose, search=args.search)
+        setup_s = time.perf_counter() - t_setup
         t0 = time.perf_counter()
         for _ in range(args.steps):
+            tq = time.perf_counter()
             r = lc.match(pts, param, pose, search=args.search)
+            query_ms.append((time.perf_counter() - tq) * 1e3)
+            search_ms.append(lc.last_search_ms)
+            exchange_ms.append(lc.last_exchange_ms)
         elapsed = time.perf_counter() - t0
         n_dev = lc.last_n_devices
+        pose_world = lc.last_pose_world.tolist()
     finally:
         lc.close()
     total = float(n_sub) * na * ns * ns * args.steps
     met, unit = _metric(args.search)
+    verify = None
+    if args.lc_verify:  # the one-device answer, same process, no communicator
+        ctx = roborts_csm.Context(0)
+        try:
+            ctx.set_grid_stack(stack, res, version=1)
+            one = ShardedLoopClosure(ctx, n_sub, res, offsets, search=args.search).match(pts, param, pose)
+        finally:
+            ctx.close()
+        verify = {"one_device": {"score": one.score, "submap": one.submap, "global_index": one.global_index,
+                                 "x": one.x, "y": one.y, "angle": one.angle},
+                  "same_as_one_device": bool(one.score == r.score and one.global_index == r.global_index and
+                                             one.submap == r.submap and one.x == r.x and one.y == r.y and
+                                             one.angle == r.angle)}
     return {
         "metric": met, "value": total / elapsed, "unit": unit, "n_gpus": args.gpus,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -381,11 +492,59 @@ def loop_closure_capi_bench(args):
                    "search": args.search, "lc": "capi",
                    "parallelism": f"one process, submaps sharded over {n_dev} devices, in-process RCCL "
                                   f"communicator (ncclCommInitAll), MAX/MIN/SUM all-reduce",
-                   "n_devices": n_dev},
+                   "n_devices": n_dev,
+                   "submaps_per_device": [hi - lo for lo, hi in (shard_range(n_sub, d, n_dev)
+                                                                 for d in range(n_dev))]},
+        "query_ms": {"median": float(np.median(query_ms)), "min": float(np.min(query_ms)),
+                     "max": float(np.max(query_ms))},
+        "search_ms_median": float(np.median(search_ms)),
+        "exchange_us": {"median": float(np.median(exchange_ms)) * 1e3, "min": float(np.min(exchange_ms)) * 1e3,
+                        "max": float(np.max(exchange_ms)) * 1e3},
+        "setup_s": setup_s,
         "roofline": None,
-        "result": {"score": r.score, "submap": r.submap, "global_index": r.global_index},
+        "result": {"score": r.score, "submap": r.submap, "global_index": r.global_index, "x": r.x, "y": r.y,
+                   "angle": r.angle, "pose_world": pose_world},
+        "verify": verify,
         "cpu_baseline": None,
     }
+
+
+def lc_leg(args) -> dict:
+    """The config-3 leg of the default line: the north
+    star's RCCL best-score exchange at args.gpus devices, in a child process
+    started before this process makes any GPU call (`--workload loop_closure
+    --lc capi --lc-verify`), under a time limit of its own so that a hung
+    communicator can cost the line this key but never the line. Called on
+    rank 0 only; the other ranks are still in the process-group rendezvous."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "loop_closure", "--lc", "capi", "--lc-verify",
+           "--gpus", str(args.gpus), "--steps", str(args.lc_steps), "--warmup", "2",
+           "--submaps", str(args.submaps)]
+    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
+            "MASTER_PORT")
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC")}
+    t = time.perf_counter()
+    out = {"command": " ".join(os.path.basename(c) if i == 1 else c for i, c in enumerate(cmd[1:], 1)),
+           "n_devices_requested": args.gpus}
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.lc_timeout, env=env)
+    except subprocess.TimeoutExpired:
+        out.update(status="timeout", limit_s=args.lc_timeout, wall_s=time.perf_counter() - t)
+        return out
+    out["wall_s"] = time.perf_counter() - t
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not lines:
+        err = [l for l in r.stderr.splitlines() if l.strip()]
+        out.update(status="failed", returncode=r.returncode, error=err[-1] if err else None,
+                   stderr_tail=r.stderr[-600:])
+        return out
+    d = json.loads(lines[-1])
+    out.update(status="ok", metric=d["metric"], value=d["value"], unit=d["unit"], steps=d["steps"],
+               ms_per_query=d["ms_per_step"], query_ms=d["query_ms"], search_ms_median=d["search_ms_median"],
+               exchange_us=d["exchange_us"], setup_s=d["setup_s"], n_devices=d["config"]["n_devices"],
+               submaps_per_device=d["config"]["submaps_per_device"], workload=d["config"]["workload"],
+               parallelism=d["config"]["parallelism"], result=d["result"], verify=d["verify"],
+               scaling="strong (512 submaps in total, whatever the device count)")
+    return out
 
 
 def lc_cpu_baseline(bases, pts, param, pose, seconds, per_submap):
@@ -409,7 +568,8 @@ def lc_cpu_baseline(bases, pts, param, pose, seconds, per_submap):
     O.set_threads(1)
     return {"value": n * per_submap / dt, "unit": "scorings/s", "cores": th, "kind": "port",
             "sample": f"{n} submap window(s) of {per_submap} candidates, B=109, {dt:.1f} s, oracle "
-                      f"best_window with {th} threads (OpenMP over theta) on {_cpu_model()}"}
+                      f"best_window with {th} threads (OpenMP over theta) on {_cpu_model()}",
+            "host_cpu_share": host_cpu_share()}
 
 
 def willow_bench(args, rank, world_size, dist, torch):
@@ -1000,6 +1160,13 @@ def main():
                     help="loop_closure: torch = one rank per GPU, the exchange over torch.distributed (RCCL); "
                          "capi = ONE process over --gpus devices through csm_loop_closure_* (in-process "
                          "RCCL communicator), what TryCloseLoop calls from C++")
+    ap.add_argument("--lc-verify", action="store_true",
+                    help="loop_closure --lc capi: also answer the query on one device holding every submap")
+    ap.add_argument("--no-lc-leg", action="store_true",
+                    help="config2: leave out the config-3 RCCL leg (loop_closure_rccl key)")
+    ap.add_argument("--lc-leg", action="store_true", help="plumbing: run the config-3 leg too (launch tests)")
+    ap.add_argument("--lc-steps", type=int, default=20, help="config-3 leg: timed queries")
+    ap.add_argument("--lc-timeout", type=float, default=240.0, help="config-3 leg: the child's time limit (s)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true",
@@ -1031,9 +1198,15 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = _device()
     if world_size != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_size}")
+    # the config-3 RCCL leg, before this process makes any GPU call (the child
+    # drives every device; the other ranks wait in the rendezvous below)
+    leg = None
+    if rank == 0 and ((args.workload == "config2" and not args.no_lc_leg) or
+                      (args.workload == "plumbing" and args.lc_leg)):
+        leg = lc_leg(args)
+    local_rank = _device()
     dist = None
     import torch
     if world_size > 1:
@@ -1051,6 +1224,8 @@ def main():
               "backend": backend_bench, "adapter": adapter_bench, "plumbing": plumbing_bench}[args.workload]
         out = fn(args, rank, world_size, dist, torch)
         if rank == 0:
+            if leg is not None:
+                out["loop_closure_rccl"] = leg
             out["world"] = world_info(dist)
             out["build"] = build_info()
             print(json.dumps(out))
@@ -1161,14 +1336,13 @@ def main():
     if os.environ.get("CSM_BENCH_NO_EVENTS") == "1":  # A/B of the event overhead only: no roofline
         print(json.dumps({"ms_per_step": elapsed / args.steps * 1e3, "events": False}))
         return
-    # device kernels only; "host:*" entries are wall-clock phases of the driver
-    kstats = [s for s in stats if not s["name"].startswith("host:")]
-    dom = max(kstats, key=lambda s: s["total_ms"])
-    avg_ms = dom["total_ms"] / dom["launches"]
+    # device kernels only (kernel_accounting: no sub-interval or host phase twice)
+    dom, avg_ms, dom_info = dominant_kernel(stats)
     rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"],
                   load_counters(args.counters_json), args.counters_json)
-    kernel_total_ms = sum(s["total_ms"] for s in kstats)
-    kernel_scorings = sum(s["scorings"] for s in kstats)
+    rl["launch_time"] = dict(dom_info, source="HIP events on the kernel stream around each one-dispatch "
+                                              "launch of the timed steps")
+    acct = kernel_accounting(stats, elapsed, args.steps)
 
     err = np.hypot(*(poses[:, :2] - batch.true_poses[:, :2]).T)
     out = {
@@ -1198,8 +1372,7 @@ def main():
                       f"{batch.points_cells.nbytes / 1e6:.1f} MB per step here, timed below as h2d_ms",
         },
         "roofline": rl,
-        "kernel_scorings_per_s": kernel_scorings / (kernel_total_ms * 1e-3) if kernel_total_ms else None,
-        "kernel_share_of_step": kernel_total_ms * 1e-3 / elapsed,
+        **acct,
         "single_scan_latency_ms": float(np.median(lat) * 1e3) if lat else None,
         "median_pose_error_m": float(np.median(err)),
         "kernels": stats,
@@ -1216,6 +1389,8 @@ def main():
                                                 label="B=109 (sim YAML, U=100): ")
     else:
         out["cpu_baseline"] = None
+    if leg is not None:
+        out["loop_closure_rccl"] = leg
     out["world"] = world_info(dist)
     out["build"] = build_info()
     print(json.dumps(out))

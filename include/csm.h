@@ -333,7 +333,8 @@ typedef struct csm_search_options {
   int32_t max_depth;       /* top level: nodes of 2^max_depth x 2^max_depth candidates;
                               < 0: automatic (the smallest with ceil(n_space / 2^d) <= 32) */
   int32_t probe_min_nodes; /* below the top, a level of at least this many nodes first
-                              scores its best node's leaves exactly (0: 4096) */
+                              scores its best node's leaves exactly (0: 4096; < 0: no
+                              probe at any level, the top included: a test hook) */
   int64_t node_capacity;   /* nodes per level list (0: 2^25; a level never gets more than it has nodes); larger levels are split */
   int32_t top_kernel;      /* 0: the top level as beam boxes when eligible, 1: per-node gathers */
   int32_t reserved;

@@ -503,11 +503,20 @@ int wait_readers(csm_gridmap* m) {
   return CSM_OK;
 }
 
+// The map's next update waits for the reads enqueued on s so far. The event
+// is created on the map's device (the reader's stream lives there: a borrow
+// from another device is refused). If it cannot be created or recorded, the
+// reads are waited for here instead: a fence is never silently dropped.
 void add_fence_locked(const csm_gridmap* m, hipStream_t s) {
+  DeviceGuard g(m->device);
   hipEvent_t ev = nullptr;
-  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipStreamSynchronize(s);
+    return;
+  }
   if (hipEventRecord(ev, s) != hipSuccess) {
     (void)hipEventDestroy(ev);
+    (void)hipStreamSynchronize(s);
     return;
   }
   g_fences[m].push_back(ev);

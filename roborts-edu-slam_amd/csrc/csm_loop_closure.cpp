@@ -12,6 +12,7 @@
 
 #include <cfloat>
 #include <cstddef>
+#include <chrono>
 #include <climits>
 #include <cstring>
 #include <mutex>
@@ -242,6 +243,11 @@ int csm_loop_closure_match(csm_loop_closure* lc, const double* pts, int32_t n_po
     centers[3 * (size_t)i + 1] = s * pose_world[1] + s * lc->offsets[2 * (size_t)i + 1];
     centers[3 * (size_t)i + 2] = pose_world[2];
   }
+  using clock = std::chrono::steady_clock;
+  const auto ms_since = [](clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(clock::now() - t).count();
+  };
+  const clock::time_point t_search = clock::now();
   // per device: its shard's best, searched concurrently
   std::vector<int> status((size_t)G, CSM_OK);
   std::vector<std::string> errs((size_t)G);
@@ -294,6 +300,8 @@ int csm_loop_closure_match(csm_loop_closure* lc, const double* pts, int32_t n_po
     if (status[(size_t)r] != CSM_OK)
       return lc->fail(status[(size_t)r], "device " + std::to_string(lc->devices[(size_t)r]) + ": " + errs[(size_t)r]);
 
+  const double search_ms = ms_since(t_search);
+  const clock::time_point t_exchange = clock::now();
   // the exchange: MAX score -> pick -> MIN index -> row -> SUM row, all enqueued
   hipError_t e;
   ncclResult_t nr;
@@ -356,6 +364,8 @@ int csm_loop_closure_match(csm_loop_closure* lc, const double* pts, int32_t n_po
         (e = hipStreamSynchronize(lc->streams[(size_t)r])) != hipSuccess)
       return abandon(lc->hip_fail(e, "exchange"));
   }
+  res->search_ms = search_ms;
+  res->exchange_ms = ms_since(t_exchange);
   res->n_devices = G;
   res->score = out->score_max;
   const bool none = out->idx_min == INT64_MAX;

@@ -69,9 +69,13 @@ struct PyramidSearch::Impl {
   Buf partials, probe_slot, probe_nodes, probe_vals;
   // device state of a search, set by one init launch: the incumbent, the
   // nodes scored per depth, and a pool of list counters (each expand appends
-  // to a fresh, already zero counter: no memset per level)
+  // to a fresh, already zero counter: no memset per level). Once the fresh
+  // slots are used up (many slices), list d counts in a slot of its own,
+  // kCountPool + d, cleared before each expand into it: never the slot of the
+  // parent list (depth d + 1) whose count that expand reads.
   static constexpr int kCountPool = 64;
-  Buf state;  // BestPartial inc | scored[kPyrMaxDepth + 1] | pool[kCountPool]
+  static constexpr int kCountSlots = kCountPool + kPyrMaxDepth + 1;
+  Buf state;  // BestPartial inc | scored[kPyrMaxDepth + 1] | pool[kCountSlots]
   int cslot[kPyrMaxDepth + 1] = {};  // pool slot of list d's count (slot 0: never written, zero)
   int next_slot = 1;
   BestPartial* inc_dev() const { return (BestPartial*)state.p; }
@@ -102,6 +106,7 @@ struct PyramidSearch::Impl {
     }
   }
   int probe_min = 4096;
+  bool probes = true;  // false: no probe at any level, the top included (a test hook)
   static constexpr int kRoots = 8;  // probe roots per probe (best partials of distinct blocks)
   PyrInputs in{};
   PyrStats* st = nullptr;
@@ -186,7 +191,7 @@ struct PyramidSearch::Impl {
     }
     const int64_t np = ((int64_t)1 << (2 * D)) * kRoots;
     if ((e = partials.ensure((size_t)pyr_blocks(INT64_MAX / 2) * sizeof(PyrPartial))) != hipSuccess) return e;
-    if ((e = state.ensure(sizeof(BestPartial) + (kPyrMaxDepth + 1 + kCountPool) * sizeof(unsigned long long))) !=
+    if ((e = state.ensure(sizeof(BestPartial) + (kPyrMaxDepth + 1 + kCountSlots) * sizeof(unsigned long long))) !=
         hipSuccess)
       return e;
     if ((e = probe_slot.ensure(kRoots * sizeof(uint64_t))) != hipSuccess) return e;
@@ -235,8 +240,8 @@ struct PyramidSearch::Impl {
     hipError_t e;
     if (next_slot < kCountPool) {
       cslot[d - 1] = next_slot++;  // zeroed by the search's init launch
-    } else {  // pool used up (many slices): the last slot, cleared each time
-      cslot[d - 1] = kCountPool - 1;
+    } else {  // fresh slots used up (many slices): list d - 1's own slot, cleared each time
+      cslot[d - 1] = kCountPool + (d - 1);
       if ((e = hipMemsetAsync(count_dev(d - 1), 0, sizeof(unsigned long long), in.stream)) != hipSuccess) return e;
     }
     st->slices += 1;
@@ -278,7 +283,7 @@ struct PyramidSearch::Impl {
     if (d == 0)
       return launch_pyr_final((const PyrPartial*)partials.p, n_partials, true, 0, inc_dev(), nullptr,
                               in.stream);
-    if ((top || n >= probe_min) && (e = probe(d, n_partials)) != hipSuccess) return e;
+    if (probes && (top || n >= probe_min) && (e = probe(d, n_partials)) != hipSuccess) return e;
     const int64_t child_upper = std::min(4 * upper, possible[d - 1]);
     if (child_upper <= capd[d - 1]) {
       if ((e = expand(d, 0, n, nd, upper)) != hipSuccess) return e;
@@ -312,6 +317,7 @@ void PyramidSearch::release() {
 void PyramidSearch::configure(int64_t node_capacity, int probe_min_nodes) {
   p_->cap = node_capacity > 0 ? std::max<int64_t>(node_capacity, 4) : ((int64_t)1 << 25);
   p_->probe_min = probe_min_nodes > 0 ? probe_min_nodes : 4096;
+  p_->probes = probe_min_nodes >= 0;
 }
 
 int64_t PyramidSearch::level_cells(int32_t sx, int32_t sy, int d) {
@@ -339,7 +345,7 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
   if ((e = I.ensure_lists(x.depth)) != hipSuccess) return fail(e, "pyramid node lists");
   for (int d = 0; d <= kPyrMaxDepth; ++d) I.cslot[d] = 0;
   I.next_slot = 1;
-  if ((e = launch_pyr_init(I.inc_dev(), I.scored_dev(), kPyrMaxDepth + 1 + Impl::kCountPool, x.stream)) != hipSuccess)
+  if ((e = launch_pyr_init(I.inc_dev(), I.scored_dev(), kPyrMaxDepth + 1 + Impl::kCountSlots, x.stream)) != hipSuccess)
     return fail(e, "pyr_init_kernel");
   int32_t ktiles, kt, col_blocks;
   const int top_blocks = pyr_top_blocks(x.L, (int32_t)nj, &ktiles, &kt, &col_blocks);

@@ -54,7 +54,12 @@ __global__ __launch_bounds__(kT) void score_split_kernel(LevelWork L, SplitWork 
       for (int t = tid; t < L.n_angles; t += kT) W.angles_out[t] = W.ang[t];
     }
   }
-  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);  // a chunk's splits share an XCD
+  // xcd_remap gives each XCD a contiguous range of about nwg / 8 blocks, so a
+  // chunk's consecutive splits usually share an XCD, but a chunk may straddle
+  // two ranges. The slab hand-off does not rely on sharing one: the partials
+  // are stored write-through (sc1) and the last block reads them with sc1
+  // loads that miss the local L2, so a block on another XCD sees them.
+  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid % W.splits;
   const int rest = bid / W.splits;
   const int chunk = rest % W.chunks;

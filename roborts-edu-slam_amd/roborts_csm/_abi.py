@@ -127,6 +127,8 @@ class CsmLoopClosureResult(C.Structure):
         ("y", C.c_double),
         ("angle", C.c_double),
         ("pose_world", C.c_double * 3),
+        ("search_ms", C.c_double),
+        ("exchange_ms", C.c_double),
     ]
 
 

@@ -177,6 +177,7 @@ class DeviceLoopClosure:
                                                      0 if search == "pyramid" else 1, C.byref(r)))
         self.last_pose_world = np.array(r.pose_world[:])
         self.last_n_devices = int(r.n_devices)
+        self.last_search_ms, self.last_exchange_ms = float(r.search_ms), float(r.exchange_ms)
         return LoopClosureResult(r.score, r.global_index, r.submap, r.x, r.y, r.angle)
 
     def close(self):

@@ -26,6 +26,27 @@ def test_bench_self_launch_gloo(n):
     assert out["rank_units"] == 4.0 * n  # every rank's units summed
 
 
+def test_bench_lc_leg_spawned_once_by_rank0():
+    """The config-3 RCCL leg at world size 2 on the CPU:
+    rank 0 alone starts the child (`--workload loop_closure --lc capi` over
+    --gpus devices) before any GPU call; with no GPU here the child fails, and
+    the line still prints with the leg's status and the child's error, never
+    the line lost."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload",
+                        "plumbing", "--backend", "gloo", "--steps", "3", "--lc-leg"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    leg = out["loop_closure_rccl"]
+    assert leg["n_devices_requested"] == 2
+    assert "--lc capi" in leg["command"] and "--gpus 2" in leg["command"] and "--lc-verify" in leg["command"]
+    assert leg["status"] == "failed" and "csm_create" in leg["error"], leg
+    assert out["world"] == {"world_size": 2, "backend": "gloo"} and out["rank_units"] == 6.0
+
+
 def test_bench_rejects_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload",

@@ -168,3 +168,25 @@ def test_bench_lc_capi_mode_runs():
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["config"]["lc"] == "capi" and d["config"]["n_devices"] == 1 and d["value"] > 0
     assert d["result"]["submap"] >= 0
+
+
+def test_bench_lc_leg_one_device():
+    """The default line's config-3 leg (bench.py lc_leg: a child over every
+    requested device through csm_loop_closure_*, RCCL exchange timed per
+    query) at one device: ok, and equal to the one-device answer computed
+    by a plain matcher context in the same child."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--workload", "plumbing", "--lc-leg",
+                        "--gpus", "1", "--submaps", "24", "--lc-steps", "3", "--steps", "2"],
+                       capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    leg = d["loop_closure_rccl"]
+    assert leg["status"] == "ok", leg
+    assert leg["n_devices"] == 1 and leg["submaps_per_device"] == [24] and leg["steps"] == 3
+    assert leg["verify"]["same_as_one_device"] is True, leg["verify"]
+    assert leg["result"]["global_index"] == leg["verify"]["one_device"]["global_index"] >= 0
+    assert leg["exchange_us"]["median"] > 0 and leg["ms_per_query"] > 0

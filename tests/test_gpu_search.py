@@ -96,6 +96,27 @@ def test_search_slices_and_probes(f1, stack5):
                     probe_min_nodes=1)
 
 
+@pytest.mark.parametrize("depth", [3, 5])
+def test_search_many_slices_without_probes(f1, stack5, depth):
+    """No probe anywhere (probe_min_nodes < 0) and the smallest node capacity:
+    the incumbent only rises at depth 0, so almost nothing is pruned early and
+    the search runs through far more than the 64 fresh list counters. Every
+    slice's parent count must survive its children's counter being cleared
+    (each depth's fallback counter is its own): same answer as exhaustive."""
+    import roborts_csm
+    from roborts_csm.loop_closure import world_to_map
+    from roborts_csm.params import CorrelationScanMatchParam
+    res = float(f1["resolution"])
+    p = CorrelationScanMatchParam(1.6, 0.05, 0.35, 0.0349, 0.5, 100, 0, False, 0)
+    with roborts_csm.Context(0) as c:
+        c.set_grid_stack(stack5, res, version=3)
+        centers = np.stack([world_to_map(f1["init_pose"], res, f1["offset"])] * stack5.shape[0])
+        b, w, st = _check_same(c, f1["points"], p, np.arange(stack5.shape[0]), centers, max_depth=depth,
+                               node_capacity=16, probe_min_nodes=-1)
+        assert st["probe_leaves"] == 0
+        assert st["syncs"] > 64, st  # each read-back follows an expand: > 64 expands
+
+
 @pytest.mark.parametrize("penalty", [False, True])
 def test_search_plateau_ties(f1, penalty):
     """Every candidate scores the same (a constant grid): the answer is the

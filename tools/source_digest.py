@@ -1,5 +1,7 @@
-"""The library's source digest (SHA-1 over csrc/*.hip, *.cpp, *.hpp: name, NUL,
-content, in sorted name order; the same as bench.py's source_digest).
+"""The library's source digest: SHA-1 over the files compiled into it —
+csrc/*.hip, *.cpp, *.hpp and the public headers include/*.h, *.hpp — each as
+its path relative to the repo root, NUL, content, in sorted path order
+(bench.py imports this function).
 
   python3 tools/source_digest.py            print it
   python3 tools/source_digest.py OUT.h      write `#define CSM_SOURCE_DIGEST "..."`
@@ -9,15 +11,19 @@ import hashlib
 import os
 import sys
 
-CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "roborts-edu-slam_amd", "csrc")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SOURCE_DIRS = ((os.path.join("roborts-edu-slam_amd", "csrc"), (".hip", ".cpp", ".hpp")),
+               ("include", (".h", ".hpp")))
 
 
-def digest(csrc: str = CSRC) -> str:
+def digest(root: str = ROOT) -> str:
+    files = []
+    for d, exts in SOURCE_DIRS:
+        files += [os.path.join(d, f) for f in os.listdir(os.path.join(root, d)) if f.endswith(exts)]
     h = hashlib.sha1()
-    for f in sorted(os.listdir(csrc)):
-        if f.endswith((".hip", ".cpp", ".hpp")):
-            with open(os.path.join(csrc, f), "rb") as fh:
-                h.update(f.encode() + b"\0" + fh.read())
+    for rel in sorted(files):
+        with open(os.path.join(root, rel), "rb") as fh:
+            h.update(rel.encode() + b"\0" + fh.read())
     return h.hexdigest()[:12]
 
 
