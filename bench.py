@@ -799,6 +799,13 @@ def online_bench(args, rank, world_size, dist, torch):
         dist.barrier()
     lat = []
     err = []
+    try:  # the 1 cm fine map: its growth (ExtendSize) per scan, for the latency tail
+        fine = fe.map(2)
+    except RuntimeError:  # no scan processed yet (--warmup 0)
+        fine = None
+    fine_size = (lambda: (fine.GetSizeX(), fine.GetSizeY())) if fine is not None else (lambda: None)
+    sizes = [fine_size()]
+    kept_flags = []
     t0 = time.perf_counter()
     if be is not None:
         be.reset_stats()
@@ -814,6 +821,8 @@ def online_bench(args, rank, world_size, dist, torch):
             be.submit(stream.points_m[k], r.pose)
         lat.append(time.perf_counter() - t)
         err.append(r.pose)
+        kept_flags.append(bool(r.map_updated))
+        sizes.append(fine_size())
     fe_elapsed = time.perf_counter() - t0
     backend = be.finish(fe_elapsed) if be is not None else None
     if torch.cuda.is_available():
@@ -826,6 +835,18 @@ def online_bench(args, rank, world_size, dist, torch):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     lat_ms = np.array(lat) * 1e3
+    # the latency tail: the slowest scans and what they did (kept / drawn into
+    # the maps, the fine map grew), and the percentiles without growth scans
+    grew = np.array([sizes[i + 1] != sizes[i] for i in range(len(lat))])
+    kept_a = np.array(kept_flags)
+    order = np.argsort(lat_ms)[::-1][:8]
+    steady = lat_ms[~grew] if (~grew).any() else lat_ms
+    tail = {"slowest": [{"scan": int(args.warmup + i), "ms": float(lat_ms[i]), "kept": bool(kept_a[i]),
+                         "fine_map_grew": bool(grew[i])} for i in order],
+            "growth_scans": int(grew.sum()), "kept_scans": int(kept_a.sum()),
+            "p50_kept_ms": float(np.median(lat_ms[kept_a])) if kept_a.any() else None,
+            "p50_not_kept_ms": float(np.median(lat_ms[~kept_a])) if (~kept_a).any() else None,
+            "p99_without_growth_ms": float(np.percentile(steady, 99))}
     mctx = fe.matcher()
     mctx.set_profiling(True)
     for k in range(n, n + n_prof):
@@ -861,9 +882,11 @@ def online_bench(args, rank, world_size, dist, torch):
             obe = O.BackEnd(BackEndParam().to_c())
         tc = time.perf_counter()
         m = 0
+        olat = []  # per-scan oracle time (front end + that scan's back-end jobs), timed scans only
         while m < n and (m < args.warmup + 2 or time.perf_counter() - tc < args.cpu_seconds):
             if m == args.warmup:
                 tc2 = time.perf_counter()
+            ts = time.perf_counter()
             res = CsmFrontendResult()
             ofe.process(stream.points_m[m], stream.odom_poses[m], res)
             if obe is not None and res.map_updated:
@@ -875,13 +898,22 @@ def online_bench(args, rank, world_size, dist, torch):
                     qs.append(stream.points_m[m]), cs.append(okept[-51:-41]), ps.append(np.array(res.pose[:]))
                 if qs:
                     obe.scan_match(make_jobs(qs, cs, ps), len(qs), np.array(res.pose[:]), ofe.map(0))
+            if m >= args.warmup:
+                olat.append((time.perf_counter() - ts) * 1e3)
             m += 1
         dtc = time.perf_counter() - tc2
         what = "front end" + (" + the back end's per-vertex jobs (near-chain link, loop-closure candidate, "
                               "logistic PubMap check)" if obe is not None else "")
+        olat = np.array(olat)
         cpu = {"value": (m - args.warmup) / dtc, "unit": "scans/s", "cores": 1, "kind": "port",
+               "latency_ms": {"p50": float(np.median(olat)), "p99": float(np.percentile(olat, 99)),
+                              "max": float(olat.max())},
                "sample": f"scans {args.warmup}..{m - 1} of the same stream through the oracle's restatement "
-                         f"of the {what} (oracle/map_oracle.cpp), single-threaded, {dtc:.1f} s on {_cpu_model()}"}
+                         f"of the {what} (oracle/map_oracle.cpp), single-threaded, unpaced, {dtc:.1f} s on "
+                         f"{_cpu_model()}"}
+        if args.rate_hz > 0:  # the paced line's value is a latency: the oracle's per-scan time beside it
+            cpu.update(value=float(np.median(olat)), unit="ms per scan (p50)",
+                       scans_per_s_unpaced=(m - args.warmup) / dtc)
         if m == n:  # the oracle kept the same scans: time its CorrectPoseAndMap too
             tco = time.perf_counter()
             try:
@@ -889,18 +921,27 @@ def online_bench(args, rank, world_size, dist, torch):
                 cpu["correct_pose_and_map_ms"] = (time.perf_counter() - tco) * 1e3
             except ValueError:
                 pass
+    if args.rate_hz > 0:  # paced: the stream's rate is the input, the latency per scan is the result
+        head = {"metric": f"front-end per-scan latency p50 (config 5 online at {args.rate_hz:g} Hz: 1081-beam "
+                          f"stream, 3-level match + map check + 3 map updates"
+                          + (", back end attached)" if be is not None else ")"),
+                "value": float(np.median(lat_ms)), "unit": "ms", "higher_is_better": False,
+                "p99_ms": float(np.percentile(lat_ms, 99)), "scans_per_s_paced": world_size * args.steps / elapsed}
+    else:
+        head = {"metric": "front-end scans/sec (config 5 online: 1081-beam stream, 3-level match + map check + 3 "
+                          "map updates)" + (", back end attached" if be is not None else ""),
+                "value": world_size * args.steps / elapsed, "unit": "scans/s", "higher_is_better": True}
     return {
-        "metric": "front-end scans/sec (config 5 online: 1081-beam stream, 3-level match + map check + 3 map "
-                  "updates)",
-        "value": world_size * args.steps / elapsed, "unit": "scans/s", "n_gpus": world_size,
+        **head, "n_gpus": world_size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic drive (roborts_csm.worlds.make_scan_stream) in the seeded 2000x2000 @5cm world; "
                 "ray-cast 1081-beam Hokuyo scans, noisy odometry",
         "config": {"workload": "config5: online front-end, simulatin_param.yaml (fine map 1 cm, coarse 8 cm, "
                                "PubMap 5 cm, U=100)", "parallelism": f"replicas x{world_size}",
                    "latency_ms": {"mean": float(lat_ms.mean()), "p50": float(np.median(lat_ms)),
                                   "p99": float(np.percentile(lat_ms, 99)), "max": float(lat_ms.max())},
+                   "latency_tail": tail,
                    "rate_40hz_headroom": float(world_size * args.steps / elapsed / 40.0),
                    "paced_hz": args.rate_hz or None,
                    "median_pose_error_m": float(np.median(perr)), "max_pose_error_m": float(perr.max()),
@@ -1160,6 +1201,8 @@ def main():
                     help="loop_closure: torch = one rank per GPU, the exchange over torch.distributed (RCCL); "
                          "capi = ONE process over --gpus devices through csm_loop_closure_* (in-process "
                          "RCCL communicator), what TryCloseLoop calls from C++")
+    ap.add_argument("--no-host-inputs", action="store_true",
+                    help="config2: skip the value_host_inputs leg (batches uploaded from pinned host memory)")
     ap.add_argument("--lc-verify", action="store_true",
                     help="loop_closure --lc capi: also answer the query on one device holding every submap")
     ap.add_argument("--no-lc-leg", action="store_true",
@@ -1275,6 +1318,7 @@ def main():
     elapsed = time.perf_counter() - t0
     stats = ctx.kernel_stats()
     ctx.set_profiling(False)
+    poses_resident = poses_w.copy()
 
     per_scan = sum(_window_cands(l) for l in levels)
     local_scorings = float(args.scans * per_scan * args.steps)
@@ -1303,6 +1347,48 @@ def main():
     t = time.perf_counter()
     ctx.load_scans(batch.points_cells, batch.offsets)
     h2d_ms = (time.perf_counter() - t) * 1e3
+
+    # value_host_inputs: every step's scans come from (pinned) host memory,
+    # uploaded on the copy stream while the previous batch is matched
+    # (csm_load_scans_async, double-buffered); the first upload is not hidden
+    host_inputs = None
+    if not args.no_host_inputs:
+        pins = [roborts_csm.PinnedArray(batch.points_cells.shape) for _ in range(2)]
+        for p in pins:
+            np.copyto(p.array, batch.points_cells)
+        t = time.perf_counter()
+        ctx.load_scans(pins[0].array, batch.offsets)
+        h2d_pinned_ms = (time.perf_counter() - t) * 1e3
+
+        def run_host(k):
+            ctx.load_scans_async(pins[0].array, batch.offsets)
+            for i in range(k):
+                if i + 1 < k:
+                    ctx.load_scans_async(pins[(i + 1) % 2].array, batch.offsets)
+                step()
+            return poses_w
+
+        run_host(max(2, min(args.warmup, 10)))
+        barrier()
+        t = time.perf_counter()
+        ph = run_host(args.steps)
+        barrier()
+        eh = time.perf_counter() - t
+        if dist is not None:
+            e = torch.tensor([eh], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            eh = float(e.item())
+        host_inputs = {"value": world_size * args.scans * sum(_window_cands(l) for l in levels) * args.steps / eh,
+                       "unit": "scorings/s", "ms_per_step": eh / args.steps * 1e3, "steps": args.steps,
+                       "bytes_per_step": int(batch.points_cells.nbytes),
+                       "h2d_pinned_ms_one_batch": h2d_pinned_ms,
+                       "same_result_as_resident": bool(np.array_equal(ph, poses_resident)),
+                       "how": "each step's 4096 scans (1081 beams, fp64) uploaded from pinned host memory "
+                              "(csm_host_alloc) on a copy stream of its own while the previous batch is matched "
+                              "(csm_load_scans_async, two device buffers); the first step's upload is not hidden"}
+        ctx.load_scans(batch.points_cells, batch.offsets)
+        for p in pins:
+            p.close()
 
     # the reference-default beam rule next to the headline: sim-YAML U=100 -> B=109
     b109 = None
@@ -1378,6 +1464,8 @@ def main():
         "kernels": stats,
     }
     out["h2d_ms"] = h2d_ms
+    if host_inputs is not None:
+        out["value_host_inputs"] = host_inputs
     if b109 is not None:
         out["b109"] = b109
     if not args.no_cpu and world_size == 1:

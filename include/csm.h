@@ -50,6 +50,7 @@
 #ifndef ROBORTS_CSM_H
 #define ROBORTS_CSM_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -213,6 +214,21 @@ int csm_load_scans(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
                    const int64_t* point_offsets);
 int csm_scan_matchers_loaded(csm_ctx* ctx, const csm_param levels[3], int32_t use_fine,
                              double* poses, double* covs, double* scores);
+
+/* Streams of batches (the reference's points come from host memory,
+ * sensor_data_manager.h:99-115): csm_load_scans_async queues a batch whose
+ * upload runs on a copy stream of its own, concurrently with whatever the
+ * context is matching; the next csm_scan_matchers_loaded takes the oldest
+ * queued batch (waiting for its upload) before it matches. At most two
+ * batches are queued. points_xy must stay unchanged until that call returns,
+ * and should be pinned (csm_host_alloc): pageable memory makes the upload
+ * synchronous. Typical loop: queue batch 0; for each i: queue batch i + 1,
+ * then csm_scan_matchers_loaded (batch i, while batch i + 1 goes up). */
+int csm_load_scans_async(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
+                         const int64_t* point_offsets);
+/* Pinned (page-locked) host memory for csm_load_scans_async inputs. */
+int csm_host_alloc(size_t bytes, void** out);
+int csm_host_free(void* p);
 
 /* --- Gauss-Newton scan matcher ---------------------- */
 /* OptimizeScanMatchParam (optimize_scan_matcher.h:33-58), filled by

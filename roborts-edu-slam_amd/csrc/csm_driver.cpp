@@ -1,0 +1,589 @@
+// csm_driver.cpp — BasedCorrelationScanMatch::ScanMatch over batches of
+// scans (correlate_scan_matcher.h:784-875) and the 3-level ScanMatchers
+// driver (scan_matchers.h:179-289): levels planned, launched, joined and
+// completed per part, with the parts of a resident batch in flight together.
+#include "csm_host.hpp"
+
+namespace csmh {
+
+// One level (BasedCorrelationScanMatch::ScanMatch) over a batch of scans,
+// split in two so a pipelined caller can overlap the host work of one half
+// with the device work of the other: level_begin plans the windows and
+// enqueues them (nothing waits), level_end joins and completes them.
+// Points must already be uploaded; offsets index them.
+struct LevelRun {
+  csm_param P{};
+  Dims D;
+  std::vector<int> scan_of;
+  std::vector<WindowPlan> plans;
+  std::vector<int64_t> pt_off;
+  std::vector<int32_t> grid;             // resident grid of each window (empty: grid 0)
+  const AngleEntry* angles = nullptr;    // pinned buffer of the slot that ran it
+  AngleEntry* rows = nullptr;            // the same, writable while the level is planned
+  const csm::FinishOut* fin = nullptr;   // ditto (device finish)
+  const double* scores = nullptr;        // ditto (host finish)
+  bool dev = false;
+  int skip_lists = 0;  // live_lists
+  PendingRun pend;
+  int tag = -1;        // 3-level driver: level * 8 + part (per-phase host timings)
+};
+
+// Which covariance lists of level l a caller of the 3-level driver can see,
+// as the finish's skip mask (bit 0 positional, bit 1 angular: skipped).
+// ComputePositionalCovariance resets the whole matrix (correlate_scan_matcher.h:891)
+// and ComputeAngularCovariance writes (2,2) only (:1018), by type (:835-858); a
+// later level that writes the same entries makes this level's value dead (the
+// reference's coarse covariance is always overwritten by the fine level).
+int live_lists(const csm_param* levels, int n_levels, int l) {
+  auto pos = [](int t) { return t == CSM_COARSE || t == CSM_FAST || t == CSM_FINE; };
+  auto ang = [](int t) { return t == CSM_COARSE || t == CSM_FAST || t == CSM_SUPER; };
+  int skip = 0;
+  for (int k = l + 1; k < n_levels; ++k) {
+    if (pos(levels[k].type)) return 3;
+    if (ang(levels[k].type)) skip |= 2;
+  }
+  return skip;
+}
+
+// Which scans of a level have windows, and its dimensions (no planning yet).
+// `reset`: responses (and argmaxes) of the batch start at kMinResponse.
+int level_prepare(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P, double* responses,
+                  int64_t* argmax_flat, LevelRun& R, const int32_t* scan_grid, int skip_lists, bool reset) {
+  R.P = P;
+  R.skip_lists = skip_lists;
+  R.scan_of.clear();
+  R.grid.clear();
+  int st = window_dims(P, R.D);
+  if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
+  R.scan_of.reserve((size_t)n_scans);
+  for (int s = 0; s < n_scans; ++s) {
+    if (reset) {
+      responses[s] = 0.0;  // kMinResponse (:1034)
+      if (argmax_flat) argmax_flat[s] = -1;
+    }
+    const int n = (int)(offsets[s + 1] - offsets[s]);
+    if (!map_ready(c) || n == 0) continue;  // :792-795
+    int step, use, n_used;
+    if (!beam_rule(n, P.use_point_size, step, use, n_used))
+      return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+    R.scan_of.push_back(s);
+    if (scan_grid) R.grid.push_back(scan_grid[s]);
+  }
+  return CSM_OK;
+}
+
+// Room for the level's plans and angle rows (pinned: uploaded by DMA).
+int level_alloc(csm_ctx* c, const int64_t* offsets, LevelRun& R, HostBuf& rows) {
+  const int nw = (int)R.scan_of.size();
+  R.plans.assign((size_t)nw, WindowPlan{});
+  R.pt_off.resize((size_t)nw);
+  for (int i = 0; i < nw; ++i) R.pt_off[(size_t)i] = offsets[R.scan_of[(size_t)i]];
+  const hipError_t he = rows.ensure((size_t)nw * (size_t)R.D.n_angles * sizeof(AngleEntry));
+  if (he != hipSuccess) return c->hip_fail(he, "hipHostMalloc(angles)");
+  R.rows = (AngleEntry*)rows.p;
+  R.angles = R.rows;
+  return CSM_OK;
+}
+
+// Plan window i of a prepared level around the scan's current pose: host
+// libm cos/sin per angle (AngleSearchLookUpTable::UpdateLookUpTable :154-172).
+void level_plan_one(LevelRun& R, const Geometry& G, const int64_t* offsets, const double* poses, int i) {
+  const int s = R.scan_of[(size_t)i];
+  double center[3];
+  G.to_map(poses + 3 * s, center);
+  WindowPlan& W = R.plans[(size_t)i];
+  plan_window_into(R.P, R.D, G, (int)(offsets[s + 1] - offsets[s]), center, R.rows + (size_t)i * (size_t)R.D.n_angles, W);
+  W.angle_off = (int64_t)i * R.D.n_angles;
+}
+
+// Device finish for the front-end windows (and enough of them to fill the
+// chip); a handful of windows finish faster on the host's std::sort.
+bool level_device_finish(const csm_ctx* c, const Dims& D, int nw) {
+  return c->device_finish && D.n_cand <= csm::kFinishMaxCand && csm::finish_lds_bytes(D.n_cand) <= 160 * 1024 &&
+         nw >= c->device_finish_min;
+}
+
+// Enqueue a planned level, or a span of it (nothing waits).
+int level_launch(csm_ctx* c, LevelRun& R, WinSpan sp = WinSpan{}) {
+  const int nw = (int)R.scan_of.size();
+  const Dims& D = R.D;
+  const Geometry G(c->info);
+  R.dev = level_device_finish(c, D, nw);
+  const int st = run_windows(c, R.P, D, G, R.plans, R.pt_off, R.angles, (size_t)nw * (size_t)D.n_angles, R.grid,
+                             nullptr, R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend, R.skip_lists, sp);
+  if (st != CSM_OK || !sp.finish) return st;
+  R.fin = R.pend.fin_host ? R.pend.fin_host : (const csm::FinishOut*)c->h_fin.p;
+  R.scores = (const double*)c->h_scores.p;
+  return CSM_OK;
+}
+
+int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
+                const double* poses, double* responses, int64_t* argmax_flat, LevelRun& R,
+                const int32_t* scan_grid, int skip_lists) {
+  int st = level_prepare(c, n_scans, offsets, P, responses, argmax_flat, R, scan_grid, skip_lists, true);
+  if (st != CSM_OK) return st;
+  const int nw = (int)R.scan_of.size();
+  if (nw == 0) return CSM_OK;
+  const double t0 = now_ms();
+  if ((st = level_alloc(c, offsets, R, c->h_angles)) != CSM_OK) return st;
+  const Geometry G(c->info);
+  const int threads = (nw >= 64) ? c->host_threads : 1;
+  c->parallel_for(nw, threads, [&](int i) { level_plan_one(R, G, offsets, poses, i); });
+  if (threads > 1) c->account_pool("plan");
+  const double t1 = now_ms();
+  if ((st = level_launch(c, R)) != CSM_OK) return st;
+  if (c->profiling) {  // per level (window size), and in all
+    c->account("host:launch", (float)(now_ms() - t1), 0.0, 0.0);
+    char nm[48];
+    std::snprintf(nm, sizeof(nm), "host:plan<%lld>", (long long)R.D.n_cand);
+    c->account("host:plan", (float)(t1 - t0), 0.0, 0.0);
+    c->account(nm, (float)(t1 - t0), 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+// level_begin with the plan in two pieces: the first `first` windows are
+// planned on the calling thread and their scoring goes out at once, the rest
+// are planned on the pool while it runs, then the finish follows for all.
+// For the 3-level driver's first part, where nothing else keeps the device
+// busy while the host plans (a call's first ~0.15 ms).
+int level_begin_split(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P, const double* poses,
+                      double* responses, LevelRun& R, const int32_t* scan_grid, int skip_lists, int first) {
+  int st = level_prepare(c, n_scans, offsets, P, responses, nullptr, R, scan_grid, skip_lists, true);
+  if (st != CSM_OK) return st;
+  const int nw = (int)R.scan_of.size();
+  if (first <= 0 || nw < 2 * first || !level_device_finish(c, R.D, nw))
+    return level_begin(c, n_scans, offsets, P, poses, responses, nullptr, R, scan_grid, skip_lists);
+  const double t0 = now_ms();
+  if ((st = level_alloc(c, offsets, R, c->h_angles)) != CSM_OK) return st;
+  const Geometry G(c->info);
+  for (int i = 0; i < first; ++i) level_plan_one(R, G, offsets, poses, i);
+  if ((st = level_launch(c, R, WinSpan{0, first, true, false})) != CSM_OK) return st;
+  if (c->profiling && c->t_call > 0.0) c->account("host:entry->first_launch", (float)(now_ms() - c->t_call), 0.0, 0.0);
+  c->parallel_for(nw - first, c->host_threads, [&](int i) { level_plan_one(R, G, offsets, poses, first + i); });
+  c->account_pool("plan");
+  if ((st = level_launch(c, R, WinSpan{first, nw, true, false})) != CSM_OK) return st;
+  if ((st = level_launch(c, R, WinSpan{0, nw, false, true})) != CSM_OK) return st;
+  if (c->profiling) {
+    char nm[48];
+    std::snprintf(nm, sizeof(nm), "host:plan+launch<%lld,split>", (long long)R.D.n_cand);
+    c->account(nm, (float)(now_ms() - t0), 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+// Join a level's launch and check its device finish.
+int level_join(csm_ctx* c, LevelRun& R) {
+  const int nw = (int)R.scan_of.size();
+  const double t1 = now_ms();
+  const int st = wait_run(c, R.pend);
+  if (st != CSM_OK) return st;
+  if (c->profiling) {
+    const float tw = (float)(now_ms() - t1);
+    c->account("host:wait", tw, 0.0, 0.0);
+    if (R.tag >= 0) {
+      char nm[48];
+      std::snprintf(nm, sizeof(nm), "host:wait<l%d,p%d>", R.tag / 8, R.tag % 8);
+      c->account(nm, tw, 0.0, 0.0);
+    }
+  }
+  if (R.dev)
+    for (int i = 0; i < nw; ++i)
+      if (R.fin[i].count < 0) return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
+  return CSM_OK;
+}
+
+// Complete window i of a joined level: pose, covariance and response
+// (BasedCorrelationScanMatch::ScanMatch :815-869).
+void level_complete_one(const LevelRun& R, const Geometry& G, double* poses, double* covs, double* responses,
+                        int64_t* argmax_flat, int i) {
+  thread_local std::vector<Entry> scratch;
+  const Dims& D = R.D;
+  const csm_param& P = R.P;
+  const int s = R.scan_of[(size_t)i];
+  const double f = P.search_space_resolution / G.mres;
+  const CandGeom C{R.plans[(size_t)i], R.angles + R.plans[(size_t)i].angle_off, f, D.n_space,
+                   (int64_t)D.n_space * D.n_space};
+  csm::FinishOut local;
+  const csm::FinishOut* o = nullptr;
+  if (R.dev) {
+    o = R.fin + i;
+  } else {
+    host_sort_finish(R.scores + (size_t)i * (size_t)D.n_cand, D, C, P, G, scratch, local);
+    o = &local;
+  }
+  if (argmax_flat) argmax_flat[s] = o->front_idx;
+  responses[s] = complete_window(*o, C, P, G, poses + 3 * s, covs + 9 * s, R.skip_lists);
+}
+
+// A signalled level with the fast pass's early signal: wait for it and split
+// the windows into those the fast pass settled and those the exact pass owes
+// (FinishOut::count == kFinishPending), the host's work on the first set
+// overlapping the exact pass.
+int level_wait_fast(csm_ctx* c, const LevelRun& R, std::vector<int>& settled, std::vector<int>& owed) {
+  const int nw = (int)R.scan_of.size();
+  const double t1 = now_ms();
+  const int st = wait_flag(c, R.pend, R.pend.fast_flag);
+  if (st != CSM_OK) return st;
+  if (c->profiling) c->account("host:wait_fast", (float)(now_ms() - t1), 0.0, 0.0);
+  settled.clear();
+  owed.clear();
+  settled.reserve((size_t)nw);
+  for (int i = 0; i < nw; ++i) (R.fin[i].count == csm::kFinishPending ? owed : settled).push_back(i);
+  return CSM_OK;
+}
+
+int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* responses,
+              int64_t* argmax_flat) {
+  const int nw = (int)R.scan_of.size();
+  if (nw == 0) return CSM_OK;
+  int st;
+  const Geometry G(c->info);
+  const int threads = (nw >= 64) ? c->host_threads : 1;
+  double t2;
+  if (R.dev && R.pend.fast_flag) {  // settled windows while the exact pass runs
+    std::vector<int> settled, owed;
+    if ((st = level_wait_fast(c, R, settled, owed)) != CSM_OK) return st;
+    t2 = now_ms();
+    c->parallel_for((int)settled.size(), threads, [&](int k) {
+      level_complete_one(R, G, poses, covs, responses, argmax_flat, settled[(size_t)k]);
+    });
+    if ((st = level_join(c, R)) != CSM_OK) return st;
+    c->parallel_for((int)owed.size(), owed.size() >= 32 ? threads : 1, [&](int k) {
+      level_complete_one(R, G, poses, covs, responses, argmax_flat, owed[(size_t)k]);
+    });
+  } else {
+    if ((st = level_join(c, R)) != CSM_OK) return st;
+    t2 = now_ms();
+    c->parallel_for(nw, threads, [&](int i) { level_complete_one(R, G, poses, covs, responses, argmax_flat, i); });
+  }
+  if (threads > 1) c->account_pool("complete");
+  if (c->profiling) {
+    const float tc = (float)(now_ms() - t2);
+    char nm[48];
+    std::snprintf(nm, sizeof(nm), "host:complete<%lld>", (long long)R.D.n_cand);
+    c->account("host:complete", tc, 0.0, 0.0);
+    c->account(nm, tc, 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+// level_end of R followed by level_begin of the next level N over the same
+// scans, fused: one pass of the host pool completes window i (its new pose)
+// and plans its next window right away, so the pool wakes once per level
+// transition instead of twice and the next launch goes out one pool round
+// trip earlier (the 3-level driver's critical path). `sum`
+// accumulates each scan's response (ScanMatchers::ScanMatch :252-256) before
+// the next level overwrites it. N's angle rows go to the other pinned buffer
+// of the slot: R's rows are still being read.
+int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const int64_t* offsets,
+                    const csm_param& P, double* poses, double* covs, double* responses, double* sum,
+                    const int32_t* scan_grid, int skip_lists) {
+  int st = level_prepare(c, n_scans, offsets, P, responses, nullptr, N, scan_grid, skip_lists, false);
+  if (st != CSM_OK) return st;
+  const int nw = (int)R.scan_of.size();
+  if (N.scan_of != R.scan_of || nw == 0) {  // not the same windows: one after the other
+    if ((st = level_end(c, R, poses, covs, responses, nullptr)) != CSM_OK) return st;
+    for (int s = 0; s < n_scans; ++s) sum[s] += responses[s];
+    return level_begin(c, n_scans, offsets, P, poses, responses, nullptr, N, scan_grid, skip_lists);
+  }
+  const bool early = R.dev && R.pend.fast_flag;
+  std::vector<int> settled, owed;
+  if ((st = early ? level_wait_fast(c, R, settled, owed) : level_join(c, R)) != CSM_OK) return st;
+  const double t2 = now_ms();
+  std::swap(c->h_angles, c->h_angles_next);
+  if ((st = level_alloc(c, offsets, N, c->h_angles)) != CSM_OK) return st;
+  const Geometry G(c->info);
+  const int threads = (nw >= 64) ? c->host_threads : 1;
+  auto one = [&](int i) {
+    level_complete_one(R, G, poses, covs, responses, nullptr, i);
+    const int s = R.scan_of[(size_t)i];
+    sum[s] += responses[s];
+    level_plan_one(N, G, offsets, poses, i);
+  };
+  if (early) {  // the settled windows while the exact pass runs, then the ones it owed
+    c->parallel_for((int)settled.size(), threads, [&](int k) { one(settled[(size_t)k]); });
+    if ((st = level_join(c, R)) != CSM_OK) return st;
+    c->parallel_for((int)owed.size(), owed.size() >= 32 ? threads : 1, [&](int k) { one(owed[(size_t)k]); });
+  } else {
+    c->parallel_for(nw, threads, one);
+  }
+  if (threads > 1) c->account_pool("complete+plan");
+  const double t3 = now_ms();
+  if ((st = level_launch(c, N)) != CSM_OK) return st;
+  if (c->profiling) {
+    c->account("host:launch", (float)(now_ms() - t3), 0.0, 0.0);
+    c->account("host:complete+plan", (float)(t3 - t2), 0.0, 0.0);
+    char nm[48];
+    std::snprintf(nm, sizeof(nm), "host:complete+plan<l%d,p%d>", R.tag / 8, R.tag % 8);
+    if (R.tag >= 0) c->account(nm, (float)(t3 - t2), 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P,
+                double* poses, double* covs, double* responses, int64_t* argmax_flat,
+                const int32_t* scan_grid, int skip_lists) {
+  if (P.type == CSM_FAST) return match_level_fast(c, n_scans, offsets, P, poses, covs, responses, argmax_flat);
+  LevelRun R;
+  int st = level_begin(c, n_scans, offsets, P, poses, responses, argmax_flat, R, scan_grid, skip_lists);
+  if (st != CSM_OK) return st;
+  return level_end(c, R, poses, covs, responses, argmax_flat);
+}
+
+// ScanMatchers::ScanMatch over a resident batch (scan_matchers.h:179-289),
+// parts in flight: while the device runs one part's level, the host
+// completes another part's previous level and plans its next one
+// (level_end_begin). Scans are independent, so the split changes no result.
+int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
+                           int n_levels, double* poses, double* covs, double* sum,
+                           const int32_t* scan_grid = nullptr) {
+  const int K = std::max(2, std::min(c->pipeline_parts, csm_ctx::kMaxParts));
+  // parts in flight share no few-window buffers: every part takes the
+  // throughput kernels (a part is hundreds of windows at the default split)
+  struct SmallOff {
+    csm_ctx* c;
+    bool was;
+    ~SmallOff() { c->small_path = was; }
+  } small_off{c, c->small_path};
+  c->small_path = false;
+  struct EarlyOn {  // level_end_begin / level_end complete settled windows early
+    csm_ctx* c;
+    ~EarlyOn() { c->early_now = false; }
+  } early_on{c};
+  c->early_now = true;
+  int32_t first[csm_ctx::kMaxParts], count[csm_ctx::kMaxParts];
+  for (int h = 0; h < K; ++h) {
+    first[h] = (int32_t)((int64_t)n_scans * h / K);
+    count[h] = (int32_t)((int64_t)n_scans * (h + 1) / K) - first[h];
+  }
+  std::vector<double> resp((size_t)n_scans, 0.0);
+  LevelRun R[2][csm_ctx::kMaxParts];  // by level parity: level l's run and level l + 1's
+  auto skip = [&](int l) { return c->skip_dead_lists ? live_lists(levels, n_levels, l) : 0; };
+  int st;
+  for (int h = 0; h < K; ++h) {
+    const int32_t s0 = first[h];
+    R[0][h].tag = h;
+    if (h > 0) c->swap_slot(h);
+    if (h == 0)  // the device waits for this one
+      st = level_begin_split(c, count[h], offsets + s0, levels[0], poses + 3 * (size_t)s0, resp.data() + s0, R[0][h],
+                             scan_grid ? scan_grid + s0 : nullptr, skip(0), c->first_windows);
+    else
+      st = level_begin(c, count[h], offsets + s0, levels[0], poses + 3 * (size_t)s0, resp.data() + s0, nullptr,
+                       R[0][h], scan_grid ? scan_grid + s0 : nullptr, skip(0));
+    if (h > 0) c->swap_slot(h);
+    if (st != CSM_OK) return st;
+  }
+  for (int l = 0; l < n_levels; ++l) {
+    for (int h = 0; h < K; ++h) {
+      const int32_t s0 = first[h];
+      LevelRun& cur = R[l & 1][h];
+      if (l + 1 < n_levels) {
+        R[(l + 1) & 1][h].tag = (l + 1) * 8 + h;
+        if (h > 0) c->swap_slot(h);
+        st = level_end_begin(c, cur, R[(l + 1) & 1][h], count[h], offsets + s0, levels[l + 1],
+                             poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, sum + s0,
+                             scan_grid ? scan_grid + s0 : nullptr, skip(l + 1));
+        if (h > 0) c->swap_slot(h);
+      } else {
+        st = level_end(c, cur, poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, nullptr);
+        for (int s = s0; s < s0 + count[h]; ++s) sum[(size_t)s] += resp[(size_t)s];
+      }
+      if (st != CSM_OK) return st;
+    }
+  }
+  return CSM_OK;
+}
+
+}  // namespace csmh
+
+using namespace csmh;
+
+extern "C" {
+
+int csm_scan_match_batch(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
+                         const csm_param* param, double* poses, double* covs, double* responses,
+                         int64_t* argmax_flat) {
+  if (!c || !param || !poses || !covs || !responses) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st;
+  if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
+  if (n_scans == 0) return CSM_OK;
+  const int64_t n_total = offsets[n_scans] - offsets[0];
+  if ((st = check_points(c, pts, n_total)) != CSM_OK) return st;
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  std::vector<int64_t> off(offsets, offsets + n_scans + 1);
+  for (auto& o : off) o -= offsets[0];
+  if ((st = upload_points(c, pts + 2 * offsets[0], n_total)) != CSM_OK) return st;
+  return match_level(c, n_scans, off.data(), *param, poses, covs, responses, argmax_flat);
+}
+
+int csm_scan_match(csm_ctx* c, const double* pts, int32_t n_points, const csm_param* param,
+                   double pose[3], double cov[9], double* response, int64_t* argmax_flat) {
+  if (!c || !response) return CSM_ERR_INVALID_ARG;
+  const int64_t off[2] = {0, n_points < 0 ? 0 : n_points};
+  if (n_points < 0) return c->fail(CSM_ERR_INVALID_ARG, "negative point count");
+  return csm_scan_match_batch(c, 1, pts, off, param, pose, cov, response, argmax_flat);
+}
+
+int csm_load_scans(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets) {
+  if (!c) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st;
+  c->loaded_n = -1;
+  c->loaded_grid.clear();
+  if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
+  const int64_t n_total = n_scans > 0 ? offsets[n_scans] - offsets[0] : 0;
+  if ((st = check_points(c, pts, n_total)) != CSM_OK) return st;
+  c->loaded_off.assign(offsets, offsets + n_scans + 1);
+  for (auto& o : c->loaded_off) o -= offsets[0];
+  if ((st = upload_points(c, n_total > 0 ? pts + 2 * offsets[0] : pts, n_total)) != CSM_OK) return st;
+  hipError_t e;
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(points)");
+  c->loaded_n = n_scans;
+  return CSM_OK;
+}
+
+int csm_load_scans_async(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets) {
+  if (!c) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st;
+  if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
+  const int64_t n_total = n_scans > 0 ? offsets[n_scans] - offsets[0] : 0;
+  if ((st = check_points(c, pts, n_total)) != CSM_OK) return st;
+  if (c->staged_count == 2) return c->fail(CSM_ERR_INVALID_ARG, "two batches already queued (csm_load_scans_async)");
+  hipError_t e;
+  if (!c->stage_stream && (e = hipStreamCreateWithFlags(&c->stage_stream, hipStreamNonBlocking)) != hipSuccess)
+    return c->hip_fail(e, "hipStreamCreate(stage)");
+  csm_ctx::Staged& S = c->staged[(c->staged_head + c->staged_count) % 2];
+  if (!S.ready && (e = hipEventCreateWithFlags(&S.ready, hipEventDisableTiming)) != hipSuccess)
+    return c->hip_fail(e, "hipEventCreate(stage)");
+  if (!S.maxabs_h && (e = hipHostMalloc((void**)&S.maxabs_h, sizeof(unsigned long long), hipHostMallocDefault)) !=
+                         hipSuccess)
+    return c->hip_fail(e, "hipHostMalloc(stage)");
+  const size_t bytes = (size_t)std::max<int64_t>(n_total, 1) * 2 * sizeof(double);
+  if ((e = S.pts.ensure(bytes)) != hipSuccess || (e = S.maxabs_dev.ensure(sizeof(unsigned long long))) != hipSuccess)
+    return c->hip_fail(e, "hipMalloc(stage)");
+  // the buffer's previous batch was matched by a call that has returned, so
+  // no kernel reads it any more
+  if ((e = hipMemsetAsync(S.maxabs_dev.p, 0, sizeof(unsigned long long), c->stage_stream)) != hipSuccess ||
+      (n_total > 0 && (e = hipMemcpyAsync(S.pts.p, pts + 2 * offsets[0], (size_t)n_total * 2 * sizeof(double),
+                                          hipMemcpyHostToDevice, c->stage_stream)) != hipSuccess) ||
+      (e = csm::launch_points_maxabs((const double*)S.pts.p, n_total, (unsigned long long*)S.maxabs_dev.p,
+                                     c->stage_stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(S.maxabs_h, S.maxabs_dev.p, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                          c->stage_stream)) != hipSuccess ||
+      (e = hipEventRecord(S.ready, c->stage_stream)) != hipSuccess)
+    return c->hip_fail(e, "csm_load_scans_async");
+  S.off.assign(offsets, offsets + n_scans + 1);
+  for (auto& o : S.off) o -= offsets[0];
+  S.n = n_scans;
+  c->staged_count++;
+  return CSM_OK;
+}
+
+int csm_host_alloc(size_t bytes, void** out) {
+  if (!out) return CSM_ERR_INVALID_ARG;
+  *out = nullptr;
+  return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocPortable) == hipSuccess ? CSM_OK : CSM_ERR_ALLOC;
+}
+
+int csm_host_free(void* p) { return (!p || hipHostFree(p) == hipSuccess) ? CSM_OK : CSM_ERR_INVALID_ARG; }
+
+int csm_scan_matchers_loaded(csm_ctx* c, const csm_param levels[3], int32_t use_fine, double* poses,
+                             double* covs, double* scores) {
+  if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (c->staged_count > 0) {  // the oldest queued batch becomes the loaded one
+    csm_ctx::Staged& S = c->staged[c->staged_head];
+    hipError_t e;
+    if ((e = hipEventSynchronize(S.ready)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize(stage)");
+    std::swap(c->pts, S.pts);
+    c->loaded_off.swap(S.off);
+    c->loaded_n = S.n;
+    c->loaded_grid.clear();
+    double m;
+    std::memcpy(&m, S.maxabs_h, sizeof(m));
+    c->pts_maxabs = m;
+    c->pts_cached = false;
+    c->staged_head = (c->staged_head + 1) % 2;
+    c->staged_count--;
+  }
+  if (c->loaded_n < 0) return c->fail(CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)");
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  const int32_t n_scans = c->loaded_n;
+  if (n_scans == 0) return CSM_OK;
+  const double t_call = now_ms();
+  c->t_call = t_call;
+  if (c->profiling && c->t_exit > 0.0) c->account("host:between_calls", (float)(t_call - c->t_exit), 0.0, 0.0);
+  // ScanMatchers::ScanMatch (scan_matchers.h:179-289), use_optimize = false:
+  // coarse, then (use_fine) fine and super-fine, pose fed forward in place.
+  std::vector<double> resp((size_t)n_scans, 0.0), sum((size_t)n_scans, 0.0);
+  const int n_levels = use_fine ? 3 : 1;
+  int st;
+  bool fast = false;
+  for (int l = 0; l < n_levels; ++l) fast |= levels[l].type == CSM_FAST;
+  const int32_t* grid = c->loaded_grid.empty() ? nullptr : c->loaded_grid.data();
+  for (int32_t s = 0; grid && s < n_scans; ++s)
+    if (grid[s] < 0 || grid[s] >= c->n_grids) return c->fail(CSM_ERR_INVALID_ARG, "scan grid outside the resident stack");
+  if (fast && grid) return c->fail(CSM_ERR_UNSUPPORTED, "FAST windows read grid 0 only");
+  if (n_scans >= c->pipeline_min && !fast) {
+    if ((st = match_levels_pipelined(c, n_scans, c->loaded_off.data(), levels, n_levels, poses, covs,
+                                     sum.data(), grid)) != CSM_OK)
+      return st;
+  } else {
+    for (int l = 0; l < n_levels; ++l) {
+      if ((st = match_level(c, n_scans, c->loaded_off.data(), levels[l], poses, covs, resp.data(), nullptr,
+                            grid, c->skip_dead_lists ? live_lists(levels, n_levels, l) : 0)) != CSM_OK)
+        return st;
+      for (int s = 0; s < n_scans; ++s) sum[(size_t)s] += resp[(size_t)s];
+    }
+  }
+  for (int s = 0; s < n_scans; ++s) scores[s] = sum[(size_t)s] / n_levels;  // :281
+  if (c->profiling) {
+    c->t_exit = now_ms();
+    c->account("host:call", (float)(c->t_exit - t_call), 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+int csm_scan_matchers_batch(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
+                            const csm_param levels[3], int32_t use_fine, double* poses, double* covs,
+                            double* scores) {
+  if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
+  const int st = csm_load_scans(c, n_scans, pts, offsets);
+  if (st != CSM_OK) return st;
+  return csm_scan_matchers_loaded(c, levels, use_fine, poses, covs, scores);
+}
+
+int csm_scan_matchers(csm_ctx* c, const double* pts, int32_t n_points, const csm_param levels[3],
+                      int32_t use_fine, double pose[3], double cov[9], double* score) {
+  if (!c || !score) return CSM_ERR_INVALID_ARG;
+  if (n_points < 0) return c->fail(CSM_ERR_INVALID_ARG, "negative point count");
+  const int64_t off[2] = {0, n_points};
+  return csm_scan_matchers_batch(c, 1, pts, off, levels, use_fine, pose, cov, score);
+}
+
+int csm_load_scans_grids(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
+                         const int32_t* grid_index) {
+  int st = csm_load_scans(c, n_scans, pts, offsets);
+  if (st != CSM_OK || !grid_index) return st;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->loaded_grid.assign(grid_index, grid_index + n_scans);
+  return CSM_OK;
+}
+
+int csm_scan_matchers_batch_grids(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
+                                  const int32_t* grid_index, const csm_param levels[3], int32_t use_fine,
+                                  double* poses, double* covs, double* scores) {
+  if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
+  const int st = csm_load_scans_grids(c, n_scans, pts, offsets, grid_index);
+  if (st != CSM_OK) return st;
+  return csm_scan_matchers_loaded(c, levels, use_fine, poses, covs, scores);
+}
+
+}  // extern "C"

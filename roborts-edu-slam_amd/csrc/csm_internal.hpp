@@ -68,6 +68,14 @@ struct LevelWork {
   // do, or the host could not have gone on) finds another tag and exits.
   int32_t* clear_word;
   int32_t clear_tag;
+  // The palette copy of gridi (score_box_palette_kernel): every cell's index
+  // into pal_vals, the grid's distinct fixed-point values (pal_vals[0] = 0,
+  // the outside value), one byte per cell in gridi's layout (row pitch
+  // `pitch` bytes, pal_stride bytes per grid). pal_n = 0: no palette.
+  int32_t pal_n;
+  const uint8_t* pal_grid;
+  const int32_t* pal_vals;
+  int64_t pal_stride;
 };
 
 // Argmax partial: best score of a block and its flat candidate index.
@@ -180,12 +188,6 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
                          hipStream_t stream, hipStream_t exact_stream = nullptr, hipEvent_t ev_fast = nullptr);
 
 // Launchers (csm_kernels.hip). All enqueue on `stream` and return hipError_t.
-hipError_t launch_score_all(const LevelWork& L, const ScanWork* d_scans,
-                            const double* d_pts, const AngleEntry* d_angles,
-                            double* d_out, int cpl, hipStream_t stream);
-hipError_t launch_score_best(const LevelWork& L, const ScanWork* d_scans,
-                             const double* d_pts, const AngleEntry* d_angles,
-                             BestPartial* d_partials, int cpl, hipStream_t stream);
 // Column kernel (v2): lane = one (theta, x) column of a window, KT rows (y)
 // per lane; L.blocks_per_scan = col_blocks * ktiles. kt = 4, 8 or 16.
 hipError_t launch_score_cols(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
@@ -196,10 +198,10 @@ hipError_t launch_score_cols(const LevelWork& L, const ScanWork* d_scans, const 
 // ceil(n_angles / (64/ns)). sq 16-byte loads per row segment (4*sq cells).
 // rows_pick_sq returns the sq of an instantiation with 4*sq >= need_seg, or 0.
 int rows_pick_sq(int ns, int need_seg);
-// dma: v4 (LDS-DMA staging, score_rowsd_kernel) instead of v3 (register staging).
+// v4: row segments staged in LDS by LDS-DMA (score_rowsd_kernel).
 hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
-                             int ns, int sq, bool dma, hipStream_t stream);
+                             int ns, int sq, hipStream_t stream);
 // FAST (branch-and-bound) tree scoring (csm_bnb.hip): every node of every
 // level, per window and angle, laid out level max_depth first.
 constexpr int kTreeMaxDepth = 12;
@@ -227,6 +229,24 @@ hipError_t launch_score_tiny(const LevelWork& L, const ScanWork* d_scans, const 
 // n_space <= 16; one wave per (window, angle), one 16-byte row piece per lane
 // per beam. blocks_per_scan = n_angles.
 bool box_supported(int ns);
+// v10 palette box kernel: one-cell steps with n_space <= kPalMaxSpace on a
+// grid of at most kPalMax distinct fixed-point values (L.pal_n > 0).
+constexpr int kPalMax = 256;
+constexpr int kPalMaxSpace = 13;
+bool box_palette_supported(int ns);
+hipError_t launch_score_box_palette(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
+                                    const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
+                                    hipStream_t stream);
+// The palette of n int32 cells (gridi with its padding): distinct values
+// (0 first, then ascending) into vals[0..kPalMax), their count into
+// state[0] (kPalMax + 1: more than kPalMax, no palette) and each cell's index
+// into idx. scratch: pal_scratch_ints(n) ints.
+int64_t pal_scratch_ints(int64_t n);
+// max over n points (x, y) of |x| + |y| (NaN if any is NaN) as the bits of a
+// non-negative double, max-ed into *out (zeroed by the caller)
+hipError_t launch_points_maxabs(const double* pts, int64_t n, unsigned long long* out, hipStream_t stream);
+hipError_t launch_build_palette(const int32_t* gridi, int64_t n, int32_t* scratch, int32_t* vals, int32_t* state,
+                                uint8_t* idx, hipStream_t stream);
 hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                             const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
                             hipStream_t stream);

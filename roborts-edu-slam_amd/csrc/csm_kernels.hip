@@ -4,15 +4,17 @@
 // MultiResolutionCorrelateScanMatcher::ScanMatch / GetResponse
 // (correlate_scan_matcher.h:552-584, 637-662) plus PenalizeResponse (:718-745).
 //
-// Mapping (DESIGN.md "Kernel"): one lane per candidate pose, CPL candidates per
-// lane, 256-thread workgroups, every workgroup inside one window (scan x level).
-// Lanes are ordered x-fastest inside a row of the window so that, for a given
-// beam, the 64 lanes of a wave gather from a few adjacent grid rows (the
-// candidate window maps onto a small patch around each beam endpoint). The
-// window's subsampled beams are staged in LDS 1024 at a time and broadcast to
-// all lanes. Each lane accumulates its beams sequentially in fp64, in the
-// reference's beam order, so the score is bit-identical to the reference's
-// for ANY fp32 grid (not only for the exactly-summable values real maps hold).
+// The general-purpose kernels, the fallbacks of the specialised families
+// (csm_box.hip one-cell steps, csm_phase.hip sub-cell steps, csm_tiny.hip
+// sub-cell spans, csm_split.hip few-window launches):
+//   v2 score_cols_kernel   any window and any grid: lane = (theta, x) column,
+//                          fp64 sums in the reference's beam order for any fp32
+//                          grid, or exact fixed-point sums (INT mode)
+//   v4 score_rowsd_kernel  INT mode, windows whose x-span fits a row segment:
+//                          row segments staged in LDS by LDS-DMA
+//   reduce_best_kernel     per-window argmax of the block partials
+// (r03 retired v1, lane per candidate, and v3, register-staged row segments:
+// every window they took, v2 or v4 takes, and no selection reached them.)
 //
 // Exactness: every double expression is evaluated in the reference's order
 // with contraction disabled (pragma below + -ffp-contract=off), the cast to
@@ -42,74 +44,6 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + (orig >> 3);
 }
 
-struct Lane {
-  double x, y, c, s, acc;
-  int64_t flat;  // reference enumeration index (theta, x, y)
-  double angle;
-  bool valid;
-};
-
-template <int CPL>
-__device__ __forceinline__ void setup_lanes(const LevelWork& L, const ScanWork& S,
-                                            const AngleEntry* __restrict__ angles,
-                                            int blk, Lane (&ln)[CPL]) {
-  const int64_t nss = (int64_t)L.n_space * L.n_space;
-#pragma unroll
-  for (int i = 0; i < CPL; ++i) {
-    const int64_t q = (int64_t)blk * (kBlock * CPL) + (int64_t)i * kBlock + threadIdx.x;
-    const bool valid = q < L.n_cand;
-    const int64_t qq = valid ? q : 0;
-    const int64_t a = qq / nss;
-    const int64_t r = qq - a * nss;
-    const int k = (int)(r / L.n_space);     // y index (row)
-    const int j = (int)(r - (int64_t)k * L.n_space);  // x index (fastest in lanes)
-    const AngleEntry ae = angles[S.angle_off + a];
-    ln[i].x = S.x0 + j * L.step_cells;      // :569
-    ln[i].y = S.y0 + k * L.step_cells;      // :572
-    ln[i].c = ae.cosine;
-    ln[i].s = ae.sine;
-    ln[i].angle = ae.angle;
-    ln[i].acc = 0.0;
-    ln[i].flat = (a * L.n_space + j) * L.n_space + k;  // order of :552-583
-    ln[i].valid = valid;
-  }
-}
-
-// Sum the window's beams for each of this lane's candidates (GetResponse
-// :645-654). All threads of the block must call this (barriers inside).
-template <int CPL>
-__device__ __forceinline__ void accumulate(const LevelWork& L, const ScanWork& S,
-                                           const double2* __restrict__ pts,
-                                           const float* __restrict__ grid,
-                                           double2* __restrict__ lds, Lane (&ln)[CPL]) {
-  const int sx = L.size_x, sy = L.size_y;
-  const float outside = L.outside;
-  for (int base = 0; base < S.n_used; base += kChunk) {
-    const int nb = min(kChunk, S.n_used - base);
-    __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += kBlock)
-      lds[b] = pts[S.pts_off + (int64_t)(base + b) * S.step];
-    __syncthreads();
-#pragma unroll 4
-    for (int b = 0; b < nb; ++b) {
-      const double2 p = lds[b];
-#pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        // LUT entry of :179-180, then the endpoint cell of :647-648.
-        const double lx = ln[i].c * p.x - ln[i].s * p.y;
-        const double ly = ln[i].s * p.x + ln[i].c * p.y;
-        const int gx = (int)((lx + ln[i].x) + 0.5);
-        const int gy = (int)((ly + ln[i].y) + 0.5);
-        const bool inb = ((unsigned)gx < (unsigned)sx) & ((unsigned)gy < (unsigned)sy);
-        const int idx = inb ? gy * sx + gx : 0;
-        float v = grid[idx];
-        v = inb ? v : outside;
-        ln[i].acc += (double)v;
-      }
-    }
-  }
-}
-
 // Divisor (:659) and centre penalty (:718-745) of one candidate.
 __device__ __forceinline__ double penalized(const LevelWork& L, const ScanWork& S, double acc,
                                            double x, double y, double angle) {
@@ -131,30 +65,6 @@ __device__ __forceinline__ double penalized(const LevelWork& L, const ScanWork& 
     }
   }
   return score;
-}
-
-__device__ __forceinline__ double finish_score(const LevelWork& L, const ScanWork& S,
-                                              const Lane& ln) {
-  return penalized(L, S, ln.acc, ln.x, ln.y, ln.angle);
-}
-
-template <int CPL>
-__global__ __launch_bounds__(kBlock) void score_all_kernel(
-    LevelWork L, const ScanWork* __restrict__ scans, const double2* __restrict__ pts,
-    const AngleEntry* __restrict__ angles, double* __restrict__ out) {
-  __shared__ double2 lds[kChunk];
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  clear_word(L);
-  const int scan = bid / L.blocks_per_scan;
-  const int blk = bid - scan * L.blocks_per_scan;
-  const ScanWork S = scans[scan];
-  const float* grid = L.grid + (int64_t)S.grid_index * L.grid_stride;
-  Lane ln[CPL];
-  setup_lanes<CPL>(L, S, angles, blk, ln);
-  accumulate<CPL>(L, S, pts, grid, lds, ln);
-#pragma unroll
-  for (int i = 0; i < CPL; ++i)
-    if (ln[i].valid) out[S.out_off + ln[i].flat] = finish_score(L, S, ln[i]);
 }
 
 __device__ __forceinline__ bool better(double s, int64_t f, double bs, int64_t bf) {
@@ -328,7 +238,18 @@ __global__ __launch_bounds__(64) void score_cols_kernel(
   }
 }
 
-// ---- v3: row-segment kernel (INT mode) -------------------------------------
+// 16-byte buffer load written straight into LDS at lds + 16 * lane. The
+// builtin has no host-side form; the guard only keeps hipcc's host pass (which
+// must still emit the kernel's launch stub) from seeing it.
+__device__ __forceinline__ void buffer_load_lds16(__amdgpu_buffer_rsrc_t rsrc,
+                                                  __attribute__((address_space(3))) int32_t* lds,
+                                                  int voffset) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, lds, 16, voffset, 0, 0, 0);
+#endif
+}
+
+// ---- v4: row-segment kernel, LDS-DMA staging (INT mode) --------------------
 // For one beam and one angle the endpoint cells of a window's candidates form
 // a separable set: ix depends only on the x step j, iy only on the y step k
 // (:647-648). With lane (theta, r) of an angle group of NS lanes:
@@ -350,194 +271,10 @@ __global__ __launch_bounds__(64) void score_cols_kernel(
 // check, x through a zero pad column of the tile. A lane whose x-span ever
 // exceeds SEG (impossible for the host's SEG; kept as a guard) is recomputed
 // exactly after the loop.
-template <int NS, int SQ, bool BEST>
-__global__ __launch_bounds__(64) void score_rows_kernel(
-    LevelWork L, const ScanWork* __restrict__ scans, const double2* __restrict__ pts,
-    const AngleEntry* __restrict__ angles, double* __restrict__ out,
-    BestPartial* __restrict__ partials) {
-  constexpr int G = 64 / NS;           // angle groups per wave
-  constexpr int R = G * NS;            // row segments per beam
-  constexpr int SEG = 4 * SQ;          // cells per row segment
-  constexpr int RS = SEG + 4;          // tile row stride: segment + zero pad (16-byte multiple)
-  constexpr int NP = R * SQ;           // 16-byte pieces per beam
-  constexpr int NI = (NP + 63) / 64;   // gathers per beam
-  typedef int32_t v4i __attribute__((ext_vector_type(4)));
-  // Groups are spaced GS floats apart with GS = GT (mod 64): a consumer read
-  // instruction (one k) then puts group g on banks [g*GT, g*GT + NS), disjoint
-  // for the groups of a wave (without the spacing 4 groups shared banks:
-  // SQ_LDS_BANK_CONFLICT was 43% of the kernel's cycles).
-  constexpr int GT = (64 / G) / 4 * 4 < 4 ? 4 : (64 / G) / 4 * 4;
-  constexpr int GS = NS * RS + (((GT - (NS * RS) % 64) % 64) + 64) % 64;
-  __shared__ __attribute__((aligned(16))) int32_t tile[G * GS + RS];  // + a sink row
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  clear_word(L);
-  const int win = bid / L.blocks_per_scan;
-  const int blk = bid - win * L.blocks_per_scan;
-  const ScanWork S = scans[win];
-  const int lane = threadIdx.x;
-  const int g = lane / NS;
-  const int r = lane - g * NS;
-  const int a_raw = blk * G + g;
-  const bool valid = (g < G) && (a_raw < L.n_angles);
-  const int a = valid ? a_raw : 0;
-  const int gbase_f = (g < G) ? g * GS : 0;  // tile float offset of this group's k = 0 row
-  const AngleEntry ae = angles[S.angle_off + a];
-  const double f = L.step_cells;
-  const double x_0 = S.x0 + 0 * f;  // :569 at j = 0
-  const double x_r = S.x0 + r * f;  // :569 at j = r
-  const double y_r = S.y0 + r * f;  // :572 at k = r
-  const int sx = L.size_x, sy = L.size_y;
-  const int pitch4 = L.pitch * 4;  // gridi row stride in bytes
-  const int xs_max = sx - SEG;     // host: sx >= SEG
-  const double2* __restrict__ P = pts + S.pts_off;
-  const int step = S.step;
-  const int n_used = S.n_used;
-  const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
-  const int32_t* gbase = (const int32_t*)(((uint64_t)hi << 32) | lo);
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)gbase, (short)0, (int)(L.gridi_stride * 4), 0x00020000);
-  constexpr int kBadOff = 0x7F800000;  // >= 4*pitch*sy (host), + 16*SQ still < 2^31: reads 0
-
-  // This lane's piece of gather i: owner row (bpermute source), byte offset
-  // inside the segment, and its tile slot (idle pieces go to the sink row).
-  int src4[NI], qoff[NI], dst[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int p = i * 64 + lane;
-    const bool act = p < NP;
-    const int rho = act ? p / SQ : 0;
-    const int q = act ? p - rho * SQ : 0;
-    src4[i] = rho * 4;
-    qoff[i] = act ? 16 * q : -1;
-    const int rg = rho / NS;
-    dst[i] = act ? (rg * GS + (rho - rg * NS) * RS + 4 * q) * 4 : G * GS * 4;
-  }
-  if (lane < R) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tile[gbase_f + r * RS + SEG + q] = 0;  // zero pad column
-  }
-
-  // Beam b: gather this lane's pieces, and the LDS byte address of its own
-  // column (the pad column when x is off the grid).
-  auto prep = [&](int b, v4i (&v)[NI], int& rd, bool& bad) {
-    const double2 p = P[(int64_t)b * step];
-    const double lx = ae.cosine * p.x - ae.sine * p.y;  // :179
-    const double ly = ae.sine * p.x + ae.cosine * p.y;  // :180
-    const int ix0 = (int)((lx + x_0) + 0.5);
-    const int ixr = (int)((lx + x_r) + 0.5);
-    const int iyr = (int)((ly + y_r) + 0.5);
-    const int xs = min(max(ix0, 0), xs_max);
-    const int rowoff = ((unsigned)iyr < (unsigned)sy) ? __mul24(iyr, pitch4) + xs * 4 : kBadOff;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int o = __builtin_amdgcn_ds_bpermute(src4[i], rowoff);
-      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, qoff[i] < 0 ? kBadOff : o + qoff[i], 0, 0);
-    }
-    const int pos = ixr - xs;
-    const bool inx = (unsigned)ixr < (unsigned)sx;
-    bad |= inx & ((unsigned)pos >= (unsigned)SEG);
-    rd = (gbase_f + (inx ? pos : SEG)) * 4;
-  };
-  auto consume = [&](const v4i (&v)[NI], int rd, int32_t (&part)[NS]) {
-    char* tb = reinterpret_cast<char*>(tile);
-#pragma unroll
-    for (int i = 0; i < NI; ++i) *reinterpret_cast<v4i*>(tb + dst[i]) = v[i];
-#pragma unroll
-    for (int k = 0; k < NS; ++k) part[k] += *reinterpret_cast<const int32_t*>(tb + rd + k * RS * 4);
-  };
-
-  int64_t acci[NS];
-#pragma unroll
-  for (int k = 0; k < NS; ++k) acci[k] = 0;
-  bool bad = false;
-  constexpr int kFold = 32;  // 32 * (2^26 - 1) < 2^31 (ensure_int_grid)
-  v4i va[NI], vb[NI];
-  int ra = 0, rb = 0;
-  prep(0, va, ra, bad);
-  for (int base = 0; base < n_used; base += kFold) {
-    const int nb = min(kFold, n_used - base);
-    int32_t part[NS];
-#pragma unroll
-    for (int k = 0; k < NS; ++k) part[k] = 0;
-    for (int b = 0; b < nb; b += 2) {
-      prep(min(base + b + 1, n_used - 1), vb, rb, bad);
-      __builtin_amdgcn_sched_barrier(0);
-      consume(va, ra, part);
-      prep(min(base + b + 2, n_used - 1), va, ra, bad);
-      __builtin_amdgcn_sched_barrier(0);
-      if (b + 1 < nb) consume(vb, rb, part);
-    }
-#pragma unroll
-    for (int k = 0; k < NS; ++k) acci[k] += part[k];
-  }
-  if (bad) {  // guard (never taken for the host's SEG): exact per-cell recompute
-#pragma unroll
-    for (int k = 0; k < NS; ++k) acci[k] = 0;
-    for (int b = 0; b < n_used; ++b) {
-      const double2 p = P[(int64_t)b * step];
-      const double lx = ae.cosine * p.x - ae.sine * p.y;
-      const double ly = ae.sine * p.x + ae.cosine * p.y;
-      const int gx = (int)((lx + x_r) + 0.5);
-      const int gx4 = ((unsigned)gx < (unsigned)sx) ? gx * 4 : -(1 << 30);
-#pragma unroll
-      for (int k = 0; k < NS; ++k) {
-        const int gy = (int)((ly + (S.y0 + k * f)) + 0.5);
-        const int o = ((unsigned)gy < (unsigned)sy && gx4 >= 0) ? __mul24(gy, pitch4) + gx4 : kBadOff;
-        acci[k] += __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0);
-      }
-    }
-  }
-  double bs = -1.0e300;
-  int64_t bf = INT64_MAX;
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    if (valid) {
-      const double acc = (double)(acci[k] + (int64_t)n_used * L.outside_i) * L.int_scale;
-      const double yk = S.y0 + k * f;  // :572
-      const double score = penalized(L, S, acc, x_r, yk, ae.angle);
-      const int64_t flat = ((int64_t)a * NS + r) * NS + k;
-      if (BEST) {
-        if (better(score, flat, bs, bf)) {
-          bs = score;
-          bf = flat;
-        }
-      } else {
-        out[S.out_off + flat] = score;
-      }
-    }
-  }
-  if (BEST) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double os = __shfl_down(bs, o, 64);
-      const int64_t of = __shfl_down(bf, o, 64);
-      if (better(os, of, bs, bf)) {
-        bs = os;
-        bf = of;
-      }
-    }
-    if (lane == 0) partials[(int64_t)win * L.blocks_per_scan + blk] = BestPartial{bs, bf};
-  }
-}
-
-// 16-byte buffer load written straight into LDS at lds + 16 * lane. The
-// builtin has no host-side form; the guard only keeps hipcc's host pass (which
-// must still emit the kernel's launch stub) from seeing it.
-__device__ __forceinline__ void buffer_load_lds16(__amdgpu_buffer_rsrc_t rsrc,
-                                                  __attribute__((address_space(3))) int32_t* lds,
-                                                  int voffset) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, lds, 16, voffset, 0, 0, 0);
-#endif
-}
-
-// ---- v4: row-segment kernel, LDS-DMA staging (INT mode) --------------------
-// v3's data flow with the 16-byte pieces written straight into LDS by
-// global_load_lds_dwordx4 (dest = wave-uniform base + 16 * lane): no VGPR
-// staging and no ds_write_b128 (13 LDS cycles each, the largest LDS cost of
-// v3). Pieces are dealt row-major, so the LDS image is [row][SEG] with rows
+//
+// The 16-byte pieces go straight into LDS by global_load_lds_dwordx4 (dest =
+// wave-uniform base + 16 * lane): no VGPR staging and no ds_write_b128 (13
+// LDS cycles each, the largest LDS cost of r01's register-staged form). Pieces are dealt row-major, so the LDS image is [row][SEG] with rows
 // contiguous; beams alternate between two images (DMA of beam b+1 in flight
 // while beam b is summed, counted vmcnt). DMA has no range check: rows outside
 // the grid point at the zero row the host appends to gridi, columns outside
@@ -796,59 +533,6 @@ __global__ __launch_bounds__(64 * BS) void score_rowsd_kernel(
   }
 }
 
-template <int CPL>
-__global__ __launch_bounds__(kBlock) void score_best_kernel(
-    LevelWork L, const ScanWork* __restrict__ scans, const double2* __restrict__ pts,
-    const AngleEntry* __restrict__ angles, BestPartial* __restrict__ partials) {
-  __shared__ double2 lds[kChunk];
-  __shared__ double red_s[kBlock / 64];
-  __shared__ int64_t red_f[kBlock / 64];
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  clear_word(L);
-  const int scan = bid / L.blocks_per_scan;
-  const int blk = bid - scan * L.blocks_per_scan;
-  const ScanWork S = scans[scan];
-  const float* grid = L.grid + (int64_t)S.grid_index * L.grid_stride;
-  Lane ln[CPL];
-  setup_lanes<CPL>(L, S, angles, blk, ln);
-  accumulate<CPL>(L, S, pts, grid, lds, ln);
-  double bs = -1.0e300;
-  int64_t bf = INT64_MAX;
-#pragma unroll
-  for (int i = 0; i < CPL; ++i) {
-    if (!ln[i].valid) continue;
-    const double s = finish_score(L, S, ln[i]);
-    if (better(s, ln[i].flat, bs, bf)) {
-      bs = s;
-      bf = ln[i].flat;
-    }
-  }
-  // wave reduce (64 lanes), then across the block's 4 waves
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double os = __shfl_down(bs, off, 64);
-    const int64_t of = __shfl_down(bf, off, 64);
-    if (better(os, of, bs, bf)) {
-      bs = os;
-      bf = of;
-    }
-  }
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane == 0) {
-    red_s[wave] = bs;
-    red_f[wave] = bf;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < kBlock / 64; ++w)
-      if (better(red_s[w], red_f[w], bs, bf)) {
-        bs = red_s[w];
-        bf = red_f[w];
-      }
-    partials[(int64_t)scan * L.blocks_per_scan + blk] = BestPartial{bs, bf};
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void reduce_best_kernel(const BestPartial* __restrict__ in,
                                                              int32_t per, BestPartial* __restrict__ out) {
   __shared__ double red_s[kBlock / 64];
@@ -889,38 +573,6 @@ __global__ __launch_bounds__(kBlock) void reduce_best_kernel(const BestPartial* 
 }
 
 }  // namespace
-
-hipError_t launch_score_all(const LevelWork& L, const ScanWork* d_scans, const double* d_pts_raw,
-                            const AngleEntry* d_angles, double* d_out, int cpl,
-                            hipStream_t stream) {
-  const double2* d_pts = reinterpret_cast<const double2*>(d_pts_raw);
-  const int64_t nblk = (int64_t)L.blocks_per_scan * L.n_scans;
-  if (nblk <= 0 || nblk > INT32_MAX) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)nblk), block(kBlock);
-  switch (cpl) {
-    case 1: hipLaunchKernelGGL(score_all_kernel<1>, grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_out); break;
-    case 2: hipLaunchKernelGGL(score_all_kernel<2>, grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_out); break;
-    case 4: hipLaunchKernelGGL(score_all_kernel<4>, grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_out); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_score_best(const LevelWork& L, const ScanWork* d_scans, const double* d_pts_raw,
-                             const AngleEntry* d_angles, BestPartial* d_partials, int cpl,
-                             hipStream_t stream) {
-  const double2* d_pts = reinterpret_cast<const double2*>(d_pts_raw);
-  const int64_t nblk = (int64_t)L.blocks_per_scan * L.n_scans;
-  if (nblk <= 0 || nblk > INT32_MAX) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)nblk), block(kBlock);
-  switch (cpl) {
-    case 1: hipLaunchKernelGGL(score_best_kernel<1>, grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_partials); break;
-    case 2: hipLaunchKernelGGL(score_best_kernel<2>, grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_partials); break;
-    case 4: hipLaunchKernelGGL(score_best_kernel<4>, grid, block, 0, stream, L, d_scans, d_pts, d_angles, d_partials); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
 
 template <int KT>
 static hipError_t launch_cols_kt(const LevelWork& L, const ScanWork* d_scans, const double2* d_pts,
@@ -1009,29 +661,16 @@ hipError_t launch_rowsd(const LevelWork& L, const ScanWork* d_scans, const doubl
 
 hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const double* d_pts_raw,
                              const AngleEntry* d_angles, double* d_out, BestPartial* d_partials,
-                             int ns, int sq, bool dma, hipStream_t stream) {
+                             int ns, int sq, hipStream_t stream) {
   const double2* d_pts = reinterpret_cast<const double2*>(d_pts_raw);
   const int64_t nblk = (int64_t)L.blocks_per_scan * L.n_scans;
   if (nblk <= 0 || nblk > INT32_MAX || !L.int_mode || L.size_x < 4 * sq) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)nblk), block(64);
-  const int bs = dma ? rows_beam_split(nblk) : 1;
-#define CSM_ROWS_LAUNCH(KERN, N, Q)                                                               \
-  do {                                                                                            \
-    if (d_partials)                                                                               \
-      hipLaunchKernelGGL((KERN<N, Q, true>), grid, block, 0, stream, L, d_scans, d_pts, d_angles, \
-                         d_out, d_partials);                                                      \
-    else                                                                                          \
-      hipLaunchKernelGGL((KERN<N, Q, false>), grid, block, 0, stream, L, d_scans, d_pts,         \
-                         d_angles, d_out, d_partials);                                            \
-  } while (0)
+  const dim3 grid((unsigned)nblk);
+  const int bs = rows_beam_split(nblk);
 #define CSM_ROWSD_LAUNCH(N, Q, B) \
   return launch_rowsd<N, Q, B>(L, d_scans, d_pts, d_angles, d_out, d_partials, grid, stream)
 #define CSM_ROWS_CASE(N, Q)                     \
   if (ns == N && sq == Q) {                     \
-    if (!dma) {                                 \
-      CSM_ROWS_LAUNCH(score_rows_kernel, N, Q); \
-      return hipGetLastError();                 \
-    }                                           \
     if (bs == 1) CSM_ROWSD_LAUNCH(N, Q, 1);     \
     if (bs == 2) CSM_ROWSD_LAUNCH(N, Q, 2);     \
     if (bs == 4) CSM_ROWSD_LAUNCH(N, Q, 4);     \
@@ -1040,8 +679,35 @@ hipError_t launch_score_rows(const LevelWork& L, const ScanWork* d_scans, const 
   CSM_ROWS_LIST(CSM_ROWS_CASE)
 #undef CSM_ROWS_CASE
 #undef CSM_ROWSD_LAUNCH
-#undef CSM_ROWS_LAUNCH
   return hipErrorInvalidValue;
+}
+
+// max |x| + |y| over a batch's points (csm_load_scans_async): the bound
+// int_mode_ok needs, found on the device while the batch uploads instead of
+// by the host reading every point. Non-negative doubles order like their
+// bits, and a NaN's bits exceed +inf's, so an integer max keeps NaN.
+__global__ __launch_bounds__(256) void points_maxabs_kernel(const double2* __restrict__ p, int64_t n,
+                                                            unsigned long long* __restrict__ out) {
+  unsigned long long m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double2 q = p[i];
+    const double a = fabs(q.x) + fabs(q.y);
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, a);
+    m = b > m ? b : m;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long t = __shfl_xor(m, o, 64);
+    m = t > m ? t : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+hipError_t launch_points_maxabs(const double* pts, int64_t n, unsigned long long* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(points_maxabs_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     reinterpret_cast<const double2*>(pts), n, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_reduce_best(const BestPartial* d_partials, int32_t blocks_per_scan,

@@ -1,0 +1,185 @@
+// csm_palette.hip — the palette copy of the fixed-point grid, read by the v10
+// palette box kernel (csm_box.hip).
+//
+// A scan-match grid holds a handful of distinct cell values: the unknown
+// value (0 in gridi, which stores value - outside), the occupied value and
+// the levels of the blur splat (occu_grid_map.h:83-105,531-576: a cell keeps
+// the max of kernel * offset). The palette is those values, 0 first then
+// ascending, and the copy holds every cell's index into it, one byte per cell
+// in gridi's own layout (same pitch, same zero columns and rows). A grid with
+// more than kPalMax distinct values has no palette (the box kernels read
+// gridi itself).
+//
+//   pal_collect_kernel  each block dedupes its slice of cells in an LDS hash
+//                       and lists its values (or marks an overflow)
+//   pal_merge_kernel    one block merges the lists, sorts them, writes the
+//                       palette and its size
+//   pal_index_kernel    every cell's index by binary search in the palette
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "csm_internal.hpp"
+
+namespace csm {
+namespace {
+
+constexpr int kPalHash = 1024;            // LDS hash slots (>= 2 * (kPalMax + 256))
+constexpr int32_t kPalEmpty = INT32_MIN;  // never a gridi value (|value| < 2^26)
+constexpr int kPalCollectBlocks = 1024;
+constexpr int kPalList = kPalMax + 1;     // per block: count, then values
+
+__device__ __forceinline__ uint32_t pal_hash(int32_t v) { return ((uint32_t)v * 2654435761u) >> 22; }
+
+// Insert v (non-zero) into the LDS set; `count` counts the distinct values.
+__device__ __forceinline__ void pal_insert(int32_t* key, int32_t* count, int32_t v) {
+  if (v == 0 || *(volatile int32_t*)count > kPalMax) return;
+  uint32_t h = pal_hash(v);
+  for (int probe = 0; probe < kPalHash; ++probe) {
+    const int32_t k = key[h];
+    if (k == v) return;
+    if (k == kPalEmpty) {
+      const int32_t old = atomicCAS(&key[h], kPalEmpty, v);
+      if (old == kPalEmpty) {
+        atomicAdd(count, 1);
+        return;
+      }
+      if (old == v) return;
+    }
+    h = (h + 1) & (kPalHash - 1);
+  }
+}
+
+__global__ __launch_bounds__(256) void pal_collect_kernel(const int4* __restrict__ g, int64_t n4, int64_t per4,
+                                                          int32_t* __restrict__ lists) {
+  __shared__ int32_t key[kPalHash];
+  __shared__ int32_t count, pos;
+  for (int i = threadIdx.x; i < kPalHash; i += 256) key[i] = kPalEmpty;
+  if (threadIdx.x == 0) {
+    count = 0;
+    pos = 0;
+  }
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * per4, b1 = min(n4, b0 + per4);
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += 256) {
+    const int4 v = g[i];
+    pal_insert(key, &count, v.x);
+    pal_insert(key, &count, v.y);
+    pal_insert(key, &count, v.z);
+    pal_insert(key, &count, v.w);
+  }
+  __syncthreads();
+  int32_t* out = lists + (int64_t)blockIdx.x * kPalList;
+  if (count > kPalMax) {
+    if (threadIdx.x == 0) out[0] = kPalMax + 1;
+    return;
+  }
+  for (int i = threadIdx.x; i < kPalHash; i += 256)
+    if (key[i] != kPalEmpty) out[1 + atomicAdd(&pos, 1)] = key[i];
+  if (threadIdx.x == 0) out[0] = count;
+}
+
+__global__ __launch_bounds__(256) void pal_merge_kernel(const int32_t* __restrict__ lists, int nb,
+                                                        int32_t* __restrict__ vals, int32_t* __restrict__ state) {
+  __shared__ int32_t key[kPalHash];
+  __shared__ int32_t sorted[256];
+  __shared__ int32_t count, pos, over;
+  for (int i = threadIdx.x; i < kPalHash; i += 256) key[i] = kPalEmpty;
+  if (threadIdx.x == 0) {
+    count = 0;
+    pos = 0;
+    over = 0;
+  }
+  __syncthreads();
+  for (int b = 0; b < nb; ++b) {
+    const int32_t* in = lists + (int64_t)b * kPalList;
+    const int32_t c = in[0];
+    if (c > kPalMax) {
+      if (threadIdx.x == 0) over = 1;
+      break;  // uniform: every thread read the same count
+    }
+    for (int i = threadIdx.x; i < c; i += 256) pal_insert(key, &count, in[1 + i]);
+  }
+  __syncthreads();
+  // index 0 is the zero value: at most kPalMax - 1 others
+  if (over || count > kPalMax - 1) {
+    if (threadIdx.x == 0) state[0] = kPalMax + 1;
+    return;
+  }
+  sorted[threadIdx.x] = INT32_MAX;
+  __syncthreads();
+  for (int i = threadIdx.x; i < kPalHash; i += 256)
+    if (key[i] != kPalEmpty) sorted[atomicAdd(&pos, 1)] = key[i];
+  __syncthreads();
+  // bitonic sort of the 256 slots (padding INT32_MAX sorts last)
+  const int t = threadIdx.x;
+  for (int size = 2; size <= 256; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int o = t ^ stride;
+      if (o > t) {
+        const bool up = (t & size) == 0;
+        const int32_t x = sorted[t], y = sorted[o];
+        if ((x > y) == up) {
+          sorted[t] = y;
+          sorted[o] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0) vals[0] = 0;
+  if (t < count) vals[1 + t] = sorted[t];
+  if (t == 0) state[0] = count + 1;
+}
+
+__global__ __launch_bounds__(256) void pal_index_kernel(const int4* __restrict__ g, int64_t n4,
+                                                        const int32_t* __restrict__ vals,
+                                                        const int32_t* __restrict__ state,
+                                                        uint32_t* __restrict__ idx4) {
+  __shared__ int32_t sv[kPalMax];
+  const int m = state[0];
+  if (m < 1 || m > kPalMax) return;  // no palette: nothing to index
+  for (int i = threadIdx.x; i < m; i += 256) sv[i] = vals[i];
+  __syncthreads();
+  auto find = [&](int32_t v) -> uint32_t {
+    if (v == 0) return 0u;
+    int lo = 1, hi = m - 1;  // sv[1..m-1] ascending; v is one of them
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sv[mid] < v)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    return (uint32_t)lo;
+  };
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int4 v = g[i];
+    idx4[i] = find(v.x) | (find(v.y) << 8) | (find(v.z) << 16) | (find(v.w) << 24);
+  }
+}
+
+}  // namespace
+
+int64_t pal_scratch_ints(int64_t n) {
+  const int64_t n4 = n / 4;
+  const int64_t nb = n4 <= 0 ? 1 : (n4 + 4095) / 4096 < kPalCollectBlocks ? (n4 + 4095) / 4096 : kPalCollectBlocks;
+  return nb * kPalList;
+}
+
+hipError_t launch_build_palette(const int32_t* gridi, int64_t n, int32_t* scratch, int32_t* vals, int32_t* state,
+                                uint8_t* idx, hipStream_t stream) {
+  if (n <= 0 || n % 4 != 0 || !gridi || !scratch || !vals || !state || !idx) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  const int nb = (int)(pal_scratch_ints(n) / kPalList);
+  const int64_t per4 = (n4 + nb - 1) / nb;
+  const int4* g = reinterpret_cast<const int4*>(gridi);
+  hipLaunchKernelGGL(pal_collect_kernel, dim3(nb), dim3(256), 0, stream, g, n4, per4, scratch);
+  hipLaunchKernelGGL(pal_merge_kernel, dim3(1), dim3(256), 0, stream, scratch, nb, vals, state);
+  const int64_t blocks = (n4 + 255) / 256 < 8192 ? (n4 + 255) / 256 : 8192;
+  hipLaunchKernelGGL(pal_index_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, g, n4, vals, state,
+                     reinterpret_cast<uint32_t*>(idx));
+  return hipGetLastError();
+}
+
+}  // namespace csm

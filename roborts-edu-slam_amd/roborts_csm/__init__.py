@@ -298,7 +298,20 @@ class Context:
         self._loaded = (pts, off)
         self._check(_lib.csm_load_scans(self._h, off.size - 1, _dptr(pts), _i64ptr(off)))
 
+    def load_scans_async(self, points, offsets):
+        """Queue a batch (csm_load_scans_async): its upload runs beside the
+        current match; the next scan_matchers_loaded takes it. `points` should
+        be pinned (pinned_empty) and must not change until then."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 2)
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        q = self.__dict__.setdefault("_queued", [])
+        self._check(_lib.csm_load_scans_async(self._h, off.size - 1, _dptr(pts), _i64ptr(off)))
+        q.append((pts, off))
+
     def scan_matchers_loaded(self, levels, poses, covs, use_fine: bool = True):
+        q = self.__dict__.get("_queued")
+        if q:  # the library takes the oldest queued batch
+            self._loaded = q.pop(0)
         n = self._loaded[1].size - 1
         assert poses.dtype == np.float64 and poses.flags.c_contiguous and poses.size == 3 * n
         assert covs.dtype == np.float64 and covs.flags.c_contiguous and covs.size == 9 * n
@@ -425,6 +438,33 @@ class Context:
                      nodes=list(st.nodes), probe_leaves=st.probe_leaves, beam_reads=st.beam_reads,
                      build_ms=st.build_ms, syncs=st.syncs, top_box=bool(st.top_box))
         return b, int(w.value), stats
+
+
+class PinnedArray:
+    """A numpy array over pinned host memory (csm_host_alloc), for
+    load_scans_async inputs; freed with the object."""
+
+    def __init__(self, shape, dtype=np.float64):
+        self.dtype = np.dtype(dtype)
+        n = int(np.prod(shape))
+        p = C.c_void_p()
+        if _lib.csm_host_alloc(max(1, n) * self.dtype.itemsize, C.byref(p)) != 0:
+            raise MemoryError("csm_host_alloc failed")
+        self._p = p
+        buf = (C.c_char * (max(1, n) * self.dtype.itemsize)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=self.dtype, count=n).reshape(shape)
+
+    def close(self):
+        if getattr(self, "_p", None) is not None and self._p.value:
+            self.array = None
+            _lib.csm_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def build_digest() -> str:

@@ -1,0 +1,187 @@
+"""GPU parity of the v10 palette box kernel (csrc/csm_box.hip
+score_box_palette_kernel, csrc/csm_palette.hip) against the CPU oracle.
+
+The kernel reads one-cell-step windows (n_space <= 13: the coarse level of
+every shipped parameter set, correlate_scan_matcher.h:552-584,637-662)
+through the palette copy of the fixed-point grid: one byte per cell, the
+index of the cell's value among the grid's distinct values. The bar is the
+same as for every other kernel: all scores bit for bit, the argmax index
+equal. Covered here: the palette's size limits (256 values: palette kernel;
+257: the grid has no palette and the v9 grouped kernel runs), cells below the
+outside value (negative fixed-point entries), windows off every edge, beams
+on rounding boundaries, a grid stack (the palette grid's per-grid stride),
+and the palette rebuilt after row and cell refreshes of a resident map.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import pyoracle as O  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def f1(golden_dir):
+    return np.load(os.path.join(golden_dir, "f1_config1.npz"))
+
+
+def _level(n_points):
+    from roborts_csm.params import SIM_YAML_LEVELS
+    lv = SIM_YAML_LEVELS[0]  # 0.6 m at 0.05 m on a 0.05 m map: 13 x 13, one-cell steps
+    return lv.with_(use_point_size=int(n_points))
+
+
+def _points(f1):
+    extra = np.array([[0.0, 0.0], [0.0, 0.0], [1.0, -2.0], [-300.0, 3.0], [2.0, -300.0], [250.0, 250.0],
+                      [0.25, 0.0]])
+    return np.ascontiguousarray(np.concatenate([f1["points"], extra]))
+
+
+def _centers(res, size=0.6):
+    half = (size / res) * 0.5
+    return [np.array(c) for c in ([100.5 + half, 200.5 + half, 0.0], [100.5 + half, 200.5 + half, 1.3],
+                                  [200.0 + 3 * 2.0 ** -43, 199.0 + 2.0 ** -43, 0.7], [3.2, 2.1, -2.5],
+                                  [396.0, 398.0, 1.0], [255.0 + 2.0 ** -44, 130.3, 3.0])]
+
+
+def _ctx(**env):
+    """A context whose single-window calls take the throughput kernels
+    (CSM_SMALL=0: not the few-window split kernel)."""
+    import roborts_csm
+    env = dict({"CSM_SMALL": "0"}, **env)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        c = roborts_csm.Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    c.set_profiling(True)
+    return c
+
+
+def _check_windows(c, m, pts, lv, centers):
+    for cen in centers:
+        want = O.score_window(m, pts, lv, cen, 30 * 13 * 13)
+        assert np.array_equal(c.score_window(pts, lv, cen), want), cen
+        got = c.best_window(pts, lv, cen)
+        s, flat = O.best_window(m, pts, lv, cen)
+        assert got.score == s and got.flat_index == flat, cen
+
+
+def _stats(c):
+    return {k["name"]: k for k in c.kernel_stats()}
+
+
+def _values(n, rng, lo=0.3125, step=2.0 ** -12):
+    """n distinct float32 values, all multiples of 2^-12 (exactly summable)."""
+    v = lo + step * np.arange(n, dtype=np.float64)
+    return rng.permutation(v).astype(np.float32)
+
+
+@pytest.mark.parametrize("n_values,palette", [(256, True), (257, False), (2, True)])
+def test_palette_size_limits(f1, n_values, palette):
+    """The outside value plus n_values - 1 others: 256 values in all take the
+    palette kernel (indices 0..255), 257 cannot and the grouped kernel runs;
+    both bit-exact."""
+    import roborts_csm
+    rng = np.random.default_rng(n_values)
+    res = float(f1["resolution"])
+    vals = np.concatenate([[np.float32(0.3)], _values(n_values - 1, rng)])
+    g = rng.choice(vals, size=f1["grid"].shape).astype(np.float32)
+    g.ravel()[:n_values] = vals  # every value present
+    m = O.Map(g, res, tuple(f1["offset"]))
+    pts = _points(f1)
+    lv = _level(pts.shape[0])
+    c = _ctx()
+    try:
+        c.set_grid(roborts_csm.ScanMatchMap(g, res, tuple(f1["offset"]), 0, 1))
+        _check_windows(c, m, pts, lv, _centers(res))
+        st = _stats(c)
+        if palette:
+            assert "score_box_palette_kernel<13,all>" in st and "score_box_palette_kernel<13,best>" in st, st.keys()
+            assert st["grid:palette"]["scorings"] == n_values
+        else:
+            assert "score_box_kernel<13,all>" in st and not any(k.startswith("score_box_palette") for k in st)
+    finally:
+        c.close()
+
+
+def test_palette_negative_values_and_blur(f1):
+    """The reference's blurred map (f1) with some cells below the outside
+    value (negative fixed-point entries) and an outside value of 0.5."""
+    import roborts_csm
+    res = float(f1["resolution"])
+    g = np.array(f1["grid"], dtype=np.float32)
+    rng = np.random.default_rng(5)
+    g[rng.random(g.shape) < 0.05] = np.float32(0.0)
+    g[rng.random(g.shape) < 0.02] = np.float32(0.125)
+    pts = _points(f1)
+    lv = _level(pts.shape[0])
+    for outside in (0.3, 0.5):
+        c = _ctx()
+        try:
+            c.set_outside_value(outside)
+            mo = O.Map(g, res, tuple(f1["offset"]), outside=outside)
+            c.set_grid(roborts_csm.ScanMatchMap(g, res, tuple(f1["offset"]), 0, 1))
+            _check_windows(c, mo, pts, lv, _centers(res))
+            assert "score_box_palette_kernel<13,all>" in _stats(c)
+        finally:
+            c.close()
+
+
+def test_palette_grid_stack(f1):
+    """best_windows over a stack of three grids with different palettes in
+    one palette copy (grid_index > 0 reads at its own stride)."""
+    res = float(f1["resolution"])
+    rng = np.random.default_rng(11)
+    base = np.array(f1["grid"], dtype=np.float32)
+    stack = np.stack([base, np.roll(base, 37, axis=0),
+                      rng.choice(np.array([0.3, 0.5, 0.75, 1.0], dtype=np.float32), size=base.shape)])
+    pts = _points(f1)
+    lv = _level(pts.shape[0])
+    cen = np.stack(_centers(res))
+    gi = np.array([0, 1, 2, 1, 2, 0], dtype=np.int32)
+    c = _ctx()
+    try:
+        c.set_grid_stack(stack, res, version=1)
+        sc, flat, x, y, a = c.best_windows(pts, lv, gi, cen)
+        for i in range(len(gi)):
+            s, fl = O.best_window(O.Map(stack[gi[i]], res, (0.0, 0.0)), pts, lv, cen[i])
+            assert sc[i] == s and flat[i] == fl, i
+        assert "score_box_palette_kernel<13,best>" in _stats(c)
+    finally:
+        c.close()
+
+
+def test_palette_follows_grid_refresh(f1):
+    """A resident map refreshed by rows and by cells, with values the palette
+    had not seen: the palette is rebuilt and the scores stay exact."""
+    import roborts_csm
+    res = float(f1["resolution"])
+    g = np.array(f1["grid"], dtype=np.float32)
+    mm = roborts_csm.ScanMatchMap(g, res, tuple(f1["offset"]), 0, 1)
+    pts = _points(f1)
+    lv = _level(pts.shape[0])
+    cen = _centers(res)[:3]
+    c = _ctx()
+    try:
+        c.set_grid(mm)
+        _check_windows(c, O.Map(g, res, tuple(f1["offset"])), pts, lv, cen)
+        g[150:170, :] = np.float32(0.8125)
+        mm.version = 2
+        c.update_grid_rows(mm, 150, 170)
+        _check_windows(c, O.Map(g, res, tuple(f1["offset"])), pts, lv, cen)
+        idx = np.arange(200 * 400 + 100, 200 * 400 + 180, dtype=np.int32)
+        g.ravel()[idx] = np.float32(0.6875)
+        mm.version = 3
+        c.update_grid_cells(mm, idx)
+        _check_windows(c, O.Map(g, res, tuple(f1["offset"])), pts, lv, cen)
+        assert _stats(c)["grid:palette"]["launches"] >= 3
+    finally:
+        c.close()

@@ -269,7 +269,7 @@ def test_headline_runs_row_segment_kernels(ctx, world2000):
     s = ctx.scan_matchers_batch(b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(), poses, covs)
     names = {k["name"] for k in ctx.kernel_stats()}
     ctx.set_profiling(False)
-    for want in ("score_box_kernel<13,all>", "score_phase_kernel<11,all>",
+    for want in ("score_box_palette_kernel<13,all>", "score_phase_kernel<11,all>",
                  "score_tiny_kernel<3,all>", "finish_kernel<5070>"):
         assert want in names, names
     m = O.Map(w.grid, w.resolution, w.offset)
@@ -388,7 +388,7 @@ def test_kernel_variants_agree(f1, grid_kind):
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
     # None: default throughput kernels (v6 box / v7 phase / v8 tiny / v4); split: few-window path
-    ctxs = [_variant_ctx(k) for k in ("v1", "v2", "v3", "v4", "v6", "v7", None, "split")]
+    ctxs = [_variant_ctx(k) for k in ("v2", "v4", "v6", "v7", None, "split")]
     params = [_param(f1["param"])] + list(SIM_YAML_LEVELS) + [l.with_(use_point_size=1081) for l in SIM_YAML_LEVELS]
     params += [l.with_(use_point_size=1081) for l in PARAM_CONFIG_LEVELS]
     for c in ctxs:
@@ -422,10 +422,12 @@ def test_box_kernel_edge_beams(world2000):
     centers = [[c0, 200.5 + half, 0.0], [c0, 200.5 + half, 1.3],
                [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
                [6.2, 3.1, -2.5], [1995.0, 1990.0, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
-    ctxs = [_variant_ctx(k) for k in (None, "v4", "split")]
+    # None: the v10 palette box kernel; CSM_BOX_PALETTE=0: the v9 grouped box kernel
+    ctxs = [_variant_ctx(k) for k in (None, "v4", "split")] + [_variant_ctx(None, CSM_BOX_PALETTE="0")]
     for c in ctxs:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
     ctxs[0].set_profiling(True)
+    ctxs[3].set_profiling(True)
     for cen in centers:
         cen = np.array(cen)
         want = O.score_window(m, pts, lv, cen, 30 * 13 * 13)
@@ -435,6 +437,8 @@ def test_box_kernel_edge_beams(world2000):
             s, flat = O.best_window(m, pts, lv, cen)
             assert got.score == s and got.flat_index == flat
     names = {k["name"] for k in ctxs[0].kernel_stats()}
+    assert "score_box_palette_kernel<13,all>" in names and "score_box_palette_kernel<13,best>" in names, names
+    names = {k["name"] for k in ctxs[3].kernel_stats()}
     assert "score_box_kernel<13,all>" in names and "score_box_kernel<13,best>" in names, names
     for c in ctxs:
         c.close()
@@ -912,3 +916,49 @@ def test_phase_kernel_batch_segments(world2000):
             assert np.array_equal(c.score_window(pts, lv, cen), O.score_window(m, pts, lv, cen, 1331))
     finally:
         c.close()
+
+
+def test_load_scans_async_queue(world2000):
+    """csm_load_scans_async: batches queued from pinned host memory (two at a
+    time), each taken by the next csm_scan_matchers_loaded, equal the oracle's
+    answer bit for bit; a third queued batch is refused."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    m = O.Map(w.grid, w.resolution, w.offset)
+    n = 48
+    halves = [(0, n), (n, 2 * n)]
+    pins, offs, want = [], [], []
+    for lo, hi in halves:
+        pts = b.points_cells[b.offsets[lo]:b.offsets[hi]]
+        p = roborts_csm.PinnedArray(pts.shape)
+        np.copyto(p.array, pts)
+        pins.append(p)
+        off = np.ascontiguousarray(b.offsets[lo:hi + 1] - b.offsets[lo])
+        offs.append(off)
+        eye = np.tile(np.eye(3).reshape(1, 9), (hi - lo, 1))
+        want.append(O.scan_matchers_batch(m, pts, off, headline_levels(), b.init_poses[lo:hi], eye.copy()))
+    env = {"CSM_PIPELINE": "16"}
+    os.environ.update(env)
+    try:
+        c = roborts_csm.Context(0)
+    finally:
+        for k in env:
+            del os.environ[k]
+    try:
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+        for rnd in range(2):
+            c.load_scans_async(pins[0].array, offs[0])
+            c.load_scans_async(pins[1].array, offs[1])
+            if rnd == 0:
+                with pytest.raises(roborts_csm.CsmError):
+                    c.load_scans_async(pins[0].array, offs[0])
+            for (lo, hi), (s2, p2, c2) in zip(halves, want):
+                poses = np.ascontiguousarray(b.init_poses[lo:hi].copy())
+                covs = np.tile(np.eye(3).reshape(1, 9), (hi - lo, 1))
+                s = c.scan_matchers_loaded(headline_levels(), poses, covs)
+                assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2), (rnd, lo)
+    finally:
+        c.close()
+        for p in pins:
+            p.close()

@@ -22,7 +22,7 @@ for step in "$@"; do
           > gpurun_out/willow_$TAG.json 2> gpurun_out/willow_$TAG.err || exit $? ;;
     prof) (cd /tmp && export TMPDIR=/tmp; true); export TMPDIR=/tmp
           timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- \
-            python3 bench.py --no-cpu --no-latency --no-b109 > gpurun_out/prof_bench_$TAG.json 2>&1 || exit $? ;;
+            python3 bench.py --no-cpu --no-latency --no-b109 --no-lc-leg > gpurun_out/prof_bench_$TAG.json 2>&1 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "step $step done"

@@ -7,7 +7,7 @@
 set -e
 OUT=${1:-gpurun_out/pmcr}
 shift || true
-ARGS=${*:-"--steps 2 --warmup 1 --no-cpu --no-latency --no-b109"}
+ARGS=${*:-"--steps 2 --warmup 1 --no-cpu --no-latency --no-b109 --no-lc-leg"}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 # every scoring dispatch a whole level-part (the 3-level driver otherwise
