@@ -553,7 +553,11 @@ __global__ __launch_bounds__(64) void score_box_palette_kernel(LevelWork L, cons
   __shared__ __attribute__((aligned(16))) int32_t run_off[kScratch + 64];
   __shared__ __attribute__((aligned(16))) uint8_t run_cnt[kScratch + 64];
   for (int s0 = 0; s0 < n_used; s0 += kPalSeg) {
+#if defined(CSM_PAL_DIAG) && CSM_PAL_DIAG >= 3  // timing diagnostic: no run lists either
+    const int nruns = 0;
+#else
     const int nruns = B.build_runs(s0, min(n_used, s0 + kPalSeg), run_off, run_cnt, kScratch, slow);
+#endif
     // whole steps, then one step of empty runs (zero block, count 0) that the
     // look-ahead reads of the last step take
     const int npad = (nruns + kStepRuns - 1) / kStepRuns * kStepRuns;
@@ -562,7 +566,7 @@ __global__ __launch_bounds__(64) void score_box_palette_kernel(LevelWork L, cons
       run_cnt[i] = 0;
     }
     __syncthreads();
-#if defined(CSM_PAL_DIAG) && CSM_PAL_DIAG == 1  // timing diagnostic (wrong scores): the run lists only
+#if defined(CSM_PAL_DIAG) && CSM_PAL_DIAG >= 1  // timing diagnostic (wrong scores): the run lists only
     if (false) {
 #else
     if (npad > 0) {
@@ -624,7 +628,9 @@ __global__ __launch_bounds__(64) void score_box_palette_kernel(LevelWork L, cons
 #pragma unroll
   for (int t = 0; t < 4; ++t) mine[t] = (kk < NS && 4 * q + t < NS) ? xch[kk * 16 + 4 * q + t] : 0;
   const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
+#if !(defined(CSM_PAL_DIAG) && CSM_PAL_DIAG >= 2)  // timing diagnostic: no cell-by-cell pass
   slow_beams<NS>(B, L, gi, slow, kk, q, ox, oy, mine);
+#endif
   box_epilogue<NS, BEST>(L, S, ae, wt, a, kk < NS, kk, q, ox, oy, nsf, mine, out, partials);
 }
 
