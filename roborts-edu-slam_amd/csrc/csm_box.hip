@@ -74,6 +74,7 @@ struct BoxWave {
   int step, n_used, lane, sx, sy, pitch4, zero_off;  // pitch4: bytes per grid row
   double x_0, y_0;  // x_ox, y_oy: the tile's first candidate
   int cell_shift = 2;  // log2 bytes per cell: 2 for gridi (int32), 0 for the palette grid (bytes)
+  int strip_bytes = 0, copy_bytes = 0;  // strip copies (offsets<true>): bytes per strip and per copy
 
   // The box test of one beam point; on success (ix0, iy0) is the box corner.
   __device__ __forceinline__ bool box_test(const double2 p, double& lx, double& ly, int& ix0, int& iy0) const {
@@ -93,13 +94,26 @@ struct BoxWave {
   // n_used, boxes wholly past the grid's high edges and rejected beams).
   // slow: bit c marks 64-beam chunk c as holding a rejected beam (bit 63:
   // some chunk >= 63), for the cell-by-cell pass at the end.
+  // STRIP: the offset in the strip copies (csm_palette.hip) of the box's first
+  // row piece: copy c = -(ix0 / 4) mod 4 puts cells (ix0 & ~3) .. +15 in one
+  // 16-byte strip row, and the corner's byte phase ix0 & 3 rides in the low
+  // bits (the piece itself is 16-byte aligned).
+  template <bool STRIP = false>
   __device__ __forceinline__ int offsets(const double2 p, int cb, uint64_t& slow) const {
     double lx, ly;
     int ix0, iy0;
     const bool clean = box_test(p, lx, ly, ix0, iy0);
     const bool live = cb + lane < n_used;
     slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean) != 0) << min(cb >> 6, 63);
-    return (live && clean && ix0 < sx && iy0 < sy) ? iy0 * pitch4 + (ix0 << cell_shift) : zero_off;
+    int o;
+    if (STRIP) {
+      const int c = (-(ix0 >> 2)) & 3;
+      const int xs = (ix0 & ~3) + 4 * c;
+      o = c * copy_bytes + (xs >> 4) * strip_bytes + iy0 * 16 + (ix0 & 3);
+    } else {
+      o = iy0 * pitch4 + (ix0 << cell_shift);
+    }
+    return (live && clean && ix0 < sx && iy0 < sy) ? o : zero_off;
   }
   __device__ __forceinline__ double2 point(int cb) const { return P[(int64_t)min(cb + lane, n_used - 1) * step]; }
 
@@ -109,7 +123,7 @@ struct BoxWave {
   // runs of boxes wholly off the grid and of rejected beams are dropped (they
   // read zeros). Slots from `scratch` on take the non-run lanes' writes
   // (branch-free). Returns the run count.
-  template <int PF = kPF, typename CT = int32_t>
+  template <int PF = kPF, typename CT = int32_t, bool STRIP = false>
   __device__ __forceinline__ int build_runs(int s0, int s1, int32_t* run_off, CT* run_cnt, int scratch,
                                             uint64_t& slow) const {
     int nruns = 0;
@@ -131,7 +145,7 @@ struct BoxWave {
         const double2 pcur = pq[u];
         pq[u] = point(cb + 64 * PF);
         __builtin_amdgcn_sched_barrier(0);
-        const int off = offsets(pcur, cb, slow);
+        const int off = offsets<STRIP>(pcur, cb, slow);
         const bool live = cb + lane < s1;
         // previous beam's corner (lane 0: none)
         const int prev = __builtin_amdgcn_mov_dpp(off, 0x138, 0xF, 0xF, false);  // wave_shr:1
@@ -634,6 +648,194 @@ __global__ __launch_bounds__(64) void score_box_palette_kernel(LevelWork L, cons
   box_epilogue<NS, BEST>(L, S, ae, wt, a, kk < NS, kk, q, ox, oy, nsf, mine, out, partials);
 }
 
+// v11 "pair" box kernel (n_space <= 13, palettes of at most kPairMaxPal
+// values, r04). Two changes to v10, one per bound it hit (TA 0.66, VALU 0.70
+// of the kernel's cycles, profiles/r04):
+//  - the box rows come from the strip copies of the index grid: a run's 13
+//    rows are 208 contiguous bytes of one strip (2.5 cache lines per run, not
+//    14 row-major), so the texture-address unit tags a fifth of the lines;
+//  - runs of equal count go in pairs (the segment's run list is counting-
+//    sorted by count): with indices below 16, one v_lshl_or per 4 cells makes
+//    the pair's code a | b << s, and a 256-entry table of V[a] + V[b] turns
+//    one lookup and one FMA into two runs' worth. The sums stay exact: every
+//    product and partial sum is an integer below 2^53 (|V| < 2^26, counts <=
+//    64, 1081 beams), so they equal the int64 sums of the other kernels.
+// An odd bin's last run pairs with the zero run (offset zero_off, index 0).
+constexpr int kPairPD = 2;  // pairs of one slot per step
+#ifndef CSM_PAIR_SEG
+#define CSM_PAIR_SEG 576
+#endif
+constexpr int kPairSeg = CSM_PAIR_SEG;
+static_assert(kPairSeg % 64 == 0 && kPairSeg >= 512, "whole 64-beam chunks; the sums' transpose reuses the list");
+
+template <int NS, bool BEST>
+__global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const ScanWork* __restrict__ scans,
+                                                            const double2* __restrict__ pts,
+                                                            const AngleEntry* __restrict__ angles,
+                                                            double* __restrict__ out,
+                                                            BestPartial* __restrict__ partials) {
+  static_assert(NS >= 1 && NS <= kPalMaxSpace, "corner phase (<= 3) + NS cells within one 16-byte row piece");
+  static_assert(kPairPD == 2, "a slot's step: one ds_read_b128 of pair offsets, one u16 of counts");
+  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
+  dev::clear_word(L);
+  const int win = bid / L.n_angles;
+  const int a = bid - win * L.n_angles;
+  const ScanWork S = scans[win];
+  const AngleEntry ae = angles[S.angle_off + a];
+  const int lane = threadIdx.x;
+  const int k = lane & 15, slot = lane >> 4;
+  const int zero_off = L.size_y * 16;  // copy 0, strip 0, first zero row
+  BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, 0, zero_off, S.x0 /* :569 */,
+            S.y0 /* :572 */, 0, L.strip_bytes, L.strip_copy_bytes};
+  const int n_used = S.n_used;
+  // pair table: tab[a | b << sh] = V[a] + V[b]
+  const int sh = L.pal_n <= 8 ? 3 : 4;
+  __shared__ double tab[256];
+  for (int i = lane; i < 256; i += 64) {
+    const int ia = i & ((1 << sh) - 1), ib = i >> sh;
+    tab[i] = (ia < L.pal_n && ib < L.pal_n) ? (double)L.pal_vals[ia] + (double)L.pal_vals[ib] : 0.0;
+  }
+  const uint8_t* pg = L.pal_strips + (int64_t)S.grid_index * L.strip_grid_bytes;
+  const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)pg);
+  const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)pg >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)phi << 32) | plo), (short)0, (int)L.strip_grid_bytes, 0x00020000);
+  // rows past the box read the last row again (no new lines) and add nothing
+  const int krow = min(k, NS - 1) * 16;
+  const uint32_t kmask = k < NS ? 0xFFFFFFFFu : 0u;
+
+  double acc[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+  uint64_t slow = 0;
+  constexpr int kStepPairs = 4 * kPairPD;  // pairs per step: slot s takes pairs [g + 2s, g + 2s + 2)
+  constexpr int kScratch = kPairSeg + 64;
+  constexpr int kPairSlots = kPairSeg + 64 + 4 * kStepPairs;  // pair members incl. odd-bin partners + padding
+  __shared__ __attribute__((aligned(16))) int32_t run_off[kScratch + 64];
+  __shared__ uint8_t run_cnt[kScratch + 64];
+  __shared__ __attribute__((aligned(16))) int32_t pair_off[kPairSlots];  // pair p: members 2p, 2p + 1
+  __shared__ __attribute__((aligned(16))) uint8_t pair_cnt[kPairSlots / 2];
+  __shared__ int32_t bin[64];  // counting sort by run count (1..64)
+  for (int s0 = 0; s0 < n_used; s0 += kPairSeg) {
+    const int nruns = B.build_runs<kPF, uint8_t, true>(s0, min(n_used, s0 + kPairSeg), run_off, run_cnt, kScratch,
+                                                       slow);
+    bin[lane] = 0;
+    __syncthreads();
+    for (int i = lane; i < nruns; i += 64) atomicAdd(&bin[run_cnt[i] - 1], 1);
+    __syncthreads();
+    // bin b: ceil(h / 2) pairs from slot 2 * (pairs of the bins below)
+    const int h = bin[lane];
+    const int pb = (h + 1) >> 1;
+    int incl = pb;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    const int npairs = __shfl(incl, 63, 64);
+    const int base = 2 * (incl - pb);
+    bin[lane] = base;
+    if (h & 1) pair_off[base + h] = zero_off;  // the odd bin's last run pairs with the zero run
+    // whole steps, then one step of empty pairs (zero runs, count 0) that the
+    // look-ahead reads of the last step take
+    const int npad = (npairs + kStepPairs - 1) / kStepPairs * kStepPairs;
+    for (int p = npairs + lane; p < npad + kStepPairs; p += 64) {
+      pair_off[2 * p] = zero_off;
+      pair_off[2 * p + 1] = zero_off;
+      pair_cnt[p] = 0;
+    }
+    __syncthreads();
+    for (int i = lane; i < nruns; i += 64) {
+      const int c = run_cnt[i];
+      const int s = atomicAdd(&bin[c - 1], 1);
+      pair_off[s] = run_off[i];
+      if ((s & 1) == 0) pair_cnt[s >> 1] = (uint8_t)c;
+    }
+    __syncthreads();
+#if defined(CSM_PAL_DIAG) && CSM_PAL_DIAG >= 1  // timing diagnostic (wrong scores): the run lists only
+    if (false) {
+#else
+    if (npad > 0) {
+#endif
+      int4 offs = *reinterpret_cast<const int4*>(&pair_off[4 * slot]);  // (A0, B0, A1, B1)
+      uint32_t cnts = (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[2 * slot]) & kmask;
+      v4i dA[kPairPD], dB[kPairPD];
+      dA[0] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.x & ~15), 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // issued in the order the loop consumes them
+      dB[0] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.y & ~15), 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      dA[1] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.z & ~15), 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      dB[1] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.w & ~15), 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      for (int g = 0; g < npad; g += kStepPairs) {
+        // the next step's pairs of this slot (the padding covers the last step's)
+        const int4 noffs = *reinterpret_cast<const int4*>(&pair_off[2 * (g + kStepPairs) + 4 * slot]);
+        const uint32_t ncnts =
+            (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[g + kStepPairs + 2 * slot]) & kmask;
+        const int curA[2] = {offs.x, offs.z}, curB[2] = {offs.y, offs.w};
+        const int nxtA[2] = {noffs.x, noffs.z}, nxtB[2] = {noffs.y, noffs.w};
+#pragma unroll
+        for (int p = 0; p < kPairPD; ++p) {
+          // the pair's two rows, each shifted by its corner's byte phase, then
+          // merged into codes a | b << sh (indices < 16: no carry between bytes)
+          const uint32_t sa = (uint32_t)curA[p] & 3u, sb = (uint32_t)curB[p] & 3u;
+          const v4i xa = dA[p], xb = dB[p];
+          uint32_t w[4];
+          w[0] = __builtin_amdgcn_alignbyte((uint32_t)xa.y, (uint32_t)xa.x, sa) |
+                 (__builtin_amdgcn_alignbyte((uint32_t)xb.y, (uint32_t)xb.x, sb) << sh);
+          w[1] = __builtin_amdgcn_alignbyte((uint32_t)xa.z, (uint32_t)xa.y, sa) |
+                 (__builtin_amdgcn_alignbyte((uint32_t)xb.z, (uint32_t)xb.y, sb) << sh);
+          w[2] = __builtin_amdgcn_alignbyte((uint32_t)xa.w, (uint32_t)xa.z, sa) |
+                 (__builtin_amdgcn_alignbyte((uint32_t)xb.w, (uint32_t)xb.z, sb) << sh);
+          w[3] = __builtin_amdgcn_alignbyte(0u, (uint32_t)xa.w, sa) |
+                 (__builtin_amdgcn_alignbyte(0u, (uint32_t)xb.w, sb) << sh);
+          const double c = (double)((cnts >> (8 * p)) & 0xFFu);
+          dA[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (nxtA[p] & ~15), 0, 0);
+          dB[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (nxtB[p] & ~15), 0, 0);
+#pragma unroll
+          for (int j = 0; j < NS; ++j) acc[j] = __builtin_fma(c, tab[(w[j >> 2] >> (8 * (j & 3))) & 0xFF], acc[j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        offs = noffs;
+        cnts = ncnts;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead loads past the list land
+    }
+    __syncthreads();  // the next segment rewrites the lists
+  }
+  // the four run slots of row k meet, then the sums go to the (row, piece)
+  // layout of the v6 epilogue through LDS (the run list's space)
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    acc[j] += __shfl_xor(acc[j], 16, 64);
+    acc[j] += __shfl_xor(acc[j], 32, 64);
+  }
+  int64_t* xch = reinterpret_cast<int64_t*>(run_off);
+  if (slot == 0 && k < NS) {
+#pragma unroll
+    for (int j = 0; j < NS; ++j) xch[k * 16 + j] = (int64_t)acc[j];
+  }
+  __syncthreads();
+  const int kk = lane >> 2, q = lane & 3;
+  int64_t mine[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) mine[t] = (kk < NS && 4 * q + t < NS) ? xch[kk * 16 + 4 * q + t] : 0;
+  const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
+  slow_beams<NS>(B, L, gi, slow, kk, q, 0, 0, mine);
+  box_epilogue<NS, BEST>(L, S, ae, win, a, kk < NS, kk, q, 0, 0, NS, mine, out, partials);
+}
+
+template <int NS>
+hipError_t launch_pair(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
+                       BestPartial* part, unsigned nblk, hipStream_t stream) {
+  if (part)
+    hipLaunchKernelGGL((score_box_pair_kernel<NS, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+  else
+    hipLaunchKernelGGL((score_box_pair_kernel<NS, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+  return hipGetLastError();
+}
+
 template <int NS>
 hipError_t launch_palette(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
                           BestPartial* part, unsigned nblk, hipStream_t stream) {
@@ -696,6 +898,30 @@ hipError_t launch_score_box_palette(const LevelWork& L, const ScanWork* d_scans,
     case 11: return launch_palette<11>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
     case 12: return launch_palette<12>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
     case 13: return launch_palette<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+bool box_pair_supported(int ns) { return ns >= 9 && ns <= kPalMaxSpace; }
+
+hipError_t launch_score_box_pair(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
+                                 const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
+                                 hipStream_t stream) {
+  const int64_t nblk = (int64_t)L.n_scans * L.n_angles;
+  const StripGeom G = strip_geom(L.size_x, L.size_y);
+  if (nblk <= 0 || nblk > INT32_MAX || !L.int_mode || L.step_cells != 1.0 || L.blocks_per_scan != L.n_angles ||
+      L.tile_n > 0 || L.pal_n < 1 || L.pal_n > kPairMaxPal || !L.pal_strips || !L.pal_vals ||
+      L.strip_bytes != G.strip_bytes || L.strip_copy_bytes != G.copy_bytes || L.strip_grid_bytes != G.grid_bytes ||
+      G.grid_bytes > INT32_MAX || (int64_t)L.size_y * 16 > INT32_MAX)
+    return hipErrorInvalidValue;
+  const double2* p = reinterpret_cast<const double2*>(d_pts);
+  const unsigned n = (unsigned)nblk;
+  switch (ns) {
+    case 9: return launch_pair<9>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 10: return launch_pair<10>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 11: return launch_pair<11>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 12: return launch_pair<12>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 13: return launch_pair<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
     default: return hipErrorInvalidValue;
   }
 }

@@ -213,6 +213,19 @@ int ensure_palette(csm_ctx* c) {
       (e = hipStreamSynchronize(c->stream)) != hipSuccess)
     return c->hip_fail(e, "palette size");
   c->pal_n = (m >= 1 && m <= csm::kPalMax) ? m : 0;
+  c->pal_strips_ok = false;
+  const csm::StripGeom SG = csm::strip_geom(c->info.size_x, c->info.size_y);
+  if (c->pair_kernel && c->pal_n >= 1 && c->pal_n <= csm::kPairMaxPal && SG.grid_bytes <= INT32_MAX) {
+    if ((e = c->pal_strips.ensure((size_t)SG.grid_bytes * (size_t)c->n_grids)) != hipSuccess)
+      return c->hip_fail(e, "hipMalloc(palette strips)");
+    const int64_t idx_stride = (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows);
+    if ((e = csm::launch_build_strips((const uint8_t*)c->pal_grid.p, c->pitch, c->info.size_x, c->info.size_y,
+                                      idx_stride, c->n_grids, (uint8_t*)c->pal_strips.p, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "pal_strips_kernel");
+    // other parts' streams read the strips next (like gridi)
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(strips)");
+    c->pal_strips_ok = true;
+  }
   c->pal_gen = c->grid_gen;
   c->pal_src = c->d_gridi;
   if (c->profiling) c->account("grid:palette", 0.f, (double)n, (double)c->pal_n);

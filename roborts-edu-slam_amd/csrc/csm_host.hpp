@@ -409,6 +409,9 @@ struct csm_ctx {
   // (palette indices) and the palette, rebuilt when grid_gen moves on
   bool palette_kernel = true;
   csmh::DevBuf pal_grid, pal_vals, pal_scratch;
+  csmh::DevBuf pal_strips;     // strip copies of pal_grid (v11 pair kernel; palettes of <= kPairMaxPal values)
+  bool pal_strips_ok = false;
+  bool pair_kernel = true;     // CSM_BOX_PAIR=0: the v10 palette kernel instead of v11
   int32_t pal_n = 0;           // palette size (0: none, e.g. more than kPalMax values)
   uint64_t pal_gen = 0;        // grid_gen the palette was built for
   const int32_t* pal_src = nullptr;  // ... and the gridi it was built from

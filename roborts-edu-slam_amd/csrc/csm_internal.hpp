@@ -76,6 +76,13 @@ struct LevelWork {
   const uint8_t* pal_grid;
   const int32_t* pal_vals;
   int64_t pal_stride;
+  // The strip copies of the palette grid (score_box_pair_kernel, pal_n <=
+  // kPairMaxPal; csm_palette.hip strip_geom): bytes per strip, per copy and
+  // per grid of the stack.
+  const uint8_t* pal_strips;
+  int32_t strip_bytes;
+  int32_t strip_copy_bytes;
+  int64_t strip_grid_bytes;
 };
 
 // Argmax partial: best score of a block and its flat candidate index.
@@ -247,6 +254,28 @@ int64_t pal_scratch_ints(int64_t n);
 hipError_t launch_points_maxabs(const double* pts, int64_t n, unsigned long long* out, hipStream_t stream);
 hipError_t launch_build_palette(const int32_t* gridi, int64_t n, int32_t* scratch, int32_t* vals, int32_t* state,
                                 uint8_t* idx, hipStream_t stream);
+// v11 pair box kernel: palettes of at most kPairMaxPal values, read from
+// kStripCopies strip copies of the index grid (copy c holds cell x at byte
+// x + 4c of its strip row; strips kStripW bytes wide, rows contiguous), so a
+// box row piece is one aligned 16-byte strip row and a box's 13 rows are 208
+// contiguous bytes (2.5 cache lines, not 13-14).
+constexpr int kPairMaxPal = 16;
+constexpr int kStripW = 16;
+constexpr int kStripCopies = 4;
+constexpr int kStripPadRows = 16;  // zero rows below the grid (box rows and the zero run's rows)
+struct StripGeom {
+  int32_t rows, n_strips;
+  int64_t strip_bytes, copy_bytes, grid_bytes;
+};
+StripGeom strip_geom(int size_x, int size_y);
+// idx: the palette index grid(s) (row pitch `pitch` bytes, idx_stride bytes
+// per grid); out: n_grids * strip_geom().grid_bytes bytes.
+hipError_t launch_build_strips(const uint8_t* idx, int pitch, int size_x, int size_y, int64_t idx_stride,
+                               int n_grids, uint8_t* out, hipStream_t stream);
+bool box_pair_supported(int ns);
+hipError_t launch_score_box_pair(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
+                                 const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
+                                 hipStream_t stream);
 hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                             const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
                             hipStream_t stream);

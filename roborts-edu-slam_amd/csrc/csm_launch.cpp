@@ -452,6 +452,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if ((st = ensure_palette(c)) != CSM_OK) return st;
     box_pal = c->pal_n > 0 && (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows) <= INT32_MAX;
   }
+  // v11: pairs of equal-count runs over the strip copies (palettes of <= 16 values)
+  const bool box_pair = box_pal && c->pair_kernel && c->pal_strips_ok && csm::box_pair_supported(D.n_space);
   // v6 over 16 x 16 tiles: the argmax of a one-cell-step window wider than 16
   // (loop-closure windows), in place of the column kernel's dword gathers
   const int tile_n = (D.n_space + 15) / 16;
@@ -490,6 +492,13 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     L.pal_grid = (const uint8_t*)c->pal_grid.p;
     L.pal_vals = (const int32_t*)c->pal_vals.p;
     L.pal_stride = (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows);
+  }
+  if (box_pair) {
+    const csm::StripGeom SG = csm::strip_geom(c->info.size_x, c->info.size_y);
+    L.pal_strips = (const uint8_t*)c->pal_strips.p;
+    L.strip_bytes = (int32_t)SG.strip_bytes;
+    L.strip_copy_bytes = (int32_t)SG.copy_bytes;
+    L.strip_grid_bytes = SG.grid_bytes;
   }
   L.n_cols = (int32_t)n_cols;
   L.ktiles = ktiles;
@@ -552,7 +561,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const double alg_bytes = beams * (double)D.n_cand * 4.0;
   const double scorings = (double)nw * (double)D.n_cand;
   char kname[48];
-  if (box_pal)
+  if (box_pair)
+    std::snprintf(kname, sizeof(kname), "score_box_pair_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
+  else if (box_pal)
     std::snprintf(kname, sizeof(kname), "score_box_palette_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (box)
     std::snprintf(kname, sizeof(kname), "score_box_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
@@ -593,6 +604,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     const ScanWork* d_sw = (const ScanWork*)c->scans.p + w0;
     if (!sp.score)
       e = hipSuccess;  // scored by earlier calls
+    else if (box_pair)
+      e = csm::launch_score_box_pair(L, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
+                                     (double*)c->scores.p, nullptr, D.n_space, c->stream);
     else if (box_pal)
       e = csm::launch_score_box_palette(L, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
                                         (double*)c->scores.p, nullptr, D.n_space, c->stream);
@@ -709,7 +723,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     const size_t pbytes = (size_t)nw * (size_t)bps * sizeof(BestPartial);
     if ((e = c->partials.ensure(pbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(partials)");
     if ((e = c->best.ensure((size_t)nw * sizeof(BestPartial))) != hipSuccess) return c->hip_fail(e, "hipMalloc(best)");
-    if (box_pal)
+    if (box_pair)
+      e = csm::launch_score_box_pair(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
+                                     (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
+                                     D.n_space, c->stream);
+    else if (box_pal)
       e = csm::launch_score_box_palette(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                         (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
                                         D.n_space, c->stream);

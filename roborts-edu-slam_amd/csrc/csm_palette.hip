@@ -15,6 +15,8 @@
 //   pal_merge_kernel    one block merges the lists, sorts them, writes the
 //                       palette and its size
 //   pal_index_kernel    every cell's index by binary search in the palette
+//   pal_strips_kernel   (palettes of at most kPairMaxPal values) the strip
+//                       copies the v11 pair box kernel reads
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -159,7 +161,59 @@ __global__ __launch_bounds__(256) void pal_index_kernel(const int4* __restrict__
   }
 }
 
+// Strip copies of the palette index grid (v11 pair box kernel): copy c holds
+// cell x of row y at byte (x + 4c) of its strip row, strips kStripW bytes
+// wide with their rows contiguous (row y of strip t at (t * rows + y) * 16).
+// One thread writes one 16-byte strip row; cells off the grid are index 0.
+__global__ __launch_bounds__(256) void pal_strips_kernel(const uint8_t* __restrict__ idx, int pitch, int sx,
+                                                         int sy, int rows, int n_strips, int64_t idx_stride,
+                                                         int64_t grid_bytes, int n_grids, uint4* __restrict__ out) {
+  const int64_t per_copy = (int64_t)n_strips * rows;
+  const int64_t total = (int64_t)n_grids * kStripCopies * per_copy;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t g = i / (kStripCopies * per_copy);
+    const int64_t r = i - g * kStripCopies * per_copy;
+    const int c = (int)(r / per_copy);
+    const int64_t sr = r - (int64_t)c * per_copy;
+    const int t = (int)(sr / rows);
+    const int y = (int)(sr - (int64_t)t * rows);
+    const uint8_t* src = idx + g * idx_stride + (int64_t)y * pitch;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (y < sy) {
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const int x = kStripW * t + b - 4 * c;
+        const uint32_t v = (x >= 0 && x < sx) ? src[x] : 0u;
+        w[b >> 2] |= v << (8 * (b & 3));
+      }
+    }
+    out[(g * grid_bytes + (int64_t)c * per_copy * kStripW) / 16 + sr] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 }  // namespace
+
+StripGeom strip_geom(int size_x, int size_y) {
+  StripGeom G{};
+  G.rows = size_y + kStripPadRows;
+  // a box row piece starts at (ix & ~3) + 4c <= size_x - 1 + 12 in copy c
+  G.n_strips = (size_x + 11) / kStripW + 1;
+  G.strip_bytes = (int64_t)G.rows * kStripW;
+  G.copy_bytes = G.strip_bytes * G.n_strips;
+  G.grid_bytes = G.copy_bytes * kStripCopies;
+  return G;
+}
+
+hipError_t launch_build_strips(const uint8_t* idx, int pitch, int size_x, int size_y, int64_t idx_stride,
+                               int n_grids, uint8_t* out, hipStream_t stream) {
+  const StripGeom G = strip_geom(size_x, size_y);
+  if (!idx || !out || n_grids < 1 || pitch < size_x) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)n_grids * kStripCopies * G.n_strips * G.rows;
+  const int64_t blocks = (total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192;
+  hipLaunchKernelGGL(pal_strips_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, idx, pitch, size_x, size_y,
+                     G.rows, G.n_strips, idx_stride, G.grid_bytes, n_grids, reinterpret_cast<uint4*>(out));
+  return hipGetLastError();
+}
 
 int64_t pal_scratch_ints(int64_t n) {
   const int64_t n4 = n / 4;

@@ -1,13 +1,16 @@
-"""GPU parity of the v10 palette box kernel (csrc/csm_box.hip
-score_box_palette_kernel, csrc/csm_palette.hip) against the CPU oracle.
+"""GPU parity of the palette box kernels (csrc/csm_box.hip
+score_box_palette_kernel v10 and score_box_pair_kernel v11, csrc/csm_palette.hip)
+against the CPU oracle.
 
 The kernel reads one-cell-step windows (n_space <= 13: the coarse level of
 every shipped parameter set, correlate_scan_matcher.h:552-584,637-662)
 through the palette copy of the fixed-point grid: one byte per cell, the
 index of the cell's value among the grid's distinct values. The bar is the
 same as for every other kernel: all scores bit for bit, the argmax index
-equal. Covered here: the palette's size limits (256 values: palette kernel;
-257: the grid has no palette and the v9 grouped kernel runs), cells below the
+equal. Covered here: the palette's size limits (up to 16 values: the v11 pair
+kernel over the strip copies, index shift 3 up to 8 values and 4 above; up to
+256: the v10 palette kernel; 257: the grid has no palette and the v9 grouped
+kernel runs; CSM_BOX_PAIR=0 keeps v10 for small palettes), cells below the
 outside value (negative fixed-point entries), windows off every edge, beams
 on rounding boundaries, a grid stack (the palette grid's per-grid stride),
 and the palette rebuilt after row and cell refreshes of a resident map.
@@ -78,17 +81,31 @@ def _stats(c):
     return {k["name"]: k for k in c.kernel_stats()}
 
 
+def _kernel(grids, outside=0.3, pair=True):
+    """The box kernel the palette of `grids` selects: its size is the number
+    of distinct values other than the outside value, plus the outside value."""
+    g = np.asarray(grids, dtype=np.float32)
+    n = len(np.unique(g[g != np.float32(outside)])) + 1
+    if n > 256:
+        return "score_box_kernel"
+    return "score_box_pair_kernel" if (pair and n <= 16) else "score_box_palette_kernel"
+
+
 def _values(n, rng, lo=0.3125, step=2.0 ** -12):
     """n distinct float32 values, all multiples of 2^-12 (exactly summable)."""
     v = lo + step * np.arange(n, dtype=np.float64)
     return rng.permutation(v).astype(np.float32)
 
 
-@pytest.mark.parametrize("n_values,palette", [(256, True), (257, False), (2, True)])
-def test_palette_size_limits(f1, n_values, palette):
-    """The outside value plus n_values - 1 others: 256 values in all take the
-    palette kernel (indices 0..255), 257 cannot and the grouped kernel runs;
-    both bit-exact."""
+@pytest.mark.parametrize("n_values,kernel", [(256, "score_box_palette_kernel"), (257, "score_box_kernel"),
+                                            (2, "score_box_pair_kernel"), (8, "score_box_pair_kernel"),
+                                            (9, "score_box_pair_kernel"), (16, "score_box_pair_kernel"),
+                                            (17, "score_box_palette_kernel")])
+def test_palette_size_limits(f1, n_values, kernel):
+    """The outside value plus n_values - 1 others: up to 16 values take the
+    pair kernel (pair codes of 3 bits per index up to 8 values, 4 above), up
+    to 256 the palette kernel (indices 0..255), 257 cannot and the grouped
+    kernel runs; all bit-exact."""
     import roborts_csm
     rng = np.random.default_rng(n_values)
     res = float(f1["resolution"])
@@ -103,16 +120,16 @@ def test_palette_size_limits(f1, n_values, palette):
         c.set_grid(roborts_csm.ScanMatchMap(g, res, tuple(f1["offset"]), 0, 1))
         _check_windows(c, m, pts, lv, _centers(res))
         st = _stats(c)
-        if palette:
-            assert "score_box_palette_kernel<13,all>" in st and "score_box_palette_kernel<13,best>" in st, st.keys()
+        assert kernel + "<13,all>" in st and kernel + "<13,best>" in st, st.keys()
+        assert len([k for k in st if k.startswith("score_box")]) == 2, st.keys()
+        if n_values <= 256:
             assert st["grid:palette"]["scorings"] == n_values
-        else:
-            assert "score_box_kernel<13,all>" in st and not any(k.startswith("score_box_palette") for k in st)
     finally:
         c.close()
 
 
-def test_palette_negative_values_and_blur(f1):
+@pytest.mark.parametrize("pair", [True, False])
+def test_palette_negative_values_and_blur(f1, pair):
     """The reference's blurred map (f1) with some cells below the outside
     value (negative fixed-point entries) and an outside value of 0.5."""
     import roborts_csm
@@ -124,18 +141,19 @@ def test_palette_negative_values_and_blur(f1):
     pts = _points(f1)
     lv = _level(pts.shape[0])
     for outside in (0.3, 0.5):
-        c = _ctx()
+        c = _ctx(CSM_BOX_PAIR="1" if pair else "0")
         try:
             c.set_outside_value(outside)
             mo = O.Map(g, res, tuple(f1["offset"]), outside=outside)
             c.set_grid(roborts_csm.ScanMatchMap(g, res, tuple(f1["offset"]), 0, 1))
             _check_windows(c, mo, pts, lv, _centers(res))
-            assert "score_box_palette_kernel<13,all>" in _stats(c)
+            assert _kernel(g, outside, pair) + "<13,all>" in _stats(c)
         finally:
             c.close()
 
 
-def test_palette_grid_stack(f1):
+@pytest.mark.parametrize("pair", [True, False])
+def test_palette_grid_stack(f1, pair):
     """best_windows over a stack of three grids with different palettes in
     one palette copy (grid_index > 0 reads at its own stride)."""
     res = float(f1["resolution"])
@@ -147,19 +165,20 @@ def test_palette_grid_stack(f1):
     lv = _level(pts.shape[0])
     cen = np.stack(_centers(res))
     gi = np.array([0, 1, 2, 1, 2, 0], dtype=np.int32)
-    c = _ctx()
+    c = _ctx(CSM_BOX_PAIR="1" if pair else "0")
     try:
         c.set_grid_stack(stack, res, version=1)
         sc, flat, x, y, a = c.best_windows(pts, lv, gi, cen)
         for i in range(len(gi)):
             s, fl = O.best_window(O.Map(stack[gi[i]], res, (0.0, 0.0)), pts, lv, cen[i])
             assert sc[i] == s and flat[i] == fl, i
-        assert "score_box_palette_kernel<13,best>" in _stats(c)
+        assert _kernel(stack, 0.3, pair) + "<13,best>" in _stats(c)
     finally:
         c.close()
 
 
-def test_palette_follows_grid_refresh(f1):
+@pytest.mark.parametrize("pair", [True, False])
+def test_palette_follows_grid_refresh(f1, pair):
     """A resident map refreshed by rows and by cells, with values the palette
     had not seen: the palette is rebuilt and the scores stay exact."""
     import roborts_csm
@@ -169,7 +188,7 @@ def test_palette_follows_grid_refresh(f1):
     pts = _points(f1)
     lv = _level(pts.shape[0])
     cen = _centers(res)[:3]
-    c = _ctx()
+    c = _ctx(CSM_BOX_PAIR="1" if pair else "0")
     try:
         c.set_grid(mm)
         _check_windows(c, O.Map(g, res, tuple(f1["offset"])), pts, lv, cen)
@@ -182,6 +201,8 @@ def test_palette_follows_grid_refresh(f1):
         mm.version = 3
         c.update_grid_cells(mm, idx)
         _check_windows(c, O.Map(g, res, tuple(f1["offset"])), pts, lv, cen)
-        assert _stats(c)["grid:palette"]["launches"] >= 3
+        st = _stats(c)
+        assert st["grid:palette"]["launches"] >= 3
+        assert _kernel(g, 0.3, pair) + "<13,all>" in st, st.keys()
     finally:
         c.close()

@@ -269,7 +269,7 @@ def test_headline_runs_row_segment_kernels(ctx, world2000):
     s = ctx.scan_matchers_batch(b.points_cells[:b.offsets[n]], b.offsets[:n + 1], headline_levels(), poses, covs)
     names = {k["name"] for k in ctx.kernel_stats()}
     ctx.set_profiling(False)
-    for want in ("score_box_palette_kernel<13,all>", "score_phase_kernel<11,all>",
+    for want in ("score_box_pair_kernel<13,all>", "score_phase_kernel<11,all>",
                  "score_tiny_kernel<3,all>", "finish_kernel<5070>"):
         assert want in names, names
     m = O.Map(w.grid, w.resolution, w.offset)
@@ -422,12 +422,14 @@ def test_box_kernel_edge_beams(world2000):
     centers = [[c0, 200.5 + half, 0.0], [c0, 200.5 + half, 1.3],
                [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
                [6.2, 3.1, -2.5], [1995.0, 1990.0, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
-    # None: the v10 palette box kernel; CSM_BOX_PALETTE=0: the v9 grouped box kernel
-    ctxs = [_variant_ctx(k) for k in (None, "v4", "split")] + [_variant_ctx(None, CSM_BOX_PALETTE="0")]
+    # None: the v11 pair box kernel (the world's 7 values); CSM_BOX_PALETTE=0: the v9
+    # grouped box kernel; CSM_BOX_PAIR=0: the v10 palette box kernel
+    ctxs = [_variant_ctx(k) for k in (None, "v4", "split")] + [_variant_ctx(None, CSM_BOX_PALETTE="0"),
+                                                              _variant_ctx(None, CSM_BOX_PAIR="0")]
     for c in ctxs:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
-    ctxs[0].set_profiling(True)
-    ctxs[3].set_profiling(True)
+    for i in (0, 3, 4):
+        ctxs[i].set_profiling(True)
     for cen in centers:
         cen = np.array(cen)
         want = O.score_window(m, pts, lv, cen, 30 * 13 * 13)
@@ -436,10 +438,9 @@ def test_box_kernel_edge_beams(world2000):
             got = c.best_window(pts, lv, cen)
             s, flat = O.best_window(m, pts, lv, cen)
             assert got.score == s and got.flat_index == flat
-    names = {k["name"] for k in ctxs[0].kernel_stats()}
-    assert "score_box_palette_kernel<13,all>" in names and "score_box_palette_kernel<13,best>" in names, names
-    names = {k["name"] for k in ctxs[3].kernel_stats()}
-    assert "score_box_kernel<13,all>" in names and "score_box_kernel<13,best>" in names, names
+    for i, kn in ((0, "score_box_pair_kernel"), (3, "score_box_kernel"), (4, "score_box_palette_kernel")):
+        names = {k["name"] for k in ctxs[i].kernel_stats()}
+        assert kn + "<13,all>" in names and kn + "<13,best>" in names, (i, names)
     for c in ctxs:
         c.close()
 

@@ -1,16 +1,18 @@
 #!/bin/bash
-# r04: palette kernel timing by phase (pdiag1: no accumulation, pdiag2: + no cell-by-cell pass,
-# pdiag3: + no run lists) — wrong scores, timing only.
+# r04: box kernels, isolated timing (tools/box_kbench.py: coarse level only, unpipelined) after the
+# palette/parity GPU tests of the v11 pair kernel. pdiag1: no accumulation (wrong scores, timing only).
 set -o pipefail
 mkdir -p gpurun_out
 T=${1:-pal3}
-for v in "" pdiag1 pdiag2 pdiag3; do
-  lib=""; [ -n "$v" ] && lib=roborts-edu-slam_amd/lib/libroborts_csm-$v.so
-  CSM_LIB=$lib timeout -k 10 300 python bench.py --no-cpu --no-lc-leg --no-b109 --no-host-inputs --steps 20 --warmup 10 > gpurun_out/bench_${T}_${v:-default}.json 2>&1 || exit $?
-  python3 - gpurun_out/bench_${T}_${v:-default}.json <<'PY'
-import json, sys
-d = json.loads([l for l in open(sys.argv[1]).read().splitlines() if l.startswith("{")][-1])
-print(sys.argv[1], round(d["ms_per_step"], 4), "ms/step",
-      [(k["name"], round(k["total_ms"] / k["launches"], 4)) for k in d["kernels"] if k["name"].startswith("score_box")])
-PY
+out=gpurun_out/kbench_${T}.txt
+: > $out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_palette.py \
+  tests/test_gpu_parity.py -k "palette or box or headline" > gpurun_out/pytest_${T}.log 2>&1 || { tail -30 gpurun_out/pytest_${T}.log; exit 1; }
+tail -2 gpurun_out/pytest_${T}.log
+timeout -k 10 120 tools/ubench/ta_probe > gpurun_out/ta_probe_${T}.txt 2>&1 || exit $?
+for env in "CSM_BOX_PALETTE=0" "CSM_BOX_PAIR=0" "CSM_BOX_PAIR=1" "CSM_BOX_PAIR=0 CSM_LIB=roborts-edu-slam_amd/lib/libroborts_csm-pdiag1.so" "CSM_BOX_PAIR=1 CSM_LIB=roborts-edu-slam_amd/lib/libroborts_csm-pdiag1.so"; do
+  echo "# $env" >> $out
+  env $env timeout -k 10 200 python tools/box_kbench.py >> $out 2>&1 || exit $?
 done
+for l in 1 2; do timeout -k 10 200 python tools/box_kbench.py --level $l >> $out 2>&1 || exit $?; done
+grep '^[{#]' $out
