@@ -232,6 +232,34 @@ int ensure_palette(csm_ctx* c) {
   return CSM_OK;
 }
 
+// The strip copies of the current gridi for the phase kernel, once per grid
+// generation (istrips_ok = false: none, the kernel reads gridi row-major).
+int ensure_istrips(csm_ctx* c) {
+  if (!c->int_ok || !c->d_gridi) {
+    c->istrips_ok = false;
+    return CSM_OK;
+  }
+  if (c->istrips_gen == c->grid_gen && c->istrips_src == c->d_gridi) return CSM_OK;
+  c->istrips_ok = false;
+  const csm::StripGeom SG = csm::istrip_geom(c->info.size_x, c->info.size_y);
+  if (SG.grid_bytes <= INT32_MAX) {
+    hipError_t e;
+    if ((e = c->istrips.ensure((size_t)SG.grid_bytes * (size_t)c->n_grids)) != hipSuccess)
+      return c->hip_fail(e, "hipMalloc(gridi strips)");
+    const int64_t stride = (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows);
+    if ((e = csm::launch_build_istrips(c->d_gridi, c->pitch, c->info.size_x, c->info.size_y, stride, c->n_grids,
+                                       (int32_t*)c->istrips.p, c->stream)) != hipSuccess)
+      return c->hip_fail(e, "istrips_kernel");
+    // other parts' streams read the strips next (like gridi)
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(istrips)");
+    c->istrips_ok = true;
+    if (c->profiling) c->account("grid:istrips", 0.f, (double)SG.grid_bytes * c->n_grids, 0.0);
+  }
+  c->istrips_gen = c->grid_gen;
+  c->istrips_src = c->d_gridi;
+  return CSM_OK;
+}
+
 }  // namespace csmh
 
 using namespace csmh;

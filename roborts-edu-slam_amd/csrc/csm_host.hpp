@@ -412,6 +412,11 @@ struct csm_ctx {
   csmh::DevBuf pal_strips;     // strip copies of pal_grid (v11 pair kernel; palettes of <= kPairMaxPal values)
   bool pal_strips_ok = false;
   bool pair_kernel = true;     // CSM_BOX_PAIR=0: the v10 palette kernel instead of v11
+  csmh::DevBuf istrips;        // strip copies of gridi (the phase kernel's strip form)
+  uint64_t istrips_gen = 0;    // grid_gen they were built for
+  const int32_t* istrips_src = nullptr;
+  bool istrips_ok = false;
+  bool phase_strips = true;    // CSM_PHASE_STRIPS=0: the phase kernel reads gridi row-major
   int32_t pal_n = 0;           // palette size (0: none, e.g. more than kPalMax values)
   uint64_t pal_gen = 0;        // grid_gen the palette was built for
   const int32_t* pal_src = nullptr;  // ... and the gridi it was built from
@@ -667,6 +672,8 @@ struct WinSpan {
 int ensure_int_grid(csm_ctx* c);
 void release_map_reader(csm_ctx* c);
 
+// csm_grid.cpp: the strip copies of gridi for the phase kernel (c->istrips_ok)
+int ensure_istrips(csm_ctx* c);
 // csm_grid.cpp: the palette copy of gridi for the v10 box kernel (c->pal_n = 0: none)
 int ensure_palette(csm_ctx* c);
 

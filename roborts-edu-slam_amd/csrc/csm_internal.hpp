@@ -83,6 +83,12 @@ struct LevelWork {
   int32_t strip_bytes;
   int32_t strip_copy_bytes;
   int64_t strip_grid_bytes;
+  // The strip copies of gridi (score_phase_kernel's strip form; csm_palette.hip
+  // istrip_geom): bytes per strip, per copy and per grid of the stack.
+  const int32_t* istrips;
+  int32_t istrip_bytes;
+  int32_t istrip_copy_bytes;
+  int64_t istrip_grid_bytes;
 };
 
 // Argmax partial: best score of a block and its flat candidate index.
@@ -273,6 +279,16 @@ StripGeom strip_geom(int size_x, int size_y);
 hipError_t launch_build_strips(const uint8_t* idx, int pitch, int size_x, int size_y, int64_t idx_stride,
                                int n_grids, uint8_t* out, hipStream_t stream);
 bool box_pair_supported(int ns);
+// Strip copies of gridi for the phase kernel: copy c (of kIStripCopies) holds
+// cell x of row y at cell x + 4c of its strip row, strips kIStripCells cells
+// (32 bytes) wide with their rows contiguous, so a 5 x 5 phase box (corner
+// phase <= 3 cells, two 16-byte pieces per row) is 160 contiguous bytes.
+constexpr int kIStripCells = 8;
+constexpr int kIStripCopies = 2;
+constexpr int kIStripPadRows = 16;
+StripGeom istrip_geom(int size_x, int size_y);
+hipError_t launch_build_istrips(const int32_t* gridi, int pitch, int size_x, int size_y, int64_t gridi_stride,
+                                int n_grids, int32_t* out, hipStream_t stream);
 hipError_t launch_score_box_pair(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
                                  const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
                                  hipStream_t stream);

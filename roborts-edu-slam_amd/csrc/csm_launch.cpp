@@ -468,6 +468,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                      csm::phase_supported(D.n_space, PT.cells, PT.nq) &&
                      c->pitch >= c->info.size_x + csm::kGridiPadCols;
   if (phase) rows_sq = 0;
+  if (phase && c->phase_strips && (st = ensure_istrips(c)) != CSM_OK) return st;
+  const bool phase_st = phase && c->phase_strips && c->istrips_ok;
   // v8 tiny-window kernel: a sub-cell step whose whole span is under one cell
   const bool tiny = !box && !phase && use_int && c->tiny_kernel && f < 1.0 && csm::tiny_supported(D.n_space, f) &&
                     c->pitch >= c->info.size_x + csm::kGridiPadCols &&
@@ -492,6 +494,13 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     L.pal_grid = (const uint8_t*)c->pal_grid.p;
     L.pal_vals = (const int32_t*)c->pal_vals.p;
     L.pal_stride = (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows);
+  }
+  if (phase_st) {
+    const csm::StripGeom SG = csm::istrip_geom(c->info.size_x, c->info.size_y);
+    L.istrips = (const int32_t*)c->istrips.p;
+    L.istrip_bytes = (int32_t)SG.strip_bytes;
+    L.istrip_copy_bytes = (int32_t)SG.copy_bytes;
+    L.istrip_grid_bytes = SG.grid_bytes;
   }
   if (box_pair) {
     const csm::StripGeom SG = csm::strip_geom(c->info.size_x, c->info.size_y);

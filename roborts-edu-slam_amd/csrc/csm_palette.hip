@@ -17,6 +17,8 @@
 //   pal_index_kernel    every cell's index by binary search in the palette
 //   pal_strips_kernel   (palettes of at most kPairMaxPal values) the strip
 //                       copies the v11 pair box kernel reads
+//   istrips_kernel      the strip copies of gridi itself that the phase
+//                       kernel reads (8-cell strips, two copies)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -191,7 +193,57 @@ __global__ __launch_bounds__(256) void pal_strips_kernel(const uint8_t* __restri
   }
 }
 
+// Strip copies of gridi (the phase kernel's strip form): copy c holds cell x
+// of row y at cell x + 4c of its 8-cell strip row. One thread per 16-byte half
+// row.
+__global__ __launch_bounds__(256) void istrips_kernel(const int32_t* __restrict__ gi, int pitch, int sx, int sy,
+                                                      int rows, int n_strips, int64_t gi_stride, int64_t grid_ints,
+                                                      int n_grids, int4* __restrict__ out) {
+  const int64_t per_copy = (int64_t)n_strips * rows * 2;  // half rows
+  const int64_t total = (int64_t)n_grids * kIStripCopies * per_copy;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t g = i / (kIStripCopies * per_copy);
+    const int64_t r = i - g * kIStripCopies * per_copy;
+    const int c = (int)(r / per_copy);
+    const int64_t hr = r - (int64_t)c * per_copy;  // half row within the copy
+    const int64_t sr = hr >> 1;
+    const int t = (int)(sr / rows);
+    const int y = (int)(sr - (int64_t)t * rows);
+    const int x0 = kIStripCells * t + 4 * (int)(hr & 1) - 4 * c;
+    const int32_t* src = gi + g * gi_stride + (int64_t)y * pitch;
+    int v[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int x = x0 + b;
+      v[b] = (y < sy && x >= 0 && x < sx) ? src[x] : 0;
+    }
+    out[(g * grid_ints + (int64_t)c * per_copy * 4) / 4 + hr] = make_int4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 }  // namespace
+
+StripGeom istrip_geom(int size_x, int size_y) {
+  StripGeom G{};
+  G.rows = size_y + kIStripPadRows;
+  // a box row starts at cell (ix & ~3) + 4c <= size_x - 1 + 4 in copy c, phase <= 3
+  G.n_strips = (size_x + 3) / kIStripCells + 1;
+  G.strip_bytes = (int64_t)G.rows * kIStripCells * 4;
+  G.copy_bytes = G.strip_bytes * G.n_strips;
+  G.grid_bytes = G.copy_bytes * kIStripCopies;
+  return G;
+}
+
+hipError_t launch_build_istrips(const int32_t* gridi, int pitch, int size_x, int size_y, int64_t gridi_stride,
+                                int n_grids, int32_t* out, hipStream_t stream) {
+  const StripGeom G = istrip_geom(size_x, size_y);
+  if (!gridi || !out || n_grids < 1 || pitch < size_x) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)n_grids * kIStripCopies * G.n_strips * G.rows * 2;
+  const int64_t blocks = (total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192;
+  hipLaunchKernelGGL(istrips_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, gridi, pitch, size_x, size_y,
+                     G.rows, G.n_strips, gridi_stride, G.grid_bytes / 4, n_grids, reinterpret_cast<int4*>(out));
+  return hipGetLastError();
+}
 
 StripGeom strip_geom(int size_x, int size_y) {
   StripGeom G{};

@@ -69,7 +69,11 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));
 #define CSM_PHASE_WAVES 4
 #endif
 
-template <int NS, int C, int NQ, bool BEST>
+// ST: the box rows come from the strip copies of gridi (L.istrips, r04): a
+// beam's 5 rows are 160 contiguous bytes of one strip instead of 5 rows of the
+// row-major grid, so a load instruction's lanes touch about half the 64-byte
+// segments (the texture-address unit's cost per instruction follows them).
+template <int NS, int C, int NQ, bool BEST, bool ST>
 __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelWork L, PhaseTable T,
                                                          const ScanWork* __restrict__ scans,
                                                          const double2* __restrict__ pts,
@@ -115,16 +119,20 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
   const double y_0 = S.y0 + 0 * f;  // :572 at k = 0
   const int sx = L.size_x, sy = L.size_y;
   const int pitch4 = L.pitch * 4;
-  const int zero_off = sy * pitch4;  // first of the zero rows
+  constexpr int kRowB = kIStripCells * 4;   // strip row bytes
+  static_assert(!ST || 4 * NPC <= kIStripCells + 4, "a box row's pieces stay within its strip row and the next");
+  const int zero_off = ST ? sy * kRowB : sy * pitch4;  // first of the zero rows (strip form: copy 0, strip 0)
   const double2* __restrict__ P = pts + S.pts_off;
   const int step = S.step;
   const int n_used = S.n_used;
   const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
-  const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
-  const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
+  const int32_t* gsrc = ST ? L.istrips + (int64_t)S.grid_index * (L.istrip_grid_bytes / 4) : gi;
+  const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gsrc);
+  const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gsrc >> 32));
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((uint64_t)ghi << 32) | glo), (short)0, (int)(L.gridi_stride * 4), 0x00020000);
-  const int voff = cv * pitch4 + ch * 16;
+      (void*)(((uint64_t)ghi << 32) | glo), (short)0, ST ? (int)L.istrip_grid_bytes : (int)(L.gridi_stride * 4),
+      0x00020000);
+  const int voff = ST ? cv * kRowB + ch * 16 : cv * pitch4 + ch * 16;
 
   for (int i = lane; i < NQ * kPhaseMaxSpace; i += 64) oxs[i / kPhaseMaxSpace][i % kPhaseMaxSpace] =
       T.ox[i / kPhaseMaxSpace][i % kPhaseMaxSpace];
@@ -159,7 +167,15 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
     const int ix0 = ok ? (int)tx : 0;
     const int iy0 = ok ? (int)ty : 0;
     const bool use = live && ok && ix0 < sx && iy0 < sy;
-    return make_int2(use ? iy0 * pitch4 + ix0 * 4 : 0, use ? qx * NQ + qy : -1);
+    int o;
+    if (ST) {  // copy c = (ix0 / 4) mod 2 puts cells (ix0 & ~3) .. +7 in one strip row
+      const int c = (ix0 >> 2) & 1;
+      const int xs = (ix0 & ~3) + 4 * c;
+      o = c * L.istrip_copy_bytes + (xs >> 3) * L.istrip_bytes + iy0 * kRowB + (ix0 & 3) * 4;
+    } else {
+      o = iy0 * pitch4 + ix0 * 4;
+    }
+    return make_int2(use ? o : 0, use ? qx * NQ + qy : -1);
   };
   auto point = [&](int b) { return P[(int64_t)min(b, n_used - 1) * step]; };
 
@@ -375,14 +391,14 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
   }
 }
 
-template <int NS, int C, int NQ>
+template <int NS, int C, int NQ, bool ST>
 hipError_t launch_phase(const LevelWork& L, const PhaseTable& T, const ScanWork* s, const double2* p,
                         const AngleEntry* an, double* out, BestPartial* part, unsigned nblk, hipStream_t stream) {
   if (part)
-    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, true>), dim3(nblk), dim3(64), 0, stream, L, T, s, p, an, out,
-                       part);
+    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, true, ST>), dim3(nblk), dim3(64), 0, stream, L, T, s, p, an,
+                       out, part);
   else
-    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, false>), dim3(nblk), dim3(64), 0, stream, L, T, s, p, an,
+    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, false, ST>), dim3(nblk), dim3(64), 0, stream, L, T, s, p, an,
                        out, part);
   return hipGetLastError();
 }
@@ -406,7 +422,14 @@ hipError_t launch_score_phase(const LevelWork& L, const PhaseTable& T, const Sca
     for (int j = 0; j < ns; ++j)
       if (T.ox[q][j] < 0 || T.ox[q][j] >= T.cells) return hipErrorInvalidValue;
   const double2* p = reinterpret_cast<const double2*>(d_pts);
-  return launch_phase<11, 5, 5>(L, T, d_scans, p, d_angles, d_out, d_partials, (unsigned)nblk, stream);
+  if (L.istrips) {
+    const StripGeom G = istrip_geom(L.size_x, L.size_y);
+    if (L.istrip_bytes != G.strip_bytes || L.istrip_copy_bytes != G.copy_bytes || L.istrip_grid_bytes != G.grid_bytes ||
+        G.grid_bytes > INT32_MAX)
+      return hipErrorInvalidValue;
+    return launch_phase<11, 5, 5, true>(L, T, d_scans, p, d_angles, d_out, d_partials, (unsigned)nblk, stream);
+  }
+  return launch_phase<11, 5, 5, false>(L, T, d_scans, p, d_angles, d_out, d_partials, (unsigned)nblk, stream);
 }
 
 }  // namespace csm

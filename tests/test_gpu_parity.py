@@ -387,8 +387,10 @@ def test_kernel_variants_agree(f1, grid_kind):
     else:
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
-    # None: default throughput kernels (v6 box / v7 phase / v8 tiny / v4); split: few-window path
+    # None: default throughput kernels (v11 pair box / v7 phase over strips / v8 tiny / v4); split:
+    # few-window path; the last: v10 palette box and the phase kernel over gridi
     ctxs = [_variant_ctx(k) for k in ("v2", "v4", "v6", "v7", None, "split")]
+    ctxs.append(_variant_ctx(None, CSM_BOX_PAIR="0", CSM_PHASE_STRIPS="0"))
     params = [_param(f1["param"])] + list(SIM_YAML_LEVELS) + [l.with_(use_point_size=1081) for l in SIM_YAML_LEVELS]
     params += [l.with_(use_point_size=1081) for l in PARAM_CONFIG_LEVELS]
     for c in ctxs:
@@ -820,7 +822,9 @@ def test_phase_kernel_edge_beams(world2000, margin_log2):
     the breakpoints 0, 0.2, 0.4, ...), beams off the grid's low edge (negative
     t) and past its high edges, windows at inexact step sums; with the default
     2^-20 margin and with a 1/32 margin that sends ~half the beams down the exact
-    path. All scores and the argmax against the oracle and the v4 row kernel."""
+    path. All scores and the argmax against the oracle and the v4 row kernel;
+    the phase kernel over the strip copies of gridi (default) and over gridi
+    itself (CSM_PHASE_STRIPS=0)."""
     import roborts_csm
     from roborts_csm.params import SIM_YAML_LEVELS
     w, b = world2000
@@ -836,10 +840,12 @@ def test_phase_kernel_edge_beams(world2000, margin_log2):
                [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
                [1.2, 0.1, -2.5], [1998.0, 1990.0, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
     env = {"CSM_PHASE_MARGIN_LOG2": margin_log2} if margin_log2 else {}
-    ctxs = [_variant_ctx(k, **env) for k in (None, "v4", "split")]
+    ctxs = [_variant_ctx(k, **env) for k in (None, "v4", "split")] + [_variant_ctx(None, CSM_PHASE_STRIPS="0",
+                                                                                **env)]
     for c in ctxs:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
     ctxs[0].set_profiling(True)
+    ctxs[3].set_profiling(True)
     for cen in centers:
         cen = np.array(cen)
         want = O.score_window(m, pts, lv, cen, 11 * 11 * 11)
@@ -848,8 +854,10 @@ def test_phase_kernel_edge_beams(world2000, margin_log2):
             got = c.best_window(pts, lv, cen)
             s, flat = O.best_window(m, pts, lv, cen)
             assert got.score == s and got.flat_index == flat
-    names = {k["name"] for k in ctxs[0].kernel_stats()}
-    assert "score_phase_kernel<11,all>" in names and "score_phase_kernel<11,best>" in names, names
+    for i, strips in ((0, True), (3, False)):
+        names = {k["name"] for k in ctxs[i].kernel_stats()}
+        assert "score_phase_kernel<11,all>" in names and "score_phase_kernel<11,best>" in names, names
+        assert ("grid:istrips" in names) == strips, names
     for c in ctxs:
         c.close()
 

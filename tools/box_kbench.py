@@ -1,5 +1,5 @@
 """Isolated timing of one level's scoring kernel: config 2's 4096 scans matched
-at the coarse level only (or --level 1/2), unpipelined (CSM_PIPELINE=0,
+at the coarse level only (or --level 1/2; csm_scan_match_batch), unpipelined (CSM_PIPELINE=0,
 CSM_FIRST_WINDOWS=0), so no other kernel of the batch runs beside it and the
 HIP-event time of each launch is the kernel's own.
 
@@ -33,16 +33,15 @@ def main():
     from roborts_csm.params import headline_levels
     w = worlds.make_world(2000, 2000, 0.05)
     b = worlds.make_scan_batch(w, a.scans, seed=7)
-    lv = [headline_levels()[a.level]]
+    lv = headline_levels()[a.level]
     c = roborts_csm.Context(0)
     c.set_grid(roborts_csm.ScanMatchMap(w.grid, w.resolution, w.offset, 0, 1))
-    c.load_scans(b.points_cells, b.offsets)
     eye = np.tile(np.eye(3).reshape(1, 9), (b.init_poses.shape[0], 1))
     for i in range(a.warmup + a.iters):
         if i == a.warmup:
             c.set_profiling(True)
         poses = np.ascontiguousarray(b.init_poses.copy())
-        c.scan_matchers_loaded(lv, poses, eye.copy())
+        c.scan_match_batch(b.points_cells, b.offsets, lv, poses, eye.copy())
     st = [k for k in c.kernel_stats() if k["name"].startswith("score_")]
     out = []
     for k in st:
