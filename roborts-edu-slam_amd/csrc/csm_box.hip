@@ -648,6 +648,19 @@ __global__ __launch_bounds__(64) void score_box_palette_kernel(LevelWork L, cons
   box_epilogue<NS, BEST>(L, S, ae, wt, a, kk < NS, kk, q, ox, oy, nsf, mine, out, partials);
 }
 
+// CSM_BOX_TRACE builds: s_memtime stamps of the pair kernel's phases for a
+// sample of waves (every 61st block), read by tools/box_trace.py through
+// csm_debug_box_trace: [0] entry, [1] first list build starts, [2] build,
+// [3] sort, [4] accumulate (cycles summed over segments), [5] the sums'
+// transpose done, [6] the cell-by-cell pass done, [7] exit, [8] runs, [9]
+// pairs (padded), [10] beams, [11] XCC/SE/CU id (HW_ID).
+#ifdef CSM_BOX_TRACE
+constexpr int kBoxTraceWaves = 4096;
+__device__ unsigned long long g_box_trace[kBoxTraceWaves][12];
+__device__ int g_box_trace_n;
+#define BOX_STAMP() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#endif
+
 // v11 "pair" box kernel (n_space <= 13, palettes of at most kPairMaxPal
 // values, r04). Two changes to v10, one per bound it hit (TA 0.66, VALU 0.70
 // of the kernel's cycles, profiles/r04):
@@ -676,6 +689,10 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
                                                             BestPartial* __restrict__ partials) {
   static_assert(NS >= 1 && NS <= kPalMaxSpace, "corner phase (<= 3) + NS cells within one 16-byte row piece");
   static_assert(kPairPD == 2, "a slot's step: one ds_read_b128 of pair offsets, one u16 of counts");
+#ifdef CSM_BOX_TRACE
+  unsigned long long tr[12] = {BOX_STAMP(), 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tq = 0;
+#endif
   const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
   dev::clear_word(L);
   const int win = bid / L.n_angles;
@@ -717,10 +734,19 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
   __shared__ __attribute__((aligned(16))) uint8_t pair_cnt[kPairSlots / 2];
   __shared__ int32_t bin[64];  // counting sort by run count (1..64)
   for (int s0 = 0; s0 < n_used; s0 += kPairSeg) {
+#ifdef CSM_BOX_TRACE
+    tq = BOX_STAMP();
+    if (s0 == 0) tr[1] = tq;
+#endif
     const int nruns = B.build_runs<kPF, uint8_t, true>(s0, min(n_used, s0 + kPairSeg), run_off, run_cnt, kScratch,
                                                        slow);
     bin[lane] = 0;
     __syncthreads();
+#ifdef CSM_BOX_TRACE
+    tr[2] += BOX_STAMP() - tq;
+    tq = BOX_STAMP();
+    tr[8] += nruns;
+#endif
     for (int i = lane; i < nruns; i += 64) atomicAdd(&bin[run_cnt[i] - 1], 1);
     __syncthreads();
     // bin b: ceil(h / 2) pairs from slot 2 * (pairs of the bins below)
@@ -752,6 +778,11 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
       if ((s & 1) == 0) pair_cnt[s >> 1] = (uint8_t)c;
     }
     __syncthreads();
+#ifdef CSM_BOX_TRACE
+    tr[3] += BOX_STAMP() - tq;
+    tq = BOX_STAMP();
+    tr[9] += npad;
+#endif
 #if defined(CSM_PAL_DIAG) && CSM_PAL_DIAG >= 1  // timing diagnostic (wrong scores): the run lists only
     if (false) {
 #else
@@ -803,6 +834,9 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead loads past the list land
     }
     __syncthreads();  // the next segment rewrites the lists
+#ifdef CSM_BOX_TRACE
+    tr[4] += BOX_STAMP() - tq;
+#endif
   }
   // the four run slots of row k meet, then the sums go to the (row, piece)
   // layout of the v6 epilogue through LDS (the run list's space)
@@ -822,8 +856,25 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
 #pragma unroll
   for (int t = 0; t < 4; ++t) mine[t] = (kk < NS && 4 * q + t < NS) ? xch[kk * 16 + 4 * q + t] : 0;
   const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
+#ifdef CSM_BOX_TRACE
+  tr[5] = BOX_STAMP();
+#endif
   slow_beams<NS>(B, L, gi, slow, kk, q, 0, 0, mine);
+#ifdef CSM_BOX_TRACE
+  tr[6] = BOX_STAMP();
+#endif
   box_epilogue<NS, BEST>(L, S, ae, win, a, kk < NS, kk, q, 0, 0, NS, mine, out, partials);
+#ifdef CSM_BOX_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tr[7] = BOX_STAMP();
+  tr[10] = (unsigned long long)n_used;
+  tr[11] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID
+  if (bid % 61 == 0 && lane == 0) {
+    const int i = atomicAdd(&g_box_trace_n, 1);
+    if (i < kBoxTraceWaves)
+      for (int j = 0; j < 12; ++j) g_box_trace[i][j] = tr[j];
+  }
+#endif
 }
 
 template <int NS>
@@ -958,3 +1009,19 @@ hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const d
 }
 
 }  // namespace csm
+
+#ifdef CSM_BOX_TRACE
+// Trace readout for tools/box_trace.py: copies and resets the stamps.
+extern "C" int csm_debug_box_trace(unsigned long long* out, int max_waves) {
+  int n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(csm::g_box_trace_n), sizeof(int)) != hipSuccess) return -1;
+  n = n < csm::kBoxTraceWaves ? n : csm::kBoxTraceWaves;
+  n = n < max_waves ? n : max_waves;
+  if (n > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(csm::g_box_trace), (size_t)n * 12 * sizeof(unsigned long long)) !=
+                   hipSuccess)
+    return -1;
+  const int zero = 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(csm::g_box_trace_n), &zero, sizeof(int));
+  return n;
+}
+#endif
