@@ -59,6 +59,13 @@ constexpr int kRunSeg = CSM_RUN_SEG;
 #define CSM_BOX_PF 6
 #endif
 constexpr int kPF = CSM_BOX_PF;  // chunks of beam points in flight while a run list is built
+// the pair kernel's list build: ILP form (below) and its points in flight
+#ifndef CSM_PAIR_ILP
+#define CSM_PAIR_ILP 1
+#endif
+#ifndef CSM_PAIR_PF
+#define CSM_PAIR_PF 4
+#endif
 // Runs in flight per wave (16 measured no better; one load per beam instead of
 // per run: 2.28 vs 1.02 ms, profiles/r01)
 constexpr int kD = 8;
@@ -75,9 +82,15 @@ struct BoxWave {
   double x_0, y_0;  // x_ox, y_oy: the tile's first candidate
   int cell_shift = 2;  // log2 bytes per cell: 2 for gridi (int32), 0 for the palette grid (bytes)
   int strip_bytes = 0, copy_bytes = 0;  // strip copies (offsets<true>): bytes per strip and per copy
+  int nspan = 0;  // candidates per axis of the wave (box_test's far test; 0: off)
 
   // The box test of one beam point; on success (ix0, iy0) is the box corner.
-  __device__ __forceinline__ bool box_test(const double2 p, double& lx, double& ly, int& ix0, int& iy0) const {
+  // far: every cell the beam reads for this wave's candidates is off the
+  // grid's low side (t_j <= -1 for every j < nspan on one axis, so trunc(t_j)
+  // <= -1 by the rounding argument above): the beam adds the outside value,
+  // zero in gridi, to every candidate, and needs no cell-by-cell pass.
+  __device__ __forceinline__ bool box_test(const double2 p, double& lx, double& ly, int& ix0, int& iy0,
+                                           bool& far) const {
     lx = ae.cosine * p.x - ae.sine * p.y;  // :179
     ly = ae.sine * p.x + ae.cosine * p.y;  // :180
     const double tx = (lx + x_0) + 0.5;
@@ -86,6 +99,8 @@ struct BoxWave {
     const double fy = ty - floor(ty);
     const bool clean = tx >= 0.0 && ty >= 0.0 && fx >= kBoxMargin && fx <= 1.0 - kBoxMargin &&
                        fy >= kBoxMargin && fy <= 1.0 - kBoxMargin;
+    const double lim = -(double)nspan - kBoxMargin;
+    far = nspan > 0 && (tx <= lim || ty <= lim);
     ix0 = clean ? (int)tx : 0;
     iy0 = clean ? (int)ty : 0;
     return clean;
@@ -102,9 +117,10 @@ struct BoxWave {
   __device__ __forceinline__ int offsets(const double2 p, int cb, uint64_t& slow) const {
     double lx, ly;
     int ix0, iy0;
-    const bool clean = box_test(p, lx, ly, ix0, iy0);
+    bool far;
+    const bool clean = box_test(p, lx, ly, ix0, iy0, far);
     const bool live = cb + lane < n_used;
-    slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean) != 0) << min(cb >> 6, 63);
+    slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean && !far) != 0) << min(cb >> 6, 63);
     int o;
     if (STRIP) {
       const int c = (-(ix0 >> 2)) & 3;
@@ -123,7 +139,7 @@ struct BoxWave {
   // runs of boxes wholly off the grid and of rejected beams are dropped (they
   // read zeros). Slots from `scratch` on take the non-run lanes' writes
   // (branch-free). Returns the run count.
-  template <int PF = kPF, typename CT = int32_t, bool STRIP = false>
+  template <int PF = kPF, typename CT = int32_t, bool STRIP = false, bool ILP = false>
   __device__ __forceinline__ int build_runs(int s0, int s1, int32_t* run_off, CT* run_cnt, int scratch,
                                             uint64_t& slow) const {
     int nruns = 0;
@@ -136,16 +152,32 @@ struct BoxWave {
       __builtin_amdgcn_sched_barrier(0);
     }
     for (int cb0 = s0; cb0 < s1; cb0 += 64 * PF) {
+      // ILP: the PF chunks' box tests first (independent dependency chains
+      // the compiler interleaves), then the next PF chunks' points are issued
+      // and the run edges found while they are in flight
+      int offv[PF];
+      if constexpr (ILP) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) offv[u] = offsets<STRIP>(pq[u], cb0 + 64 * u, slow);
+#pragma unroll
+        for (int u = 0; u < PF; ++u) pq[u] = point(cb0 + 64 * (u + PF));
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         // no early exit: a chunk at or past s1 adds no run (live is false for
         // every lane), and an exit here made the compiler drain vmcnt(0) per
         // chunk instead of keeping PF chunks of points in flight
         const int cb = cb0 + 64 * u;
-        const double2 pcur = pq[u];
-        pq[u] = point(cb + 64 * PF);
-        __builtin_amdgcn_sched_barrier(0);
-        const int off = offsets<STRIP>(pcur, cb, slow);
+        int off;
+        if constexpr (ILP) {
+          off = offv[u];
+        } else {
+          const double2 pcur = pq[u];
+          pq[u] = point(cb + 64 * PF);
+          __builtin_amdgcn_sched_barrier(0);
+          off = offsets<STRIP>(pcur, cb, slow);
+        }
         const bool live = cb + lane < s1;
         // previous beam's corner (lane 0: none)
         const int prev = __builtin_amdgcn_mov_dpp(off, 0x138, 0xF, 0xF, false);  // wave_shr:1
@@ -169,11 +201,18 @@ struct BoxWave {
 
 // Rejected beams, cell by cell with the reference's expressions: only the
 // marked chunks are revisited, and only their rejected beams summed into the
-// lane's candidates (j = 4q .. 4q+3, row k).
+// lane's candidates (j = 4q .. 4q+3, row k). Beams go four at a time, their 16
+// gathers issued together (one at a time, a wave near the grid's low edge
+// paid a dependent round trip per beam: 20 % of the pair kernel's time).
 template <int NS>
 __device__ __forceinline__ void slow_beams(const BoxWave& B, const LevelWork& L, const int32_t* gi, uint64_t slow,
                                            int k, int q, int ox, int oy, int64_t (&acc)[4]) {
   const double f = L.step_cells;
+  const int64_t zero_cell = (int64_t)B.sy * L.pitch;  // first of the zero rows
+  const double yk = B.S.y0 + (oy + k) * f;           // :572
+  double xj[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) xj[t] = B.S.x0 + (ox + 4 * q + t) * f;  // :569
   for (uint64_t m = slow; m != 0; m &= m - 1) {
     const int c0 = (int)__builtin_ctzll(m);
     const int c_end = c0 == 63 ? (B.n_used + 63) / 64 : c0 + 1;
@@ -181,22 +220,31 @@ __device__ __forceinline__ void slow_beams(const BoxWave& B, const LevelWork& L,
       const int cb = c * 64;
       double lx, ly;
       int ix0, iy0;
-      const bool clean = B.box_test(B.point(cb), lx, ly, ix0, iy0);
-      for (uint64_t rej = __builtin_amdgcn_ballot_w64(cb + B.lane < B.n_used && !clean); rej != 0; rej &= rej - 1) {
-        const int l = (int)__builtin_ctzll(rej);  // uniform: one beam for the whole wave
-        const double bx = dev::bcast_lane(lx, l);
-        const double by = dev::bcast_lane(ly, l);
-        const int gy = (int)((by + (B.S.y0 + (oy + k) * f)) + 0.5);
-        const bool iny = (unsigned)gy < (unsigned)B.sy;
+      bool far;
+      const bool clean = B.box_test(B.point(cb), lx, ly, ix0, iy0, far);
+      uint64_t rej = __builtin_amdgcn_ballot_w64(cb + B.lane < B.n_used && !clean && !far);
+      while (rej != 0) {  // uniform
+        int32_t v[4][4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = 4 * q + t;
-          if (j < NS) {
-            const int gx = (int)((bx + (B.S.x0 + (ox + j) * f)) + 0.5);
-            const bool in = iny && (unsigned)gx < (unsigned)B.sx;
-            acc[t] += gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)B.sy * L.pitch];
+        for (int u = 0; u < 4; ++u) {
+          const bool have = rej != 0;
+          const int l = have ? (int)__builtin_ctzll(rej) : 0;  // uniform: one beam for the whole wave
+          rej &= rej - 1;
+          const double bx = dev::bcast_lane(lx, l);
+          const double by = dev::bcast_lane(ly, l);
+          const int gy = (int)((by + yk) + 0.5);
+          const bool iny = have && (unsigned)gy < (unsigned)B.sy;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int gx = (int)((bx + xj[t]) + 0.5);
+            const bool in = iny && (unsigned)gx < (unsigned)B.sx && 4 * q + t < NS;
+            v[u][t] = gi[in ? (int64_t)gy * L.pitch + gx : zero_cell];
           }
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[t] += v[u][t];
       }
     }
   }
@@ -278,7 +326,7 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   const int pitch4 = L.pitch * 4;
   const BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, pitch4,
                   L.size_y * pitch4 /* first of the zero rows */, S.x0 + ox * L.step_cells /* :569, j = ox */,
-                  S.y0 + oy * L.step_cells /* :572, k = oy */};
+                  S.y0 + oy * L.step_cells /* :572, k = oy */, 2, 0, 0, NS};
   const int n_used = S.n_used;
   const int zero_off = B.zero_off;
   const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
@@ -403,7 +451,7 @@ __global__ __launch_bounds__(64) void score_box_grouped_kernel(LevelWork L, cons
   const int pitch4 = L.pitch * 4;
   const BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, pitch4,
                   L.size_y * pitch4 /* first of the zero rows */, S.x0 + ox * L.step_cells /* :569, j = ox */,
-                  S.y0 + oy * L.step_cells /* :572, k = oy */};
+                  S.y0 + oy * L.step_cells /* :572, k = oy */, 2, 0, 0, NS};
   const int n_used = S.n_used;
   const int zero_off = B.zero_off;
   const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
@@ -545,7 +593,7 @@ __global__ __launch_bounds__(64) void score_box_palette_kernel(LevelWork L, cons
   const int rowb = L.pitch;  // palette bytes per row (= gridi cells per row)
   const BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, rowb,
                   L.size_y * rowb /* first of the zero rows */, S.x0 + ox * L.step_cells /* :569, j = ox */,
-                  S.y0 + oy * L.step_cells /* :572, k = oy */, 0};
+                  S.y0 + oy * L.step_cells /* :572, k = oy */, 0, 0, 0, NS};
   const int n_used = S.n_used;
   const int zero_off = B.zero_off;
   __shared__ double tab[kPalMax];
@@ -703,7 +751,7 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
   const int k = lane & 15, slot = lane >> 4;
   const int zero_off = L.size_y * 16;  // copy 0, strip 0, first zero row
   BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, 0, zero_off, S.x0 /* :569 */,
-            S.y0 /* :572 */, 0, L.strip_bytes, L.strip_copy_bytes};
+            S.y0 /* :572 */, 0, L.strip_bytes, L.strip_copy_bytes, NS};
   const int n_used = S.n_used;
   // pair table: tab[a | b << sh] = V[a] + V[b]
   const int sh = L.pal_n <= 8 ? 3 : 4;
@@ -738,8 +786,8 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
     tq = BOX_STAMP();
     if (s0 == 0) tr[1] = tq;
 #endif
-    const int nruns = B.build_runs<kPF, uint8_t, true>(s0, min(n_used, s0 + kPairSeg), run_off, run_cnt, kScratch,
-                                                       slow);
+    const int nruns = B.build_runs<CSM_PAIR_PF, uint8_t, true, CSM_PAIR_ILP != 0>(
+        s0, min(n_used, s0 + kPairSeg), run_off, run_cnt, kScratch, slow);
     bin[lane] = 0;
     __syncthreads();
 #ifdef CSM_BOX_TRACE

@@ -163,7 +163,12 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
     const int qx = bucket(fx, ok);
     const int qy = bucket(fy, ok);
     const bool live = cb + lane < lim;
-    rejected = live && !ok;
+    // far: every candidate's cell is off the grid's low side on one axis
+    // (t_j = t + j*f <= -1 for all j, with the rounding margin): the beam adds
+    // the outside value (zero in gridi) everywhere and skips the exact pass
+    const double lim_far = -1.0 - (NS - 1) * f - 0x1p-20;
+    const bool far = tx <= lim_far || ty <= lim_far;
+    rejected = live && !ok && !far;
     const int ix0 = ok ? (int)tx : 0;
     const int iy0 = ok ? (int)ty : 0;
     const bool use = live && ok && ix0 < sx && iy0 < sy;
@@ -327,7 +332,8 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
     }
   }
 
-  // rejected beams, cell by cell with the reference's expressions
+  // rejected beams, cell by cell with the reference's expressions, four beams
+  // at a time (their gathers issued together)
   for (uint64_t m = slow; m != 0; m &= m - 1) {
     const int c0 = (int)__builtin_ctzll(m);
     const int c_end = c0 == 63 ? (n_used + 63) / 64 : c0 + 1;
@@ -336,21 +342,30 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
       double lx, ly;
       bool rej;
       (void)classify(point(cb + lane), cb, n_used, lx, ly, rej);
-      for (uint64_t rm = __builtin_amdgcn_ballot_w64(rej); rm != 0; rm &= rm - 1) {
-        const int l = (int)__builtin_ctzll(rm);  // uniform: one beam for the whole wave
-        const double bx = dev::bcast_lane(lx, l);
-        const double by = dev::bcast_lane(ly, l);
+      uint64_t rm = __builtin_amdgcn_ballot_w64(rej);
+      while (rm != 0) {  // uniform
+        int32_t v[4][R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int t = lane + 64 * r;
-          if (t < NC) {
-            const int j = t / NS, k = t - (t / NS) * NS;
+        for (int u = 0; u < 4; ++u) {
+          const bool have = rm != 0;
+          const int l = have ? (int)__builtin_ctzll(rm) : 0;  // uniform: one beam for the whole wave
+          rm &= rm - 1;
+          const double bx = dev::bcast_lane(lx, l);
+          const double by = dev::bcast_lane(ly, l);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int t = lane + 64 * r;
+            const int j = t < NC ? t / NS : 0, k = t < NC ? t - (t / NS) * NS : 0;
             const int gx = (int)((bx + (S.x0 + j * f)) + 0.5);
             const int gy = (int)((by + (S.y0 + k * f)) + 0.5);
-            const bool in = (unsigned)gx < (unsigned)sx && (unsigned)gy < (unsigned)sy;
-            sum[r] += gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)sy * L.pitch];
+            const bool in = have && t < NC && (unsigned)gx < (unsigned)sx && (unsigned)gy < (unsigned)sy;
+            v[u][r] = gi[in ? (int64_t)gy * L.pitch + gx : (int64_t)sy * L.pitch];
           }
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int r = 0; r < R; ++r) sum[r] += v[u][r];
       }
     }
   }
