@@ -806,6 +806,7 @@ def online_bench(args, rank, world_size, dist, torch):
     fine_size = (lambda: (fine.GetSizeX(), fine.GetSizeY())) if fine is not None else (lambda: None)
     sizes = [fine_size()]
     kept_flags = []
+    phases = []  # per scan: the front end's host phases (csm_frontend_last_phases)
     t0 = time.perf_counter()
     if be is not None:
         be.reset_stats()
@@ -820,6 +821,7 @@ def online_bench(args, rank, world_size, dist, torch):
         if be is not None and r.map_updated:  # a kept scan: a new vertex for the back end
             be.submit(stream.points_m[k], r.pose)
         lat.append(time.perf_counter() - t)
+        phases.append(fe.last_phases())
         err.append(r.pose)
         kept_flags.append(bool(r.map_updated))
         sizes.append(fine_size())
@@ -841,8 +843,16 @@ def online_bench(args, rank, world_size, dist, torch):
     kept_a = np.array(kept_flags)
     order = np.argsort(lat_ms)[::-1][:8]
     steady = lat_ms[~grew] if (~grew).any() else lat_ms
+    ph_names = ("prepare", "match", "map_check", "update_map")
+    ph = np.array([[p[n] for n in ph_names] for p in phases]) if phases else np.zeros((1, 4))
     tail = {"slowest": [{"scan": int(args.warmup + i), "ms": float(lat_ms[i]), "kept": bool(kept_a[i]),
-                         "fine_map_grew": bool(grew[i])} for i in order],
+                         "fine_map_grew": bool(grew[i]),
+                         "phases_ms": {n: round(float(ph[i, c]), 4) for c, n in enumerate(ph_names)},
+                         "outside_call_ms": round(float(lat_ms[i] - ph[i].sum()), 4)} for i in order],
+            "phase_ms": {n: {"p50": float(np.median(ph[:, c])), "p99": float(np.percentile(ph[:, c], 99)),
+                             "max": float(ph[:, c].max())} for c, n in enumerate(ph_names)},
+            "p99_not_kept_ms": float(np.percentile(lat_ms[~kept_a], 99)) if (~kept_a).any() else None,
+            "p99_kept_ms": float(np.percentile(lat_ms[kept_a], 99)) if kept_a.any() else None,
             "growth_scans": int(grew.sum()), "kept_scans": int(kept_a.sum()),
             "p50_kept_ms": float(np.median(lat_ms[kept_a])) if kept_a.any() else None,
             "p50_not_kept_ms": float(np.median(lat_ms[~kept_a])) if (~kept_a).any() else None,

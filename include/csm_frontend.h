@@ -110,6 +110,12 @@ int csm_frontend_matcher(csm_frontend* fe, csm_ctx** ctx);
 int csm_frontend_correct_pose_and_map(csm_frontend* fe, int32_t n, const int32_t* ids, const double* poses);
 /* Kept scans so far (*n in: capacity of poses, out: count) and their poses. */
 int csm_frontend_kept_scans(csm_frontend* fe, int32_t* n, double* poses);
+/* Host wall time (ms) of the last csm_frontend_process call's phases:
+ * [0] points scaled to the three resolutions, [1] the 3-level match
+ * (ScanMatchers::ScanMatch), [2] the map check (MapCheckPenalize), [3] the
+ * three map updates (UpdateMap; 0 when the scan was not kept). Diagnostics of
+ * the latency tail (no reference counterpart). */
+int csm_frontend_last_phases(const csm_frontend* fe, double ms[4]);
 
 #ifdef __cplusplus
 }

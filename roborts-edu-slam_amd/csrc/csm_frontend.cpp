@@ -83,6 +83,7 @@ struct csm_frontend {
   bool timing = false;
   double t_phase[6] = {0, 0, 0, 0, 0, 0};
   int64_t n_timed = 0;
+  double last_phase[6] = {0, 0, 0, 0, 0, 0};  // the last call's (csm_frontend_last_phases)
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -177,10 +178,12 @@ int csm_frontend_process(csm_frontend* f, const double* pts, int32_t n, const do
   int st;
   using clk = std::chrono::steady_clock;
   auto tp = clk::now();
+  for (double& t : f->last_phase) t = 0.0;
   auto lap = [&](int k) {
-    if (!f->timing) return;
     const auto now = clk::now();
-    f->t_phase[k] += std::chrono::duration<double, std::milli>(now - tp).count();
+    const double ms = std::chrono::duration<double, std::milli>(now - tp).count();
+    f->last_phase[k] += ms;
+    if (f->timing) f->t_phase[k] += ms;
     tp = now;
   };
   const bool first = f->data_index == 0;  // IsFirstRangeData
@@ -324,6 +327,15 @@ int csm_frontend_correct_pose_and_map(csm_frontend* f, int32_t n, const int32_t*
                                                    ps.data(), blur[k], 0);
     if (st != CSM_OK) return f->fail(st, std::string("InitMapWithRangeVec: ") + csm_gridmap_last_error(f->maps[k]));
   }
+  return CSM_OK;
+}
+
+int csm_frontend_last_phases(const csm_frontend* f, double ms[4]) {
+  if (!f || !ms) return CSM_ERR_INVALID_ARG;
+  ms[0] = f->last_phase[0];
+  ms[1] = f->last_phase[3];
+  ms[2] = f->last_phase[4];
+  ms[3] = f->last_phase[5];
   return CSM_OK;
 }
 

@@ -42,6 +42,7 @@ EXPORTED = (
     # include/csm_frontend.h
     "csm_frontend_create", "csm_frontend_destroy", "csm_frontend_last_error", "csm_frontend_process",
     "csm_frontend_map", "csm_frontend_correct_pose_and_map", "csm_frontend_kept_scans", "csm_frontend_matcher",
+    "csm_frontend_last_phases",
     # include/csm_loop_closure.h
     "csm_loop_closure_create", "csm_loop_closure_destroy", "csm_loop_closure_last_error",
     "csm_loop_closure_set_submaps", "csm_loop_closure_match",
@@ -251,6 +252,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_frontend_process": (C.c_int, [C.c_void_p, _dp, C.c_int32, _dp, C.c_void_p]),
         "csm_frontend_map": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
         "csm_frontend_matcher": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+        "csm_frontend_last_phases": (C.c_int, [C.c_void_p, _dp]),
         "csm_frontend_correct_pose_and_map": (C.c_int, [C.c_void_p, C.c_int32, _i32p, _dp]),
         "csm_frontend_kept_scans": (C.c_int, [C.c_void_p, _i32p, _dp]),
         "csm_load_scans_grids": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, _i32p]),

@@ -158,6 +158,13 @@ class SlamFrontEnd:
             raise RuntimeError(f"csm_frontend_process: status {st}: {_lib.csm_frontend_last_error(self._h).decode()}")
         return FrontEndResult.from_c(r)
 
+    def last_phases(self) -> dict:
+        """Host wall time (ms) of the last process() call's phases
+        (csm_frontend_last_phases): prepare, match, map_check, update_map."""
+        out = np.zeros(4)
+        _lib.csm_frontend_last_phases(self._h, out.ctypes.data_as(C.POINTER(C.c_double)))
+        return dict(zip(("prepare", "match", "map_check", "update_map"), (float(x) for x in out)))
+
     def map(self, which: int) -> OccuGridMap:
         h = C.c_void_p()
         st = _lib.csm_frontend_map(self._h, int(which), C.byref(h))
