@@ -948,6 +948,10 @@ __device__ __forceinline__ void fast_signal(const FinishArgs& A) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+#if defined(CSM_FAST_SYS_RELEASE) && CSM_FAST_SYS_RELEASE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope, per block (diagnostic variant)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     const int t = __hip_atomic_fetch_add(A.done_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (int)gridDim.x - 1) {
       __hip_atomic_store(A.done_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

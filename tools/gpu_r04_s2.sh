@@ -26,3 +26,12 @@ for k in d["kernels"]:
     if k["name"].startswith(("score_", "finish_kernel")):
         print(" ", k["name"], k["launches"], round(k["total_ms"] / k["launches"], 4))
 PY
+timeout -k 10 300 python bench.py --workload online --steps 400 --warmup 20 > gpurun_out/online_${T}.json \
+  2> gpurun_out/online_${T}.err || { tail -20 gpurun_out/online_${T}.err; exit 1; }
+python3 - gpurun_out/online_${T}.json <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]).read().splitlines() if l.startswith("{")][-1])
+c = d["config"]
+print("online", round(d["value"], 1), "scans/s", c["latency_ms"])
+print(json.dumps(c["latency_tail"])[:3000])
+PY
