@@ -26,7 +26,30 @@ struct LevelRun {
   int skip_lists = 0;  // live_lists
   PendingRun pend;
   int tag = -1;        // 3-level driver: level * 8 + part (per-phase host timings)
+  // CSM_DEBUG_FIN: each window's FinishOut as completed, and how (1 settled
+  // early, 2 owed by the exact pass, 3 joined)
+  std::vector<csm::FinishOut>* snap = nullptr;
+  std::vector<char>* how = nullptr;
+  // a window's FinishOut never matched its seal (pinned host memory): 1
+  mutable int err = 0;
 };
+
+// Seals (csm_internal.hpp) are waited for at most this long: they land within
+// microseconds of the flag; a seal that never matches is a failure, not a hang.
+constexpr double kSealWaitMs = 2000.0;
+
+// Window i's FinishOut from the pinned host memory the finish wrote, whole:
+// spin until its seal names a final writer for this launch and the copy's
+// pieces match it (the pieces can land after the launch's flag).
+bool sealed_copy(const LevelRun& R, int i, csm::FinishOut& out) {
+  const double t0 = now_ms();
+  for (uint32_t spin = 1;; ++spin) {
+    const uint32_t w = read_sealed(R.fin + i, R.pend.flag_value, out);
+    if (w == csm::kSealFast || w == csm::kSealExact) return true;
+    if ((spin & 255) == 0 && now_ms() - t0 > kSealWaitMs) return false;
+    __builtin_ia32_pause();
+  }
+}
 
 // Which covariance lists of level l a caller of the 3-level driver can see,
 // as the finish's skip mask (bit 0 positional, bit 1 angular: skipped).
@@ -187,9 +210,16 @@ int level_join(csm_ctx* c, LevelRun& R) {
       c->account(nm, tw, 0.0, 0.0);
     }
   }
-  if (R.dev)
+  if (R.dev && !R.pend.fin_host)  // (sealed windows are checked as they are completed)
     for (int i = 0; i < nw; ++i)
       if (R.fin[i].count < 0) return c->fail(CSM_ERR_HIP, "finish_kernel: work loop bound exceeded");
+  return CSM_OK;
+}
+
+// After a level's windows are completed: a sealed window that never matched
+// its seal (or carried the exact pass's overflow count) fails the call.
+int level_check(csm_ctx* c, const LevelRun& R) {
+  if (R.err) return c->fail(CSM_ERR_HIP, "finish: a window's FinishOut did not match its seal (or overflowed)");
   return CSM_OK;
 }
 
@@ -206,7 +236,14 @@ void level_complete_one(const LevelRun& R, const Geometry& G, double* poses, dou
                    (int64_t)D.n_space * D.n_space};
   csm::FinishOut local;
   const csm::FinishOut* o = nullptr;
-  if (R.dev) {
+  if (R.dev && R.pend.fin_host) {  // pinned host memory the finish wrote: a sealed copy
+    if (!sealed_copy(R, i, local) || local.count < 0) {
+      __atomic_store_n(&R.err, 1, __ATOMIC_RELAXED);
+      return;
+    }
+    o = &local;
+    if (R.snap) (*R.snap)[(size_t)i] = local;
+  } else if (R.dev) {
     o = R.fin + i;
   } else {
     host_sort_finish(R.scores + (size_t)i * (size_t)D.n_cand, D, C, P, G, scratch, local);
@@ -229,7 +266,22 @@ int level_wait_fast(csm_ctx* c, const LevelRun& R, std::vector<int>& settled, st
   settled.clear();
   owed.clear();
   settled.reserve((size_t)nw);
-  for (int i = 0; i < nw; ++i) (R.fin[i].count == csm::kFinishPending ? owed : settled).push_back(i);
+  // the seal's first word says who wrote the window for this launch (spin on
+  // one whose seal has not landed yet)
+  for (int i = 0; i < nw; ++i) {
+    uint32_t w = seal_writer(R.fin + i, R.pend.flag_value);
+    for (uint32_t spin = 1; w == 0; ++spin) {
+      if ((spin & 255) == 0 && now_ms() - t1 > kSealWaitMs)
+        return c->fail(CSM_ERR_HIP, "finish: a window's seal never landed after the fast pass's signal");
+      __builtin_ia32_pause();
+      w = seal_writer(R.fin + i, R.pend.flag_value);
+    }
+    (w == csm::kSealPending ? owed : settled).push_back(i);
+  }
+  if (R.how) {
+    for (int i : settled) (*R.how)[(size_t)i] = 1;
+    for (int i : owed) (*R.how)[(size_t)i] = 2;
+  }
   return CSM_OK;
 }
 
@@ -257,6 +309,7 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
     t2 = now_ms();
     c->parallel_for(nw, threads, [&](int i) { level_complete_one(R, G, poses, covs, responses, argmax_flat, i); });
   }
+  if ((st = level_check(c, R)) != CSM_OK) return st;
   if (threads > 1) c->account_pool("complete");
   if (c->profiling) {
     const float tc = (float)(now_ms() - t2);
@@ -308,6 +361,7 @@ int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const
   } else {
     c->parallel_for(nw, threads, one);
   }
+  if ((st = level_check(c, R)) != CSM_OK) return st;
   if (threads > 1) c->account_pool("complete+plan");
   const double t3 = now_ms();
   if ((st = level_launch(c, N)) != CSM_OK) return st;
@@ -359,6 +413,8 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
   }
   std::vector<double> resp((size_t)n_scans, 0.0);
   LevelRun R[2][csm_ctx::kMaxParts];  // by level parity: level l's run and level l + 1's
+  std::vector<csm::FinishOut> snaps[csm_ctx::kMaxParts];  // CSM_DEBUG_FIN
+  std::vector<char> hows[csm_ctx::kMaxParts];
   auto skip = [&](int l) { return c->skip_dead_lists ? live_lists(levels, n_levels, l) : 0; };
   int st;
   for (int h = 0; h < K; ++h) {
@@ -386,10 +442,33 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
                              scan_grid ? scan_grid + s0 : nullptr, skip(l + 1));
         if (h > 0) c->swap_slot(h);
       } else {
+        if (c->debug_fin) {
+          snaps[h].assign(cur.scan_of.size(), csm::FinishOut{});
+          hows[h].assign(cur.scan_of.size(), (char)3);
+          cur.snap = &snaps[h];
+          cur.how = &hows[h];
+        }
         st = level_end(c, cur, poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, nullptr);
         for (int s = s0; s < s0 + count[h]; ++s) sum[(size_t)s] += resp[(size_t)s];
       }
       if (st != CSM_OK) return st;
+    }
+  }
+  if (c->debug_fin) {  // the device idle: what the finish left against what was completed
+    (void)hipDeviceSynchronize();
+    for (int h = 0; h < K; ++h) {
+      const LevelRun& L = R[(n_levels - 1) & 1][h];
+      if (!L.dev || !L.fin) continue;
+      for (size_t i = 0; i < snaps[h].size(); ++i) {
+        const csm::FinishOut& a = snaps[h][i];
+        const csm::FinishOut& b = L.fin[i];
+        if (std::memcmp(&a, &b, sizeof(a)) == 0) continue;
+        std::fprintf(stderr,
+                     "csm debug_fin: part %d window %zu (scan %d) how %d: completed count %d n_pos %d n_ang %d front %d "
+                     "ang0 %.17g | final count %d n_pos %d n_ang %d front %d ang0 %.17g\n",
+                     h, i, first[h] + L.scan_of[i], (int)hows[h][i], a.count, a.n_pos, a.n_ang, a.front_idx,
+                     a.ang_score[0], b.count, b.n_pos, b.n_ang, b.front_idx, b.ang_score[0]);
+      }
     }
   }
   return CSM_OK;

@@ -503,6 +503,46 @@ __device__ void sort_small(double* keys, uint16_t* vals, int base, int m, int de
 
 }  // namespace
 
+constexpr int kSysWriteThrough = 17;  // buffer cache policy sc0 | sc1: system-coherent, written through L2
+
+// One wave stores a window's FinishOut, assembled in LDS (src), to dst: the
+// pieces `lists` selects and the seal (kind = writer | lists << 2, and the
+// checksum of those pieces and the tag, csm_internal.hpp). Into host memory
+// (A.host_flag) as write-through sc0 sc1 stores, nothing left dirty in the
+// XCD's L2; plain stores otherwise (device memory, copied back after the launch).
+__device__ __forceinline__ void emit_sealed(const FinishArgs& A, const FinishOut* src, FinishOut* dst, int lists,
+                                            uint32_t writer, int lane) {
+  static_assert(sizeof(FinishOut) == 560 && offsetof(FinishOut, pos_idx) == 64 &&
+                    offsetof(FinishOut, ang_idx) == 144 && offsetof(FinishOut, pos_score) == 224 &&
+                    offsetof(FinishOut, ang_score) == 384 &&
+                    offsetof(FinishOut, seal_tag_kind) == 16 * kFinishSealPiece,
+                "FinishOut pieces: header 0-3, pos_idx 4-8, ang_idx 9-13, pos_score 14-23, ang_score 24-33, seal 34");
+  const int n_pieces = finish_n_pieces(lists);
+  const uint64_t tk = (uint64_t)(uint32_t)A.flag_value | ((uint64_t)(writer | (uint32_t)lists << 2) << 32);
+  const int pc = lane < n_pieces ? finish_piece(lane, lists) : kFinishSealPiece;
+  int4 piece = lane < n_pieces ? reinterpret_cast<const int4*>(src)[pc] : make_int4(0, 0, 0, 0);
+  uint64_t h = lane < n_pieces ? finish_piece_hash(pc, (uint32_t)piece.x, (uint32_t)piece.y, (uint32_t)piece.z,
+                                                   (uint32_t)piece.w)
+                               : 0ull;
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+  h += finish_seal_share(tk);
+  if (lane == n_pieces) piece = make_int4((int32_t)(uint32_t)tk, (int32_t)(uint32_t)(tk >> 32), (int32_t)(uint32_t)h,
+                                          (int32_t)(uint32_t)(h >> 32));
+  if (lane > n_pieces) return;
+  if (A.host_flag) {
+    const uint64_t base = (uint64_t)(uintptr_t)dst;
+    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((uint64_t)bhi << 32) | blo), (short)0, (int)sizeof(FinishOut), 0x00020000);
+    typedef int32_t v4i_t __attribute__((ext_vector_type(4)));
+    const v4i_t v = {piece.x, piece.y, piece.z, piece.w};
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, pc * 16, 0, kSysWriteThrough);
+  } else {
+    reinterpret_cast<int4*>(dst)[pc] = piece;
+  }
+}
+
 // The exact pass over one window (4 waves). Waves 1-3 return before the
 // list scans; the caller's barrier joins them.
 __device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ scans,
@@ -681,14 +721,14 @@ __device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ 
   auto cx = [&](int idx) { return S.x0 + ((idx / ns) % ns) * f; };
   auto cy = [&](int idx) { return S.y0 + (idx % ns) * f; };
   const double best = keys[0];
-  FinishOut* o = out + w;
+  FinishOut* o = reinterpret_cast<FinishOut*>(smem + Lo.fout);  // stored sealed at the end (emit_sealed)
   // The window's angle rows (cos, sin) in LDS for FindBest's sequential sums:
   // one dependent global load per prefix element made the loop latency-bound
   // (the super-fine level's prefix holds most of its 189 candidates). The
   // partition scratch (lpos .. stack) is free until stage 2 rewrites it.
   const int n_ang = n / nss;
   double2* acs = reinterpret_cast<double2*>(smem + Lo.lpos);
-  const bool staged = (size_t)n_ang * sizeof(double2) <= Lo.total - Lo.lpos;
+  const bool staged = (size_t)n_ang * sizeof(double2) <= Lo.fout - Lo.lpos;  // (not into the FinishOut)
   if (staged)
     for (int t = threadIdx.x; t < n_ang; t += 64 * kWaves) {
       const AngleEntry ae = angles[S.angle_off + t];
@@ -847,6 +887,10 @@ __device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ 
     }
     if (lane == 0) o->n_ang = min(nang, kCovPoints);
   }
+  // the LDS FinishOut (thread 0's header, the lanes' list entries) to memory, sealed
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  emit_sealed(A, o, out + w, (want_pos ? 1 : 0) | (want_ang ? 2 : 0), kSealExact, lane);
   CSM_STAMP(6);
 }
 
@@ -913,7 +957,6 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
 // 256 candidates per pass), and the window's angle rows sit in LDS for the
 // sequential FindBest sums. T = 1024 for launches of few windows (the
 // reference's single-scan levels), 256 otherwise.
-constexpr int kSysWriteThrough = 17;  // buffer cache policy sc0 | sc1: system-coherent, written through L2
 constexpr int kFastCap = 512;      // compacted candidates of step 2
 constexpr int kFastNearCap = 512;  // compacted near-best candidates of step 3
 constexpr int kFastLevels = 8;     // thresholds best - {0.01, 0.02, ..., 0.64}, then everything > bound
@@ -1044,11 +1087,14 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   auto flag = [&]() {  // thread 0: the exact pass takes this window
     *need = 1;
     if (A.exact_list) A.exact_list[2 + atomicAdd(A.exact_list, 1)] = w;
-    if (A.host_fast_flag) {  // header count = pending, written through to host memory
+    if (A.host_fast_flag) {  // seal = pending (the exact pass owes it), written through to host memory
       const uint64_t base = (uint64_t)(uintptr_t)(out + w);
       const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(uintptr_t)base, (short)0, (int)sizeof(FinishOut), 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32(kFinishPending, r, (int)offsetof(FinishOut, count), 0, kSysWriteThrough);
+      const uint64_t tk = (uint64_t)(uint32_t)A.flag_value | ((uint64_t)kSealPending << 32);
+      typedef int32_t v2i_t __attribute__((ext_vector_type(2)));
+      const v2i_t v = {(int32_t)(uint32_t)tk, (int32_t)(uint32_t)(tk >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)offsetof(FinishOut, seal_tag_kind), 0, kSysWriteThrough);
     }
   };
   // the scores, every load in flight (index clamped, value masked after)
@@ -1205,39 +1251,10 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   // Only the pieces the host reads are stored: the header, plus the lists the
   // level keeps (skip_lists) -- 64 B per window instead of 544 B on a level
   // whose lists are dead, the bytes that cross to host memory with a host signal.
-  static_assert(sizeof(FinishOut) == 544 && offsetof(FinishOut, pos_idx) == 64 &&
-                    offsetof(FinishOut, ang_idx) == 144 && offsetof(FinishOut, pos_score) == 224 &&
-                    offsetof(FinishOut, ang_score) == 384,
-                "FinishOut pieces: header 0-3, pos_idx 4-8, ang_idx 9-13, pos_score 14-23, ang_score 24-33");
-  const int n_pieces = 4 + (want_pos ? 15 : 0) + (want_ang ? 15 : 0);
-  auto piece_of = [&](int t) {  // t < n_pieces: the t-th stored piece
-    if (t < 4) return t;
-    t -= 4;
-    if (want_pos) {
-      if (t < 5) return 4 + t;             // pos_idx
-      if (t < 15) return 14 + (t - 5);     // pos_score
-      t -= 15;
-    }
-    return t < 5 ? 9 + t : 24 + (t - 5);  // ang_idx, ang_score
-  };
-  auto emit = [&]() {  // all threads: the LDS FinishOut to out[w]
+  const int lists = (want_pos ? 1 : 0) | (want_ang ? 2 : 0);
+  auto emit = [&]() {  // all threads: the LDS FinishOut and its seal to out[w]
     __syncthreads();
-    if (tid < n_pieces) {
-      const int pc = piece_of(tid);
-      const int4 piece = reinterpret_cast<const int4*>(&so)[pc];
-      if (A.host_flag) {  // host memory: write-through (sc0 sc1), nothing left dirty in the XCD's L2
-        const uint64_t base = (uint64_t)(uintptr_t)(out + w);
-        const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-        const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(((uint64_t)bhi << 32) | blo), (short)0, (int)sizeof(FinishOut), 0x00020000);
-        typedef int32_t v4i_t __attribute__((ext_vector_type(4)));
-        const v4i_t v = {piece.x, piece.y, piece.z, piece.w};
-        __builtin_amdgcn_raw_buffer_store_b128(v, r, pc * 16, 0, kSysWriteThrough);
-      } else {
-        reinterpret_cast<int4*>(out + w)[pc] = piece;
-      }
-    }
+    if (wave == 0) emit_sealed(A, &so, out + w, lists, kSealFast, lane);
   };
   if (tid == 0) {  // :676-707, the same sequential sums as finish_kernel
     double ax = 0.0, ay = 0.0, thx = 0.0, thy = 0.0, ssum = 0.0;

@@ -173,6 +173,15 @@ struct CandGeom {
 void host_sort_finish(const double* scores, const Dims& D, const CandGeom& C, const csm_param& P,
                       const Geometry& G, std::vector<Entry>& e, csm::FinishOut& o);
 int own_lists_skip(int type);
+// A window's FinishOut that a finish wrote into pinned host memory, checked
+// against its seal (csm_internal.hpp): copied to `out`, then kSealFast or
+// kSealExact when the copy is whole for launch tag `tag`, kSealPending when the
+// fast pass left the window to the exact pass, 0 when its pieces or its seal
+// have not all landed yet.
+uint32_t read_sealed(const csm::FinishOut* src, int32_t tag, csm::FinishOut& out);
+// The writer the seal names for `tag`, from the seal's first word alone (0:
+// not landed yet).
+uint32_t seal_writer(const csm::FinishOut* src, int32_t tag);
 double complete_window(const csm::FinishOut& o, const CandGeom& C, const csm_param& P,
                        const Geometry& G, double pose[3], double cov[9], int skip_lists = 0);
 
@@ -361,6 +370,11 @@ struct csm_ctx {
   // sorts the flagged ones (FinishArgs::host_fast_flag). CSM_EARLY_COMPLETE=0: off.
   bool early_complete = true;
   bool early_now = false;  // set by match_levels_pipelined
+  // CSM_DEBUG_FIN=1: the 3-level driver snapshots the last level's FinishOut
+  // as each window is completed and, once the device is idle, compares it with
+  // what the finish finally left in host memory (stderr; diagnostics of the
+  // host-signal paths)
+  bool debug_fin = false;
   std::mutex mu;
   std::string err;
   float outside = 0.3f;  // kMapUnknownCellProb (slam/slam_processor.h:264)

@@ -5,6 +5,8 @@
 // the device's node table (BranchAndBoundCorrelateScanMatcher, :271-502).
 #include "csm_host.hpp"
 
+#include <cstring>
+
 namespace csmh {
 
 // Host sort path: std::sort of the window's candidates and the three ordered
@@ -80,6 +82,27 @@ int own_lists_skip(int type) {
 // 835-869, covariance :887-1019). Returns the response.
 // skip_lists: covariances a later level overwrites (live_lists) are not
 // computed; their lists were not filled.
+uint32_t seal_writer(const csm::FinishOut* src, int32_t tag) {
+  const uint64_t tk = __atomic_load_n(&src->seal_tag_kind, __ATOMIC_ACQUIRE);
+  return (uint32_t)tk == (uint32_t)tag ? (uint32_t)(tk >> 32) & 3u : 0u;
+}
+
+uint32_t read_sealed(const csm::FinishOut* src, int32_t tag, csm::FinishOut& out) {
+  std::memcpy(&out, src, sizeof(out));
+  const uint64_t tk = out.seal_tag_kind;
+  if ((uint32_t)tk != (uint32_t)tag) return 0u;
+  const uint32_t kind = (uint32_t)(tk >> 32), writer = kind & 3u;
+  if (writer == csm::kSealPending) return writer;
+  const int lists = (int)(kind >> 2) & 3;
+  uint64_t h = csm::finish_seal_share(tk);
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(&out);
+  for (int t = 0, n = csm::finish_n_pieces(lists); t < n; ++t) {
+    const int pc = csm::finish_piece(t, lists);
+    h += csm::finish_piece_hash(pc, words[4 * pc], words[4 * pc + 1], words[4 * pc + 2], words[4 * pc + 3]);
+  }
+  return h == out.seal_chk ? writer : 0u;
+}
+
 double complete_window(const csm::FinishOut& o, const CandGeom& C, const csm_param& P,
                        const Geometry& G, double pose[3], double cov[9], int skip_lists) {
   const double best_score = o.best_score;

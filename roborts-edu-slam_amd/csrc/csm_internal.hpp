@@ -127,12 +127,11 @@ struct FinishArgs {
   // (256 otherwise); 0 selects kFinishWideWindows
   int32_t wide_windows;
   // Early host signal (nullable, with host_flag): the fast pass's last block
-  // stores flag_value here once every window's FinishOut header is written --
-  // a flagged window's with count = kFinishPending -- so the host completes
-  // the settled windows while the exact pass sorts the rest.
+  // stores flag_value here once every window is sealed -- a flagged window's
+  // seal says pending (kSealPending) -- so the host completes the settled
+  // windows while the exact pass sorts the rest.
   int32_t* host_fast_flag;
 };
-constexpr int32_t kFinishPending = -2;  // FinishOut::count of a window the exact pass still owes
 constexpr int kFinishWideWindows = 64;
 
 // What the host needs to complete BasedCorrelationScanMatch::ScanMatch for
@@ -148,7 +147,52 @@ struct FinishOut {
   int32_t ang_idx[kCovPoints];
   double pos_score[kCovPoints];
   double ang_score[kCovPoints];
+  // The seal (r04). The finishes write FinishOut into pinned host memory and
+  // the host spins on a flag; the pieces of a window can land after that flag
+  // (tools/stress_ties.py + CSM_DEBUG_FIN caught a header whose n_pos / n_ang
+  // were still the previous level's, with and without a per-block system-scope
+  // release). So every writer ends a window with a seal: the launch's tag, who
+  // wrote it and which lists it stored (tag_kind = tag | kind << 32), and a
+  // checksum of the stored pieces and the tag (finish_seal_chk). The host
+  // completes a window only from a copy whose checksum matches.
+  uint64_t seal_tag_kind;
+  uint64_t seal_chk;
 };
+
+// Seal kinds: the writer in bits 0-1, the lists stored in bits 2-3
+// (bit 2 positional, bit 3 angular).
+constexpr uint32_t kSealFast = 1, kSealExact = 2, kSealPending = 3;
+constexpr int kFinishSealPiece = 34;  // 16-byte piece of the seal
+
+// FinishOut's 16-byte pieces a writer stores for lists = (positional ? 1 : 0)
+// | (angular ? 2 : 0): the header (0-3), then pos_idx (4-8) and pos_score
+// (14-23) if positional, ang_idx (9-13) and ang_score (24-33) if angular.
+__host__ __device__ inline int finish_n_pieces(int lists) {
+  return 4 + ((lists & 1) ? 15 : 0) + ((lists & 2) ? 15 : 0);
+}
+__host__ __device__ inline int finish_piece(int t, int lists) {  // t < finish_n_pieces(lists)
+  if (t < 4) return t;
+  t -= 4;
+  if (lists & 1) {
+    if (t < 5) return 4 + t;          // pos_idx
+    if (t < 15) return 14 + (t - 5);  // pos_score
+    t -= 15;
+  }
+  return t < 5 ? 9 + t : 24 + (t - 5);  // ang_idx, ang_score
+}
+// One piece's share of the checksum (pieces add up in any order: the device
+// sums its lanes' shares, the host its copy's).
+__host__ __device__ inline uint64_t finish_piece_hash(int pc, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  const uint64_t a = ((uint64_t)w1 << 32) | w0, b = ((uint64_t)w3 << 32) | w2;
+  uint64_t h = (a * 0x9E3779B97F4A7C15ull) ^ (b + 0xC2B2AE3D27D4EB4Full * (uint64_t)(pc + 1));
+  h ^= h >> 31;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 29;
+  return h;
+}
+__host__ __device__ inline uint64_t finish_seal_share(uint64_t tag_kind) {
+  return finish_piece_hash(kFinishSealPiece, (uint32_t)tag_kind, (uint32_t)(tag_kind >> 32), 0x5EA1u, 0u);
+}
 
 constexpr int kFinishWaveScratch = 640;  // bytes of per-wave scratch
 #ifndef CSM_FINISH_WAVES
@@ -160,13 +204,13 @@ constexpr int kFinishWaves = CSM_FINISH_WAVES;  // waves per window of the exact
 constexpr size_t kFinishMisc = (48 + 16 * (size_t)kFinishWaves + 4 + 15) & ~(size_t)15;
 
 struct FinishLayout {
-  size_t wave_scratch, defer, keys, vals, lpos, rpos, stack, total;
+  size_t wave_scratch, defer, keys, vals, lpos, rpos, stack, fout, total;
 };
 constexpr int kFinishDefer = 64;  // segments the partial sort may set aside (12 B each)
 
 // LDS carve of the finish kernel for n candidates (16-byte aligned pieces):
 // misc | kFinishWaves wave scratches | deferred segments | keys f64[n] | vals u16[n] |
-// lpos u16[n] | rpos u16[n] | shared segment stack.
+// lpos u16[n] | rpos u16[n] | shared segment stack | FinishOut.
 constexpr FinishLayout finish_layout(int64_t n) {
   FinishLayout L{};
   size_t o = kFinishMisc;
@@ -184,6 +228,8 @@ constexpr FinishLayout finish_layout(int64_t n) {
   o += ((size_t)n * 2 + 15) & ~(size_t)15;
   L.stack = o;
   o += ((size_t)(n / 16 + 64) * 12 + 15) & ~(size_t)15;  // live segments
+  L.fout = o;  // the window's FinishOut, assembled here and stored sealed
+  o += (sizeof(FinishOut) + 15) & ~(size_t)15;
   L.total = o;
   return L;
 }
