@@ -64,7 +64,7 @@ def _metric(search):
 # fp64 arithmetic: FP64 vector peak = half the FP32 rate).
 HBM_PEAK_GBS = 8000.0
 N_CU, N_SIMD, CLK_GHZ = 256, 1024, 2.4
-COUNTERS_JSON = os.path.join(ROOT, "profiles", "r03", "counters.json")
+COUNTERS_JSON = os.path.join(ROOT, "profiles", "r04", "counters.json")
 # the loop-closure / willow legs' counters (tools/pmc_topbox.sh: the search's top-level kernel)
 COUNTERS_LC_JSON = os.path.join(ROOT, "profiles", "r03", "counters_lc.json")
 CSRC = os.path.join(ROOT, "roborts-edu-slam_amd", "csrc")

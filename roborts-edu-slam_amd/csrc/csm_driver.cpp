@@ -165,13 +165,16 @@ int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
   return CSM_OK;
 }
 
-// level_begin with the plan in two pieces: the first `first` windows are
-// planned on the calling thread and their scoring goes out at once, the rest
-// are planned on the pool while it runs, then the finish follows for all.
-// For the 3-level driver's first part, where nothing else keeps the device
-// busy while the host plans (a call's first ~0.15 ms).
+// level_begin with the plan in growing pieces: the pool plans the first
+// `first` windows and their scoring goes out at once, then the next
+// span_growth times as many while those score, and so on; the finish follows
+// for all. For the 3-level driver's first part, where nothing else keeps the
+// device busy while the host plans (a call's first ~0.3 ms with the whole
+// level planned before one launch). The spans are whole-window
+// ranges of one level: results are the one-launch level's.
 int level_begin_split(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param& P, const double* poses,
                       double* responses, LevelRun& R, const int32_t* scan_grid, int skip_lists, int first) {
+  const double t_in = now_ms();
   int st = level_prepare(c, n_scans, offsets, P, responses, nullptr, R, scan_grid, skip_lists, true);
   if (st != CSM_OK) return st;
   const int nw = (int)R.scan_of.size();
@@ -180,12 +183,20 @@ int level_begin_split(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const
   const double t0 = now_ms();
   if ((st = level_alloc(c, offsets, R, c->h_angles)) != CSM_OK) return st;
   const Geometry G(c->info);
-  for (int i = 0; i < first; ++i) level_plan_one(R, G, offsets, poses, i);
-  if ((st = level_launch(c, R, WinSpan{0, first, true, false})) != CSM_OK) return st;
-  if (c->profiling && c->t_call > 0.0) c->account("host:entry->first_launch", (float)(now_ms() - c->t_call), 0.0, 0.0);
-  c->parallel_for(nw - first, c->host_threads, [&](int i) { level_plan_one(R, G, offsets, poses, first + i); });
-  c->account_pool("plan");
-  if ((st = level_launch(c, R, WinSpan{first, nw, true, false})) != CSM_OK) return st;
+  if (c->profiling) c->account("host:first:prepare+alloc", (float)(now_ms() - t_in), 0.0, 0.0);
+  int w0 = 0;
+  for (int64_t sz = first; w0 < nw; sz *= std::max(2, c->span_growth)) {
+    // the last span takes the rest when it would leave less than a span behind
+    const int w1 = (nw - w0 <= 2 * sz) ? nw : w0 + (int)sz;
+    const double tp = now_ms();
+    c->parallel_for(w1 - w0, c->host_threads, [&](int i) { level_plan_one(R, G, offsets, poses, w0 + i); });
+    c->account_pool("plan");
+    if (c->profiling && w0 == 0) c->account("host:first:plan", (float)(now_ms() - tp), 0.0, 0.0);
+    if ((st = level_launch(c, R, WinSpan{w0, w1, true, false})) != CSM_OK) return st;
+    if (w0 == 0 && c->profiling && c->t_call > 0.0)
+      c->account("host:entry->first_launch", (float)(now_ms() - c->t_call), 0.0, 0.0);
+    w0 = w1;
+  }
   if ((st = level_launch(c, R, WinSpan{0, nw, false, true})) != CSM_OK) return st;
   if (c->profiling) {
     char nm[48];

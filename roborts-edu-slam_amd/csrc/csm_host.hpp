@@ -583,7 +583,8 @@ struct csm_ctx {
   int pipeline_min = 512;    // fewest scans the 3-level driver splits into parts (CSM_PIPELINE)
   bool skip_dead_lists = true;  // live_lists (CSM_SKIP_DEAD_LISTS=0: every level fills both lists)
   int pipeline_parts = 2;    // parts in flight (CSM_PIPELINE_PARTS: 2..kMaxParts; 2 measured fastest)
-  int first_windows = 64;    // level_begin_split: windows the first part's first launch takes (CSM_FIRST_WINDOWS; 0: one launch)
+  int first_windows = 128;   // level_begin_split: windows the first part's first launch takes (CSM_FIRST_WINDOWS; 0: one launch)
+  int span_growth = 4;       // ... and each later span's growth (CSM_SPAN_GROWTH)
   void swap_slot(int i) {    // i >= 1: exchange the current buffer set with alt[i - 1]
     Slot& a = alt[i - 1];
     std::swap(scans, a.scans);

@@ -594,7 +594,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   // pass exit, so the slot's next scoring need not wait for it)
   if (c->profiling && sp.score && w0 == 0 && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess)
     return c->hip_fail(e, "hipEventRecord");
-  if (c->profiling && sp.score && w0 > 0) {  // a later span: the gap since the first one ends here
+  // a later span: the gap since the first one ends here (only the first gap is
+  // taken out of the level's kernel time; later ones are short, spans overlap)
+  if (c->profiling && sp.score && w0 > 0 && !c->span_gap) {
     if ((e = hipEventRecord(c->ev_g1, c->stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
     c->span_gap = true;
   }

@@ -58,10 +58,10 @@ def _short(name: str) -> str:
         args = [a.strip() for a in name[i:name.index(">", i)].split(",")]
         return f"score_tiny_kernel<{args[0]},{'best' if args[-1] == 'true' else 'all'}>"
     key = "score_phase_kernel<"
-    if key in name:  # <int NS, int C, int NQ, bool BEST>
+    if key in name:  # <int NS, int C, int NQ, bool BEST[, bool ST]> (r04: the strip form's flag last)
         i = name.index(key) + len(key)
         args = [a.strip() for a in name[i:name.index(">", i)].split(",")]
-        return f"score_phase_kernel<{args[0]},{'best' if args[-1] == 'true' else 'all'}>"
+        return f"score_phase_kernel<{args[0]},{'best' if args[3] == 'true' else 'all'}>"
     for key in ("score_all_kernel<", "score_best_kernel<"):
         if key in name:
             i = name.index(key)
