@@ -32,6 +32,26 @@ struct LevelRun {
   std::vector<char>* how = nullptr;
   // a window's FinishOut never matched its seal (pinned host memory): 1
   mutable int err = 0;
+  // back to a fresh run, the vectors' capacity kept
+  void reset() {
+    P = csm_param{};
+    D = Dims{};
+    scan_of.clear();
+    plans.clear();
+    pt_off.clear();
+    grid.clear();
+    angles = nullptr;
+    rows = nullptr;
+    fin = nullptr;
+    scores = nullptr;
+    dev = false;
+    skip_lists = 0;
+    pend = PendingRun{};
+    tag = -1;
+    snap = nullptr;
+    how = nullptr;
+    err = 0;
+  }
 };
 
 // Seals (csm_internal.hpp) are waited for at most this long: they land within
@@ -41,12 +61,14 @@ constexpr double kSealWaitMs = 2000.0;
 // Window i's FinishOut from the pinned host memory the finish wrote, whole:
 // spin until its seal names a final writer for this launch and the copy's
 // pieces match it (the pieces can land after the launch's flag).
-bool sealed_copy(const LevelRun& R, int i, csm::FinishOut& out) {
+// Returns the writer (kSealFast / kSealExact), kSealPending when `pending_ok`
+// and the fast pass left the window to the exact pass, 0 on a timeout.
+uint32_t sealed_copy(const LevelRun& R, int i, csm::FinishOut& out, bool pending_ok) {
   const double t0 = now_ms();
   for (uint32_t spin = 1;; ++spin) {
     const uint32_t w = read_sealed(R.fin + i, R.pend.flag_value, out);
-    if (w == csm::kSealFast || w == csm::kSealExact) return true;
-    if ((spin & 255) == 0 && now_ms() - t0 > kSealWaitMs) return false;
+    if (w == csm::kSealFast || w == csm::kSealExact || (pending_ok && w == csm::kSealPending)) return w;
+    if ((spin & 255) == 0 && now_ms() - t0 > kSealWaitMs) return 0u;
     __builtin_ia32_pause();
   }
 }
@@ -236,8 +258,10 @@ int level_check(csm_ctx* c, const LevelRun& R) {
 
 // Complete window i of a joined level: pose, covariance and response
 // (BasedCorrelationScanMatch::ScanMatch :815-869).
-void level_complete_one(const LevelRun& R, const Geometry& G, double* poses, double* covs, double* responses,
-                        int64_t* argmax_flat, int i) {
+// defer (early completion): a window whose seal says the exact pass still owes
+// it is not completed; returns false and the caller completes it after the join.
+bool level_complete_one(const LevelRun& R, const Geometry& G, double* poses, double* covs, double* responses,
+                        int64_t* argmax_flat, int i, bool defer = false) {
   thread_local std::vector<Entry> scratch;
   const Dims& D = R.D;
   const csm_param& P = R.P;
@@ -248,12 +272,18 @@ void level_complete_one(const LevelRun& R, const Geometry& G, double* poses, dou
   csm::FinishOut local;
   const csm::FinishOut* o = nullptr;
   if (R.dev && R.pend.fin_host) {  // pinned host memory the finish wrote: a sealed copy
-    if (!sealed_copy(R, i, local) || local.count < 0) {
+    const uint32_t w = sealed_copy(R, i, local, defer);
+    if (w == csm::kSealPending) {
+      if (R.how) (*R.how)[(size_t)i] = 2;
+      return false;
+    }
+    if (w == 0 || local.count < 0) {
       __atomic_store_n(&R.err, 1, __ATOMIC_RELAXED);
-      return;
+      return true;
     }
     o = &local;
     if (R.snap) (*R.snap)[(size_t)i] = local;
+    if (R.how && (*R.how)[(size_t)i] != 2) (*R.how)[(size_t)i] = 1;
   } else if (R.dev) {
     o = R.fin + i;
   } else {
@@ -262,37 +292,17 @@ void level_complete_one(const LevelRun& R, const Geometry& G, double* poses, dou
   }
   if (argmax_flat) argmax_flat[s] = o->front_idx;
   responses[s] = complete_window(*o, C, P, G, poses + 3 * s, covs + 9 * s, R.skip_lists);
+  return true;
 }
 
-// A signalled level with the fast pass's early signal: wait for it and split
-// the windows into those the fast pass settled and those the exact pass owes
-// (FinishOut::count == kFinishPending), the host's work on the first set
-// overlapping the exact pass.
-int level_wait_fast(csm_ctx* c, const LevelRun& R, std::vector<int>& settled, std::vector<int>& owed) {
-  const int nw = (int)R.scan_of.size();
+// A signalled level with the fast pass's early signal: wait for it. The
+// windows it settled are then completed while the exact pass sorts the rest;
+// which are which, each window's seal says (level_complete_one's defer).
+int level_wait_fast(csm_ctx* c, const LevelRun& R) {
   const double t1 = now_ms();
   const int st = wait_flag(c, R.pend, R.pend.fast_flag);
   if (st != CSM_OK) return st;
   if (c->profiling) c->account("host:wait_fast", (float)(now_ms() - t1), 0.0, 0.0);
-  settled.clear();
-  owed.clear();
-  settled.reserve((size_t)nw);
-  // the seal's first word says who wrote the window for this launch (spin on
-  // one whose seal has not landed yet)
-  for (int i = 0; i < nw; ++i) {
-    uint32_t w = seal_writer(R.fin + i, R.pend.flag_value);
-    for (uint32_t spin = 1; w == 0; ++spin) {
-      if ((spin & 255) == 0 && now_ms() - t1 > kSealWaitMs)
-        return c->fail(CSM_ERR_HIP, "finish: a window's seal never landed after the fast pass's signal");
-      __builtin_ia32_pause();
-      w = seal_writer(R.fin + i, R.pend.flag_value);
-    }
-    (w == csm::kSealPending ? owed : settled).push_back(i);
-  }
-  if (R.how) {
-    for (int i : settled) (*R.how)[(size_t)i] = 1;
-    for (int i : owed) (*R.how)[(size_t)i] = 2;
-  }
   return CSM_OK;
 }
 
@@ -305,14 +315,16 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
   const int threads = (nw >= 64) ? c->host_threads : 1;
   double t2;
   if (R.dev && R.pend.fast_flag) {  // settled windows while the exact pass runs
-    std::vector<int> settled, owed;
-    if ((st = level_wait_fast(c, R, settled, owed)) != CSM_OK) return st;
+    if ((st = level_wait_fast(c, R)) != CSM_OK) return st;
     t2 = now_ms();
-    c->parallel_for((int)settled.size(), threads, [&](int k) {
-      level_complete_one(R, G, poses, covs, responses, argmax_flat, settled[(size_t)k]);
+    std::vector<int> owed((size_t)nw);
+    int n_owed = 0;
+    c->parallel_for(nw, threads, [&](int i) {
+      if (!level_complete_one(R, G, poses, covs, responses, argmax_flat, i, true))
+        owed[(size_t)__atomic_fetch_add(&n_owed, 1, __ATOMIC_RELAXED)] = i;
     });
     if ((st = level_join(c, R)) != CSM_OK) return st;
-    c->parallel_for((int)owed.size(), owed.size() >= 32 ? threads : 1, [&](int k) {
+    c->parallel_for(n_owed, n_owed >= 32 ? threads : 1, [&](int k) {
       level_complete_one(R, G, poses, covs, responses, argmax_flat, owed[(size_t)k]);
     });
   } else {
@@ -352,25 +364,29 @@ int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const
     return level_begin(c, n_scans, offsets, P, poses, responses, nullptr, N, scan_grid, skip_lists);
   }
   const bool early = R.dev && R.pend.fast_flag;
-  std::vector<int> settled, owed;
-  if ((st = early ? level_wait_fast(c, R, settled, owed) : level_join(c, R)) != CSM_OK) return st;
+  if ((st = early ? level_wait_fast(c, R) : level_join(c, R)) != CSM_OK) return st;
   const double t2 = now_ms();
   std::swap(c->h_angles, c->h_angles_next);
   if ((st = level_alloc(c, offsets, N, c->h_angles)) != CSM_OK) return st;
   const Geometry G(c->info);
   const int threads = (nw >= 64) ? c->host_threads : 1;
-  auto one = [&](int i) {
-    level_complete_one(R, G, poses, covs, responses, nullptr, i);
+  auto one = [&](int i, bool defer) {
+    if (!level_complete_one(R, G, poses, covs, responses, nullptr, i, defer)) return false;
     const int s = R.scan_of[(size_t)i];
     sum[s] += responses[s];
     level_plan_one(N, G, offsets, poses, i);
+    return true;
   };
   if (early) {  // the settled windows while the exact pass runs, then the ones it owed
-    c->parallel_for((int)settled.size(), threads, [&](int k) { one(settled[(size_t)k]); });
+    std::vector<int> owed((size_t)nw);
+    int n_owed = 0;
+    c->parallel_for(nw, threads, [&](int i) {
+      if (!one(i, true)) owed[(size_t)__atomic_fetch_add(&n_owed, 1, __ATOMIC_RELAXED)] = i;
+    });
     if ((st = level_join(c, R)) != CSM_OK) return st;
-    c->parallel_for((int)owed.size(), owed.size() >= 32 ? threads : 1, [&](int k) { one(owed[(size_t)k]); });
+    c->parallel_for(n_owed, n_owed >= 32 ? threads : 1, [&](int k) { one(owed[(size_t)k], false); });
   } else {
-    c->parallel_for(nw, threads, one);
+    c->parallel_for(nw, threads, [&](int i) { one(i, false); });
   }
   if ((st = level_check(c, R)) != CSM_OK) return st;
   if (threads > 1) c->account_pool("complete+plan");
@@ -423,7 +439,13 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
     count[h] = (int32_t)((int64_t)n_scans * (h + 1) / K) - first[h];
   }
   std::vector<double> resp((size_t)n_scans, 0.0);
-  LevelRun R[2][csm_ctx::kMaxParts];  // by level parity: level l's run and level l + 1's
+  // by level parity: level l's run and level l + 1's. Kept per thread across
+  // calls: a fresh run's window plans (64 B each, 128 KB per 2048 windows) came
+  // from mmap and paid ~40 us of page faults at every level start (r04,
+  // host:first:prepare+alloc); reused, their vectors keep their capacity.
+  static thread_local LevelRun R[2][csm_ctx::kMaxParts];
+  for (auto& row : R)
+    for (LevelRun& r : row) r.reset();
   std::vector<csm::FinishOut> snaps[csm_ctx::kMaxParts];  // CSM_DEBUG_FIN
   std::vector<char> hows[csm_ctx::kMaxParts];
   auto skip = [&](int l) { return c->skip_dead_lists ? live_lists(levels, n_levels, l) : 0; };
