@@ -843,12 +843,12 @@ def online_bench(args, rank, world_size, dist, torch):
     kept_a = np.array(kept_flags)
     order = np.argsort(lat_ms)[::-1][:8]
     steady = lat_ms[~grew] if (~grew).any() else lat_ms
-    ph_names = ("prepare", "match", "map_check", "update_map")
-    ph = np.array([[p[n] for n in ph_names] for p in phases]) if phases else np.zeros((1, 4))
+    ph_names = ("prepare", "match", "map_check", "update_map", "update_pub", "update_coarse", "update_fine")
+    ph = np.array([[p[n] for n in ph_names] for p in phases]) if phases else np.zeros((1, len(ph_names)))
     tail = {"slowest": [{"scan": int(args.warmup + i), "ms": float(lat_ms[i]), "kept": bool(kept_a[i]),
                          "fine_map_grew": bool(grew[i]),
                          "phases_ms": {n: round(float(ph[i, c]), 4) for c, n in enumerate(ph_names)},
-                         "outside_call_ms": round(float(lat_ms[i] - ph[i].sum()), 4)} for i in order],
+                         "outside_call_ms": round(float(lat_ms[i] - ph[i, :4].sum()), 4)} for i in order],
             "phase_ms": {n: {"p50": float(np.median(ph[:, c])), "p99": float(np.percentile(ph[:, c], 99)),
                              "max": float(ph[:, c].max())} for c, n in enumerate(ph_names)},
             "p99_not_kept_ms": float(np.percentile(lat_ms[~kept_a], 99)) if (~kept_a).any() else None,

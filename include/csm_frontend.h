@@ -113,9 +113,10 @@ int csm_frontend_kept_scans(csm_frontend* fe, int32_t* n, double* poses);
 /* Host wall time (ms) of the last csm_frontend_process call's phases:
  * [0] points scaled to the three resolutions, [1] the 3-level match
  * (ScanMatchers::ScanMatch), [2] the map check (MapCheckPenalize), [3] the
- * three map updates (UpdateMap; 0 when the scan was not kept). Diagnostics of
+ * three map updates (UpdateMap; 0 when the scan was not kept), and of those
+ * [4] the PubMap's, [5] the coarse map's, [6] the fine map's. Diagnostics of
  * the latency tail (no reference counterpart). */
-int csm_frontend_last_phases(const csm_frontend* fe, double ms[4]);
+int csm_frontend_last_phases(const csm_frontend* fe, double ms[7]);
 
 #ifdef __cplusplus
 }

@@ -84,6 +84,7 @@ struct csm_frontend {
   double t_phase[6] = {0, 0, 0, 0, 0, 0};
   int64_t n_timed = 0;
   double last_phase[6] = {0, 0, 0, 0, 0, 0};  // the last call's (csm_frontend_last_phases)
+  double last_update[3] = {0, 0, 0};          // ... its three map updates: pub, coarse, fine
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -179,6 +180,7 @@ int csm_frontend_process(csm_frontend* f, const double* pts, int32_t n, const do
   using clk = std::chrono::steady_clock;
   auto tp = clk::now();
   for (double& t : f->last_phase) t = 0.0;
+  for (double& t : f->last_update) t = 0.0;
   auto lap = [&](int k) {
     const auto now = clk::now();
     const double ms = std::chrono::duration<double, std::milli>(now - tp).count();
@@ -256,14 +258,20 @@ int csm_frontend_process(csm_frontend* f, const double* pts, int32_t n, const do
     if (st != CSM_OK) return f->check(st, "pub map cell params");
     int32_t up = 0;
     const double* pose = f->current_pose;
+    const auto tu0 = clk::now();
     if ((st = csm_gridmap_update_by_range(pub, f->pub_pts.data(), n, nullptr, pose, 0, &up)) != CSM_OK)
       return f->check(st, "UpdateMapByRange(pub)");
+    const auto tu1 = clk::now();
     if ((st = csm_gridmap_update_by_range(f->maps[CSM_COARSE_MAP], f->coarse_pts.data(), n, nullptr, pose,
                                           p.coarse_map_use_blur, &up)) != CSM_OK)
       return f->check(st, "UpdateMapByRange(coarse)");
+    const auto tu2 = clk::now();
     if ((st = csm_gridmap_update_by_range(f->maps[CSM_FINE_MAP], f->fine_pts.data(), n, nullptr, pose,
                                           p.fine_map_use_blur, &up)) != CSM_OK)
       return f->check(st, "UpdateMapByRange(fine)");
+    f->last_update[0] = std::chrono::duration<double, std::milli>(tu1 - tu0).count();
+    f->last_update[1] = std::chrono::duration<double, std::milli>(tu2 - tu1).count();
+    f->last_update[2] = std::chrono::duration<double, std::milli>(clk::now() - tu2).count();
     std::memcpy(f->last_map_update_pose, f->current_pose, sizeof(f->current_pose));
     updated = true;
   }
@@ -330,12 +338,15 @@ int csm_frontend_correct_pose_and_map(csm_frontend* f, int32_t n, const int32_t*
   return CSM_OK;
 }
 
-int csm_frontend_last_phases(const csm_frontend* f, double ms[4]) {
+int csm_frontend_last_phases(const csm_frontend* f, double ms[7]) {
   if (!f || !ms) return CSM_ERR_INVALID_ARG;
   ms[0] = f->last_phase[0];
   ms[1] = f->last_phase[3];
   ms[2] = f->last_phase[4];
   ms[3] = f->last_phase[5];
+  ms[4] = f->last_update[0];
+  ms[5] = f->last_update[1];
+  ms[6] = f->last_update[2];
   return CSM_OK;
 }
 

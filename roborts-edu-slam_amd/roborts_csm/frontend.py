@@ -160,10 +160,12 @@ class SlamFrontEnd:
 
     def last_phases(self) -> dict:
         """Host wall time (ms) of the last process() call's phases
-        (csm_frontend_last_phases): prepare, match, map_check, update_map."""
-        out = np.zeros(4)
+        (csm_frontend_last_phases): prepare, match, map_check, update_map and
+        the latter's three maps."""
+        out = np.zeros(7)
         _lib.csm_frontend_last_phases(self._h, out.ctypes.data_as(C.POINTER(C.c_double)))
-        return dict(zip(("prepare", "match", "map_check", "update_map"), (float(x) for x in out)))
+        return dict(zip(("prepare", "match", "map_check", "update_map", "update_pub", "update_coarse", "update_fine"),
+                        (float(x) for x in out)))
 
     def map(self, which: int) -> OccuGridMap:
         h = C.c_void_p()
