@@ -122,10 +122,11 @@ struct BoxWave {
     const bool live = cb + lane < n_used;
     slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean && !far) != 0) << min(cb >> 6, 63);
     int o;
-    if (STRIP) {
-      const int c = (-(ix0 >> 2)) & 3;
-      const int xs = (ix0 & ~3) + 4 * c;
-      o = c * copy_bytes + (xs >> 4) * strip_bytes + iy0 * 16 + (ix0 & 3);
+    if (STRIP) {  // (kStripShift: 4 or 1 cells between copies)
+      constexpr int S = kStripShift, LS = S == 4 ? 2 : 0;
+      const int c = (-(ix0 >> LS)) & (kStripCopies - 1);
+      const int xs = (ix0 & ~(S - 1)) + S * c;
+      o = c * copy_bytes + (xs >> 4) * strip_bytes + iy0 * 16 + (ix0 & (S - 1));
     } else {
       o = iy0 * pitch4 + (ix0 << cell_shift);
     }
@@ -858,17 +859,24 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
         for (int p = 0; p < kPairPD; ++p) {
           // the pair's two rows, each shifted by its corner's byte phase, then
           // merged into codes a | b << sh (indices < 16: no carry between bytes)
-          const uint32_t sa = (uint32_t)curA[p] & 3u, sb = (uint32_t)curB[p] & 3u;
           const v4i xa = dA[p], xb = dB[p];
           uint32_t w[4];
-          w[0] = __builtin_amdgcn_alignbyte((uint32_t)xa.y, (uint32_t)xa.x, sa) |
-                 (__builtin_amdgcn_alignbyte((uint32_t)xb.y, (uint32_t)xb.x, sb) << sh);
-          w[1] = __builtin_amdgcn_alignbyte((uint32_t)xa.z, (uint32_t)xa.y, sa) |
-                 (__builtin_amdgcn_alignbyte((uint32_t)xb.z, (uint32_t)xb.y, sb) << sh);
-          w[2] = __builtin_amdgcn_alignbyte((uint32_t)xa.w, (uint32_t)xa.z, sa) |
-                 (__builtin_amdgcn_alignbyte((uint32_t)xb.w, (uint32_t)xb.z, sb) << sh);
-          w[3] = __builtin_amdgcn_alignbyte(0u, (uint32_t)xa.w, sa) |
-                 (__builtin_amdgcn_alignbyte(0u, (uint32_t)xb.w, sb) << sh);
+          if constexpr (kStripShift == 1) {  // every row at byte 0 of its strip row
+            w[0] = (uint32_t)xa.x | ((uint32_t)xb.x << sh);
+            w[1] = (uint32_t)xa.y | ((uint32_t)xb.y << sh);
+            w[2] = (uint32_t)xa.z | ((uint32_t)xb.z << sh);
+            w[3] = (uint32_t)xa.w | ((uint32_t)xb.w << sh);
+          } else {
+            const uint32_t sa = (uint32_t)curA[p] & 3u, sb = (uint32_t)curB[p] & 3u;
+            w[0] = __builtin_amdgcn_alignbyte((uint32_t)xa.y, (uint32_t)xa.x, sa) |
+                   (__builtin_amdgcn_alignbyte((uint32_t)xb.y, (uint32_t)xb.x, sb) << sh);
+            w[1] = __builtin_amdgcn_alignbyte((uint32_t)xa.z, (uint32_t)xa.y, sa) |
+                   (__builtin_amdgcn_alignbyte((uint32_t)xb.z, (uint32_t)xb.y, sb) << sh);
+            w[2] = __builtin_amdgcn_alignbyte((uint32_t)xa.w, (uint32_t)xa.z, sa) |
+                   (__builtin_amdgcn_alignbyte((uint32_t)xb.w, (uint32_t)xb.z, sb) << sh);
+            w[3] = __builtin_amdgcn_alignbyte(0u, (uint32_t)xa.w, sa) |
+                   (__builtin_amdgcn_alignbyte(0u, (uint32_t)xb.w, sb) << sh);
+          }
           const double c = (double)((cnts >> (8 * p)) & 0xFFu);
           dA[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (nxtA[p] & ~15), 0, 0);
           dB[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (nxtB[p] & ~15), 0, 0);

@@ -313,7 +313,15 @@ hipError_t launch_build_palette(const int32_t* gridi, int64_t n, int32_t* scratc
 // contiguous bytes (2.5 cache lines, not 13-14).
 constexpr int kPairMaxPal = 16;
 constexpr int kStripW = 16;
-constexpr int kStripCopies = 4;
+#ifndef CSM_STRIP_COPIES
+#define CSM_STRIP_COPIES 4
+#endif
+// copies of the index grid, each kStripShift cells further along: 4 leaves a
+// box row at a byte phase ix0 & 3 the kernel aligns (v_alignbyte); 16 puts
+// every row at byte 0 of its strip row (64 MB for a 2000^2 grid)
+constexpr int kStripCopies = CSM_STRIP_COPIES;
+constexpr int kStripShift = kStripW / kStripCopies;
+static_assert(kStripCopies == 4 || kStripCopies == 16, "strip copies: 4 or 16");
 constexpr int kStripPadRows = 16;  // zero rows below the grid (box rows and the zero run's rows)
 struct StripGeom {
   int32_t rows, n_strips;

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void pal_index_kernel(const int4* __restrict__
 }
 
 // Strip copies of the palette index grid (v11 pair box kernel): copy c holds
-// cell x of row y at byte (x + 4c) of its strip row, strips kStripW bytes
+// cell x of row y at byte (x + kStripShift c) of its strip row, strips kStripW bytes
 // wide with their rows contiguous (row y of strip t at (t * rows + y) * 16).
 // One thread writes one 16-byte strip row; cells off the grid are index 0.
 __global__ __launch_bounds__(256) void pal_strips_kernel(const uint8_t* __restrict__ idx, int pitch, int sx,
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void pal_strips_kernel(const uint8_t* __restri
     if (y < sy) {
 #pragma unroll
       for (int b = 0; b < 16; ++b) {
-        const int x = kStripW * t + b - 4 * c;
+        const int x = kStripW * t + b - kStripShift * c;
         const uint32_t v = (x >= 0 && x < sx) ? src[x] : 0u;
         w[b >> 2] |= v << (8 * (b & 3));
       }
@@ -248,8 +248,8 @@ hipError_t launch_build_istrips(const int32_t* gridi, int pitch, int size_x, int
 StripGeom strip_geom(int size_x, int size_y) {
   StripGeom G{};
   G.rows = size_y + kStripPadRows;
-  // a box row piece starts at (ix & ~3) + 4c <= size_x - 1 + 12 in copy c
-  G.n_strips = (size_x + 11) / kStripW + 1;
+  // a box row piece starts at (ix & ~(S - 1)) + S c <= size_x - 1 + 16 - S in copy c (S = kStripShift)
+  G.n_strips = (size_x + 15 - kStripShift) / kStripW + 1;
   G.strip_bytes = (int64_t)G.rows * kStripW;
   G.copy_bytes = G.strip_bytes * G.n_strips;
   G.grid_bytes = G.copy_bytes * kStripCopies;
