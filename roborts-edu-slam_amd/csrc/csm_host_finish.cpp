@@ -5,6 +5,7 @@
 // the device's node table (BranchAndBoundCorrelateScanMatcher, :271-502).
 #include "csm_host.hpp"
 
+#include <cstddef>
 #include <cstring>
 
 namespace csmh {
@@ -87,20 +88,36 @@ uint32_t seal_writer(const csm::FinishOut* src, int32_t tag) {
   return (uint32_t)tk == (uint32_t)tag ? (uint32_t)(tk >> 32) & 3u : 0u;
 }
 
+// Only the pieces the seal names are copied (and hashed): the GPU wrote them
+// into memory no CPU cache holds, so every line read is a memory round trip
+// (a coarse window's header is 2 of the structure's 9 lines).
 uint32_t read_sealed(const csm::FinishOut* src, int32_t tag, csm::FinishOut& out) {
-  std::memcpy(&out, src, sizeof(out));
-  const uint64_t tk = out.seal_tag_kind;
+  const uint64_t tk = __atomic_load_n(&src->seal_tag_kind, __ATOMIC_ACQUIRE);
   if ((uint32_t)tk != (uint32_t)tag) return 0u;
   const uint32_t kind = (uint32_t)(tk >> 32), writer = kind & 3u;
   if (writer == csm::kSealPending) return writer;
   const int lists = (int)(kind >> 2) & 3;
+  const uint64_t chk = __atomic_load_n(&src->seal_chk, __ATOMIC_RELAXED);
+  const char* in = reinterpret_cast<const char*>(src);
+  char* o = reinterpret_cast<char*>(&out);
+  std::memcpy(o, in, 64);                                              // header, pieces 0-3
+  if (lists & 1) {
+    std::memcpy(o + offsetof(csm::FinishOut, pos_idx), in + offsetof(csm::FinishOut, pos_idx), 80);
+    std::memcpy(o + offsetof(csm::FinishOut, pos_score), in + offsetof(csm::FinishOut, pos_score), 160);
+  }
+  if (lists & 2) {
+    std::memcpy(o + offsetof(csm::FinishOut, ang_idx), in + offsetof(csm::FinishOut, ang_idx), 80);
+    std::memcpy(o + offsetof(csm::FinishOut, ang_score), in + offsetof(csm::FinishOut, ang_score), 160);
+  }
+  out.seal_tag_kind = tk;
+  out.seal_chk = chk;
   uint64_t h = csm::finish_seal_share(tk);
   const uint32_t* words = reinterpret_cast<const uint32_t*>(&out);
   for (int t = 0, n = csm::finish_n_pieces(lists); t < n; ++t) {
     const int pc = csm::finish_piece(t, lists);
     h += csm::finish_piece_hash(pc, words[4 * pc], words[4 * pc + 1], words[4 * pc + 2], words[4 * pc + 3]);
   }
-  return h == out.seal_chk ? writer : 0u;
+  return h == chk ? writer : 0u;
 }
 
 double complete_window(const csm::FinishOut& o, const CandGeom& C, const csm_param& P,

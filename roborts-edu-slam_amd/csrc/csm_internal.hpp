@@ -314,11 +314,12 @@ hipError_t launch_build_palette(const int32_t* gridi, int64_t n, int32_t* scratc
 constexpr int kPairMaxPal = 16;
 constexpr int kStripW = 16;
 #ifndef CSM_STRIP_COPIES
-#define CSM_STRIP_COPIES 4
+#define CSM_STRIP_COPIES 16
 #endif
-// copies of the index grid, each kStripShift cells further along: 4 leaves a
-// box row at a byte phase ix0 & 3 the kernel aligns (v_alignbyte); 16 puts
-// every row at byte 0 of its strip row (64 MB for a 2000^2 grid)
+// copies of the index grid, each kStripShift cells further along: 16 puts
+// every box row at byte 0 of its strip row (64 MB for a 2000^2 grid); 4
+// leaves a byte phase ix0 & 3 the kernel aligns (v_alignbyte, 16 MB). r04,
+// isolated coarse launch of 4096 windows: 1.404 ms with 4, 1.358 with 16.
 constexpr int kStripCopies = CSM_STRIP_COPIES;
 constexpr int kStripShift = kStripW / kStripCopies;
 static_assert(kStripCopies == 4 || kStripCopies == 16, "strip copies: 4 or 16");

@@ -68,9 +68,6 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));
 #ifndef CSM_PHASE_WAVES
 #define CSM_PHASE_WAVES 4
 #endif
-#ifndef CSM_PHASE_PAIRFLUSH
-#define CSM_PHASE_PAIRFLUSH 0
-#endif
 
 // ST: the box rows come from the strip copies of gridi (L.istrips, r04): a
 // beam's 5 rows are 160 contiguous bytes of one strip instead of 5 rows of the
@@ -281,29 +278,17 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
       }
       int32_t part[4] = {0, 0, 0, 0};
       int t_prev = __builtin_amdgcn_readfirstlane((int)gtag[0]);
+      // (r04: adding slot pairs in registers first, half the lanes and half
+      // the same-address atomics, took the isolated 4096-window launch from
+      // 0.508 to 0.573 ms: the shuffles cost more than the conflicts)
       auto flush = [&](int tag) {  // uniform tag: pair tag >> 1
         int64_t* dst = psum + (tag >> 1) * PC + lane_cell;
-#if CSM_PHASE_PAIRFLUSH
-        // slots 2s and 2s + 1 meet in registers first (LPS lanes apart): half
-        // the lanes add, with half as many on one address (the same-address
-        // atomics were the kernel's LDS bank conflicts)
-        const bool adder = cact && (slot & 1) == 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int32_t o = __shfl_down(part[t], LPS, 64);
-          if (adder && 4 * ch + t < C)
-            __hip_atomic_fetch_add(dst + t, (int64_t)part[t] + (slot + 1 < SL ? o : 0), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-          part[t] = 0;
-        }
-#else
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           if (cact && 4 * ch + t < C)
             __hip_atomic_fetch_add(dst + t, (int64_t)part[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           part[t] = 0;
         }
-#endif
       };
       int gev = gtag[lane & (kD - 1)];
       // the list entries (this lane's slot) whose loads a block issues are read
