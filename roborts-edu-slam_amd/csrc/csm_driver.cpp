@@ -436,9 +436,15 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
   } early_on{c};
   c->early_now = true;
   int32_t first[csm_ctx::kMaxParts], count[csm_ctx::kMaxParts];
+  // part 0 takes part0_permille of the scans, the others split the rest: a
+  // larger first part shortens what nothing hides, the last part's
+  // super-fine completion at the end of the call and its fine -> super-fine
+  // hand-off (the device has only part 0's super-fine level to run meanwhile)
+  const int64_t n0 = (K == 2 && c->part0_permille > 0) ? (int64_t)n_scans * c->part0_permille / 1000
+                                                        : (int64_t)n_scans / K;
   for (int h = 0; h < K; ++h) {
-    first[h] = (int32_t)((int64_t)n_scans * h / K);
-    count[h] = (int32_t)((int64_t)n_scans * (h + 1) / K) - first[h];
+    first[h] = h == 0 ? 0 : (int32_t)(n0 + (int64_t)(n_scans - n0) * (h - 1) / (K - 1));
+    count[h] = (h == 0 ? (int32_t)n0 : (int32_t)(n0 + (int64_t)(n_scans - n0) * h / (K - 1))) - first[h];
   }
   std::vector<double> resp((size_t)n_scans, 0.0);
   // by level parity: level l's run and level l + 1's. Kept per thread across
