@@ -17,7 +17,7 @@ print(sys.argv[2], "p50 %.3f p99 %.3f max %.3f" % (l["p50"], l["p99"], l["max"])
 PY
 }
 run default env
-run eager env HIP_ENABLE_DEFERRED_LOADING=0
+# (HIP_ENABLE_DEFERRED_LOADING=0 segfaulted at load on the box, r04)
 run pinned taskset -c 8-23
 run threads4 env CSM_HOST_THREADS=4
 run default2 env
