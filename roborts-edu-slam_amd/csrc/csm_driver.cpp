@@ -354,9 +354,14 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
 // accumulates each scan's response (ScanMatchers::ScanMatch :252-256) before
 // the next level overwrites it. N's angle rows go to the other pinned buffer
 // of the slot: R's rows are still being read.
+// split: N goes out in two spans, its first half as soon as R's first half is
+// completed (owed windows included, after the join), then the second half --
+// for the hand-off nothing else on the device hides (the last part's
+// fine -> super-fine: the device has only the other part's short super-fine
+// level to run meanwhile).
 int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const int64_t* offsets,
                     const csm_param& P, double* poses, double* covs, double* responses, double* sum,
-                    const int32_t* scan_grid, int skip_lists) {
+                    const int32_t* scan_grid, int skip_lists, bool split = false) {
   int st = level_prepare(c, n_scans, offsets, P, responses, nullptr, N, scan_grid, skip_lists, false);
   if (st != CSM_OK) return st;
   const int nw = (int)R.scan_of.size();
@@ -379,7 +384,20 @@ int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const
     level_plan_one(N, G, offsets, poses, i);
     return true;
   };
-  if (early) {  // the settled windows while the exact pass runs, then the ones it owed
+  split = split && early && nw >= c->split_handoff_min && level_device_finish(c, N.D, nw);
+  if (split) {  // [0, h) completed, planned and scored while [h, nw) is completed and planned
+    const int h = nw / 2;
+    std::vector<int> owed((size_t)nw);
+    int n_owed = 0;
+    c->parallel_for(h, threads, [&](int i) {
+      if (!one(i, true)) owed[(size_t)__atomic_fetch_add(&n_owed, 1, __ATOMIC_RELAXED)] = i;
+    });
+    if ((st = level_join(c, R)) != CSM_OK) return st;
+    c->parallel_for(n_owed, n_owed >= 32 ? threads : 1, [&](int k) { one(owed[(size_t)k], false); });
+    if ((st = level_check(c, R)) != CSM_OK) return st;
+    if ((st = level_launch(c, N, WinSpan{0, h, true, false})) != CSM_OK) return st;
+    c->parallel_for(nw - h, threads, [&](int i) { one(h + i, false); });
+  } else if (early) {  // the settled windows while the exact pass runs, then the ones it owed
     std::vector<int> owed((size_t)nw);
     int n_owed = 0;
     c->parallel_for(nw, threads, [&](int i) {
@@ -393,7 +411,13 @@ int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const
   if ((st = level_check(c, R)) != CSM_OK) return st;
   if (threads > 1) c->account_pool("complete+plan");
   const double t3 = now_ms();
-  if ((st = level_launch(c, N)) != CSM_OK) return st;
+  if (split) {
+    if ((st = level_launch(c, N, WinSpan{nw / 2, nw, true, false})) != CSM_OK ||
+        (st = level_launch(c, N, WinSpan{0, nw, false, true})) != CSM_OK)
+      return st;
+  } else if ((st = level_launch(c, N)) != CSM_OK) {
+    return st;
+  }
   if (c->profiling) {
     c->account("host:launch", (float)(now_ms() - t3), 0.0, 0.0);
     c->account("host:complete+plan", (float)(t3 - t2), 0.0, 0.0);
@@ -480,7 +504,8 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
         if (h > 0) c->swap_slot(h);
         st = level_end_begin(c, cur, R[(l + 1) & 1][h], count[h], offsets + s0, levels[l + 1],
                              poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, sum + s0,
-                             scan_grid ? scan_grid + s0 : nullptr, skip(l + 1));
+                             scan_grid ? scan_grid + s0 : nullptr, skip(l + 1),
+                             c->split_last_handoff && h == K - 1 && l + 2 == n_levels);
         if (h > 0) c->swap_slot(h);
       } else {
         if (c->debug_fin) {

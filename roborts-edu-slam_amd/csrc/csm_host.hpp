@@ -585,6 +585,8 @@ struct csm_ctx {
   int pipeline_parts = 2;    // parts in flight (CSM_PIPELINE_PARTS: 2..kMaxParts; 2 measured fastest)
   int first_windows = 128;   // level_begin_split: windows the first part's first launch takes (CSM_FIRST_WINDOWS; 0: one launch)
   int span_growth = 4;       // ... and each later span's growth (CSM_SPAN_GROWTH)
+  bool split_last_handoff = true;  // the last part's hand-off to the last level in two spans (CSM_SPLIT_HANDOFF)
+  int split_handoff_min = 256;     // ... for parts of at least this many windows (CSM_SPLIT_HANDOFF_MIN)
   int part0_permille = 550;  // two parts: the first one's share of the scans (CSM_PART0_PERMILLE;
                              // r04 A/B, 2 runs each: 500 9.40, 550 9.61, 600 9.56, 650 9.47 G scorings/s)
   void swap_slot(int i) {    // i >= 1: exchange the current buffer set with alt[i - 1]

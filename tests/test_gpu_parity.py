@@ -723,7 +723,9 @@ def test_host_signal_split_levels_with_ties(world2000):
     from roborts_csm.params import headline_levels
     w, b = world2000
     grid = np.round(np.asarray(w.grid, dtype=np.float32) * 2.0).astype(np.float32) / np.float32(2.0)
-    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2", "CSM_FIRST_WINDOWS": "5"}
+    # growing first-level spans from 5 windows, the last part's hand-off to
+    # the super-fine level in two spans (from parts of 8 windows)
+    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2", "CSM_FIRST_WINDOWS": "5", "CSM_SPLIT_HANDOFF_MIN": "8"}
     os.environ.update(env)
     try:
         c = roborts_csm.Context(0)

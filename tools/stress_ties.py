@@ -19,6 +19,7 @@ sys.path[:0] = [os.path.join(ROOT, "roborts-edu-slam_amd"), os.path.join(ROOT, "
 os.environ.setdefault("CSM_PIPELINE", "16")
 os.environ.setdefault("CSM_PIPELINE_PARTS", "2")
 os.environ.setdefault("CSM_FIRST_WINDOWS", "5")
+os.environ.setdefault("CSM_SPLIT_HANDOFF_MIN", "8")
 
 import numpy as np  # noqa: E402
 
