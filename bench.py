@@ -1211,6 +1211,8 @@ def main():
                     help="loop_closure: torch = one rank per GPU, the exchange over torch.distributed (RCCL); "
                          "capi = ONE process over --gpus devices through csm_loop_closure_* (in-process "
                          "RCCL communicator), what TryCloseLoop calls from C++")
+    ap.add_argument("--sync-steps", action="store_true",
+                    help="config2: one csm_scan_matchers_loaded call per step (no batches in flight back to back)")
     ap.add_argument("--no-host-inputs", action="store_true",
                     help="config2: skip the value_host_inputs leg (batches uploaded from pinned host memory)")
     ap.add_argument("--lc-verify", action="store_true",
@@ -1302,12 +1304,29 @@ def main():
     covs0 = np.ascontiguousarray(np.tile(np.eye(3).reshape(1, 9), (args.scans, 1)))
 
     poses_w, covs_w = np.empty_like(poses0), np.empty_like(covs0)  # reset in place each step
+    # submitted batches (csm_scan_matchers_submit): each step is one whole
+    # batch, but step k + 1's first launch goes out before step k's last level
+    # is completed; two sets of outputs alternate (a batch's are final once
+    # the next submit returns), the timed region ends with the last one's wait
+    sets = [(np.empty_like(poses0), np.empty_like(covs0), np.zeros(args.scans)) for _ in range(2)]
+    k_step = [0]
 
     def step():
-        np.copyto(poses_w, poses0)
-        np.copyto(covs_w, covs0)
-        ctx.scan_matchers_loaded(levels, poses_w, covs_w)
-        return poses_w
+        if args.sync_steps:
+            np.copyto(poses_w, poses0)
+            np.copyto(covs_w, covs0)
+            ctx.scan_matchers_loaded(levels, poses_w, covs_w)
+            return poses_w
+        p, c, sc = sets[k_step[0] % 2]
+        k_step[0] += 1
+        np.copyto(p, poses0)
+        np.copyto(c, covs0)
+        ctx.scan_matchers_submit(levels, p, c, sc)
+        return p
+
+    def settle():  # the last submitted step completes
+        if not args.sync_steps:
+            ctx.scan_matchers_wait()
 
     def barrier():
         if dist is not None:
@@ -1317,6 +1336,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    settle()
     # HIP events around every launch feed the live roofline below; the A/B knob
     # CSM_BENCH_NO_EVENTS=1 leaves them out to price their overhead
     ctx.set_profiling(os.environ.get("CSM_BENCH_NO_EVENTS") != "1")
@@ -1324,11 +1344,12 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         poses = step()
+    settle()
     barrier()
     elapsed = time.perf_counter() - t0
     stats = ctx.kernel_stats()
     ctx.set_profiling(False)
-    poses_resident = poses_w.copy()
+    poses_resident = poses.copy()
 
     per_scan = sum(_window_cands(l) for l in levels)
     local_scorings = float(args.scans * per_scan * args.steps)
@@ -1372,11 +1393,13 @@ def main():
 
         def run_host(k):
             ctx.load_scans_async(pins[0].array, batch.offsets)
+            res = None
             for i in range(k):
                 if i + 1 < k:
                     ctx.load_scans_async(pins[(i + 1) % 2].array, batch.offsets)
-                step()
-            return poses_w
+                res = step()
+            settle()
+            return res
 
         run_host(max(2, min(args.warmup, 10)))
         barrier()
@@ -1463,6 +1486,10 @@ def main():
             "scans_per_gpu": args.scans,
             "scorings_per_scan": per_scan,
             "parallelism": f"replicas x{world_size} (scan-sharded, no collective)",
+            "batches": ("one csm_scan_matchers_loaded call per step" if args.sync_steps else
+                        "submitted back to back (csm_scan_matchers_submit): step k + 1's first launch goes out "
+                        "before step k's last level is completed; every step is one whole batch, the timed "
+                        "region ends when the last one is complete"),
             "inputs": "grid and scans resident in HBM before the timed region (csm_load_scans); the "
                       f"host-buffer entry points add one H2D copy of the points: "
                       f"{batch.points_cells.nbytes / 1e6:.1f} MB per step here, timed below as h2d_ms",

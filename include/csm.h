@@ -226,6 +226,19 @@ int csm_scan_matchers_loaded(csm_ctx* ctx, const csm_param levels[3], int32_t us
  * then csm_scan_matchers_loaded (batch i, while batch i + 1 goes up). */
 int csm_load_scans_async(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
                          const int64_t* point_offsets);
+/* Batches in flight back to back (no reference counterpart: a stream of
+ * ScanMatchers::ScanMatch batches, scan_matchers.h:179-289, over the loaded
+ * scans). csm_scan_matchers_submit does what csm_scan_matchers_loaded does
+ * except that the batch's last level is left pending: the next submit's first
+ * launch goes out before that level is completed, so the device does not wait
+ * for the host between batches. poses / covs / scores of a submitted batch
+ * are final once the next submit, csm_scan_matchers_wait, or any other call on
+ * the context returns (every other entry point completes a pending batch
+ * first); they must stay valid until then. Results equal
+ * csm_scan_matchers_loaded's bit for bit. */
+int csm_scan_matchers_submit(csm_ctx* ctx, const csm_param levels[3], int32_t use_fine, double* poses, double* covs,
+                             double* scores);
+int csm_scan_matchers_wait(csm_ctx* ctx);
 /* Pinned (page-locked) host memory for csm_load_scans_async inputs. */
 int csm_host_alloc(size_t bytes, void** out);
 int csm_host_free(void* p);

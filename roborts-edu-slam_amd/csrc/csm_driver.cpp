@@ -438,28 +438,64 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
   return level_end(c, R, poses, covs, responses, argmax_flat);
 }
 
-// ScanMatchers::ScanMatch over a resident batch (scan_matchers.h:179-289),
-// parts in flight: while the device runs one part's level, the host
-// completes another part's previous level and plans its next one
-// (level_end_begin). Scans are independent, so the split changes no result.
-int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
-                           int n_levels, double* poses, double* covs, double* sum,
-                           const int32_t* scan_grid = nullptr) {
-  const int K = std::max(2, std::min(c->pipeline_parts, csm_ctx::kMaxParts));
-  // parts in flight share no few-window buffers: every part takes the
-  // throughput kernels (a part is hundreds of windows at the default split)
-  struct SmallOff {
-    csm_ctx* c;
-    bool was;
-    ~SmallOff() { c->small_path = was; }
-  } small_off{c, c->small_path};
-  c->small_path = false;
-  struct EarlyOn {  // level_end_begin / level_end complete settled windows early
-    csm_ctx* c;
-    ~EarlyOn() { c->early_now = false; }
-  } early_on{c};
-  c->early_now = true;
-  int32_t first[csm_ctx::kMaxParts], count[csm_ctx::kMaxParts];
+// One batch through the 3-level driver (match_levels_pipelined). With
+// csm_scan_matchers_submit the batch's last level is launched but its
+// completion deferred: the next submitted batch's first launch goes out first
+// (into the other half of the buffer slots), then the deferred completion runs
+// while that one scores -- the device no longer idles between batches.
+struct PipeJob {
+  int K = 2, n_levels = 0, slot0 = 0;  // parts, levels, the parts' first buffer slot
+  int32_t n_scans = 0;
+  const int64_t* offsets = nullptr;
+  const int32_t* scan_grid = nullptr;
+  csm_param levels[3]{};
+  double *poses = nullptr, *covs = nullptr, *sum = nullptr;
+  double* scores = nullptr;  // submitted: scores[s] = sum[s] / n_levels when complete
+  std::vector<double> resp, own_sum;
+  int32_t first[csm_ctx::kMaxParts]{}, count[csm_ctx::kMaxParts]{};
+  // by level parity: level l's run and level l + 1's, per part. Reused across
+  // batches: a fresh run's window plans (64 B each, 128 KB per 2048 windows)
+  // came from mmap and paid ~40 us of page faults at every level start (r04).
+  LevelRun R[2][csm_ctx::kMaxParts];
+  bool pending = false;  // the last level launched, its completion deferred
+  std::vector<csm::FinishOut> snaps[csm_ctx::kMaxParts];  // CSM_DEBUG_FIN
+  std::vector<char> hows[csm_ctx::kMaxParts];
+};
+
+struct PipeState {
+  PipeJob job[2];
+  int next = 0;  // the job slot the next submit takes (its parts: slots next * K ...)
+};
+
+PipeState& pipe_of(csm_ctx* c) {
+  if (!c->pipe) c->pipe = new PipeState();
+  return *static_cast<PipeState*>(c->pipe);
+}
+
+// part h of J with its buffer slot swapped in (slot 0 is the context's own)
+template <typename F>
+int with_slot(csm_ctx* c, const PipeJob& J, int h, F&& f) {
+  const int sidx = J.slot0 + h;
+  if (sidx > 0) c->swap_slot(sidx);
+  const int st = f();
+  if (sidx > 0) c->swap_slot(sidx);
+  return st;
+}
+
+void job_setup(csm_ctx* c, PipeJob& J, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
+               int n_levels, double* poses, double* covs, double* sum, const int32_t* scan_grid, int K, int slot0) {
+  J.K = K;
+  J.n_levels = n_levels;
+  J.slot0 = slot0;
+  J.n_scans = n_scans;
+  J.offsets = offsets;
+  J.scan_grid = scan_grid;
+  for (int l = 0; l < n_levels; ++l) J.levels[l] = levels[l];
+  J.poses = poses;
+  J.covs = covs;
+  J.sum = sum;
+  J.scores = nullptr;
+  J.pending = false;
   // part 0 takes part0_permille of the scans, the others split the rest: a
   // larger first part shortens what nothing hides, the last part's
   // super-fine completion at the end of the call and its fine -> super-fine
@@ -467,66 +503,85 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
   const int64_t n0 = (K == 2 && c->part0_permille > 0) ? (int64_t)n_scans * c->part0_permille / 1000
                                                         : (int64_t)n_scans / K;
   for (int h = 0; h < K; ++h) {
-    first[h] = h == 0 ? 0 : (int32_t)(n0 + (int64_t)(n_scans - n0) * (h - 1) / (K - 1));
-    count[h] = (h == 0 ? (int32_t)n0 : (int32_t)(n0 + (int64_t)(n_scans - n0) * h / (K - 1))) - first[h];
+    J.first[h] = h == 0 ? 0 : (int32_t)(n0 + (int64_t)(n_scans - n0) * (h - 1) / (K - 1));
+    J.count[h] = (h == 0 ? (int32_t)n0 : (int32_t)(n0 + (int64_t)(n_scans - n0) * h / (K - 1))) - J.first[h];
   }
-  std::vector<double> resp((size_t)n_scans, 0.0);
-  // by level parity: level l's run and level l + 1's. Kept per thread across
-  // calls: a fresh run's window plans (64 B each, 128 KB per 2048 windows) came
-  // from mmap and paid ~40 us of page faults at every level start (r04,
-  // host:first:prepare+alloc); reused, their vectors keep their capacity.
-  static thread_local LevelRun R[2][csm_ctx::kMaxParts];
-  for (auto& row : R)
+  J.resp.assign((size_t)n_scans, 0.0);
+  for (auto& row : J.R)
     for (LevelRun& r : row) r.reset();
-  std::vector<csm::FinishOut> snaps[csm_ctx::kMaxParts];  // CSM_DEBUG_FIN
-  std::vector<char> hows[csm_ctx::kMaxParts];
-  auto skip = [&](int l) { return c->skip_dead_lists ? live_lists(levels, n_levels, l) : 0; };
+}
+
+int job_skip(const csm_ctx* c, const PipeJob& J, int l) {
+  return c->skip_dead_lists ? live_lists(J.levels, J.n_levels, l) : 0;
+}
+
+// Level 0 of part h planned and launched (the first part in growing spans:
+// the device waits for it).
+int job_begin(csm_ctx* c, PipeJob& J, int h) {
+  const int32_t s0 = J.first[h];
+  J.R[0][h].tag = h;
+  return with_slot(c, J, h, [&] {
+    const int32_t* g = J.scan_grid ? J.scan_grid + s0 : nullptr;
+    if (h == 0)
+      return level_begin_split(c, J.count[h], J.offsets + s0, J.levels[0], J.poses + 3 * (size_t)s0,
+                               J.resp.data() + s0, J.R[0][h], g, job_skip(c, J, 0), c->first_windows);
+    return level_begin(c, J.count[h], J.offsets + s0, J.levels[0], J.poses + 3 * (size_t)s0, J.resp.data() + s0,
+                       nullptr, J.R[0][h], g, job_skip(c, J, 0));
+  });
+}
+
+// Every level transition of J: its last level launched, its completion left
+// to job_finish (J.pending).
+int job_levels(csm_ctx* c, PipeJob& J) {
+  const int K = J.K, n_levels = J.n_levels;
   int st;
-  for (int h = 0; h < K; ++h) {
-    const int32_t s0 = first[h];
-    R[0][h].tag = h;
-    if (h > 0) c->swap_slot(h);
-    if (h == 0)  // the device waits for this one
-      st = level_begin_split(c, count[h], offsets + s0, levels[0], poses + 3 * (size_t)s0, resp.data() + s0, R[0][h],
-                             scan_grid ? scan_grid + s0 : nullptr, skip(0), c->first_windows);
-    else
-      st = level_begin(c, count[h], offsets + s0, levels[0], poses + 3 * (size_t)s0, resp.data() + s0, nullptr,
-                       R[0][h], scan_grid ? scan_grid + s0 : nullptr, skip(0));
-    if (h > 0) c->swap_slot(h);
-    if (st != CSM_OK) return st;
-  }
-  for (int l = 0; l < n_levels; ++l) {
+  for (int l = 0; l + 1 < n_levels; ++l) {
     for (int h = 0; h < K; ++h) {
-      const int32_t s0 = first[h];
-      LevelRun& cur = R[l & 1][h];
-      if (l + 1 < n_levels) {
-        R[(l + 1) & 1][h].tag = (l + 1) * 8 + h;
-        if (h > 0) c->swap_slot(h);
-        st = level_end_begin(c, cur, R[(l + 1) & 1][h], count[h], offsets + s0, levels[l + 1],
-                             poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, sum + s0,
-                             scan_grid ? scan_grid + s0 : nullptr, skip(l + 1),
-                             c->split_last_handoff && h == K - 1 && l + 2 == n_levels);
-        if (h > 0) c->swap_slot(h);
-      } else {
-        if (c->debug_fin) {
-          snaps[h].assign(cur.scan_of.size(), csm::FinishOut{});
-          hows[h].assign(cur.scan_of.size(), (char)3);
-          cur.snap = &snaps[h];
-          cur.how = &hows[h];
-        }
-        st = level_end(c, cur, poses + 3 * (size_t)s0, covs + 9 * (size_t)s0, resp.data() + s0, nullptr);
-        for (int s = s0; s < s0 + count[h]; ++s) sum[(size_t)s] += resp[(size_t)s];
-      }
+      const int32_t s0 = J.first[h];
+      J.R[(l + 1) & 1][h].tag = (l + 1) * 8 + h;
+      st = with_slot(c, J, h, [&] {
+        return level_end_begin(c, J.R[l & 1][h], J.R[(l + 1) & 1][h], J.count[h], J.offsets + s0, J.levels[l + 1],
+                               J.poses + 3 * (size_t)s0, J.covs + 9 * (size_t)s0, J.resp.data() + s0, J.sum + s0,
+                               J.scan_grid ? J.scan_grid + s0 : nullptr, job_skip(c, J, l + 1),
+                               c->split_last_handoff && h == K - 1 && l + 2 == n_levels);
+      });
       if (st != CSM_OK) return st;
     }
   }
+  J.pending = true;
+  return CSM_OK;
+}
+
+// J's last level: every part's windows completed, responses summed (and the
+// submitted batch's scores written).
+int job_finish(csm_ctx* c, PipeJob& J) {
+  if (!J.pending) return CSM_OK;
+  J.pending = false;
+  const int K = J.K, last = J.n_levels - 1;
+  int st;
+  for (int h = 0; h < K; ++h) {
+    const int32_t s0 = J.first[h];
+    LevelRun& cur = J.R[last & 1][h];
+    if (c->debug_fin) {
+      J.snaps[h].assign(cur.scan_of.size(), csm::FinishOut{});
+      J.hows[h].assign(cur.scan_of.size(), (char)3);
+      cur.snap = &J.snaps[h];
+      cur.how = &J.hows[h];
+    }
+    if ((st = level_end(c, cur, J.poses + 3 * (size_t)s0, J.covs + 9 * (size_t)s0, J.resp.data() + s0, nullptr)) !=
+        CSM_OK)
+      return st;
+    for (int s = s0; s < s0 + J.count[h]; ++s) J.sum[(size_t)s] += J.resp[(size_t)s];
+  }
+  if (J.scores)
+    for (int s = 0; s < J.n_scans; ++s) J.scores[s] = J.sum[(size_t)s] / J.n_levels;  // :281
   if (c->debug_fin) {  // the device idle: what the finish left against what was completed
     (void)hipDeviceSynchronize();
     for (int h = 0; h < K; ++h) {
-      const LevelRun& L = R[(n_levels - 1) & 1][h];
+      const LevelRun& L = J.R[last & 1][h];
       if (!L.dev || !L.fin) continue;
-      for (size_t i = 0; i < snaps[h].size(); ++i) {
-        const csm::FinishOut& a = snaps[h][i];
+      for (size_t i = 0; i < J.snaps[h].size(); ++i) {
+        const csm::FinishOut& a = J.snaps[h][i];
         const csm::FinishOut& b = L.fin[i];
         // the pieces the final seal names (the completed copy holds only those)
         const int lists = (int)(b.seal_tag_kind >> 34) & 3;
@@ -540,11 +595,76 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
         std::fprintf(stderr,
                      "csm debug_fin: part %d window %zu (scan %d) how %d: completed count %d n_pos %d n_ang %d front %d "
                      "ang0 %.17g | final count %d n_pos %d n_ang %d front %d ang0 %.17g\n",
-                     h, i, first[h] + L.scan_of[i], (int)hows[h][i], a.count, a.n_pos, a.n_ang, a.front_idx,
+                     h, i, J.first[h] + L.scan_of[i], (int)J.hows[h][i], a.count, a.n_pos, a.n_ang, a.front_idx,
                      a.ang_score[0], b.count, b.n_pos, b.n_ang, b.front_idx, b.ang_score[0]);
       }
     }
   }
+  return CSM_OK;
+}
+
+// The driver's knobs for a pipelined batch: every part on the throughput
+// kernels (parts in flight share no few-window buffers), early completion on.
+struct PipeMode {
+  csm_ctx* c;
+  bool small_was;
+  explicit PipeMode(csm_ctx* cc) : c(cc), small_was(cc->small_path) {
+    c->small_path = false;
+    c->early_now = true;
+  }
+  ~PipeMode() {
+    c->small_path = small_was;
+    c->early_now = false;
+  }
+};
+
+// After a failure with a batch in flight: nothing stays pending, and nothing
+// enqueued may still touch the buffers.
+int pipe_abort(csm_ctx* c, int st) {
+  if (c->pipe)
+    for (PipeJob& J : static_cast<PipeState*>(c->pipe)->job) J.pending = false;
+  (void)hipStreamSynchronize(c->stream);
+  if (c->x_stream) (void)hipStreamSynchronize(c->x_stream);
+  (void)hipStreamSynchronize(c->h2d);
+  (void)hipStreamSynchronize(c->d2h);
+  return st;
+}
+
+// A submitted batch whose last level is still pending is completed (every
+// entry point but submit itself calls this first: the pending kernels read
+// the loaded scans, the grid and the buffer slots).
+int pipe_drain(csm_ctx* c) {
+  if (!c->pipe) return CSM_OK;
+  PipeState& PS = *static_cast<PipeState*>(c->pipe);
+  for (PipeJob& J : PS.job)
+    if (J.pending) {
+      DeviceGuard g(c->device);
+      const int st = job_finish(c, J);
+      if (st != CSM_OK) return pipe_abort(c, st);
+    }
+  return CSM_OK;
+}
+
+void pipe_free(csm_ctx* c) {
+  delete static_cast<PipeState*>(c->pipe);
+  c->pipe = nullptr;
+}
+
+// ScanMatchers::ScanMatch over a resident batch (scan_matchers.h:179-289),
+// parts in flight: while the device runs one part's level, the host
+// completes another part's previous level and plans its next one
+// (level_end_begin). Scans are independent, so the split changes no result.
+int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
+                           int n_levels, double* poses, double* covs, double* sum,
+                           const int32_t* scan_grid = nullptr) {
+  const int K = std::max(2, std::min(c->pipeline_parts, csm_ctx::kMaxParts));
+  PipeMode mode(c);
+  PipeJob& J = pipe_of(c).job[0];
+  job_setup(c, J, n_scans, offsets, levels, n_levels, poses, covs, sum, scan_grid, K, 0);
+  int st;
+  for (int h = 0; h < K; ++h)
+    if ((st = job_begin(c, J, h)) != CSM_OK) return pipe_abort(c, st);
+  if ((st = job_levels(c, J)) != CSM_OK || (st = job_finish(c, J)) != CSM_OK) return pipe_abort(c, st);
   return CSM_OK;
 }
 
@@ -560,6 +680,7 @@ int csm_scan_match_batch(csm_ctx* c, int32_t n_scans, const double* pts, const i
   if (!c || !param || !poses || !covs || !responses) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   int st;
   if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
   if (n_scans == 0) return CSM_OK;
@@ -584,6 +705,7 @@ int csm_load_scans(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t
   if (!c) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   int st;
   c->loaded_n = -1;
   c->loaded_grid.clear();
@@ -646,26 +768,102 @@ int csm_host_alloc(size_t bytes, void** out) {
 
 int csm_host_free(void* p) { return (!p || hipHostFree(p) == hipSuccess) ? CSM_OK : CSM_ERR_INVALID_ARG; }
 
+}  // extern "C"
+
+namespace csmh {
+// The oldest queued batch (csm_load_scans_async) becomes the loaded one.
+int take_staged(csm_ctx* c) {
+  if (c->staged_count <= 0) return CSM_OK;
+  csm_ctx::Staged& S = c->staged[c->staged_head];
+  hipError_t e;
+  if ((e = hipEventSynchronize(S.ready)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize(stage)");
+  std::swap(c->pts, S.pts);
+  c->loaded_off.swap(S.off);
+  c->loaded_n = S.n;
+  c->loaded_grid.clear();
+  double m;
+  std::memcpy(&m, S.maxabs_h, sizeof(m));
+  c->pts_maxabs = m;
+  c->pts_cached = false;
+  c->staged_head = (c->staged_head + 1) % 2;
+  c->staged_count--;
+  return CSM_OK;
+}
+}  // namespace csmh
+
+extern "C" {
+
+int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_fine, double* poses, double* covs,
+                             double* scores) {
+  if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st;
+  if (c->staged_count > 0) {  // the pending batch reads the loaded scans the staged one replaces
+    if ((st = pipe_drain(c)) != CSM_OK || (st = take_staged(c)) != CSM_OK) return st;
+  }
+  if (c->loaded_n < 0) return c->fail(CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)");
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
+  const int32_t n_scans = c->loaded_n;
+  const int n_levels = use_fine ? 3 : 1;
+  bool fast = false;
+  for (int l = 0; l < n_levels; ++l) fast |= levels[l].type == CSM_FAST;
+  const int32_t* grid = c->loaded_grid.empty() ? nullptr : c->loaded_grid.data();
+  const int K = std::max(2, std::min(c->pipeline_parts, csm_ctx::kMaxParts));
+  if (n_scans == 0 || fast || grid || n_scans < c->pipeline_min || 2 * K > csm_ctx::kMaxParts) {
+    // nothing to overlap (or no second set of buffer slots): the batch completes here
+    if ((st = pipe_drain(c)) != CSM_OK) return st;
+    return matchers_loaded_locked(c, levels, use_fine, poses, covs, scores);
+  }
+  const double t_call = now_ms();
+  c->t_call = t_call;
+  PipeState& PS = pipe_of(c);
+  PipeJob& J = PS.job[PS.next];
+  PipeJob& P = PS.job[PS.next ^ 1];
+  if (J.pending && (st = pipe_drain(c)) != CSM_OK) return st;  // (cannot happen: submits alternate)
+  PipeMode mode(c);
+  job_setup(c, J, n_scans, c->loaded_off.data(), levels, n_levels, poses, covs, nullptr, nullptr, K, PS.next * K);
+  J.own_sum.assign((size_t)n_scans, 0.0);
+  J.sum = J.own_sum.data();
+  J.scores = scores;
+  // this batch's first launch, then the previous batch's deferred last level
+  // while that scores, then the rest of this batch up to its last level
+  if ((st = job_begin(c, J, 0)) != CSM_OK) return pipe_abort(c, st);
+  if (P.pending && (st = job_finish(c, P)) != CSM_OK) return pipe_abort(c, st);
+  for (int h = 1; h < K; ++h)
+    if ((st = job_begin(c, J, h)) != CSM_OK) return pipe_abort(c, st);
+  if ((st = job_levels(c, J)) != CSM_OK) return pipe_abort(c, st);
+  PS.next ^= 1;
+  if (c->profiling) {
+    c->t_exit = now_ms();
+    c->account("host:submit", (float)(c->t_exit - t_call), 0.0, 0.0);
+  }
+  return CSM_OK;
+}
+
+int csm_scan_matchers_wait(csm_ctx* c) {
+  if (!c) return CSM_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return pipe_drain(c);
+}
+
 int csm_scan_matchers_loaded(csm_ctx* c, const csm_param levels[3], int32_t use_fine, double* poses,
                              double* covs, double* scores) {
   if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  if (c->staged_count > 0) {  // the oldest queued batch becomes the loaded one
-    csm_ctx::Staged& S = c->staged[c->staged_head];
-    hipError_t e;
-    if ((e = hipEventSynchronize(S.ready)) != hipSuccess) return c->hip_fail(e, "hipEventSynchronize(stage)");
-    std::swap(c->pts, S.pts);
-    c->loaded_off.swap(S.off);
-    c->loaded_n = S.n;
-    c->loaded_grid.clear();
-    double m;
-    std::memcpy(&m, S.maxabs_h, sizeof(m));
-    c->pts_maxabs = m;
-    c->pts_cached = false;
-    c->staged_head = (c->staged_head + 1) % 2;
-    c->staged_count--;
-  }
+  int st0;
+  if ((st0 = pipe_drain(c)) != CSM_OK || (st0 = take_staged(c)) != CSM_OK) return st0;
+  return matchers_loaded_locked(c, levels, use_fine, poses, covs, scores);
+}
+
+}  // extern "C"
+
+namespace csmh {
+// csm_scan_matchers_loaded once locked, nothing pending, the staged batch taken.
+int matchers_loaded_locked(csm_ctx* c, const csm_param levels[3], int32_t use_fine, double* poses, double* covs,
+                           double* scores) {
   if (c->loaded_n < 0) return c->fail(CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)");
   if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
   const int32_t n_scans = c->loaded_n;
@@ -703,6 +901,9 @@ int csm_scan_matchers_loaded(csm_ctx* c, const csm_param levels[3], int32_t use_
   }
   return CSM_OK;
 }
+}  // namespace csmh
+
+extern "C" {
 
 int csm_scan_matchers_batch(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
                             const csm_param levels[3], int32_t use_fine, double* poses, double* covs,
@@ -726,6 +927,7 @@ int csm_load_scans_grids(csm_ctx* c, int32_t n_scans, const double* pts, const i
   int st = csm_load_scans(c, n_scans, pts, offsets);
   if (st != CSM_OK || !grid_index) return st;
   std::lock_guard<std::mutex> lk(c->mu);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   c->loaded_grid.assign(grid_index, grid_index + n_scans);
   return CSM_OK;
 }

@@ -320,6 +320,7 @@ int csm_set_grid(csm_ctx* c, const void* cells, int64_t stride, const csm_map_in
   if (!c || !info) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   int st = check_grid_args(c, cells, stride, info);
   if (st != CSM_OK) return st;
   select_grid(c, cells);
@@ -335,6 +336,7 @@ int csm_update_grid_rows(csm_ctx* c, const void* cells, int64_t stride, const cs
   if (!c || !info) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   int st = check_grid_args(c, cells, stride, info);
   if (st != CSM_OK) return st;
   if (row_begin < 0 || row_end > info->size_y || row_begin > row_end)
@@ -370,6 +372,7 @@ int csm_update_grid_cells(csm_ctx* c, const void* cells, int64_t stride, const c
   if (!c || !info) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   int st = check_grid_args(c, cells, stride, info);
   if (st != CSM_OK) return st;
   if (n_indices < 0 || (n_indices > 0 && !cell_indices)) return c->fail(CSM_ERR_INVALID_ARG, "cell index list");
@@ -461,6 +464,7 @@ int csm_set_grid_device(csm_ctx* c, const float* dev, const csm_map_info* info) 
   if (!c || !info) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);  // the read fence is created and recorded on the context's device
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   release_map_reader(c);
   return set_grid_device_locked(c, dev, info);
 }
@@ -470,6 +474,7 @@ int csm_set_grid_gridmap(csm_ctx* c, csm_gridmap* map) {
   float outside;
   {
     std::lock_guard<std::mutex> lk(c->mu);
+    if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
     outside = c->outside;
   }
   // the map's fixed-point mirror (kept by the map kernels from the cells each
@@ -482,6 +487,7 @@ int csm_set_grid_gridmap(csm_ctx* c, csm_gridmap* map) {
   if (v.device != c->device) return c->fail(CSM_ERR_INVALID_ARG, "map lives on another device");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   // the matcher's kernels run after the map's last update, and the map's
   // next update after the matcher's reads (csm::gridmap_add_reader)
   hipError_t e = hipStreamWaitEvent(c->stream, v.ready, 0);
@@ -516,6 +522,7 @@ int csm_set_grid_stack(csm_ctx* c, const float* cells, int32_t n_grids, const cs
   if (!c || !info || !cells || n_grids <= 0) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   release_map_reader(c);
   if (info->size_x <= 0 || info->size_y <= 0 || !(info->resolution > 0.0))
     return c->fail(CSM_ERR_INVALID_ARG, "grid size and resolution must be positive");
@@ -555,6 +562,7 @@ int csm_set_grid_stack_gridmaps(csm_ctx* c, csm_gridmap* const* maps, int32_t n_
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   release_map_reader(c);
   park_current(c);
   const csm::GridMapView& a = v[0];

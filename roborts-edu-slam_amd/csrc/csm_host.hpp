@@ -585,6 +585,7 @@ struct csm_ctx {
   int pipeline_parts = 2;    // parts in flight (CSM_PIPELINE_PARTS: 2..kMaxParts; 2 measured fastest)
   int first_windows = 128;   // level_begin_split: windows the first part's first launch takes (CSM_FIRST_WINDOWS; 0: one launch)
   int span_growth = 4;       // ... and each later span's growth (CSM_SPAN_GROWTH)
+  void* pipe = nullptr;  // csm_driver.cpp PipeState: submitted batches (csm_scan_matchers_submit)
   bool split_last_handoff = true;  // the last part's hand-off to the last level in two spans (CSM_SPLIT_HANDOFF)
   int split_handoff_min = 256;     // ... for parts of at least this many windows (CSM_SPLIT_HANDOFF_MIN)
   int part0_permille = 550;  // two parts: the first one's share of the scans (CSM_PART0_PERMILLE;
@@ -731,5 +732,13 @@ constexpr double kOptCostPointSize = 1000;                // optimize_scan_match
 constexpr double kOptMaxCost = 1.0 * kOptCostPointSize;   // :235
 
 inline bool map_ready(const csm_ctx* c) { return c->has_grid && c->info.update_index >= 0; }
+
+// csm_driver.cpp: a submitted batch still pending is completed (every entry
+// point but csm_scan_matchers_submit calls it first); the state's release
+int pipe_drain(csm_ctx* c);
+void pipe_free(csm_ctx* c);
+int take_staged(csm_ctx* c);
+int matchers_loaded_locked(csm_ctx* c, const csm_param levels[3], int32_t use_fine, double* poses, double* covs,
+                           double* scores);
 
 }  // namespace csmh

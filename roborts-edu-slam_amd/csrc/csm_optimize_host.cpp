@@ -213,6 +213,7 @@ int csm_optimize_scan_match_batch(csm_ctx* c, int32_t n_scans, const double* pts
   if (!c || !param || (n_scans > 0 && (!poses || !costs))) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   int st;
   if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
   if (n_scans == 0) return CSM_OK;
@@ -238,6 +239,7 @@ int csm_optimize_update_cost(csm_ctx* c, const double* pts, int32_t n_points, co
   if (!c || !est_map || !cost || !H || !b) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
   int st;
   if (n_points < 0) return c->fail(CSM_ERR_INVALID_ARG, "negative point count");
   if ((st = check_points(c, pts, n_points)) != CSM_OK) return st;

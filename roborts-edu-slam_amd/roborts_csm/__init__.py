@@ -321,6 +321,24 @@ class Context:
                                                   _dptr(covs), _dptr(scores)))
         return scores
 
+    def scan_matchers_submit(self, levels, poses, covs, scores, use_fine: bool = True):
+        """csm_scan_matchers_submit: scan_matchers_loaded with the batch's last
+        level left pending; poses / covs / scores (float64, caller-owned) are
+        final after the next submit, scan_matchers_wait() or any other call,
+        and must stay alive until then (they are kept referenced here)."""
+        n = self._loaded[1].size - 1
+        for a, k in ((poses, 3), (covs, 9), (scores, 1)):
+            assert a.dtype == np.float64 and a.flags.c_contiguous and a.size == k * n
+        lv = (CsmParam * 3)(*[_as_param(l) for l in levels])
+        keep = self.__dict__.setdefault("_submitted", [])
+        keep.append((poses, covs, scores))
+        del keep[:-2]  # the two batches the library may still write
+        self._check(_lib.csm_scan_matchers_submit(self._h, lv, 1 if use_fine else 0, _dptr(poses), _dptr(covs),
+                                                  _dptr(scores)))
+
+    def scan_matchers_wait(self):
+        self._check(_lib.csm_scan_matchers_wait(self._h))
+
     def optimize_scan_match(self, points_cells, param, pose: np.ndarray) -> float:
         """BasedOptimizeScanMatch::ScanMatch on the current grid; pose updated in place."""
         pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)

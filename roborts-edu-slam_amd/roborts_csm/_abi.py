@@ -27,7 +27,7 @@ EXPORTED = (
     "csm_update_grid_rows",
     "csm_window_dims", "csm_scan_match", "csm_scan_matchers",
     "csm_scan_match_batch", "csm_scan_matchers_batch", "csm_score_window",
-    "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded", "csm_load_scans_async",
+    "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded", "csm_scan_matchers_submit", "csm_scan_matchers_wait", "csm_load_scans_async",
     "csm_host_alloc", "csm_host_free",
     "csm_set_profiling", "csm_kernel_stats", "csm_sort_order", "csm_phase_buckets",
     "csm_set_grid_stack", "csm_best_windows", "csm_optimize_scan_match", "csm_optimize_scan_match_batch",
@@ -212,6 +212,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),
         "csm_host_free": (C.c_int, [C.c_void_p]),
         "csm_scan_matchers_loaded": (C.c_int, [_ctx, C.POINTER(CsmParam), C.c_int32, _dp, _dp, _dp]),
+        "csm_scan_matchers_submit": (C.c_int, [_ctx, C.POINTER(CsmParam), C.c_int32, _dp, _dp, _dp]),
+        "csm_scan_matchers_wait": (C.c_int, [C.c_void_p]),
         "csm_set_profiling": (C.c_int, [_ctx, C.c_int32]),
         "csm_kernel_stats": (C.c_int, [_ctx, C.POINTER(CsmKernelStat), C.c_int32, _i32p]),
         "csm_sort_order": (C.c_int, [_ctx, _dp, C.c_int64, _i64p]),

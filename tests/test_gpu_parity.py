@@ -975,3 +975,52 @@ def test_load_scans_async_queue(world2000):
         c.close()
         for p in pins:
             p.close()
+
+
+@pytest.mark.parametrize("quantised", [False, True])
+def test_submitted_batches_equal_loaded(world2000, quantised):
+    """csm_scan_matchers_submit: batches in flight back to back (a batch's
+    last level completed while the next one's first launch scores, in the
+    other half of the buffer slots) give csm_scan_matchers_loaded's answers
+    bit for bit; a synchronous call in between completes the pending batch
+    first; on the 3-value map every level's exact pass has windows."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    grid = w.grid
+    if quantised:
+        grid = np.round(np.asarray(w.grid, dtype=np.float32) * 2.0).astype(np.float32) / np.float32(2.0)
+    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2", "CSM_FIRST_WINDOWS": "5", "CSM_SPLIT_HANDOFF_MIN": "8"}
+    os.environ.update(env)
+    try:
+        c = roborts_csm.Context(0)
+    finally:
+        for k in env:
+            del os.environ[k]
+    try:
+        c.set_grid(_map(grid, w.resolution, w.offset, version=1))
+        c.load_scans(b.points_cells, b.offsets)
+        n = b.init_poses.shape[0]
+        rng = np.random.default_rng(3)
+        inits = [np.ascontiguousarray(b.init_poses + rng.uniform(-1, 1, size=(n, 3)) * [0.05, 0.05, 0.02])
+                 for _ in range(5)]
+        eye = np.tile(np.eye(3).reshape(1, 9), (n, 1))
+        want = []
+        for p0 in inits:
+            p, cv = p0.copy(), eye.copy()
+            s = c.scan_matchers_loaded(headline_levels(), p, cv)
+            want.append((s, p, cv))
+        got = [(np.zeros(n), p0.copy(), eye.copy()) for p0 in inits]
+        for k in (0, 1):
+            c.scan_matchers_submit(headline_levels(), got[k][1], got[k][2], got[k][0])
+        p, cv = inits[2].copy(), eye.copy()  # completes batch 1 first
+        s = c.scan_matchers_loaded(headline_levels(), p, cv)
+        got[2] = (s, p, cv)
+        for k in (3, 4):
+            c.scan_matchers_submit(headline_levels(), got[k][1], got[k][2], got[k][0])
+        c.scan_matchers_wait()
+        for k in range(5):
+            for a, e in zip(got[k], want[k]):
+                assert np.array_equal(a, e), k
+    finally:
+        c.close()
