@@ -43,9 +43,10 @@ struct DBuf {
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
+    const size_t want = csm::grow_bytes(bytes, cap);
     release();
-    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
-    if (e == hipSuccess) cap = bytes;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
     return e;
   }
   void release() {
@@ -238,11 +239,12 @@ int upload_ends(csm_gridmap* m, const std::vector<GmEnd>& v) {
   const size_t bytes = v.size() * sizeof(GmEnd);
   GM_HIP(hipEventSynchronize(m->staged));
   if (bytes > m->h_cap) {
+    const size_t want = csm::grow_bytes(bytes, m->h_cap);
     if (m->h_ends) (void)hipHostFree(m->h_ends);
     m->h_ends = nullptr;
     m->h_cap = 0;
-    GM_HIP(hipHostMalloc(&m->h_ends, bytes, hipHostMallocDefault));
-    m->h_cap = bytes;
+    GM_HIP(hipHostMalloc(&m->h_ends, want, hipHostMallocDefault));
+    m->h_cap = want;
   }
   if (bytes > m->ends.cap) {
     GM_HIP(hipStreamSynchronize(m->stream));  // the old buffer may still be read

@@ -5,9 +5,25 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <cstddef>
 #include <cstdint>
 
 namespace csm {
+
+// Capacity to allocate for a buffer that must hold `bytes` and holds `cap`
+// now: at least 64 KiB, and half as much again as before (at most 256 MiB
+// more than asked), so per-scan sizes that creep up (a scan's points and
+// endpoints) do not reallocate scan after scan — hipFree / hipHostFree
+// synchronise the device, a few hundred microseconds in the online path.
+inline size_t grow_bytes(size_t bytes, size_t cap) {
+  size_t want = bytes < ((size_t)64 << 10) ? ((size_t)64 << 10) : bytes;
+  if (cap) {
+    size_t more = cap + cap / 2, lim = bytes + ((size_t)256 << 20);
+    if (more > lim) more = lim;
+    if (more > want) want = more;
+  }
+  return want;
+}
 
 enum { kGmProbability = 0, kGmCount = 1 };
 

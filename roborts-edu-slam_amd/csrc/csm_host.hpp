@@ -99,11 +99,12 @@ struct DevBuf {
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
+    const size_t want = csm::grow_bytes(bytes, cap);
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t e = hipMalloc(&p, bytes);
-    if (e == hipSuccess) cap = bytes;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
     return e;
   }
   void release() {
@@ -119,11 +120,12 @@ struct HostBuf {  // pinned staging for device->host score copies
   // flags: hipHostMallocCoherent for buffers kernels write straight into
   hipError_t ensure(size_t bytes, unsigned flags = hipHostMallocDefault) {
     if (bytes <= cap) return hipSuccess;
+    const size_t want = csm::grow_bytes(bytes, cap);
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t e = hipHostMalloc(&p, bytes, flags);
-    if (e == hipSuccess) cap = bytes;
+    hipError_t e = hipHostMalloc(&p, want, flags);
+    if (e == hipSuccess) cap = want;
     return e;
   }
   void release() {
