@@ -799,9 +799,12 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   int st;
-  if (c->staged_count > 0) {  // the pending batch reads the loaded scans the staged one replaces
-    if ((st = pipe_drain(c)) != CSM_OK || (st = take_staged(c)) != CSM_OK) return st;
-  }
+  // A queued batch (csm_load_scans_async) becomes the loaded one without
+  // completing the pending batch: every kernel of that batch is launched and
+  // holds the old points buffer, which the swap parks in a staging slot; the
+  // next upload into that slot comes after this call, which completes the
+  // pending batch (its host completion reads no points or offsets).
+  if (c->staged_count > 0 && (st = take_staged(c)) != CSM_OK) return st;
   if (c->loaded_n < 0) return c->fail(CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)");
   if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
   const int32_t n_scans = c->loaded_n;

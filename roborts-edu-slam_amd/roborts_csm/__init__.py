@@ -325,7 +325,12 @@ class Context:
         """csm_scan_matchers_submit: scan_matchers_loaded with the batch's last
         level left pending; poses / covs / scores (float64, caller-owned) are
         final after the next submit, scan_matchers_wait() or any other call,
-        and must stay alive until then (they are kept referenced here)."""
+        and must stay alive until then (they are kept referenced here). The
+        oldest queued batch (load_scans_async) is taken first, as by
+        scan_matchers_loaded, without completing the pending one."""
+        q = self.__dict__.get("_queued")
+        if q:
+            self._loaded = q.pop(0)
         n = self._loaded[1].size - 1
         for a, k in ((poses, 3), (covs, 9), (scores, 1)):
             assert a.dtype == np.float64 and a.flags.c_contiguous and a.size == k * n

@@ -1024,3 +1024,48 @@ def test_submitted_batches_equal_loaded(world2000, quantised):
                 assert np.array_equal(a, e), k
     finally:
         c.close()
+
+
+def test_submitted_batches_from_staged_scans(world2000):
+    """csm_load_scans_async + csm_scan_matchers_submit, a different batch of
+    scans per submit: the queued batch is taken while the previous one is
+    still pending (its points parked in a staging slot until it completes),
+    and every batch's answers equal its own synchronous load + match."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2", "CSM_FIRST_WINDOWS": "5", "CSM_SPLIT_HANDOFF_MIN": "8"}
+    os.environ.update(env)
+    try:
+        c = roborts_csm.Context(0)
+    finally:
+        for k in env:
+            del os.environ[k]
+    n = b.init_poses.shape[0]
+    eye = np.tile(np.eye(3).reshape(1, 9), (n, 1))
+    batches = [np.ascontiguousarray(b.points_cells * f) for f in (1.0, 0.98, 1.02, 0.99, 1.01)]
+    pins = []
+    try:
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+        want = []
+        for q in batches:
+            c.load_scans(q, b.offsets)
+            p, cv = b.init_poses.copy(), eye.copy()
+            want.append((c.scan_matchers_loaded(headline_levels(), p, cv), p, cv))
+        for q in batches:
+            pins.append(roborts_csm.PinnedArray(q.shape))
+            np.copyto(pins[-1].array, q)
+        got = [(np.zeros(n), b.init_poses.copy(), eye.copy()) for _ in batches]
+        c.load_scans_async(pins[0].array, b.offsets)
+        for k in range(len(batches)):
+            if k + 1 < len(batches):
+                c.load_scans_async(pins[k + 1].array, b.offsets)
+            c.scan_matchers_submit(headline_levels(), got[k][1], got[k][2], got[k][0])
+        c.scan_matchers_wait()
+        for k in range(len(batches)):
+            for a, e in zip(got[k], want[k]):
+                assert np.array_equal(a, e), k
+    finally:
+        c.close()
+        for p in pins:
+            p.close()
