@@ -544,10 +544,9 @@ __device__ __forceinline__ void emit_sealed(const FinishArgs& A, const FinishOut
 }
 
 // The exact pass over one window (4 waves). Waves 1-3 return before the
-// list scans; the caller's barrier joins them. Lean: the copy called by
-// finish_side_kernel only (register-allocated under its launch bounds).
-template <int Lean>
-__device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ scans,
+// list scans; the caller's barrier joins them. Inlined into finish_kernel
+// (as a call it took 211 VGPRs and scratch; inlined 129 and none, r04).
+__device__ __forceinline__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ scans,
                               const AngleEntry* __restrict__ angles, const double* __restrict__ scores,
                               FinishOut* __restrict__ out, const int w, char* smem) {
   const int n = (int)A.n_cand;
@@ -900,7 +899,6 @@ __device__ void finish_window(const FinishArgs& A, const ScanWork* __restrict__ 
 // With the fast finish's list of flagged windows, a small grid walks the list
 // (a block per window of all n_windows cost ~50 us of dispatch at 2048
 // windows even though almost every block exits at once).
-template <int Lean>
 __device__ __forceinline__ void finish_entry(const FinishArgs& A, const ScanWork* __restrict__ scans,
                                              const AngleEntry* __restrict__ angles, const double* __restrict__ scores,
                                              FinishOut* __restrict__ out, char* smem) {
@@ -911,7 +909,7 @@ __device__ __forceinline__ void finish_entry(const FinishArgs& A, const ScanWork
                                             __HIP_MEMORY_SCOPE_AGENT);
     const int cnt = (uint32_t)(head >> 32) == (uint32_t)A.flag_value ? (int)(uint32_t)head : 0;
     for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
-      finish_window<Lean>(A, scans, angles, scores, out, A.exact_list[2 + i], smem);
+      finish_window(A, scans, angles, scores, out, A.exact_list[2 + i], smem);
       __syncthreads();  // the next window reuses the LDS carve
     }
     if (A.host_flag && cnt > 0) {  // (nothing flagged: the fast pass signalled the host)
@@ -932,7 +930,7 @@ __device__ __forceinline__ void finish_entry(const FinishArgs& A, const ScanWork
   }
   const int w = blockIdx.x;
   if (A.need_exact && A.need_exact[w] == 0) return;  // the fast finish settled this window
-  finish_window<Lean>(A, scans, angles, scores, out, w, smem);
+  finish_window(A, scans, angles, scores, out, w, smem);
 }
 
 __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const ScanWork* __restrict__ scans,
@@ -940,29 +938,7 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
                                                              const double* __restrict__ scores,
                                                              FinishOut* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  finish_entry<0>(A, scans, angles, scores, out, smem);
-}
-
-// The same exact pass for the side stream, held to 64 VGPRs (8 waves per
-// SIMD; the rest spills to scratch). finish_kernel takes 211 VGPRs: a block
-// (one wave per SIMD) fits on a CU only where 4 of the 8 waves of the
-// 60-VGPR scoring kernel running beside it have retired on every SIMD at
-// once, which in practice is that kernel's tail -- the exact pass's dispatch
-// then spans the other part's whole coarse launch. At 64 VGPRs a block fits
-// wherever one scoring block has retired. CSM_FINISH_SIDE=1 selects it.
-__global__ __launch_bounds__(64 * kWaves, 8) void finish_side_kernel(FinishArgs A, const ScanWork* __restrict__ scans,
-                                                                     const AngleEntry* __restrict__ angles,
-                                                                     const double* __restrict__ scores,
-                                                                     FinishOut* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  finish_entry<1>(A, scans, angles, scores, out, smem);
-}
-inline bool finish_side_lean() {
-  static const bool on = [] {
-    const char* e = std::getenv("CSM_FINISH_SIDE");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
+  finish_entry(A, scans, angles, scores, out, smem);
 }
 
 // ---- fast finish: no sort when no tie can matter ----------------------------
@@ -1441,10 +1417,9 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
 #else
     const int max_dyn = 160 * 1024;
 #endif
-    for (const void* k : {reinterpret_cast<const void*>(&finish_kernel), reinterpret_cast<const void*>(&finish_side_kernel)}) {
-      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_dyn);
-      if (e != hipSuccess) return e;
-    }
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&finish_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, max_dyn);
+    if (e != hipSuccess) return e;
     attr_set = true;
   }
   const bool listed = A.need_exact && A.exact_list && !A.order_out;
@@ -1468,10 +1443,7 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
   if (A.order_out) B.need_exact = nullptr;  // the permutation hook always sorts
   if (!listed) B.exact_list = nullptr;
   const dim3 grid(listed ? std::min(n_windows, 512) : n_windows);
-  if (xs != stream && finish_side_lean())
-    hipLaunchKernelGGL(finish_side_kernel, grid, dim3(64 * kWaves), lds, xs, B, d_scans, d_angles, d_scores, d_out);
-  else
-    hipLaunchKernelGGL(finish_kernel, grid, dim3(64 * kWaves), lds, xs, B, d_scans, d_angles, d_scores, d_out);
+  hipLaunchKernelGGL(finish_kernel, grid, dim3(64 * kWaves), lds, xs, B, d_scans, d_angles, d_scores, d_out);
   return hipGetLastError();
 }
 
