@@ -52,6 +52,7 @@ bench)
   rm -rf $O/prof_online $O/prof_adapter
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_online -o run --output-format csv -- python3 bench.py --workload online --steps 200 --warmup 20 --no-cpu > $O/prof_online.json 2> $O/prof_online.err || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_adapter -o run --output-format csv -- tests/cpp/build/adapter_run bench 41 3000 > $O/prof_adapter.json 2> $O/prof_adapter.err || exit $?
+  timeout -k 10 200 python tools/online_probe.py 42 120 > $O/online_probe.txt 2> $O/online_probe.err || exit $?
   echo "bench done" ;;
 *) echo "usage: $0 tests|pmc|bench"; exit 2 ;;
 esac
