@@ -457,7 +457,8 @@ struct PipeJob {
   // batches: a fresh run's window plans (64 B each, 128 KB per 2048 windows)
   // came from mmap and paid ~40 us of page faults at every level start (r04).
   LevelRun R[2][csm_ctx::kMaxParts];
-  bool pending = false;  // the last level launched, its completion deferred
+  bool pending = false;  // levels launched up to the last part's last hand-off; that and the completion deferred
+  bool last_handoff_done = false;
   std::vector<csm::FinishOut> snaps[csm_ctx::kMaxParts];  // CSM_DEBUG_FIN
   std::vector<char> hows[csm_ctx::kMaxParts];
 };
@@ -496,6 +497,7 @@ void job_setup(csm_ctx* c, PipeJob& J, int32_t n_scans, const int64_t* offsets, 
   J.sum = sum;
   J.scores = nullptr;
   J.pending = false;
+  J.last_handoff_done = false;
   // part 0 takes part0_permille of the scans, the others split the rest: a
   // larger first part shortens what nothing hides, the last part's
   // super-fine completion at the end of the call and its fine -> super-fine
@@ -530,35 +532,50 @@ int job_begin(csm_ctx* c, PipeJob& J, int h) {
   });
 }
 
-// Every level transition of J: its last level launched, its completion left
-// to job_finish (J.pending).
+// The level transition (l -> l + 1) of part h.
+int job_handoff(csm_ctx* c, PipeJob& J, int l, int h) {
+  const int32_t s0 = J.first[h];
+  J.R[(l + 1) & 1][h].tag = (l + 1) * 8 + h;
+  return with_slot(c, J, h, [&] {
+    return level_end_begin(c, J.R[l & 1][h], J.R[(l + 1) & 1][h], J.count[h], J.offsets + s0, J.levels[l + 1],
+                           J.poses + 3 * (size_t)s0, J.covs + 9 * (size_t)s0, J.resp.data() + s0, J.sum + s0,
+                           J.scan_grid ? J.scan_grid + s0 : nullptr, job_skip(c, J, l + 1),
+                           c->split_last_handoff && h == J.K - 1 && l + 2 == J.n_levels);
+  });
+}
+
+// Every level transition of J but the last part's last one, which is left to
+// job_last_handoff (J.pending): when a submitted batch returns, the device
+// still has the last part's previous level and the other parts' last level
+// queued, enough to cover the host's way to the next batch's first launch.
 int job_levels(csm_ctx* c, PipeJob& J) {
   const int K = J.K, n_levels = J.n_levels;
   int st;
-  for (int l = 0; l + 1 < n_levels; ++l) {
+  for (int l = 0; l + 1 < n_levels; ++l)
     for (int h = 0; h < K; ++h) {
-      const int32_t s0 = J.first[h];
-      J.R[(l + 1) & 1][h].tag = (l + 1) * 8 + h;
-      st = with_slot(c, J, h, [&] {
-        return level_end_begin(c, J.R[l & 1][h], J.R[(l + 1) & 1][h], J.count[h], J.offsets + s0, J.levels[l + 1],
-                               J.poses + 3 * (size_t)s0, J.covs + 9 * (size_t)s0, J.resp.data() + s0, J.sum + s0,
-                               J.scan_grid ? J.scan_grid + s0 : nullptr, job_skip(c, J, l + 1),
-                               c->split_last_handoff && h == K - 1 && l + 2 == n_levels);
-      });
-      if (st != CSM_OK) return st;
+      if (l + 2 == n_levels && h == K - 1) continue;
+      if ((st = job_handoff(c, J, l, h)) != CSM_OK) return st;
     }
-  }
   J.pending = true;
+  J.last_handoff_done = n_levels < 2;
   return CSM_OK;
+}
+
+// The last part's last level transition (the last launch of J).
+int job_last_handoff(csm_ctx* c, PipeJob& J) {
+  if (!J.pending || J.last_handoff_done) return CSM_OK;
+  J.last_handoff_done = true;
+  return job_handoff(c, J, J.n_levels - 2, J.K - 1);
 }
 
 // J's last level: every part's windows completed, responses summed (and the
 // submitted batch's scores written).
 int job_finish(csm_ctx* c, PipeJob& J) {
   if (!J.pending) return CSM_OK;
+  int st;
+  if ((st = job_last_handoff(c, J)) != CSM_OK) return st;
   J.pending = false;
   const int K = J.K, last = J.n_levels - 1;
-  int st;
   for (int h = 0; h < K; ++h) {
     const int32_t s0 = J.first[h];
     LevelRun& cur = J.R[last & 1][h];
@@ -639,7 +656,21 @@ int pipe_drain(csm_ctx* c) {
   for (PipeJob& J : PS.job)
     if (J.pending) {
       DeviceGuard g(c->device);
+      PipeMode mode(c);  // its last hand-off launches as the rest of the batch did
       const int st = job_finish(c, J);
+      if (st != CSM_OK) return pipe_abort(c, st);
+    }
+  return CSM_OK;
+}
+
+// Every launch of a pending batch made (its last part's last hand-off): the
+// loaded points may change after this.
+int pipe_last_launches(csm_ctx* c) {
+  if (!c->pipe) return CSM_OK;
+  for (PipeJob& J : static_cast<PipeState*>(c->pipe)->job)
+    if (J.pending && !J.last_handoff_done) {
+      PipeMode mode(c);
+      const int st = job_last_handoff(c, J);
       if (st != CSM_OK) return pipe_abort(c, st);
     }
   return CSM_OK;
@@ -800,11 +831,13 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
   DeviceGuard g(c->device);
   int st;
   // A queued batch (csm_load_scans_async) becomes the loaded one without
-  // completing the pending batch: every kernel of that batch is launched and
-  // holds the old points buffer, which the swap parks in a staging slot; the
-  // next upload into that slot comes after this call, which completes the
-  // pending batch (its host completion reads no points or offsets).
-  if (c->staged_count > 0 && (st = take_staged(c)) != CSM_OK) return st;
+  // completing the pending batch: once that batch's last launch is made, its
+  // kernels hold the old points buffer, which the swap parks in a staging
+  // slot; the next upload into that slot comes after this call, which
+  // completes the pending batch (its completion reads no points or offsets).
+  if (c->staged_count > 0) {
+    if ((st = pipe_last_launches(c)) != CSM_OK || (st = take_staged(c)) != CSM_OK) return st;
+  }
   if (c->loaded_n < 0) return c->fail(CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)");
   if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
   const int32_t n_scans = c->loaded_n;
@@ -829,12 +862,15 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
   J.own_sum.assign((size_t)n_scans, 0.0);
   J.sum = J.own_sum.data();
   J.scores = scores;
-  // this batch's first launch, then the previous batch's deferred last level
-  // while that scores, then the rest of this batch up to its last level
+  // this batch's first part's first level, the previous batch's last launch
+  // (its last part's last hand-off), this batch's other parts' first level,
+  // then the previous batch's completion while those score, then the rest of
+  // this batch up to its last part's last hand-off
   if ((st = job_begin(c, J, 0)) != CSM_OK) return pipe_abort(c, st);
-  if (P.pending && (st = job_finish(c, P)) != CSM_OK) return pipe_abort(c, st);
+  if (P.pending && (st = job_last_handoff(c, P)) != CSM_OK) return pipe_abort(c, st);
   for (int h = 1; h < K; ++h)
     if ((st = job_begin(c, J, h)) != CSM_OK) return pipe_abort(c, st);
+  if (P.pending && (st = job_finish(c, P)) != CSM_OK) return pipe_abort(c, st);
   if ((st = job_levels(c, J)) != CSM_OK) return pipe_abort(c, st);
   PS.next ^= 1;
   if (c->profiling) {
