@@ -553,11 +553,11 @@ int job_levels(csm_ctx* c, PipeJob& J) {
   int st;
   for (int l = 0; l + 1 < n_levels; ++l)
     for (int h = 0; h < K; ++h) {
-      if (l + 2 == n_levels && h == K - 1) continue;
+      if (c->defer_last_handoff && l + 2 == n_levels && h == K - 1) continue;
       if ((st = job_handoff(c, J, l, h)) != CSM_OK) return st;
     }
   J.pending = true;
-  J.last_handoff_done = n_levels < 2;
+  J.last_handoff_done = n_levels < 2 || !c->defer_last_handoff;
   return CSM_OK;
 }
 

@@ -590,6 +590,7 @@ struct csm_ctx {
   void* pipe = nullptr;  // csm_driver.cpp PipeState: submitted batches (csm_scan_matchers_submit)
   bool split_last_handoff = true;  // the last part's hand-off to the last level in two spans (CSM_SPLIT_HANDOFF)
   int split_handoff_min = 256;     // ... for parts of at least this many windows (CSM_SPLIT_HANDOFF_MIN)
+  bool defer_last_handoff = true;  // a submitted batch leaves its last part's last hand-off to the next call (CSM_DEFER_HANDOFF)
   int part0_permille = 550;  // two parts: the first one's share of the scans (CSM_PART0_PERMILLE;
                              // r04 A/B, 2 runs each: 500 9.40, 550 9.61, 600 9.56, 650 9.47 G scorings/s)
   void swap_slot(int i) {    // i >= 1: exchange the current buffer set with alt[i - 1]
