@@ -99,18 +99,25 @@ def kernel_accounting(stats, elapsed_s: float, steps: int) -> dict:
 
 def dominant_kernel(stats):
     """The scoring or finish kernel with the most device time, and its average
-    launch time over the launches that went out as ONE dispatch (the first
-    part's coarse level is two dispatches, "span2:<name>", each with its own
-    ramp and tail: a rocprof dispatch mean compares with the one-span mean)."""
+    launch time as rocprof sees it over whole-part dispatches
+    (`CSM_FIRST_WINDOWS=0`). The first part's coarse level goes out in spans
+    ("span2:<name>", each with its own ramp and tail) and the parts differ in
+    size (`CSM_PART0_PERMILLE`), so the time is the one-dispatch launches' bytes
+    per ms at the mean launch's algorithmic bytes."""
     ks = [s for s in stats if s["name"].startswith(("score_", "finish_kernel"))]
     dom = max(ks, key=lambda s: s["total_ms"])
     two = next((s for s in stats if s["name"] == "span2:" + dom["name"]), None)
     n1 = dom["launches"] - (two["launches"] if two else 0)
     info = {"launches": dom["launches"], "two_span_launches": two["launches"] if two else 0}
+    mean_bytes = dom["algorithmic_bytes"] / dom["launches"]
     if two and n1 > 0:
-        avg = (dom["total_ms"] - two["total_ms"]) / n1
+        t1 = dom["total_ms"] - two["total_ms"]
+        b1 = dom["algorithmic_bytes"] - two["algorithmic_bytes"]
+        avg = mean_bytes * t1 / b1 if b1 > 0 and mean_bytes > 0 else t1 / n1
+        info["avg_ms_one_dispatch_launches"] = t1 / n1
         info["avg_ms_all_launches"] = dom["total_ms"] / dom["launches"]
         info["avg_ms_two_span_launches"] = two["total_ms"] / two["launches"]
+        info["how"] = "one-dispatch launches' bytes per ms, at the mean launch's bytes"
     else:
         avg = dom["total_ms"] / dom["launches"]
     return dom, avg, info

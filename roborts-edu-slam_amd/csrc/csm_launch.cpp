@@ -105,9 +105,9 @@ int account_run(csm_ctx* c, const PendingRun& p) {
     }
     c->account(p.kname, ms, p.alg_bytes, p.scorings);
     if (p.gap0) {  // the same launch again under "span2:": two dispatches, each with its own ramp and tail
-      char nm[48];
+      char nm[48];  // (its bytes too: the one-dispatch launches' bytes per ms are then known)
       std::snprintf(nm, sizeof(nm), "span2:%.41s", p.kname);
-      c->account(nm, ms, 0.0, 0.0);
+      c->account(nm, ms, p.alg_bytes, 0.0);
     }
     if (p.device_finish) {
       if ((e = hipEventElapsedTime(&ms, p.ev1, p.ev2)) != hipSuccess) return c->hip_fail(e, "hipEventElapsedTime");
