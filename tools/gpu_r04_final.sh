@@ -30,6 +30,11 @@ for k, v in b['kernels'].items():
 json.dump(a, open('gpurun_out/r04/counters_lc.json', 'w'), indent=1)
 PY
   cp $O/pmcr/counters.json $O/counters.json; echo "pmc done" ;;
+pmcbench)
+  # one call: counters of this build, copied where bench.py reads them, then every bench line
+  bash "$0" pmc || exit $?
+  cp $O/counters.json $O/counters_lc.json $O/counters_small.json profiles/r04/ || exit $?
+  bash "$0" bench || exit $? ;;
 trace2)
   rm -rf $O/prof_config2
   CSM_FIRST_WINDOWS=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_config2 -o run --output-format csv -- python3 bench.py --no-cpu --no-latency --no-b109 > $O/prof_config2.json 2> $O/prof_config2.err || exit $?
