@@ -445,6 +445,7 @@ int match_level(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
 // while that one scores -- the device no longer idles between batches.
 struct PipeJob {
   int K = 2, n_levels = 0, slot0 = 0;  // parts, levels, the parts' first buffer slot
+  int first_windows = 0;                // the first part's first span (level_begin_split)
   int32_t n_scans = 0;
   const int64_t* offsets = nullptr;
   const int32_t* scan_grid = nullptr;
@@ -484,8 +485,11 @@ int with_slot(csm_ctx* c, const PipeJob& J, int h, F&& f) {
 }
 
 void job_setup(csm_ctx* c, PipeJob& J, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
-               int n_levels, double* poses, double* covs, double* sum, const int32_t* scan_grid, int K, int slot0) {
+               int n_levels, double* poses, double* covs, double* sum, const int32_t* scan_grid, int K, int slot0,
+               bool submitted = false) {
   J.K = K;
+  J.first_windows = submitted ? c->first_windows_submit : c->first_windows;
+  const int permille = submitted ? c->part0_permille_submit : c->part0_permille;
   J.n_levels = n_levels;
   J.slot0 = slot0;
   J.n_scans = n_scans;
@@ -502,7 +506,7 @@ void job_setup(csm_ctx* c, PipeJob& J, int32_t n_scans, const int64_t* offsets, 
   // larger first part shortens what nothing hides, the last part's
   // super-fine completion at the end of the call and its fine -> super-fine
   // hand-off (the device has only part 0's super-fine level to run meanwhile)
-  const int64_t n0 = (K == 2 && c->part0_permille > 0) ? (int64_t)n_scans * c->part0_permille / 1000
+  const int64_t n0 = (K == 2 && permille > 0) ? (int64_t)n_scans * permille / 1000
                                                         : (int64_t)n_scans / K;
   for (int h = 0; h < K; ++h) {
     J.first[h] = h == 0 ? 0 : (int32_t)(n0 + (int64_t)(n_scans - n0) * (h - 1) / (K - 1));
@@ -526,7 +530,7 @@ int job_begin(csm_ctx* c, PipeJob& J, int h) {
     const int32_t* g = J.scan_grid ? J.scan_grid + s0 : nullptr;
     if (h == 0)
       return level_begin_split(c, J.count[h], J.offsets + s0, J.levels[0], J.poses + 3 * (size_t)s0,
-                               J.resp.data() + s0, J.R[0][h], g, job_skip(c, J, 0), c->first_windows);
+                               J.resp.data() + s0, J.R[0][h], g, job_skip(c, J, 0), J.first_windows);
     return level_begin(c, J.count[h], J.offsets + s0, J.levels[0], J.poses + 3 * (size_t)s0, J.resp.data() + s0,
                        nullptr, J.R[0][h], g, job_skip(c, J, 0));
   });
@@ -858,7 +862,8 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
   PipeJob& P = PS.job[PS.next ^ 1];
   if (J.pending && (st = pipe_drain(c)) != CSM_OK) return st;  // (cannot happen: submits alternate)
   PipeMode mode(c);
-  job_setup(c, J, n_scans, c->loaded_off.data(), levels, n_levels, poses, covs, nullptr, nullptr, K, PS.next * K);
+  job_setup(c, J, n_scans, c->loaded_off.data(), levels, n_levels, poses, covs, nullptr, nullptr, K, PS.next * K,
+            true);
   J.own_sum.assign((size_t)n_scans, 0.0);
   J.sum = J.own_sum.data();
   J.scores = scores;

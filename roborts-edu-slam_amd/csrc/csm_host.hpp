@@ -586,6 +586,9 @@ struct csm_ctx {
   bool skip_dead_lists = true;  // live_lists (CSM_SKIP_DEAD_LISTS=0: every level fills both lists)
   int pipeline_parts = 2;    // parts in flight (CSM_PIPELINE_PARTS: 2..kMaxParts; 2 measured fastest)
   int first_windows = 128;   // level_begin_split: windows the first part's first launch takes (CSM_FIRST_WINDOWS; 0: one launch)
+  // submitted batches (the device has the previous batch's work queued): one
+  // launch (r04 A/B, 2 runs each: 0 10.77 / 10.98, 128 10.39 / 10.41 G scorings/s)
+  int first_windows_submit = 0;  // (CSM_FIRST_WINDOWS_SUBMIT; CSM_FIRST_WINDOWS sets both)
   int span_growth = 4;       // ... and each later span's growth (CSM_SPAN_GROWTH)
   void* pipe = nullptr;  // csm_driver.cpp PipeState: submitted batches (csm_scan_matchers_submit)
   bool split_last_handoff = true;  // the last part's hand-off to the last level in two spans (CSM_SPLIT_HANDOFF)
@@ -593,6 +596,8 @@ struct csm_ctx {
   bool defer_last_handoff = true;  // a submitted batch leaves its last part's last hand-off to the next call (CSM_DEFER_HANDOFF)
   int part0_permille = 550;  // two parts: the first one's share of the scans (CSM_PART0_PERMILLE;
                              // r04 A/B, 2 runs each: 500 9.40, 550 9.61, 600 9.56, 650 9.47 G scorings/s)
+  int part0_permille_submit = 500;  // ... for submitted batches (CSM_PART0_PERMILLE_SUBMIT; r04 A/B with
+                                    // the deferred hand-off: 500 10.45 / 10.48, 550 10.39 / 10.41 G)
   void swap_slot(int i) {    // i >= 1: exchange the current buffer set with alt[i - 1]
     Slot& a = alt[i - 1];
     std::swap(scans, a.scans);
