@@ -835,13 +835,30 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
   DeviceGuard g(c->device);
   int st;
   // A queued batch (csm_load_scans_async) becomes the loaded one without
-  // completing the pending batch: once that batch's last launch is made, its
-  // kernels hold the old points buffer, which the swap parks in a staging
-  // slot; the next upload into that slot comes after this call, which
-  // completes the pending batch (its completion reads no points or offsets).
+  // completing the pending batch: the swap parks the pending batch's points
+  // in a staging slot, its last launch below borrows them back, and the next
+  // upload into that slot comes after this call, which completes the pending
+  // batch (its completion reads no points or offsets).
+  int parked = -1;
+  double parked_maxabs = 0.0;
   if (c->staged_count > 0) {
-    if ((st = pipe_last_launches(c)) != CSM_OK || (st = take_staged(c)) != CSM_OK) return st;
+    parked = c->staged_head;  // the slot take_staged swaps the current points into
+    parked_maxabs = c->pts_maxabs;
+    if ((st = take_staged(c)) != CSM_OK) return st;
   }
+  // the pending batch's last launch (its last part's last hand-off), on its own points
+  auto prior_last_launches = [&]() {
+    if (parked >= 0) {
+      std::swap(c->pts, c->staged[parked].pts);
+      std::swap(c->pts_maxabs, parked_maxabs);
+    }
+    const int r = pipe_last_launches(c);
+    if (parked >= 0) {
+      std::swap(c->pts, c->staged[parked].pts);
+      std::swap(c->pts_maxabs, parked_maxabs);
+    }
+    return r;
+  };
   if (c->loaded_n < 0) return c->fail(CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)");
   if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
   const int32_t n_scans = c->loaded_n;
@@ -852,7 +869,7 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
   const int K = std::max(2, std::min(c->pipeline_parts, csm_ctx::kMaxParts));
   if (n_scans == 0 || fast || grid || n_scans < c->pipeline_min || 2 * K > csm_ctx::kMaxParts) {
     // nothing to overlap (or no second set of buffer slots): the batch completes here
-    if ((st = pipe_drain(c)) != CSM_OK) return st;
+    if ((st = prior_last_launches()) != CSM_OK || (st = pipe_drain(c)) != CSM_OK) return st;
     return matchers_loaded_locked(c, levels, use_fine, poses, covs, scores);
   }
   const double t_call = now_ms();
@@ -860,7 +877,8 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
   PipeState& PS = pipe_of(c);
   PipeJob& J = PS.job[PS.next];
   PipeJob& P = PS.job[PS.next ^ 1];
-  if (J.pending && (st = pipe_drain(c)) != CSM_OK) return st;  // (cannot happen: submits alternate)
+  if (J.pending && ((st = prior_last_launches()) != CSM_OK || (st = pipe_drain(c)) != CSM_OK))
+    return st;  // (cannot happen: submits alternate)
   PipeMode mode(c);
   job_setup(c, J, n_scans, c->loaded_off.data(), levels, n_levels, poses, covs, nullptr, nullptr, K, PS.next * K,
             true);
@@ -872,7 +890,7 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
   // then the previous batch's completion while those score, then the rest of
   // this batch up to its last part's last hand-off
   if ((st = job_begin(c, J, 0)) != CSM_OK) return pipe_abort(c, st);
-  if (P.pending && (st = job_last_handoff(c, P)) != CSM_OK) return pipe_abort(c, st);
+  if ((st = prior_last_launches()) != CSM_OK) return pipe_abort(c, st);
   for (int h = 1; h < K; ++h)
     if ((st = job_begin(c, J, h)) != CSM_OK) return pipe_abort(c, st);
   if (P.pending && (st = job_finish(c, P)) != CSM_OK) return pipe_abort(c, st);
