@@ -63,3 +63,31 @@ def test_search_lines_use_their_own_metric():
     assert bench._metric("pyramid") == (bench.RESOLVED_METRIC, "candidates/s")
     assert bench._metric("exhaustive") == (bench.METRIC, "scorings/s")
     assert bench.RESOLVED_METRIC != bench.METRIC
+
+
+def test_roofline_launch_time_and_kernel_accounting():
+    """The roofline's launch time: the one-dispatch launches' bytes per ms at
+    the mean launch's bytes (parts of different sizes, a first part in spans);
+    kernel_share counts scoring launches and the fast finish passes once."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    # part 0: 1.2 GB in spans over 1.0 ms (span2 entry), part 1: 0.8 GB in 0.4 ms, per step, 2 steps
+    stats = [
+        {"name": "score_box_pair_kernel<13,all>", "launches": 4, "total_ms": 2 * (1.0 + 0.4),
+         "algorithmic_bytes": 2 * (1.2e9 + 0.8e9), "scorings": 4.0},
+        {"name": "span2:score_box_pair_kernel<13,all>", "launches": 2, "total_ms": 2.0,
+         "algorithmic_bytes": 2.4e9, "scorings": 0.0},
+        {"name": "finish_kernel<5070>", "launches": 4, "total_ms": 1.0, "algorithmic_bytes": 0.0, "scorings": 0.0},
+        {"name": "finish:fast<5070>", "launches": 4, "total_ms": 0.2, "algorithmic_bytes": 0.0, "scorings": 0.0},
+        {"name": "finish:exact<5070>", "launches": 4, "total_ms": 0.8, "algorithmic_bytes": 0.0, "scorings": 0.0},
+        {"name": "host:wait", "launches": 9, "total_ms": 5.0, "algorithmic_bytes": 0.0, "scorings": 0.0},
+    ]
+    dom, avg, info = bench.dominant_kernel(stats)
+    assert dom["name"] == "score_box_pair_kernel<13,all>"
+    # one-dispatch rate 0.8 GB / 0.4 ms = 2 GB/ms; the mean launch is 1.0 GB -> 0.5 ms
+    assert abs(avg - 0.5) < 1e-12 and info["two_span_launches"] == 2
+    acct = bench.kernel_accounting(stats, elapsed_s=4e-3, steps=2)
+    assert abs(acct["kernel_stream_ms_per_step"] - (2.8 + 0.2) / 2) < 1e-12
+    assert abs(acct["exact_finish_side_stream_ms_per_step"] - 0.4) < 1e-12
+    assert acct["kernel_share_of_step"] <= 1.0
