@@ -977,8 +977,8 @@ def test_load_scans_async_queue(world2000):
             p.close()
 
 
-@pytest.mark.parametrize("quantised", [False, True])
-def test_submitted_batches_equal_loaded(world2000, quantised):
+@pytest.mark.parametrize("quantised,defer", [(False, "1"), (True, "1"), (True, "0")])
+def test_submitted_batches_equal_loaded(world2000, quantised, defer):
     """csm_scan_matchers_submit: batches in flight back to back (a batch's
     last level completed while the next one's first launch scores, in the
     other half of the buffer slots) give csm_scan_matchers_loaded's answers
@@ -990,7 +990,8 @@ def test_submitted_batches_equal_loaded(world2000, quantised):
     grid = w.grid
     if quantised:
         grid = np.round(np.asarray(w.grid, dtype=np.float32) * 2.0).astype(np.float32) / np.float32(2.0)
-    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2", "CSM_FIRST_WINDOWS": "5", "CSM_SPLIT_HANDOFF_MIN": "8"}
+    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2", "CSM_FIRST_WINDOWS": "5", "CSM_SPLIT_HANDOFF_MIN": "8",
+           "CSM_DEFER_HANDOFF": defer}
     os.environ.update(env)
     try:
         c = roborts_csm.Context(0)
@@ -1026,7 +1027,8 @@ def test_submitted_batches_equal_loaded(world2000, quantised):
         c.close()
 
 
-def test_submitted_batches_from_staged_scans(world2000):
+@pytest.mark.parametrize("first_windows", ["5", None])
+def test_submitted_batches_from_staged_scans(world2000, first_windows):
     """csm_load_scans_async + csm_scan_matchers_submit, a different batch of
     scans per submit: the queued batch is taken while the previous one is
     still pending (its points parked in a staging slot until it completes),
@@ -1034,7 +1036,9 @@ def test_submitted_batches_from_staged_scans(world2000):
     import roborts_csm
     from roborts_csm.params import headline_levels
     w, b = world2000
-    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2", "CSM_FIRST_WINDOWS": "5", "CSM_SPLIT_HANDOFF_MIN": "8"}
+    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2", "CSM_SPLIT_HANDOFF_MIN": "8"}
+    if first_windows is not None:  # None: the submitted batches' own defaults (one first launch, 50/50)
+        env["CSM_FIRST_WINDOWS"] = first_windows
     os.environ.update(env)
     try:
         c = roborts_csm.Context(0)
