@@ -123,10 +123,11 @@ def dominant_kernel(stats):
     return dom, avg, info
 
 
-def cpu_baseline(world, batch, levels, seconds: float, threads: int = 1, label: str = ""):
+def cpu_baseline(world, batch, levels, seconds: float, threads: int = 1, label: str = "", collect=None):
     """Oracle (test infrastructure, CPU restatement) on a bounded sample.
     threads > 1: the all-cores variant (OpenMP over theta inside each window;
-    identical results)."""
+    identical results). collect: a list that receives (n, (scores, poses,
+    covs)) of the sample (scans 0 .. n-1), the parity check's expected values."""
     import pyoracle as O
     O.set_threads(threads)
     m = O.Map(world.grid, world.resolution, world.offset)
@@ -136,14 +137,16 @@ def cpu_baseline(world, batch, levels, seconds: float, threads: int = 1, label: 
         off = batch.offsets[k0:k1 + 1] - batch.offsets[k0]
         pts = batch.points_cells[batch.offsets[k0]:batch.offsets[k1]]
         t = time.perf_counter()
-        O.scan_matchers_batch(m, pts, off, levels, batch.init_poses[k0:k1],
-                              np.tile(eye, (k1 - k0, 1)))
-        return time.perf_counter() - t
+        res = O.scan_matchers_batch(m, pts, off, levels, batch.init_poses[k0:k1],
+                                    np.tile(eye, (k1 - k0, 1)))
+        return time.perf_counter() - t, res
 
-    probe = run(0, 2) / 2
+    probe = run(0, 2)[0] / 2
     n = int(max(2, min(batch.offsets.size - 1, seconds / max(probe, 1e-6))))
-    dt = run(0, n)
+    dt, res = run(0, n)
     O.set_threads(1)
+    if collect is not None:
+        collect.append((n, res))
     per_scan = sum(_window_cands(l) for l in levels)
     how = "single-threaded" if threads == 1 else f"{threads} threads (OpenMP over theta)"
     out = {"value": n * per_scan / dt, "unit": "scorings/s", "cores": threads, "kind": "port",
@@ -152,6 +155,50 @@ def cpu_baseline(world, batch, levels, seconds: float, threads: int = 1, label: 
     if threads > 1:
         out["host_cpu_share"] = host_cpu_share()
     return out
+
+
+def parity_check(gpu, runs, what: str) -> dict:
+    """The timed configuration's own outputs against the oracle's: gpu =
+    (scores, poses, covs) of the last timed step, runs = cpu_baseline's
+    collected samples (scans 0 .. n-1 of the same batch from the same initial
+    poses). Bit for bit; a mismatching scan is one whose score, pose or
+    covariance differs in any bit."""
+    n, (s2, p2, c2) = max(runs, key=lambda r: r[0])
+    s, p, c = (np.asarray(a)[:n] for a in gpu)
+    bad = (s != s2) | np.any(p.reshape(n, 3) != p2.reshape(n, 3), axis=1) | \
+        np.any(c.reshape(n, 9) != c2.reshape(n, 9), axis=1)
+    out = {"scans_checked": int(n), "mismatches": int(np.sum(bad)),
+           "what": f"{what}: scores, poses and covariances of the last timed step, bit for bit, against "
+                   "oracle/csm_oracle.cpp on the cpu_baseline samples (scans 0 .. scans_checked-1)"}
+    if out["mismatches"]:
+        out["first_mismatch"] = int(np.argmax(bad))
+    return out
+
+
+def oracle_sample(world, batch, levels, n: int, threads: int):
+    """The oracle's outputs for scans 0 .. n-1 (parity only, not timed)."""
+    import pyoracle as O
+    n = int(max(1, min(n, batch.offsets.size - 1)))
+    O.set_threads(threads)
+    try:
+        m = O.Map(world.grid, world.resolution, world.offset)
+        res = O.scan_matchers_batch(m, batch.points_cells[:batch.offsets[n]], batch.offsets[:n + 1], levels,
+                                    batch.init_poses[:n], np.tile(np.eye(3).reshape(1, 9), (n, 1)))
+    finally:
+        O.set_threads(1)
+    return n, res
+
+
+def _beams_summed(offsets, use_point_size: int) -> dict:
+    """Beams GetResponse sums per candidate (correlate_scan_matcher.h:561-566):
+    N < 2U -> every point, else every (N / (U - 1))-th. The scans keep only
+    in-range beams (roborts_slam_node.cpp:300), so N varies per scan."""
+    n = np.diff(np.asarray(offsets, dtype=np.int64))
+    u = int(use_point_size)
+    step = np.where(n < 2 * u, 1, n // max(1, u - 1))
+    b = -(-n // np.maximum(step, 1))
+    return {"mean": float(np.mean(b)), "max": int(np.max(b)), "use_point_size": u,
+            "laser_beams": 1081}
 
 
 def _window_cands(p) -> int:
@@ -634,6 +681,9 @@ def main():
     ap.add_argument("--lc-steps", type=int, default=20, help="config-3 leg: timed queries")
     ap.add_argument("--lc-timeout", type=float, default=240.0, help="config-3 leg: the child's time limit (s)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--parity-scans", type=int, default=256,
+                    help="config2: scans each rank checks against the oracle when no cpu_baseline runs "
+                         "(N > 1 or --no-cpu)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-scan latency probe (profiling runs: keeps rocprof "
@@ -722,18 +772,19 @@ def main():
     sets = [(np.empty_like(poses0), np.empty_like(covs0), np.zeros(args.scans)) for _ in range(2)]
     k_step = [0]
 
-    def step():
+    def step(lv=levels):
+        """One whole batch; returns its (scores, poses, covs), final after settle()."""
         if args.sync_steps:
             np.copyto(poses_w, poses0)
             np.copyto(covs_w, covs0)
-            ctx.scan_matchers_loaded(levels, poses_w, covs_w)
-            return poses_w
+            sc = ctx.scan_matchers_loaded(lv, poses_w, covs_w)
+            return sc, poses_w, covs_w
         p, c, sc = sets[k_step[0] % 2]
         k_step[0] += 1
         np.copyto(p, poses0)
         np.copyto(c, covs0)
-        ctx.scan_matchers_submit(levels, p, c, sc)
-        return p
+        ctx.scan_matchers_submit(lv, p, c, sc)
+        return sc, p, c
 
     def settle():  # the last submitted step completes
         if not args.sync_steps:
@@ -745,21 +796,28 @@ def main():
         if torch.cuda.is_available():
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step()
-    settle()
-    # HIP events around every launch feed the live roofline below; the A/B knob
-    # CSM_BENCH_NO_EVENTS=1 leaves them out to price their overhead
-    ctx.set_profiling(os.environ.get("CSM_BENCH_NO_EVENTS") != "1")
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        poses = step()
-    settle()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    stats = ctx.kernel_stats()
-    ctx.set_profiling(False)
+    def timed(lv, warmup, steps, events=True):
+        """warmup untimed steps, then exactly `steps` timed ones between
+        barriers; returns (elapsed s, kernel stats, last step's outputs)."""
+        for _ in range(warmup):
+            step(lv)
+        settle()
+        # HIP events around every launch feed the live roofline below
+        ctx.set_profiling(events)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = step(lv)
+        settle()
+        barrier()
+        el = time.perf_counter() - t0
+        st = ctx.kernel_stats()
+        ctx.set_profiling(False)
+        return el, st, tuple(np.array(a, copy=True) for a in res)
+
+    # the A/B knob CSM_BENCH_NO_EVENTS=1 leaves the HIP events out to price their overhead
+    elapsed, stats, final = timed(levels, args.warmup, args.steps, os.environ.get("CSM_BENCH_NO_EVENTS") != "1")
+    poses = final[1]
     poses_resident = poses.copy()
 
     per_scan = sum(_window_cands(l) for l in levels)
@@ -810,7 +868,7 @@ def main():
                     ctx.load_scans_async(pins[(i + 1) % 2].array, batch.offsets)
                 res = step()
             settle()
-            return res
+            return res[1]
 
         run_host(max(2, min(args.warmup, 10)))
         barrier()
@@ -834,33 +892,56 @@ def main():
         for p in pins:
             p.close()
 
-    # the reference-default beam rule next to the headline: sim-YAML U=100 -> B=109
+    # the reference-default beam rule next to the headline: sim-YAML U=100 ->
+    # B=109, driven exactly as the headline (submitted batches, HIP events)
     b109 = None
     if args.levels == "headline" and not args.no_b109:
-        def step109():
-            p, c = poses0.copy(), covs0.copy()
-            ctx.scan_matchers_loaded(SIM_YAML_LEVELS, p, c)
-        for _ in range(args.warmup):
-            step109()
-        barrier()
-        t = time.perf_counter()
-        for _ in range(args.steps):
-            step109()
-        barrier()
-        e109 = time.perf_counter() - t
+        e109, stats109, final109 = timed(SIM_YAML_LEVELS, args.warmup, args.steps)
         if dist is not None:
             e = torch.tensor([e109], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
             dist.all_reduce(e, op=dist.ReduceOp.MAX)
             e109 = float(e.item())
         ps = sum(_window_cands(l) for l in SIM_YAML_LEVELS)
         b109 = {"value": world_size * args.scans * ps * args.steps / e109, "unit": "scorings/s",
-                "ms_per_step": e109 / args.steps * 1e3, "beams_summed": 109,
-                "levels": "sim YAML (U=100 at every level: B=109)"}
+                "ms_per_step": e109 / args.steps * 1e3, "beams_summed": _beams_summed(batch.offsets, 100),
+                "levels": "sim YAML (U=100 at every level: B=109)",
+                "batches": "submitted back to back, as the headline"}
+
+    # parity of the timed configuration itself: every rank checks its own
+    # batch's last timed step against the oracle (rank 0 at N = 1 on the
+    # cpu_baseline samples, which run anyway; otherwise a bounded sample)
+    runs, runs109 = [], []
+    cpu = cpu_all = cpu109 = None
+    if rank == 0 and world_size == 1 and not args.no_cpu:
+        cpu = cpu_baseline(world, batch, levels, args.cpu_seconds, collect=runs)
+        cpu_all = cpu_baseline(world, batch, levels, args.cpu_seconds / 2, threads=_host_threads(), collect=runs)
+        if b109 is not None:
+            cpu109 = cpu_baseline(world, batch, SIM_YAML_LEVELS, args.cpu_seconds / 2,
+                                  label="B=109 (sim YAML, U=100): ", collect=runs109)
+    else:
+        th = max(1, _host_threads() // int(os.environ.get("LOCAL_WORLD_SIZE", world_size)))
+        runs.append(oracle_sample(world, batch, levels, args.parity_scans, th))
+        if b109 is not None:
+            runs109.append(oracle_sample(world, batch, SIM_YAML_LEVELS, args.parity_scans, th))
+    parity = parity_check(final, runs, "headline (B=1081)")
+    parity109 = parity_check(final109, runs109, "B=109") if b109 is not None else None
+    if dist is not None:  # summed over ranks: each checked its own scans
+        for d in (parity, parity109):
+            if d is None:
+                continue
+            t = torch.tensor([d["scans_checked"], d["mismatches"]], dtype=torch.float64,
+                             device="cuda" if torch.cuda.is_available() else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            d["scans_checked"], d["mismatches"] = int(t[0].item()), int(t[1].item())
+            d["ranks"] = world_size
+    failed = parity["mismatches"] > 0 or (parity109 is not None and parity109["mismatches"] > 0)
 
     if rank != 0:
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
+        if failed:
+            sys.exit(1)
         return
 
     if os.environ.get("CSM_BENCH_NO_EVENTS") == "1":  # A/B of the event overhead only: no roofline
@@ -893,7 +974,7 @@ def main():
             "workload": "config2: 1081-beam scans vs 2000x2000 @5cm fp32 grid, full 3-level "
                         "coarse->fine->super-fine (sim-YAML windows 5070+1331+189 candidates/scan)",
             "levels": args.levels,
-            "beams_summed": 1081 if args.levels == "headline" else 109,
+            "beams_summed": _beams_summed(batch.offsets, levels[0].use_point_size),
             "scans_per_gpu": args.scans,
             "scorings_per_scan": per_scan,
             "parallelism": f"replicas x{world_size} (scan-sharded, no collective)",
@@ -914,25 +995,26 @@ def main():
     out["h2d_ms"] = h2d_ms
     if host_inputs is not None:
         out["value_host_inputs"] = host_inputs
+    out["parity"] = parity
     if b109 is not None:
+        b109["parity"] = parity109
+        if cpu109 is not None:
+            b109["cpu_baseline"] = cpu109
         out["b109"] = b109
-    if not args.no_cpu and world_size == 1:
-        out["cpu_baseline"] = cpu_baseline(world, batch, levels, args.cpu_seconds)
-        th = _host_threads()
-        out["cpu_baseline_all_cores"] = cpu_baseline(world, batch, levels, args.cpu_seconds / 2, threads=th)
-        if b109 is not None:
-            b109["cpu_baseline"] = cpu_baseline(world, batch, SIM_YAML_LEVELS, args.cpu_seconds / 2,
-                                                label="B=109 (sim YAML, U=100): ")
-    else:
-        out["cpu_baseline"] = None
+    out["cpu_baseline"] = cpu
+    if cpu_all is not None:
+        out["cpu_baseline_all_cores"] = cpu_all
     if leg is not None:
         out["loop_closure_rccl"] = leg
     out["world"] = world_info(dist)
     out["build"] = build_info()
     print(json.dumps(out))
+    sys.stdout.flush()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if failed:
+        sys.exit("bench.py: the timed configuration's outputs differ from the oracle's (parity.mismatches)")
 
 
 if __name__ == "__main__":

@@ -209,7 +209,10 @@ int csm_scan_matchers_batch(csm_ctx* ctx, int32_t n_scans, const double* points_
 /* Device-resident scan sets: csm_load_scans uploads a batch of scans once;
  * csm_scan_matchers_loaded runs the 3-level driver over it (poses/covs/scores
  * as in csm_scan_matchers_batch). Any other call that takes host points
- * replaces the loaded set. */
+ * replaces the loaded set. csm_load_scans, and the calls built on it
+ * (csm_scan_matchers, csm_scan_matchers_batch, the *_grids forms), drop the
+ * batches queued with csm_load_scans_async: the batch they load is the one
+ * that is matched. */
 int csm_load_scans(csm_ctx* ctx, int32_t n_scans, const double* points_xy,
                    const int64_t* point_offsets);
 int csm_scan_matchers_loaded(csm_ctx* ctx, const csm_param levels[3], int32_t use_fine,
@@ -242,6 +245,32 @@ int csm_scan_matchers_wait(csm_ctx* ctx);
 /* Pinned (page-locked) host memory for csm_load_scans_async inputs. */
 int csm_host_alloc(size_t bytes, void** out);
 int csm_host_free(void* p);
+
+/* --- host placement (one process per GPU) -------------------- */
+/* A context's host worker pool (window planning and completion) runs on a
+ * slice of the CPUs near its GPU: the process's affinity mask intersected with
+ * the GPU's NUMA node, split into disjoint slices among the local ranks whose
+ * GPUs share that node, and as many threads as the rank's share of the
+ * cgroup's CPU quota allows (quota / local ranks, at most 16). csm_create takes
+ * the local rank and count from LOCAL_RANK / LOCAL_WORLD_SIZE (torchrun,
+ * bench.py), rank r driving device r; CSM_HOST_THREADS overrides the count.
+ * No reference counterpart: the reference matches on one host thread. */
+#define CSM_HOST_PLAN_MAX_CPUS 512
+typedef struct csm_host_plan {
+  int32_t threads;        /* pool size, the calling thread included */
+  int32_t numa_node;      /* the GPU's NUMA node, -1 unknown */
+  int32_t quota_cpus;     /* the cgroup's CPU quota in whole CPUs, -1 none */
+  int32_t affinity_cpus;  /* CPUs in the process's affinity mask */
+  int32_t n_cpus;         /* CPUs the pool's workers are pinned to (0: not pinned) */
+  int32_t cpus[CSM_HOST_PLAN_MAX_CPUS];
+} csm_host_plan;
+/* The plan of local rank local_rank of local_world on this host, without a
+ * GPU: numa_of_rank[r] is rank r's GPU NUMA node (-1 unknown; null: all
+ * unknown), quota_cpus 0 reads the cgroup, -1 means none, > 0 is taken as is. */
+int csm_host_plan_compute(int32_t local_rank, int32_t local_world, const int32_t* numa_of_rank,
+                          int32_t quota_cpus, csm_host_plan* out);
+/* The plan a context runs with. */
+int csm_get_host_plan(csm_ctx* ctx, csm_host_plan* out);
 
 /* --- Gauss-Newton scan matcher ---------------------- */
 /* OptimizeScanMatchParam (optimize_scan_matcher.h:33-58), filled by

@@ -703,6 +703,38 @@ int match_levels_pipelined(csm_ctx* c, int32_t n_scans, const int64_t* offsets, 
   return CSM_OK;
 }
 
+// Batches queued with csm_load_scans_async are dropped (their uploads are
+// waited for): a synchronous load names the batch the next match runs, so
+// csm_scan_matchers / csm_scan_matchers_batch never match a queued batch
+// into output arrays sized for their own scans.
+int drop_staged(csm_ctx* c) {
+  if (c->staged_count <= 0) return CSM_OK;
+  hipError_t e;
+  if (c->stage_stream && (e = hipStreamSynchronize(c->stage_stream)) != hipSuccess)
+    return c->hip_fail(e, "hipStreamSynchronize(stage)");
+  c->staged_count = 0;
+  return CSM_OK;
+}
+
+// csm_load_scans once locked.
+int load_scans_locked(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets) {
+  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
+  int st;
+  c->loaded_n = -1;
+  c->loaded_grid.clear();
+  if ((st = drop_staged(c)) != CSM_OK) return st;
+  if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
+  const int64_t n_total = n_scans > 0 ? offsets[n_scans] - offsets[0] : 0;
+  if ((st = check_points(c, pts, n_total)) != CSM_OK) return st;
+  c->loaded_off.assign(offsets, offsets + n_scans + 1);
+  for (auto& o : c->loaded_off) o -= offsets[0];
+  if ((st = upload_points(c, n_total > 0 ? pts + 2 * offsets[0] : pts, n_total)) != CSM_OK) return st;
+  hipError_t e;
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(points)");
+  c->loaded_n = n_scans;
+  return CSM_OK;
+}
+
 }  // namespace csmh
 
 using namespace csmh;
@@ -740,20 +772,7 @@ int csm_load_scans(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t
   if (!c) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
-  int st;
-  c->loaded_n = -1;
-  c->loaded_grid.clear();
-  if ((st = check_offsets(c, n_scans, offsets)) != CSM_OK) return st;
-  const int64_t n_total = n_scans > 0 ? offsets[n_scans] - offsets[0] : 0;
-  if ((st = check_points(c, pts, n_total)) != CSM_OK) return st;
-  c->loaded_off.assign(offsets, offsets + n_scans + 1);
-  for (auto& o : c->loaded_off) o -= offsets[0];
-  if ((st = upload_points(c, n_total > 0 ? pts + 2 * offsets[0] : pts, n_total)) != CSM_OK) return st;
-  hipError_t e;
-  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return c->hip_fail(e, "hipStreamSynchronize(points)");
-  c->loaded_n = n_scans;
-  return CSM_OK;
+  return load_scans_locked(c, n_scans, pts, offsets);
 }
 
 int csm_load_scans_async(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets) {
@@ -839,6 +858,10 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
   // in a staging slot, its last launch below borrows them back, and the next
   // upload into that slot comes after this call, which completes the pending
   // batch (its completion reads no points or offsets).
+  // (checked before the swap: an early return after it would leave a pending
+  // batch's last hand-off to launch on the new batch's points)
+  if (c->staged_count == 0 && c->loaded_n < 0) return c->fail(CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)");
+  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
   int parked = -1;
   double parked_maxabs = 0.0;
   if (c->staged_count > 0) {
@@ -859,8 +882,6 @@ int csm_scan_matchers_submit(csm_ctx* c, const csm_param levels[3], int32_t use_
     }
     return r;
   };
-  if (c->loaded_n < 0) return c->fail(CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)");
-  if (!c->has_grid) return c->fail(CSM_ERR_NO_GRID, "no grid set");
   const int32_t n_scans = c->loaded_n;
   const int n_levels = use_fine ? 3 : 1;
   bool fast = false;
@@ -971,9 +992,11 @@ int csm_scan_matchers_batch(csm_ctx* c, int32_t n_scans, const double* pts, cons
                             const csm_param levels[3], int32_t use_fine, double* poses, double* covs,
                             double* scores) {
   if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
-  const int st = csm_load_scans(c, n_scans, pts, offsets);
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const int st = load_scans_locked(c, n_scans, pts, offsets);
   if (st != CSM_OK) return st;
-  return csm_scan_matchers_loaded(c, levels, use_fine, poses, covs, scores);
+  return matchers_loaded_locked(c, levels, use_fine, poses, covs, scores);
 }
 
 int csm_scan_matchers(csm_ctx* c, const double* pts, int32_t n_points, const csm_param levels[3],
@@ -986,10 +1009,11 @@ int csm_scan_matchers(csm_ctx* c, const double* pts, int32_t n_points, const csm
 
 int csm_load_scans_grids(csm_ctx* c, int32_t n_scans, const double* pts, const int64_t* offsets,
                          const int32_t* grid_index) {
-  int st = csm_load_scans(c, n_scans, pts, offsets);
-  if (st != CSM_OK || !grid_index) return st;
+  if (!c) return CSM_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  if (const int dst = pipe_drain(c)) return dst;  // a submitted batch still reads the context
+  DeviceGuard g(c->device);
+  const int st = load_scans_locked(c, n_scans, pts, offsets);
+  if (st != CSM_OK || !grid_index) return st;
   c->loaded_grid.assign(grid_index, grid_index + n_scans);
   return CSM_OK;
 }
@@ -998,9 +1022,12 @@ int csm_scan_matchers_batch_grids(csm_ctx* c, int32_t n_scans, const double* pts
                                   const int32_t* grid_index, const csm_param levels[3], int32_t use_fine,
                                   double* poses, double* covs, double* scores) {
   if (!c || !levels || !poses || !covs || !scores) return CSM_ERR_INVALID_ARG;
-  const int st = csm_load_scans_grids(c, n_scans, pts, offsets, grid_index);
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int st = load_scans_locked(c, n_scans, pts, offsets);
   if (st != CSM_OK) return st;
-  return csm_scan_matchers_loaded(c, levels, use_fine, poses, covs, scores);
+  if (grid_index) c->loaded_grid.assign(grid_index, grid_index + n_scans);
+  return matchers_loaded_locked(c, levels, use_fine, poses, covs, scores);
 }
 
 }  // extern "C"

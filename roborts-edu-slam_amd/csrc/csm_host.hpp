@@ -187,6 +187,11 @@ uint32_t seal_writer(const csm::FinishOut* src, int32_t tag);
 double complete_window(const csm::FinishOut& o, const CandGeom& C, const csm_param& P,
                        const Geometry& G, double pose[3], double cov[9], int skip_lists = 0);
 
+// csm_placement.cpp
+void pin_to_plan(const csm_host_plan& p);
+void context_host_plan(int device, int rank, int world, csm_host_plan* out);
+int create_context(int device, int local_rank, int local_world, csm_ctx** out);
+
 // Persistent worker pool for the per-window host work (angle tables before a
 // launch, completion after it). Workers sleep on a condition variable between
 // jobs; the calling thread works too and returns as soon as every item is done,
@@ -199,9 +204,8 @@ double complete_window(const csm::FinishOut& o, const CandGeom& C, const csm_par
 // touches the finished job.
 class ThreadPool {
  public:
-  ThreadPool(int threads, int spin_us) : n_threads_(std::max(1, threads)), spin_us_(std::max(0, spin_us)) {
-    if (const char* e = std::getenv("CSM_POOL_CHUNK_DIV")) chunk_div_ = std::max(1, std::atoi(e));
-  }
+  // workers pinned to the plan's CPUs (csm_placement.cpp; the caller's thread is not)
+  ThreadPool(int threads, const csm_host_plan& plan) : n_threads_(std::max(1, threads)), plan_(plan) {}
   ~ThreadPool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -284,17 +288,11 @@ class ThreadPool {
     wanted_ = want;
   }
   void loop(int id) {
+    pin_to_plan(plan_);
     uint64_t seen = 0;
     for (;;) {
       const std::function<void(int)>* job = nullptr;
       int n = 0, chunk = 1;
-      if (spin_us_ > 0) {  // optional: stay awake for the next job a while
-        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
-        for (int k = 1; epoch_.load(std::memory_order_acquire) == seen; ++k) {
-          __builtin_ia32_pause();
-          if ((k & 255) == 0 && std::chrono::steady_clock::now() > until) break;
-        }
-      }
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return stop_ || (epoch_.load() != seen && id < wanted_); });
@@ -307,8 +305,9 @@ class ThreadPool {
       drain(*job, n, chunk, (uint32_t)seen, true);
     }
   }
-  int n_threads_, spin_us_;
-  int chunk_div_ = 8;  // chunks per thread and job (CSM_POOL_CHUNK_DIV)
+  int n_threads_;
+  csm_host_plan plan_;
+  static constexpr int chunk_div_ = 8;  // chunks per thread and job
   std::vector<std::thread> workers_;
   std::mutex mu_;
   std::condition_variable cv_;
@@ -380,11 +379,12 @@ struct csm_ctx {
   std::mutex mu;
   std::string err;
   float outside = 0.3f;  // kMapUnknownCellProb (slam/slam_processor.h:264)
-  int host_threads = 1, pool_spin_us = 0;
+  int host_threads = 1;
+  csm_host_plan host_plan{};  // where the pool runs (csm_placement.cpp)
   std::unique_ptr<csmh::ThreadPool> pool;
   template <class F>
   void parallel_for(int n, int threads, F&& fn) {
-    if (!pool) pool.reset(new csmh::ThreadPool(host_threads, pool_spin_us));
+    if (!pool) pool.reset(new csmh::ThreadPool(host_threads, host_plan));
     pool->run(n, threads, std::forward<F>(fn));
   }
 

@@ -252,6 +252,7 @@ class Context:
         p = _as_param(param)
         resp = C.c_double(0.0)
         am = C.c_int64(-1)
+        self._loaded = None  # host points replace the loaded set (include/csm.h)
         self._check(_lib.csm_scan_match(self._h, _dptr(pts), pts.shape[0], C.byref(p), _dptr(pose),
                                         _dptr(cov), C.byref(resp), C.byref(am)))
         return (resp.value, am.value) if return_argmax else resp.value
@@ -260,6 +261,8 @@ class Context:
         pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
         lv = (CsmParam * 3)(*[_as_param(l) for l in levels])
         sc = C.c_double(0.0)
+        self.__dict__.pop("_queued", None)  # csm_scan_matchers loads: queued batches are dropped
+        self._loaded = (pts, np.array([0, pts.shape[0]], dtype=np.int64))  # it is the loaded set now
         self._check(_lib.csm_scan_matchers(self._h, _dptr(pts), pts.shape[0], lv, 1 if use_fine else 0,
                                            _dptr(pose), _dptr(cov), C.byref(sc)))
         return sc.value
@@ -274,6 +277,7 @@ class Context:
         resp = np.zeros(n)
         am = np.full(n, -1, dtype=np.int64)
         p = _as_param(param)
+        self._loaded = None  # host points replace the loaded set (include/csm.h)
         self._check(_lib.csm_scan_match_batch(self._h, n, _dptr(pts), _i64ptr(off), C.byref(p),
                                               _dptr(poses), _dptr(covs), _dptr(resp), _i64ptr(am)))
         return resp, am
@@ -286,6 +290,8 @@ class Context:
         assert covs.dtype == np.float64 and covs.flags.c_contiguous and covs.size == 9 * n
         scores = np.zeros(n)
         lv = (CsmParam * 3)(*[_as_param(l) for l in levels])
+        self.__dict__.pop("_queued", None)  # a synchronous load: queued batches are dropped
+        self._loaded = (pts, off)  # it is the loaded set now
         self._check(_lib.csm_scan_matchers_batch(self._h, n, _dptr(pts), _i64ptr(off), lv,
                                                  1 if use_fine else 0, _dptr(poses), _dptr(covs),
                                                  _dptr(scores)))
@@ -296,23 +302,32 @@ class Context:
         pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 2)
         off = np.ascontiguousarray(offsets, dtype=np.int64)
         self._loaded = (pts, off)
+        self.__dict__.pop("_queued", None)  # the library drops queued batches too
         self._check(_lib.csm_load_scans(self._h, off.size - 1, _dptr(pts), _i64ptr(off)))
 
     def load_scans_async(self, points, offsets):
         """Queue a batch (csm_load_scans_async): its upload runs beside the
-        current match; the next scan_matchers_loaded takes it. `points` should
-        be pinned (pinned_empty) and must not change until then."""
+        current match; the next scan_matchers_loaded / scan_matchers_submit
+        takes it (load_scans, scan_matchers and scan_matchers_batch drop it).
+        `points` should be pinned (a PinnedArray's array) and must not change
+        until then; the arrays are kept referenced here meanwhile."""
         pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 2)
         off = np.ascontiguousarray(offsets, dtype=np.int64)
         q = self.__dict__.setdefault("_queued", [])
         self._check(_lib.csm_load_scans_async(self._h, off.size - 1, _dptr(pts), _i64ptr(off)))
         q.append((pts, off))
 
-    def scan_matchers_loaded(self, levels, poses, covs, use_fine: bool = True):
+    def _take_loaded(self) -> int:
+        """The scan count of the batch the next loaded / submitted match runs."""
         q = self.__dict__.get("_queued")
         if q:  # the library takes the oldest queued batch
             self._loaded = q.pop(0)
-        n = self._loaded[1].size - 1
+        if self.__dict__.get("_loaded") is None:
+            raise CsmError(_abi.CSM_ERR_INVALID_ARG, "no scans loaded (csm_load_scans)")
+        return self._loaded[1].size - 1
+
+    def scan_matchers_loaded(self, levels, poses, covs, use_fine: bool = True):
+        n = self._take_loaded()
         assert poses.dtype == np.float64 and poses.flags.c_contiguous and poses.size == 3 * n
         assert covs.dtype == np.float64 and covs.flags.c_contiguous and covs.size == 9 * n
         scores = np.zeros(n)
@@ -328,10 +343,7 @@ class Context:
         and must stay alive until then (they are kept referenced here). The
         oldest queued batch (load_scans_async) is taken first, as by
         scan_matchers_loaded, without completing the pending one."""
-        q = self.__dict__.get("_queued")
-        if q:
-            self._loaded = q.pop(0)
-        n = self._loaded[1].size - 1
+        n = self._take_loaded()
         for a, k in ((poses, 3), (covs, 9), (scores, 1)):
             assert a.dtype == np.float64 and a.flags.c_contiguous and a.size == k * n
         lv = (CsmParam * 3)(*[_as_param(l) for l in levels])
@@ -383,6 +395,12 @@ class Context:
         out = np.empty(k.size, dtype=np.int64)
         self._check(_lib.csm_sort_order(self._h, _dptr(k), k.size, _i64ptr(out)))
         return out
+
+    def host_plan(self) -> dict:
+        """csm_get_host_plan: the CPUs and thread count of this context's pool."""
+        p = _abi.CsmHostPlan()
+        self._check(_lib.csm_get_host_plan(self._h, C.byref(p)))
+        return p.as_dict()
 
     def set_profiling(self, on: bool = True):
         self._check(_lib.csm_set_profiling(self._h, 1 if on else 0))
@@ -463,31 +481,58 @@ class Context:
         return b, int(w.value), stats
 
 
+class _PinnedBlock:
+    """One csm_host_alloc allocation, freed when the last array over it dies."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        if _lib.csm_host_alloc(max(1, nbytes), C.byref(p)) != 0:
+            raise MemoryError("csm_host_alloc failed")
+        self.p = p
+
+    def __del__(self):
+        try:
+            if self.p is not None and self.p.value:
+                _lib.csm_host_free(self.p)
+            self.p = None
+        except Exception:
+            pass
+
+
 class PinnedArray:
     """A numpy array over pinned host memory (csm_host_alloc), for
-    load_scans_async inputs; freed with the object."""
+    load_scans_async inputs. The allocation belongs to the array's buffer
+    (``array.base``), so it lives as long as any view of it does: close()
+    only drops this object's reference."""
 
     def __init__(self, shape, dtype=np.float64):
         self.dtype = np.dtype(dtype)
         n = int(np.prod(shape))
-        p = C.c_void_p()
-        if _lib.csm_host_alloc(max(1, n) * self.dtype.itemsize, C.byref(p)) != 0:
-            raise MemoryError("csm_host_alloc failed")
-        self._p = p
-        buf = (C.c_char * (max(1, n) * self.dtype.itemsize)).from_address(p.value)
+        nbytes = max(1, n) * self.dtype.itemsize
+        block = _PinnedBlock(nbytes)
+        buf = (C.c_char * nbytes).from_address(block.p.value)
+        buf._block = block  # the numpy array's base keeps the allocation alive
         self.array = np.frombuffer(buf, dtype=self.dtype, count=n).reshape(shape)
 
     def close(self):
-        if getattr(self, "_p", None) is not None and self._p.value:
-            self.array = None
-            _lib.csm_host_free(self._p)
-            self._p = None
+        self.array = None
 
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+
+def host_plan(local_rank: int, local_world: int, numa_of_rank=None, quota_cpus: int = 0) -> dict:
+    """csm_host_plan_compute (no GPU needed): the pool a context of local rank
+    `local_rank` of `local_world` would get. numa_of_rank: each local rank's
+    GPU NUMA node (None: unknown); quota_cpus: 0 reads the cgroup, -1 none."""
+    p = _abi.CsmHostPlan()
+    arr = None
+    if numa_of_rank is not None:
+        arr = np.ascontiguousarray(numa_of_rank, dtype=np.int32)
+        assert arr.size == local_world
+    st = _lib.csm_host_plan_compute(int(local_rank), int(local_world),
+                                    None if arr is None else arr.ctypes.data_as(_abi._i32p), int(quota_cpus),
+                                    C.byref(p))
+    if st != _abi.CSM_OK:
+        raise CsmError(st, "csm_host_plan_compute: invalid rank / world")
+    return p.as_dict()
 
 
 def build_digest() -> str:

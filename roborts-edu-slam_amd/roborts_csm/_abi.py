@@ -32,7 +32,7 @@ EXPORTED = (
     "csm_set_profiling", "csm_kernel_stats", "csm_sort_order", "csm_phase_buckets",
     "csm_set_grid_stack", "csm_best_windows", "csm_optimize_scan_match", "csm_optimize_scan_match_batch",
     "csm_optimize_update_cost", "csm_load_scans_grids", "csm_scan_matchers_batch_grids",
-    "csm_search_windows",
+    "csm_search_windows", "csm_host_plan_compute", "csm_get_host_plan",
     # include/csm_gridmap.h
     "csm_gridmap_create", "csm_gridmap_destroy", "csm_gridmap_last_error",
     "csm_gridmap_set_options", "csm_gridmap_set_cell_params", "csm_gridmap_set_map_offset",
@@ -116,6 +116,25 @@ class CsmSearchStats(C.Structure):
         ("top_box", C.c_int32),
         ("reserved", C.c_int32),
     ]
+
+
+CSM_HOST_PLAN_MAX_CPUS = 512
+
+
+class CsmHostPlan(C.Structure):
+    """csm_host_plan (include/csm.h): where a context's host worker pool runs."""
+    _fields_ = [
+        ("threads", C.c_int32),
+        ("numa_node", C.c_int32),
+        ("quota_cpus", C.c_int32),
+        ("affinity_cpus", C.c_int32),
+        ("n_cpus", C.c_int32),
+        ("cpus", C.c_int32 * CSM_HOST_PLAN_MAX_CPUS),
+    ]
+
+    def as_dict(self) -> dict:
+        return {"threads": self.threads, "numa_node": self.numa_node, "quota_cpus": self.quota_cpus,
+                "affinity_cpus": self.affinity_cpus, "cpus": [int(c) for c in self.cpus[:self.n_cpus]]}
 
 
 class CsmLoopClosureResult(C.Structure):
@@ -225,6 +244,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_search_windows": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), C.c_int32, _i32p, _dp,
                                          C.POINTER(CsmSearchOptions), C.POINTER(CsmBest), _i32p,
                                          C.POINTER(CsmSearchStats)]),
+        "csm_host_plan_compute": (C.c_int, [C.c_int32, C.c_int32, _i32p, C.c_int32, C.POINTER(CsmHostPlan)]),
+        "csm_get_host_plan": (C.c_int, [_ctx, C.POINTER(CsmHostPlan)]),
         "csm_optimize_scan_match": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmOptimizeParam), _dp, _dp]),
         "csm_optimize_scan_match_batch": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, C.POINTER(CsmOptimizeParam), _dp,
                                                     _dp, _i32p]),

@@ -1073,3 +1073,179 @@ def test_submitted_batches_from_staged_scans(world2000, first_windows):
         c.close()
         for p in pins:
             p.close()
+
+
+def test_sync_entry_points_drop_queued_batches(world2000):
+    """A batch queued with csm_load_scans_async is dropped, not matched, by
+    the calls that load their own scans (csm_scan_matchers,
+    csm_scan_matchers_batch, csm_load_scans): each returns its own scans'
+    answers (the r04 driver handed them the queued batch's, written into
+    arrays sized for their own scans). A batch queued afterwards is still
+    taken by the next csm_scan_matchers_loaded."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    m = O.Map(w.grid, w.resolution, w.offset)
+    lv = headline_levels()
+    other = np.ascontiguousarray(b.points_cells * 0.98)
+    pin = roborts_csm.PinnedArray(other.shape)
+    np.copyto(pin.array, other)
+    c = roborts_csm.Context(0)
+    try:
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+        # one scan
+        c.load_scans_async(pin.array, b.offsets)
+        one = b.points_cells[b.offsets[0]:b.offsets[1]]
+        pose, cov = b.init_poses[0].copy(), np.eye(3).reshape(9).copy()
+        s = c.scan_matchers(one, lv, pose, cov)
+        s2, p2, c2 = O.scan_matchers(m, one, lv, b.init_poses[0], np.eye(3).reshape(9))
+        assert s == s2 and np.array_equal(pose, p2) and np.array_equal(cov, c2)
+        # a batch of 8
+        c.load_scans_async(pin.array, b.offsets)
+        c.load_scans_async(pin.array, b.offsets)
+        n = 8
+        sub = b.points_cells[:b.offsets[n]]
+        off = np.ascontiguousarray(b.offsets[:n + 1])
+        eye = np.tile(np.eye(3).reshape(1, 9), (n, 1))
+        poses = np.ascontiguousarray(b.init_poses[:n].copy())
+        covs = eye.copy()
+        s = c.scan_matchers_batch(sub, off, lv, poses, covs)
+        s2, p2, c2 = O.scan_matchers_batch(m, sub, off, lv, b.init_poses[:n], eye.copy())
+        assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2)
+        # csm_load_scans drops the queue too; the loaded call runs the loaded scans
+        c.load_scans_async(pin.array, b.offsets)
+        c.load_scans(sub, off)
+        poses, covs = np.ascontiguousarray(b.init_poses[:n].copy()), eye.copy()
+        s = c.scan_matchers_loaded(lv, poses, covs)
+        assert np.array_equal(s, s2) and np.array_equal(poses, p2) and np.array_equal(covs, c2)
+        # queued after the synchronous calls: taken
+        nb = b.init_poses.shape[0]
+        c.load_scans_async(pin.array, b.offsets)
+        poses, covs = np.ascontiguousarray(b.init_poses.copy()), np.tile(np.eye(3).reshape(1, 9), (nb, 1))
+        s = c.scan_matchers_loaded(lv, poses, covs)
+        s3, p3, c3 = O.scan_matchers_batch(m, other, b.offsets, lv, b.init_poses,
+                                           np.tile(np.eye(3).reshape(1, 9), (nb, 1)))
+        assert np.array_equal(s, s3) and np.array_equal(poses, p3) and np.array_equal(covs, c3)
+    finally:
+        c.close()
+        pin.close()
+
+
+def test_submitted_batches_of_varied_sizes(world2000):
+    """Queued batches of different scan counts submitted back to back, one
+    below CSM_PIPELINE (the synchronous fallback between pipelined submits,
+    which completes the pending batch on its parked points): every batch
+    equals its own synchronous load + match."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    env = {"CSM_PIPELINE": "16", "CSM_PIPELINE_PARTS": "2"}
+    os.environ.update(env)
+    try:
+        c = roborts_csm.Context(0)
+    finally:
+        for k in env:
+            del os.environ[k]
+    lv = headline_levels()
+    sizes, scales = (96, 40, 10, 96, 64, 17), (1.0, 0.98, 1.02, 0.99, 1.01, 0.97)
+    batches = []
+    for n, f in zip(sizes, scales):
+        off = np.ascontiguousarray(b.offsets[:n + 1])
+        batches.append((np.ascontiguousarray(b.points_cells[:b.offsets[n]] * f), off, n))
+    pins = []
+    try:
+        c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
+        want = []
+        for q, off, n in batches:
+            c.load_scans(q, off)
+            p, cv = b.init_poses[:n].copy(), np.tile(np.eye(3).reshape(1, 9), (n, 1))
+            want.append((c.scan_matchers_loaded(lv, p, cv), p, cv))
+        for q, _, _ in batches:
+            pins.append(roborts_csm.PinnedArray(q.shape))
+            np.copyto(pins[-1].array, q)
+        got = [(np.zeros(n), b.init_poses[:n].copy(), np.tile(np.eye(3).reshape(1, 9), (n, 1)))
+               for _, _, n in batches]
+        c.load_scans_async(pins[0].array, batches[0][1])
+        for k in range(len(batches)):
+            if k + 1 < len(batches):
+                c.load_scans_async(pins[k + 1].array, batches[k + 1][1])
+            c.scan_matchers_submit(lv, got[k][1], got[k][2], got[k][0])
+        c.scan_matchers_wait()
+        for k in range(len(batches)):
+            for a, e in zip(got[k], want[k]):
+                assert np.array_equal(a, e), (k, sizes[k])
+    finally:
+        c.close()
+        for p in pins:
+            p.close()
+
+
+@pytest.fixture(scope="module")
+def world2000_bench():
+    """The bench's own config-2 inputs: the seeded 2000 x 2000 world and
+    rank 0's 4096-scan batch (bench.py main)."""
+    from roborts_csm import worlds
+    w = worlds.make_world(2000, 2000, 0.05, seed=20261015)
+    b = worlds.make_scan_batch(w, 4096, seed=1000)
+    return w, b
+
+
+@pytest.mark.parametrize("quantised", [False, True])
+def test_timed_configuration_against_oracle(world2000_bench, quantised):
+    """The configuration bench.py times, with no CSM_* overrides: 4096 scans
+    (two parts of 2048 windows), batches queued from pinned host memory
+    (csm_load_scans_async) and submitted back to back with the library's
+    submitted-batch defaults (first coarse launch whole, 50/50 part split,
+    deferred last hand-off). Three different batches, each against the
+    oracle bit for bit (scores, poses, covariances); on the 3-value map
+    every level's exact pass has windows."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000_bench
+    grid = w.grid
+    if quantised:
+        grid = np.round(np.asarray(w.grid, dtype=np.float32) * 2.0).astype(np.float32) / np.float32(2.0)
+    assert not any(k.startswith("CSM_") for k in os.environ), "the defaults are under test"
+    lv = headline_levels()
+    n = b.init_poses.shape[0]
+    eye = np.tile(np.eye(3).reshape(1, 9), (n, 1))
+    rng = np.random.default_rng(11)
+    scans = [np.ascontiguousarray(b.points_cells * f) for f in (1.0, 0.995, 1.005)]
+    inits = [np.ascontiguousarray(b.init_poses + rng.uniform(-1, 1, size=(n, 3)) * [0.03, 0.03, 0.01])
+             for _ in scans]
+    m = O.Map(grid, w.resolution, w.offset)
+    O.set_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    try:
+        want = [O.scan_matchers_batch(m, q, b.offsets, lv, p0, eye.copy()) for q, p0 in zip(scans, inits)]
+    finally:
+        O.set_threads(1)
+    c = roborts_csm.Context(0)
+    pins = []
+    try:
+        c.set_grid(_map(grid, w.resolution, w.offset, version=1))
+        for q in scans:
+            pins.append(roborts_csm.PinnedArray(q.shape))
+            np.copyto(pins[-1].array, q)
+        got = [(np.zeros(n), p0.copy(), eye.copy()) for p0 in inits]
+        c.set_profiling(True)
+        c.load_scans_async(pins[0].array, b.offsets)
+        for k in range(len(scans)):
+            if k + 1 < len(scans):
+                c.load_scans_async(pins[k + 1].array, b.offsets)
+            c.scan_matchers_submit(lv, got[k][1], got[k][2], got[k][0])
+        c.scan_matchers_wait()
+        st = {k["name"]: k for k in c.kernel_stats()}
+        c.set_profiling(False)
+        for k in range(len(scans)):
+            s2, p2, c2 = want[k]
+            assert np.array_equal(got[k][0], s2), (k, int(np.sum(got[k][0] != s2)))
+            assert np.array_equal(got[k][1], p2), (k, int(np.sum(np.any(got[k][1] != p2, axis=1))))
+            assert np.array_equal(got[k][2], c2), (k, int(np.sum(np.any(got[k][2] != c2, axis=1))))
+        assert st["score_box_pair_kernel<13,all>"]["launches"] >= 2 * len(scans), st.keys()
+        if quantised:
+            ex = [k for nm, k in st.items() if nm.startswith("finish:exact_windows<")]
+            assert len(ex) == 3 and all(k["scorings"] > 0 for k in ex), ex
+    finally:
+        c.close()
+        for p in pins:
+            p.close()
