@@ -604,6 +604,22 @@ def build_info() -> dict:
     return {"library_digest": lib, "source_digest": source_digest(), "match": lib == source_digest()}
 
 
+def host_plans(plan: dict, dist, torch) -> list:
+    """Every rank's host worker pool (csm_get_host_plan): threads, NUMA node
+    and the CPU slice it is pinned to, gathered to rank 0."""
+    cpus = plan["cpus"]
+    row = [plan["threads"], plan["numa_node"], len(cpus), min(cpus) if cpus else -1, max(cpus) if cpus else -1,
+           plan["quota_cpus"]]
+    rows = [row]
+    if dist is not None:
+        t = torch.tensor(row, dtype=torch.int64, device="cuda" if torch.cuda.is_available() else "cpu")
+        out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(out, t)
+        rows = [[int(v) for v in o.tolist()] for o in out]
+    return [{"rank": r, "threads": a, "numa_node": b, "n_cpus": c, "cpu_min": d, "cpu_max": e, "quota_cpus": f}
+            for r, (a, b, c, d, e, f) in enumerate(rows)]
+
+
 def world_info(dist) -> dict:
     """What actually ran: world size and backend of the process group."""
     if dist is None:
@@ -763,6 +779,7 @@ def main():
     ctx.load_scans(batch.points_cells, batch.offsets)
     poses0 = np.ascontiguousarray(batch.init_poses)
     covs0 = np.ascontiguousarray(np.tile(np.eye(3).reshape(1, 9), (args.scans, 1)))
+    host = host_plans(ctx.host_plan(), dist, torch)
 
     poses_w, covs_w = np.empty_like(poses0), np.empty_like(covs0)  # reset in place each step
     # submitted batches (csm_scan_matchers_submit): each step is one whole
@@ -1006,6 +1023,7 @@ def main():
         out["cpu_baseline_all_cores"] = cpu_all
     if leg is not None:
         out["loop_closure_rccl"] = leg
+    out["host_threads"] = host
     out["world"] = world_info(dist)
     out["build"] = build_info()
     print(json.dumps(out))

@@ -397,306 +397,6 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   box_epilogue<NS, BEST>(L, S, ae, wt, a, act, k, q, ox, oy, nsf, acc, out, partials);
 }
 
-// passes over the run list of the grouped kernel (rows per pass: ceil(NS / passes))
-#ifndef CSM_BOX_PASSES
-#define CSM_BOX_PASSES 2
-#endif
-constexpr int kBoxPasses = CSM_BOX_PASSES;
-
-// x from the lane `ctrl` names in the same 16-lane row (DPP row_ror), 64-bit.
-template <int CTRL>
-__device__ __forceinline__ int64_t row_ror64(int64_t x) {
-  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)x >> 32), CTRL, 0xF, 0xF, false);
-  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
-// v9 "grouped" box kernel (box rows of four 16-byte pieces: 13 <= NS <= 16).
-// The v6 kernel above gives one load instruction to one run: lanes (row k,
-// piece q), 52 of 64 busy at NS = 13, and the texture-address unit spends its
-// cycles on all 64 lanes' 16 bytes. Here one instruction serves 16 runs: lane
-// (run rr, piece q) loads row k of run rr's box, and the instruction index is
-// the row, so NS instructions cover 16 runs with every lane busy (13 per 16
-// runs instead of 16 at NS = 13, the same bytes and cache lines per run). The
-// row is uniform, so it is the scalar offset (k * pitch) and the run's corner
-// the vector offset; the per-lane count multiplies per lane. Each lane keeps
-// the integer sums of its piece for every row, NS x 4 int64, and the 16 lanes
-// of one piece add theirs up once at the end of the wave (integer sums: the
-// order is free). Loads run 8 instructions ahead across group boundaries.
-template <int NS, bool BEST>
-__global__ __launch_bounds__(64) void score_box_grouped_kernel(LevelWork L, const ScanWork* __restrict__ scans,
-                                                               const double2* __restrict__ pts,
-                                                               const AngleEntry* __restrict__ angles,
-                                                               double* __restrict__ out,
-                                                               BestPartial* __restrict__ partials) {
-  static_assert(NS >= 13 && NS <= 16, "four 16-byte pieces per box row");
-  constexpr int RG = 16;  // runs per group: lane = (run rr, piece q)
-  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
-  dev::clear_word(L);
-  const int wt = bid / L.n_angles;
-  const int a = bid - wt * L.n_angles;
-  int win = wt, ox = 0, oy = 0, nsf = NS;
-  if (L.tile_n > 0) {
-    const int tpw = L.tile_n * L.tile_n;
-    win = wt / tpw;
-    const int t = wt - win * tpw;
-    const int ti = t / L.tile_n;
-    nsf = L.tile_ns;
-    ox = min(ti * NS, nsf - NS);
-    oy = min((t - ti * L.tile_n) * NS, nsf - NS);
-  }
-  const ScanWork S = scans[win];
-  const AngleEntry ae = angles[S.angle_off + a];
-  const int lane = threadIdx.x;
-  const int q = lane & 3, rr = lane >> 2;
-  const int pitch4 = L.pitch * 4;
-  const BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, pitch4,
-                  L.size_y * pitch4 /* first of the zero rows */, S.x0 + ox * L.step_cells /* :569, j = ox */,
-                  S.y0 + oy * L.step_cells /* :572, k = oy */, 2, 0, 0, NS};
-  const int n_used = S.n_used;
-  const int zero_off = B.zero_off;
-  const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
-  const uint32_t glo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gi);
-  const uint32_t ghi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)gi >> 32));
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((uint64_t)ghi << 32) | glo), (short)0, (int)(L.gridi_stride * 4), 0x00020000);
-  auto load = [&](int voff, int row) { return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, row * pitch4, 0); };
-
-  uint64_t slow = 0;
-  constexpr int kScratch = kRunSeg + 64 + 2 * RG;
-  __shared__ int32_t run_off[kScratch + 64];
-  __shared__ uint8_t run_cnt[kScratch + 64];  // run lengths 1..64 (bytes: 6.6 KB of LDS per wave, not 10.5)
-  // lane (rr, q) ends with row k = rr: candidates (j = 4q .. 4q+3, k)
-  const int k = rr;
-  int64_t mine[4] = {0, 0, 0, 0};
-  // Rows [K0, K1) of every run in the list: the sums of those rows, one group
-  // of loads in flight (row k of the next group issued as row k of this one
-  // is summed), then the 16 lanes of each piece add theirs up and lane
-  // (rr = k, q) keeps row k. The rows go in two passes over the list so only
-  // half of the box's sums are live at a time (4 waves per SIMD, not 2).
-  auto pass = [&](const int K0, int npad) {
-    constexpr int KN = (NS + kBoxPasses - 1) / kBoxPasses;  // rows per pass (the last pass's may run out)
-    int64_t acc[KN][4];
-#pragma unroll
-    for (int kk = 0; kk < KN; ++kk)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[kk][t] = 0;
-    int voff = run_off[rr] + 16 * q;
-    int cnt = run_cnt[rr];
-    v4i b[KN];
-#pragma unroll
-    for (int kk = 0; kk < KN; ++kk)
-      if (K0 + kk < NS) b[kk] = load(voff, K0 + kk);  // (uniform test)
-    for (int g0 = 0; g0 < npad; g0 += RG) {
-      const int voff_n = run_off[g0 + RG + rr] + 16 * q;
-      const int cnt_n = run_cnt[g0 + RG + rr];
-#pragma unroll
-      for (int kk = 0; kk < KN; ++kk) {
-        if (K0 + kk < NS) {
-          v4i v = b[kk];
-          asm volatile("" : "+v"(v));  // consume row kk here, in order
-          acc[kk][0] += (int64_t)cnt * v.x;
-          acc[kk][1] += (int64_t)cnt * v.y;
-          acc[kk][2] += (int64_t)cnt * v.z;
-          acc[kk][3] += (int64_t)cnt * v.w;
-          asm volatile("" : "+v"(acc[kk][0]), "+v"(acc[kk][1]), "+v"(acc[kk][2]), "+v"(acc[kk][3]));
-          b[kk] = load(voff_n, K0 + kk);  // the next group's row
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      voff = voff_n;
-      cnt = cnt_n;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead loads past the list land
-#pragma unroll
-    for (int kk = 0; kk < KN; ++kk) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        int64_t x = acc[kk][t];
-        x += row_ror64<0x124>(x);  // row_ror:4 -- the 4 lanes of piece q in a 16-lane row
-        x += row_ror64<0x128>(x);  // row_ror:8
-        x += __shfl_xor(x, 16, 64);
-        x += __shfl_xor(x, 32, 64);
-        mine[t] += (k == K0 + kk) ? x : 0;
-      }
-      __builtin_amdgcn_sched_barrier(0);  // one row's chains at a time: few temporaries live
-    }
-  };
-  for (int s0 = 0; s0 < n_used; s0 += kRunSeg) {
-    const int nruns = B.build_runs(s0, min(n_used, s0 + kRunSeg), run_off, run_cnt, kScratch, slow);
-    // whole groups, then one group of empty runs (zero block, count 0) that
-    // the last group's look-ahead loads read
-    const int npad = (nruns + RG - 1) / RG * RG;
-    for (int i = nruns + lane; i < npad + RG; i += 64) {
-      run_off[i] = zero_off;
-      run_cnt[i] = 0;
-    }
-    __syncthreads();
-    if (npad > 0) {
-#pragma unroll 1
-      for (int k0 = 0; k0 < NS; k0 += (NS + kBoxPasses - 1) / kBoxPasses) pass(k0, npad);  // one copy of the code
-    }
-    __syncthreads();  // the next segment rewrites the list
-  }
-  slow_beams<NS>(B, L, gi, slow, k, q, ox, oy, mine);
-  box_epilogue<NS, BEST>(L, S, ae, wt, a, k < NS, k, q, ox, oy, nsf, mine, out, partials);
-}
-
-// v10 "palette" box kernel (n_space <= 13, r04). The v6/v9 kernels read
-// every run's box as 13 rows of 64 bytes of gridi: ~19 cache lines and ~20
-// texture-address cycles per run, the kernel's bound (TA 0.67-0.73). A
-// scan-match grid holds few distinct values (unknown, occupied and the blur
-// kernel's levels), so here the box is read from the palette copy of gridi:
-// one byte per cell, the index of the cell's value in the grid's palette
-// (L.pal_vals, at most kPalMax values, 0 = the outside value). A box row is
-// then 16 bytes: lane (run slot r, row k) loads row k of run r's box with one
-// buffer_load_dwordx4 at the corner's dword (4 runs per instruction, 13 of
-// 16 row lanes busy), shifts it by the corner's byte phase (v_alignbyte) and
-// adds count * palette[index] to its 13 candidates (j, k), the palette read
-// from LDS as doubles. Every product and partial sum is an integer below
-// 2^53 (|value| < 2^26, counts <= 1081), so the fp64 FMAs are exact and the
-// sums equal the int64 sums of the other kernels bit for bit; the four slots'
-// sums meet across lanes at the end, then the v6 epilogue (rejected beams
-// cell by cell from gridi, penalty, store) runs on the (row, piece) layout.
-#ifndef CSM_PAL_SEG
-#define CSM_PAL_SEG 576
-#endif
-constexpr int kPalSeg = CSM_PAL_SEG;  // beams per run-list segment (LDS: ~5.6 KB per wave with the palette)
-static_assert(kPalSeg % 64 == 0 && kPalSeg >= 512, "whole 64-beam chunks; the sums' transpose reuses the list");
-constexpr int kPalPD = 4;  // runs of one slot per step (their loads in flight during the previous step)
-
-template <int NS, bool BEST>
-__global__ __launch_bounds__(64) void score_box_palette_kernel(LevelWork L, const ScanWork* __restrict__ scans,
-                                                               const double2* __restrict__ pts,
-                                                               const AngleEntry* __restrict__ angles,
-                                                               double* __restrict__ out,
-                                                               BestPartial* __restrict__ partials) {
-  static_assert(NS >= 1 && NS <= kPalMaxSpace, "corner phase (<= 3) + NS cells within one 16-byte row piece");
-  static_assert(kPalPD == 4, "a slot's step: one ds_read_b128 of offsets, one dword of counts");
-  const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
-  dev::clear_word(L);
-  const int wt = bid / L.n_angles;
-  const int a = bid - wt * L.n_angles;
-  int win = wt, ox = 0, oy = 0, nsf = NS;
-  if (L.tile_n > 0) {
-    const int tpw = L.tile_n * L.tile_n;
-    win = wt / tpw;
-    const int t = wt - win * tpw;
-    const int ti = t / L.tile_n;
-    nsf = L.tile_ns;
-    ox = min(ti * NS, nsf - NS);
-    oy = min((t - ti * L.tile_n) * NS, nsf - NS);
-  }
-  const ScanWork S = scans[win];
-  const AngleEntry ae = angles[S.angle_off + a];
-  const int lane = threadIdx.x;
-  const int k = lane & 15, slot = lane >> 4;
-  const int rowb = L.pitch;  // palette bytes per row (= gridi cells per row)
-  const BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, rowb,
-                  L.size_y * rowb /* first of the zero rows */, S.x0 + ox * L.step_cells /* :569, j = ox */,
-                  S.y0 + oy * L.step_cells /* :572, k = oy */, 0, 0, 0, NS};
-  const int n_used = S.n_used;
-  const int zero_off = B.zero_off;
-  __shared__ double tab[kPalMax];
-  for (int i = lane; i < L.pal_n; i += 64) tab[i] = (double)L.pal_vals[i];
-  const uint8_t* pg = L.pal_grid + (int64_t)S.grid_index * L.pal_stride;
-  const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)pg);
-  const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)pg >> 32));
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((uint64_t)phi << 32) | plo), (short)0, (int)L.pal_stride, 0x00020000);
-  const int krow = k * rowb;
-  const uint32_t kmask = k < NS ? 0xFFFFFFFFu : 0u;  // rows past the box add nothing
-
-  double acc[NS];
-#pragma unroll
-  for (int j = 0; j < NS; ++j) acc[j] = 0.0;
-  uint64_t slow = 0;
-  constexpr int kStepRuns = 4 * kPalPD;  // runs per step: slot s takes runs [g + 4s, g + 4s + 4)
-  constexpr int kScratch = kPalSeg + 64 + 2 * kStepRuns;
-  __shared__ __attribute__((aligned(16))) int32_t run_off[kScratch + 64];
-  __shared__ __attribute__((aligned(16))) uint8_t run_cnt[kScratch + 64];
-  for (int s0 = 0; s0 < n_used; s0 += kPalSeg) {
-#if defined(CSM_PAL_DIAG) && CSM_PAL_DIAG >= 3  // timing diagnostic: no run lists either
-    const int nruns = 0;
-#else
-    const int nruns = B.build_runs(s0, min(n_used, s0 + kPalSeg), run_off, run_cnt, kScratch, slow);
-#endif
-    // whole steps, then one step of empty runs (zero block, count 0) that the
-    // look-ahead reads of the last step take
-    const int npad = (nruns + kStepRuns - 1) / kStepRuns * kStepRuns;
-    for (int i = nruns + lane; i < npad + kStepRuns; i += 64) {
-      run_off[i] = zero_off;
-      run_cnt[i] = 0;
-    }
-    __syncthreads();
-#if defined(CSM_PAL_DIAG) && CSM_PAL_DIAG >= 1  // timing diagnostic (wrong scores): the run lists only
-    if (false) {
-#else
-    if (npad > 0) {
-#endif
-      int4 offs = *reinterpret_cast<const int4*>(&run_off[4 * slot]);
-      uint32_t cnts = *reinterpret_cast<const uint32_t*>(&run_cnt[4 * slot]) & kmask;
-      v4i d[kPalPD];
-      d[0] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.x & ~3), 0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // issued in the order the loop consumes them
-      d[1] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.y & ~3), 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      d[2] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.z & ~3), 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      d[3] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.w & ~3), 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      for (int g = 0; g < npad; g += kStepRuns) {
-        // the next step's runs of this slot (the padding covers the last step's)
-        const int4 noffs = *reinterpret_cast<const int4*>(&run_off[g + kStepRuns + 4 * slot]);
-        const uint32_t ncnts = *reinterpret_cast<const uint32_t*>(&run_cnt[g + kStepRuns + 4 * slot]) & kmask;
-        const int cur[4] = {offs.x, offs.y, offs.z, offs.w};
-        const int nxt[4] = {noffs.x, noffs.y, noffs.z, noffs.w};
-#pragma unroll
-        for (int p = 0; p < kPalPD; ++p) {
-          // run p of the slot: its row shifted by the corner's byte phase; the
-          // register is then free for the next step's run p
-          const uint32_t sh = (uint32_t)cur[p] & 3u;
-          const uint32_t w[4] = {__builtin_amdgcn_alignbyte((uint32_t)d[p].y, (uint32_t)d[p].x, sh),
-                                 __builtin_amdgcn_alignbyte((uint32_t)d[p].z, (uint32_t)d[p].y, sh),
-                                 __builtin_amdgcn_alignbyte((uint32_t)d[p].w, (uint32_t)d[p].z, sh),
-                                 __builtin_amdgcn_alignbyte(0u, (uint32_t)d[p].w, sh)};
-          const double c = (double)((cnts >> (8 * p)) & 0xFFu);
-          d[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (nxt[p] & ~3), 0, 0);
-#pragma unroll
-          for (int j = 0; j < NS; ++j) acc[j] = __builtin_fma(c, tab[(w[j >> 2] >> (8 * (j & 3))) & 0xFF], acc[j]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        offs = noffs;
-        cnts = ncnts;
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead loads past the list land
-    }
-    __syncthreads();  // the next segment rewrites the list
-  }
-  // the four run slots of row k meet, then the sums go to the (row, piece)
-  // layout of the v6 epilogue through LDS (the run list's space)
-#pragma unroll
-  for (int j = 0; j < NS; ++j) {
-    acc[j] += __shfl_xor(acc[j], 16, 64);
-    acc[j] += __shfl_xor(acc[j], 32, 64);
-  }
-  int64_t* xch = reinterpret_cast<int64_t*>(run_off);
-  if (slot == 0 && k < NS) {
-#pragma unroll
-    for (int j = 0; j < NS; ++j) xch[k * 16 + j] = (int64_t)acc[j];
-  }
-  __syncthreads();
-  const int kk = lane >> 2, q = lane & 3;
-  int64_t mine[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) mine[t] = (kk < NS && 4 * q + t < NS) ? xch[kk * 16 + 4 * q + t] : 0;
-  const int32_t* gi = L.gridi + (int64_t)S.grid_index * L.gridi_stride;
-#if !(defined(CSM_PAL_DIAG) && CSM_PAL_DIAG >= 2)  // timing diagnostic: no cell-by-cell pass
-  slow_beams<NS>(B, L, gi, slow, kk, q, ox, oy, mine);
-#endif
-  box_epilogue<NS, BEST>(L, S, ae, wt, a, kk < NS, kk, q, ox, oy, nsf, mine, out, partials);
-}
-
 // CSM_BOX_TRACE builds: s_memtime stamps of the pair kernel's phases for a
 // sample of waves (every 61st block), read by tools/box_trace.py through
 // csm_debug_box_trace: [0] entry, [1] first list build starts, [2] build,
@@ -711,8 +411,13 @@ __device__ int g_box_trace_n;
 #endif
 
 // v11 "pair" box kernel (n_space <= 13, palettes of at most kPairMaxPal
-// values, r04). Two changes to v10, one per bound it hit (TA 0.66, VALU 0.70
-// of the kernel's cycles, profiles/r04):
+// values, r04). It reads the box through the grid's palette: a scan-match grid
+// holds few distinct values (unknown, occupied and the blur kernel's levels),
+// so every cell is a byte, the index of its value in the palette (L.pal_vals,
+// 0 = the outside value), and a run's count times the value is an exact fp64
+// FMA (every product and partial sum an integer below 2^53). Two changes to
+// the r04 one-run-per-row palette form (v10, retired in r05), one per bound it
+// hit (TA 0.66, VALU 0.70 of the kernel's cycles, profiles/r04):
 //  - the box rows come from the strip copies of the index grid: a run's 13
 //    rows are 208 contiguous bytes of one strip (2.5 cache lines per run, not
 //    14 row-major), so the texture-address unit tags a fifth of the lines;
@@ -944,35 +649,6 @@ hipError_t launch_pair(const LevelWork& L, const ScanWork* s, const double2* p, 
 }
 
 template <int NS>
-hipError_t launch_palette(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
-                          BestPartial* part, unsigned nblk, hipStream_t stream) {
-  if (part)
-    hipLaunchKernelGGL((score_box_palette_kernel<NS, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
-  else
-    hipLaunchKernelGGL((score_box_palette_kernel<NS, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out,
-                       part);
-  return hipGetLastError();
-}
-
-template <int NS>
-hipError_t launch_grouped(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
-                          BestPartial* part, unsigned nblk, hipStream_t stream) {
-  if (part)
-    hipLaunchKernelGGL((score_box_grouped_kernel<NS, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
-  else
-    hipLaunchKernelGGL((score_box_grouped_kernel<NS, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
-  return hipGetLastError();
-}
-
-int grouped_mode() {  // CSM_BOX_GROUPED=0: the v6 kernel for every box level
-  static const int m = [] {
-    const char* e = getenv("CSM_BOX_GROUPED");
-    return e ? atoi(e) : 1;
-  }();
-  return m;
-}
-
-template <int NS>
 hipError_t launch_ns(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
                      BestPartial* part, unsigned nblk, hipStream_t stream) {
   if (part)
@@ -985,30 +661,6 @@ hipError_t launch_ns(const LevelWork& L, const ScanWork* s, const double2* p, co
 }  // namespace
 
 bool box_supported(int ns) { return ns >= 9 && ns <= 16; }
-bool box_palette_supported(int ns) { return ns >= 9 && ns <= kPalMaxSpace; }
-
-hipError_t launch_score_box_palette(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
-                                    const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
-                                    hipStream_t stream) {
-  const int64_t tiles = L.tile_n > 0 ? (int64_t)L.tile_n * L.tile_n : 1;
-  const int64_t nblk = (int64_t)L.n_scans * tiles * L.n_angles;
-  if (nblk <= 0 || nblk > INT32_MAX || !L.int_mode || L.step_cells != 1.0 || L.blocks_per_scan != L.n_angles ||
-      L.pitch < L.size_x + kGridiPadCols || L.pitch % 4 != 0 || L.pal_n < 1 || L.pal_n > kPalMax || !L.pal_grid ||
-      !L.pal_vals || L.pal_stride < (int64_t)L.pitch * (L.size_y + kGridiPadRows) || L.pal_stride > INT32_MAX ||
-      L.tile_n > 0)
-    return hipErrorInvalidValue;
-  const double2* p = reinterpret_cast<const double2*>(d_pts);
-  const unsigned n = (unsigned)nblk;
-  switch (ns) {
-    case 9: return launch_palette<9>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 10: return launch_palette<10>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 11: return launch_palette<11>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 12: return launch_palette<12>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 13: return launch_palette<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    default: return hipErrorInvalidValue;
-  }
-}
-
 bool box_pair_supported(int ns) { return ns >= 9 && ns <= kPalMaxSpace; }
 
 hipError_t launch_score_box_pair(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
@@ -1052,14 +704,10 @@ hipError_t launch_score_box(const LevelWork& L, const ScanWork* d_scans, const d
     case 10: return launch_ns<10>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
     case 11: return launch_ns<11>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
     case 12: return launch_ns<12>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 13: return grouped_mode() ? launch_grouped<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)
-                                   : launch_ns<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 14: return grouped_mode() ? launch_grouped<14>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)
-                                   : launch_ns<14>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 15: return grouped_mode() ? launch_grouped<15>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)
-                                   : launch_ns<15>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
-    case 16: return grouped_mode() ? launch_grouped<16>(L, d_scans, p, d_angles, d_out, d_partials, n, stream)
-                                   : launch_ns<16>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 13: return launch_ns<13>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 14: return launch_ns<14>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 15: return launch_ns<15>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
+    case 16: return launch_ns<16>(L, d_scans, p, d_angles, d_out, d_partials, n, stream);
     default: return hipErrorInvalidValue;
   }
 }

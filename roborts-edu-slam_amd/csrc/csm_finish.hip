@@ -913,12 +913,11 @@ __device__ __forceinline__ void finish_entry(const FinishArgs& A, const ScanWork
       __syncthreads();  // the next window reuses the LDS carve
     }
     if (A.host_flag && cnt > 0) {  // (nothing flagged: the fast pass signalled the host)
-      // every block's FinishOut stores land, then the last block signals the host
+      // every block's sealed FinishOut stores complete, then the last block
+      // signals the host (the ordering argument: DESIGN §7 "Host signals")
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int t = __hip_atomic_fetch_add(A.done_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t == (int)gridDim.x - 1) {
           __hip_atomic_store(A.done_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -968,15 +967,6 @@ constexpr int kFastCap = 512;      // compacted candidates of step 2
 constexpr int kFastNearCap = 512;  // compacted near-best candidates of step 3
 constexpr int kFastLevels = 8;     // thresholds best - {0.01, 0.02, ..., 0.64}, then everything > bound
 constexpr int kFastAngles = 256;   // angle rows staged in LDS (more: read from memory)
-// <128, 11> for 1025..1408 candidates (CSM_FAST_HALF=0: <256, 6>, the A/B)
-inline bool fast_half_blocks() {
-  static const bool on = [] {
-    const char* e = std::getenv("CSM_FAST_HALF");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
-
 __device__ __forceinline__ double wave_max_d(double v) {
   for (int o = 32; o > 0; o >>= 1) {
     const double t = __shfl_xor(v, o, 64);
@@ -985,23 +975,19 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
-// Host signal (A.host_flag): every block's FinishOut stores land (write-
+// Host signal (A.host_flag): every block's FinishOut stores complete (write-
 // through sc0 sc1 stores to the coherent host buffer, each wave waits for
 // them), the blocks count in; the last one, if no window was flagged for the
 // exact pass, stores the flag value itself -- the exact launch behind it then
-// returns at once and is off the host's critical path.
-// (Measured: with plain stores and no per-block system-scope release the host
-// read stale FinishOut fields -- the lines sat in the XCD's L2 -- and that
-// release, a write-back of the whole L2 per block, cost 25-50 us per
-// 1024-window launch; write-through stores leave nothing to write back.)
+// returns at once and is off the host's critical path. The count-in is
+// relaxed: the host reads every window through its seal, so a flag seen
+// before a window's stores costs a spin, never a wrong result (DESIGN §7
+// "Host signals"; a per-block system-scope release, one L2 write-back per
+// block, cost 25-50 us per launch).
 __device__ __forceinline__ void fast_signal(const FinishArgs& A) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-#if defined(CSM_FAST_SYS_RELEASE) && CSM_FAST_SYS_RELEASE
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope, per block (diagnostic variant)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     const int t = __hip_atomic_fetch_add(A.done_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (int)gridDim.x - 1) {
       __hip_atomic_store(A.done_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1398,7 +1384,7 @@ hipError_t launch_fast(const FinishArgs& A, const ScanWork* s, const AngleEntry*
   if (n <= 1024) return launch_fast_tv<256, 4>(A, s, a, sc, o, nw, stream);
   // two waves a window (20 KB of LDS, ~80 VGPRs): 8 blocks a CU, where
   // <256, 6> held 7 (66 VGPRs, 23.2 KB)
-  if (n <= 1408 && fast_half_blocks()) return launch_fast_tv<128, 11>(A, s, a, sc, o, nw, stream);
+  if (n <= 1408) return launch_fast_tv<128, 11>(A, s, a, sc, o, nw, stream);
   if (n <= 1536) return launch_fast_tv<256, 6>(A, s, a, sc, o, nw, stream);
   if (n <= 2560) return launch_fast_tv<256, 10>(A, s, a, sc, o, nw, stream);
   if (n <= 5120) return launch_fast_tv<256, 20>(A, s, a, sc, o, nw, stream);

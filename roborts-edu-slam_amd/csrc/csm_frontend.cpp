@@ -134,8 +134,9 @@ int csm_frontend_create(int device, const csm_frontend_param* param, csm_fronten
   auto* f = new csm_frontend();
   f->device = device;
   f->p = *param;
-  const char* tm = std::getenv("CSM_FE_TIMING");
-  f->timing = tm && std::atoi(tm) != 0;
+#ifdef CSM_FE_TIMING  // diagnostic builds: per-phase host timings of every call
+  f->timing = true;
+#endif
   int st = csm_create(device, &f->ctx);
   if (st == CSM_OK && param->use_optimize_scan_match) st = csm_create(device, &f->ctx_coarse);
   if (st != CSM_OK) {

@@ -363,15 +363,15 @@ struct csm_ctx {
   // The exact finish pass (a few latency-bound blocks per launch: the flagged
   // windows' sort chains) runs here, after the fast pass (ev_fast), so it
   // overlaps the other part's scoring on `stream`; the part's results go down
-  // after it (ev_k on this stream). CSM_EXACT_STREAM=0: everything on `stream`.
+  // after it (ev_k on this stream).
   hipStream_t x_stream = nullptr;
   hipEvent_t ev_fast = nullptr;
   // Signalled levels of the 3-level driver: the host completes (and plans the
   // next level of) the windows the fast pass settled while the exact pass
-  // sorts the flagged ones (FinishArgs::host_fast_flag). CSM_EARLY_COMPLETE=0: off.
+  // sorts the flagged ones (FinishArgs::host_fast_flag).
   bool early_complete = true;
   bool early_now = false;  // set by match_levels_pipelined
-  // CSM_DEBUG_FIN=1: the 3-level driver snapshots the last level's FinishOut
+  // CSM_DEBUG_FIN builds: the 3-level driver snapshots the last level's FinishOut
   // as each window is completed and, once the device is idle, compares it with
   // what the finish finally left in host memory (stderr; diagnostics of the
   // host-signal paths)
@@ -421,13 +421,12 @@ struct csm_ctx {
   bool phase_kernel = true;   // v7 phase kernel for sub-cell window steps (CSM_KERNEL=v7 or unset)
   bool tiny_kernel = true;    // v8 tiny-window kernel, spans under one cell (CSM_KERNEL=v8 or unset)
   int phase_margin_log2 = 20; // CSM_PHASE_MARGIN_LOG2 (tests: a wider margin sends more beams to the exact path)
-  // v10 palette box kernel (CSM_BOX_PALETTE=0: off): the byte copy of gridi
-  // (palette indices) and the palette, rebuilt when grid_gen moves on
-  bool palette_kernel = true;
+  // the grid's palette: the byte copy of gridi (palette indices) and the
+  // palette, rebuilt when grid_gen moves on (the pair box kernel's source)
   csmh::DevBuf pal_grid, pal_vals, pal_scratch;
   csmh::DevBuf pal_strips;     // strip copies of pal_grid (v11 pair kernel; palettes of <= kPairMaxPal values)
   bool pal_strips_ok = false;
-  bool pair_kernel = true;     // CSM_BOX_PAIR=0: the v10 palette kernel instead of v11
+  bool pair_kernel = true;     // v11 pair box kernel where the grid has a palette (CSM_KERNEL set: off)
   csmh::DevBuf istrips;        // strip copies of gridi (the phase kernel's strip form)
   uint64_t istrips_gen = 0;    // grid_gen they were built for
   const int32_t* istrips_src = nullptr;
@@ -447,9 +446,9 @@ struct csm_ctx {
   csmh::HostBuf h_small_in, h_small_out;
   uint32_t flag_seq = 0;
   bool small_path = true;      // CSM_SMALL=0: few-window launches take the throughput kernels
-  int small_max_windows = 32;  // CSM_SMALL_WINDOWS
-  int split_target_blocks = 512;  // CSM_SPLIT_TARGET: blocks a split launch aims for
-  int fast_wide_windows = 0;      // CSM_FAST_WIDE: fast finishes of <= this many windows on 1024 threads (0: 64; -1: never)
+  int small_max_windows = 32;  // launches of at most this many windows take the few-window path
+  int split_target_blocks = 512;  // blocks a split launch aims for
+  int fast_wide_windows = 0;      // fast finishes of <= this many windows on 1024 threads (0: 64)
   csmh::HostBuf h_pack;  // pinned staging of packed grid rows / cell updates (grid uploads)
   hipEvent_t ev_pack = nullptr;  // the last copy out of h_pack (cell updates return before it ends)
   bool ev_pack_used = false;
@@ -588,15 +587,15 @@ struct csm_ctx {
   int first_windows = 128;   // level_begin_split: windows the first part's first launch takes (CSM_FIRST_WINDOWS; 0: one launch)
   // submitted batches (the device has the previous batch's work queued): one
   // launch (r04 A/B, 2 runs each: 0 10.77 / 10.98, 128 10.39 / 10.41 G scorings/s)
-  int first_windows_submit = 0;  // (CSM_FIRST_WINDOWS_SUBMIT; CSM_FIRST_WINDOWS sets both)
-  int span_growth = 4;       // ... and each later span's growth (CSM_SPAN_GROWTH)
+  int first_windows_submit = 0;  // (CSM_FIRST_WINDOWS sets both)
+  int span_growth = 4;       // ... and each later span's growth
   void* pipe = nullptr;  // csm_driver.cpp PipeState: submitted batches (csm_scan_matchers_submit)
-  bool split_last_handoff = true;  // the last part's hand-off to the last level in two spans (CSM_SPLIT_HANDOFF)
+  bool split_last_handoff = true;  // the last part's hand-off to the last level in two spans
   int split_handoff_min = 256;     // ... for parts of at least this many windows (CSM_SPLIT_HANDOFF_MIN)
   bool defer_last_handoff = true;  // a submitted batch leaves its last part's last hand-off to the next call (CSM_DEFER_HANDOFF)
-  int part0_permille = 550;  // two parts: the first one's share of the scans (CSM_PART0_PERMILLE;
+  int part0_permille = 550;  // two parts: the first one's share of the scans (
                              // r04 A/B, 2 runs each: 500 9.40, 550 9.61, 600 9.56, 650 9.47 G scorings/s)
-  int part0_permille_submit = 500;  // ... for submitted batches (CSM_PART0_PERMILLE_SUBMIT; r04 A/B with
+  int part0_permille_submit = 500;  // ... for submitted batches (r04 A/B with
                                     // the deferred hand-off: 500 10.45 / 10.48, 550 10.39 / 10.41 G)
   void swap_slot(int i) {    // i >= 1: exchange the current buffer set with alt[i - 1]
     Slot& a = alt[i - 1];

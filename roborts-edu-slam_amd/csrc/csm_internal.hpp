@@ -68,7 +68,7 @@ struct LevelWork {
   // do, or the host could not have gone on) finds another tag and exits.
   int32_t* clear_word;
   int32_t clear_tag;
-  // The palette copy of gridi (score_box_palette_kernel): every cell's index
+  // The palette copy of gridi (score_box_pair_kernel's source): every cell's index
   // into pal_vals, the grid's distinct fixed-point values (pal_vals[0] = 0,
   // the outside value), one byte per cell in gridi's layout (row pitch
   // `pitch` bytes, pal_stride bytes per grid). pal_n = 0: no palette.
@@ -288,14 +288,10 @@ hipError_t launch_score_tiny(const LevelWork& L, const ScanWork* d_scans, const 
 // n_space <= 16; one wave per (window, angle), one 16-byte row piece per lane
 // per beam. blocks_per_scan = n_angles.
 bool box_supported(int ns);
-// v10 palette box kernel: one-cell steps with n_space <= kPalMaxSpace on a
-// grid of at most kPalMax distinct fixed-point values (L.pal_n > 0).
+// The grid's palette (the pair box kernel below): at most kPalMax distinct
+// fixed-point values (L.pal_n > 0); boxes of n_space <= kPalMaxSpace.
 constexpr int kPalMax = 256;
 constexpr int kPalMaxSpace = 13;
-bool box_palette_supported(int ns);
-hipError_t launch_score_box_palette(const LevelWork& L, const ScanWork* d_scans, const double* d_pts,
-                                    const AngleEntry* d_angles, double* d_out, BestPartial* d_partials, int ns,
-                                    hipStream_t stream);
 // The palette of n int32 cells (gridi with its padding): distinct values
 // (0 first, then ascending) into vals[0..kPalMax), their count into
 // state[0] (kPalMax + 1: more than kPalMax, no palette) and each cell's index

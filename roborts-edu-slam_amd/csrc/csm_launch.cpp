@@ -446,14 +446,15 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const bool box = use_int && c->box_kernel && f == 1.0 && csm::box_supported(D.n_space) &&
                    c->pitch >= c->info.size_x + csm::kGridiPadCols;
   if (box) rows_sq = 0;
-  // v10: the box read through the grid's palette (one byte per cell)
+  // v11: the box read through the grid's palette (one byte per cell), pairs
+  // of equal-count runs over the strip copies (palettes of <= 16 values);
+  // otherwise the v6 kernel reads gridi
   bool box_pal = false;
-  if (box && c->palette_kernel && csm::box_palette_supported(D.n_space)) {
+  if (box && c->pair_kernel && csm::box_pair_supported(D.n_space)) {
     if ((st = ensure_palette(c)) != CSM_OK) return st;
     box_pal = c->pal_n > 0 && (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows) <= INT32_MAX;
   }
-  // v11: pairs of equal-count runs over the strip copies (palettes of <= 16 values)
-  const bool box_pair = box_pal && c->pair_kernel && c->pal_strips_ok && csm::box_pair_supported(D.n_space);
+  const bool box_pair = box_pal && c->pal_strips_ok;
   // v6 over 16 x 16 tiles: the argmax of a one-cell-step window wider than 16
   // (loop-closure windows), in place of the column kernel's dword gathers
   const int tile_n = (D.n_space + 15) / 16;
@@ -489,7 +490,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   LevelWork L = make_level_work(c, P, D, G, nr, use_int);
   L.blocks_per_scan = box_tiled ? D.n_angles : (int32_t)bps;  // per (window, tile) when tiled
   L.tile_n = box_tiled ? tile_n : 0;
-  if (box_pal) {
+  if (box_pair) {
     L.pal_n = c->pal_n;
     L.pal_grid = (const uint8_t*)c->pal_grid.p;
     L.pal_vals = (const int32_t*)c->pal_vals.p;
@@ -572,8 +573,6 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   char kname[48];
   if (box_pair)
     std::snprintf(kname, sizeof(kname), "score_box_pair_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
-  else if (box_pal)
-    std::snprintf(kname, sizeof(kname), "score_box_palette_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (box)
     std::snprintf(kname, sizeof(kname), "score_box_kernel<%d,%s>", D.n_space, best_out ? "best" : "all");
   else if (box_tiled)
@@ -618,9 +617,6 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     else if (box_pair)
       e = csm::launch_score_box_pair(L, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
                                      (double*)c->scores.p, nullptr, D.n_space, c->stream);
-    else if (box_pal)
-      e = csm::launch_score_box_palette(L, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
-                                        (double*)c->scores.p, nullptr, D.n_space, c->stream);
     else if (box)
       e = csm::launch_score_box(L, d_sw, (const double*)c->pts.p,
                                 (const AngleEntry*)c->angles.p, (double*)c->scores.p, nullptr, D.n_space,
@@ -738,10 +734,6 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       e = csm::launch_score_box_pair(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                      (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
                                      D.n_space, c->stream);
-    else if (box_pal)
-      e = csm::launch_score_box_palette(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
-                                        (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,
-                                        D.n_space, c->stream);
     else if (box || box_tiled)
       e = csm::launch_score_box(L, (const ScanWork*)c->scans.p, (const double*)c->pts.p,
                                 (const AngleEntry*)c->angles.p, nullptr, (BestPartial*)c->partials.p,

@@ -893,16 +893,9 @@ hipError_t launch_pyr_widen(const PyrGrid& src, const PyrGrid& dst, int32_t n_gr
   return hipGetLastError();
 }
 
-// fewest beams a split top-level wave takes (CSM_TOPBOX_MIN_BEAMS; each
-// split wave adds its nj^2 node sums with global atomics)
-int topbox_min_beams() {
-  static const int v = [] {
-    const char* e = std::getenv("CSM_TOPBOX_MIN_BEAMS");
-    const int x = e ? std::atoi(e) : 32;
-    return x < 1 ? 1 : x;
-  }();
-  return v;
-}
+// fewest beams a split top-level wave takes (each split wave adds its nj^2
+// node sums with global atomics)
+constexpr int kTopboxMinBeams = 32;
 
 hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32_t nj, const ScanWork* scans,
                              const AngleEntry* angles, const double* pts, int32_t n_used, int32_t step,
@@ -918,7 +911,7 @@ hipError_t launch_pyr_topbox(const LevelWork& L, const PyrGrid& tb, int d, int32
   // few (window, angle) pairs: split each one's beams over up to 16 waves (at
   // least 128 beams each) so the launch fills the chip
   int split = 1;
-  while (split < kPyrTopMaxSplit && blocks * split < 4096 && n_used / (2 * split) >= topbox_min_beams()) split *= 2;
+  while (split < kPyrTopMaxSplit && blocks * split < 4096 && n_used / (2 * split) >= kTopboxMinBeams) split *= 2;
   if (split > 1 && !slab) split = 1;
   if (split_out) *split_out = split;
   hipError_t e;

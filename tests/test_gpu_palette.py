@@ -1,6 +1,5 @@
-"""GPU parity of the palette box kernels (csrc/csm_box.hip
-score_box_palette_kernel v10 and score_box_pair_kernel v11, csrc/csm_palette.hip)
-against the CPU oracle.
+"""GPU parity of the palette box kernel (csrc/csm_box.hip
+score_box_pair_kernel v11, csrc/csm_palette.hip) against the CPU oracle.
 
 The kernel reads one-cell-step windows (n_space <= 13: the coarse level of
 every shipped parameter set, correlate_scan_matcher.h:552-584,637-662)
@@ -8,9 +7,9 @@ through the palette copy of the fixed-point grid: one byte per cell, the
 index of the cell's value among the grid's distinct values. The bar is the
 same as for every other kernel: all scores bit for bit, the argmax index
 equal. Covered here: the palette's size limits (up to 16 values: the v11 pair
-kernel over the strip copies, index shift 3 up to 8 values and 4 above; up to
-256: the v10 palette kernel; 257: the grid has no palette and the v9 grouped
-kernel runs; CSM_BOX_PAIR=0 keeps v10 for small palettes), cells below the
+kernel over the strip copies, index shift 3 up to 8 values and 4 above; more:
+the v6 box kernel reads gridi; CSM_KERNEL=v8 runs v6 for small palettes too,
+the comparison), cells below the
 outside value (negative fixed-point entries), windows off every edge, beams
 on rounding boundaries, a grid stack (the palette grid's per-grid stride),
 and the palette rebuilt after row and cell refreshes of a resident map.
@@ -86,9 +85,7 @@ def _kernel(grids, outside=0.3, pair=True):
     of distinct values other than the outside value, plus the outside value."""
     g = np.asarray(grids, dtype=np.float32)
     n = len(np.unique(g[g != np.float32(outside)])) + 1
-    if n > 256:
-        return "score_box_kernel"
-    return "score_box_pair_kernel" if (pair and n <= 16) else "score_box_palette_kernel"
+    return "score_box_pair_kernel" if (pair and n <= 16) else "score_box_kernel"
 
 
 def _values(n, rng, lo=0.3125, step=2.0 ** -12):
@@ -97,15 +94,14 @@ def _values(n, rng, lo=0.3125, step=2.0 ** -12):
     return rng.permutation(v).astype(np.float32)
 
 
-@pytest.mark.parametrize("n_values,kernel", [(256, "score_box_palette_kernel"), (257, "score_box_kernel"),
+@pytest.mark.parametrize("n_values,kernel", [(256, "score_box_kernel"), (257, "score_box_kernel"),
                                             (2, "score_box_pair_kernel"), (8, "score_box_pair_kernel"),
                                             (9, "score_box_pair_kernel"), (16, "score_box_pair_kernel"),
-                                            (17, "score_box_palette_kernel")])
+                                            (17, "score_box_kernel")])
 def test_palette_size_limits(f1, n_values, kernel):
     """The outside value plus n_values - 1 others: up to 16 values take the
-    pair kernel (pair codes of 3 bits per index up to 8 values, 4 above), up
-    to 256 the palette kernel (indices 0..255), 257 cannot and the grouped
-    kernel runs; all bit-exact."""
+    pair kernel (pair codes of 3 bits per index up to 8 values, 4 above),
+    more the v6 box kernel over gridi; all bit-exact."""
     import roborts_csm
     rng = np.random.default_rng(n_values)
     res = float(f1["resolution"])
@@ -141,7 +137,7 @@ def test_palette_negative_values_and_blur(f1, pair):
     pts = _points(f1)
     lv = _level(pts.shape[0])
     for outside in (0.3, 0.5):
-        c = _ctx(CSM_BOX_PAIR="1" if pair else "0")
+        c = _ctx(**({} if pair else {"CSM_KERNEL": "v8"}))
         try:
             c.set_outside_value(outside)
             mo = O.Map(g, res, tuple(f1["offset"]), outside=outside)
@@ -165,7 +161,7 @@ def test_palette_grid_stack(f1, pair):
     lv = _level(pts.shape[0])
     cen = np.stack(_centers(res))
     gi = np.array([0, 1, 2, 1, 2, 0], dtype=np.int32)
-    c = _ctx(CSM_BOX_PAIR="1" if pair else "0")
+    c = _ctx(**({} if pair else {"CSM_KERNEL": "v8"}))
     try:
         c.set_grid_stack(stack, res, version=1)
         sc, flat, x, y, a = c.best_windows(pts, lv, gi, cen)
@@ -188,7 +184,7 @@ def test_palette_follows_grid_refresh(f1, pair):
     pts = _points(f1)
     lv = _level(pts.shape[0])
     cen = _centers(res)[:3]
-    c = _ctx(CSM_BOX_PAIR="1" if pair else "0")
+    c = _ctx(**({} if pair else {"CSM_KERNEL": "v8"}))
     try:
         c.set_grid(mm)
         _check_windows(c, O.Map(g, res, tuple(f1["offset"])), pts, lv, cen)
@@ -202,7 +198,8 @@ def test_palette_follows_grid_refresh(f1, pair):
         c.update_grid_cells(mm, idx)
         _check_windows(c, O.Map(g, res, tuple(f1["offset"])), pts, lv, cen)
         st = _stats(c)
-        assert st["grid:palette"]["launches"] >= 3
+        if pair:  # (the v6 kernel reads gridi: no palette is built)
+            assert st["grid:palette"]["launches"] >= 3
         assert _kernel(g, 0.3, pair) + "<13,all>" in st, st.keys()
     finally:
         c.close()

@@ -388,9 +388,9 @@ def test_kernel_variants_agree(f1, grid_kind):
         g = rng.choice(np.array([0.3, 0.41, 0.88, 1.0], dtype=np.float32), size=(400, 400))
     m = O.Map(g, float(f1["resolution"]), tuple(f1["offset"]))
     # None: default throughput kernels (v11 pair box / v7 phase over strips / v8 tiny / v4); split:
-    # few-window path; the last: v10 palette box and the phase kernel over gridi
+    # few-window path; the last: v6 box and the phase kernel over gridi
     ctxs = [_variant_ctx(k) for k in ("v2", "v4", "v6", "v7", None, "split")]
-    ctxs.append(_variant_ctx(None, CSM_BOX_PAIR="0", CSM_PHASE_STRIPS="0"))
+    ctxs.append(_variant_ctx("v8", CSM_PHASE_STRIPS="0"))
     params = [_param(f1["param"])] + list(SIM_YAML_LEVELS) + [l.with_(use_point_size=1081) for l in SIM_YAML_LEVELS]
     params += [l.with_(use_point_size=1081) for l in PARAM_CONFIG_LEVELS]
     for c in ctxs:
@@ -424,13 +424,11 @@ def test_box_kernel_edge_beams(world2000):
     centers = [[c0, 200.5 + half, 0.0], [c0, 200.5 + half, 1.3],
                [1020.0 + 3 * 2.0 ** -43, 1019.0 + 2.0 ** -43, 0.7],
                [6.2, 3.1, -2.5], [1995.0, 1990.0, 1.0], [511.0 + 2.0 ** -44, 250.3, 3.0]]
-    # None: the v11 pair box kernel (the world's 7 values); CSM_BOX_PALETTE=0: the v9
-    # grouped box kernel; CSM_BOX_PAIR=0: the v10 palette box kernel
-    ctxs = [_variant_ctx(k) for k in (None, "v4", "split")] + [_variant_ctx(None, CSM_BOX_PALETTE="0"),
-                                                              _variant_ctx(None, CSM_BOX_PAIR="0")]
+    # None: the v11 pair box kernel (the world's 7 values); v8: the v6 box kernel over gridi
+    ctxs = [_variant_ctx(k) for k in (None, "v4", "split", "v8")]
     for c in ctxs:
         c.set_grid(_map(w.grid, w.resolution, w.offset, version=1))
-    for i in (0, 3, 4):
+    for i in (0, 3):
         ctxs[i].set_profiling(True)
     for cen in centers:
         cen = np.array(cen)
@@ -440,7 +438,7 @@ def test_box_kernel_edge_beams(world2000):
             got = c.best_window(pts, lv, cen)
             s, flat = O.best_window(m, pts, lv, cen)
             assert got.score == s and got.flat_index == flat
-    for i, kn in ((0, "score_box_pair_kernel"), (3, "score_box_kernel"), (4, "score_box_palette_kernel")):
+    for i, kn in ((0, "score_box_pair_kernel"), (3, "score_box_kernel")):
         names = {k["name"] for k in ctxs[i].kernel_stats()}
         assert kn + "<13,all>" in names and kn + "<13,best>" in names, (i, names)
     for c in ctxs:

@@ -3,8 +3,8 @@ every level, so the exact finish pass has windows at every level): the
 configuration of tests/test_gpu_parity.py::test_host_signal_split_levels_with_ties,
 repeated --iters times in one process against the oracle's answer. Prints one
 JSON line: the iterations that differed and, for the first few, the scans and
-fields that differ. Run it under the driver's knobs (CSM_EARLY_COMPLETE,
-CSM_HOST_SIGNAL, CSM_FIRST_WINDOWS, CSM_EXACT_STREAM) to see which path an
+fields that differ. Run it under the driver's knobs (CSM_HOST_SIGNAL,
+CSM_FIRST_WINDOWS, CSM_DEFER_HANDOFF) to see which path an
 intermittent mismatch needs.
 
   python tools/stress_ties.py [--iters 40] [--scans 96]
