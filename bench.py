@@ -922,7 +922,12 @@ def main():
         b109 = {"value": world_size * args.scans * ps * args.steps / e109, "unit": "scorings/s",
                 "ms_per_step": e109 / args.steps * 1e3, "beams_summed": _beams_summed(batch.offsets, 100),
                 "levels": "sim YAML (U=100 at every level: B=109)",
-                "batches": "submitted back to back, as the headline"}
+                "batches": "submitted back to back, as the headline",
+                **kernel_accounting(stats109, e109, args.steps)}
+        dom109, avg109, info109 = dominant_kernel(stats109)
+        b109["dominant_kernel"] = {"name": dom109["name"], "avg_ms": avg109,
+                                   "share_of_step": dom109["total_ms"] * 1e-3 / e109, **info109}
+        b109["kernels"] = stats109
 
     # parity of the timed configuration itself: every rank checks its own
     # batch's last timed step against the oracle (rank 0 at N = 1 on the

@@ -32,6 +32,9 @@ struct LevelRun {
   std::vector<char>* how = nullptr;
   // a window's FinishOut never matched its seal (pinned host memory): 1
   mutable int err = 0;
+  // the order its windows take the scans in (nullptr: scan order; the
+  // 3-level driver's spatial order, window_order)
+  const int32_t* order = nullptr;
   // back to a fresh run, the vectors' capacity kept
   void reset() {
     P = csm_param{};
@@ -51,6 +54,7 @@ struct LevelRun {
     snap = nullptr;
     how = nullptr;
     err = 0;
+    order = nullptr;
   }
 };
 
@@ -101,7 +105,8 @@ int level_prepare(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm
   int st = window_dims(P, R.D);
   if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
   R.scan_of.reserve((size_t)n_scans);
-  for (int s = 0; s < n_scans; ++s) {
+  for (int k = 0; k < n_scans; ++k) {
+    const int s = R.order ? R.order[k] : k;
     if (reset) {
       responses[s] = 0.0;  // kMinResponse (:1034)
       if (argmax_flat) argmax_flat[s] = -1;
@@ -460,6 +465,7 @@ struct PipeJob {
   LevelRun R[2][csm_ctx::kMaxParts];
   bool pending = false;  // levels launched up to the last part's last hand-off; that and the completion deferred
   bool last_handoff_done = false;
+  std::vector<int32_t> order[csm_ctx::kMaxParts];  // each part's scans in window order (window_order)
   std::vector<csm::FinishOut> snaps[csm_ctx::kMaxParts];  // CSM_DEBUG_FIN
   std::vector<char> hows[csm_ctx::kMaxParts];
 };
@@ -482,6 +488,44 @@ int with_slot(csm_ctx* c, const PipeJob& J, int h, F&& f) {
   const int st = f();
   if (sidx > 0) c->swap_slot(sidx);
   return st;
+}
+
+// The order a part's windows take its scans in. Consecutive windows go to
+// one XCD (dev::xcd_remap: XCD x takes the x-th eighth of the launch), so the
+// scans are ranked by the Morton code of their initial map cell (64-cell
+// tiles) and rank m goes to launch position (m % 8) * n / 8 + m / 8: every
+// XCD's share spans the whole map (the same work mix on every XCD), and at
+// any moment the eight XCDs score windows that lie close together, which
+// their L2s and the MALL share. r05 A/B: the pair kernel 0.637
+// -> 0.613 ms, the phase kernel 0.252 -> 0.245; ranks in contiguous eighths
+// (each XCD one region of the map) made the pair kernel 0.848 ms, the XCDs'
+// regions holding unequal work. Scans are independent: no result changes.
+#ifndef CSM_WINDOW_ORDER  // 0: scan order (A/B builds)
+#define CSM_WINDOW_ORDER 1
+#endif
+void window_order(const Geometry& G, const double* poses, int32_t n, std::vector<int32_t>& out) {
+  out.resize((size_t)n);
+  std::vector<std::pair<uint64_t, int32_t>> key((size_t)n);
+  auto spread = [](uint64_t v) {  // 16 bits -> every other bit
+    v &= 0xFFFF;
+    v = (v | (v << 8)) & 0x00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0Full;
+    v = (v | (v << 2)) & 0x33333333ull;
+    v = (v | (v << 1)) & 0x55555555ull;
+    return v;
+  };
+  for (int32_t s = 0; s < n; ++s) {
+    double m[3];
+    G.to_map(poses + 3 * (size_t)s, m);
+    const double qx = std::floor(m[0] / 64.0), qy = std::floor(m[1] / 64.0);
+    const uint64_t ix = (uint64_t)(int64_t)std::max(-32768.0, std::min(32767.0, qx)) + 32768;
+    const uint64_t iy = (uint64_t)(int64_t)std::max(-32768.0, std::min(32767.0, qy)) + 32768;
+    key[(size_t)s] = {spread(ix) | (spread(iy) << 1), s};
+  }
+  std::sort(key.begin(), key.end());
+  int32_t pos = 0;
+  for (int x = 0; x < 8; ++x)
+    for (int32_t m = x; m < n; m += 8) out[(size_t)pos++] = key[(size_t)m].second;
 }
 
 void job_setup(csm_ctx* c, PipeJob& J, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
@@ -515,6 +559,15 @@ void job_setup(csm_ctx* c, PipeJob& J, int32_t n_scans, const int64_t* offsets, 
   J.resp.assign((size_t)n_scans, 0.0);
   for (auto& row : J.R)
     for (LevelRun& r : row) r.reset();
+  const Geometry G(c->info);
+  for (int h = 0; h < K; ++h) {
+    if (CSM_WINDOW_ORDER) {
+      window_order(G, poses + 3 * (size_t)J.first[h], J.count[h], J.order[h]);
+      J.R[0][h].order = J.R[1][h].order = J.order[h].data();
+    } else {
+      J.order[h].clear();
+    }
+  }
 }
 
 int job_skip(const csm_ctx* c, const PipeJob& J, int l) {
