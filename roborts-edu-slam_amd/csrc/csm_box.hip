@@ -34,6 +34,7 @@
 #include <cstdlib>
 
 #include "csm_device.hpp"
+#include "csm_tail.hpp"
 #include "csm_internal.hpp"
 
 namespace csm {
@@ -257,10 +258,13 @@ template <int NS, bool BEST>
 __device__ __forceinline__ void box_epilogue(const LevelWork& L, const ScanWork& S, const AngleEntry& ae, int win,
                                              int a, bool act, int k, int q, int ox, int oy, int nsf,
                                              const int64_t (&acc)[4], double* __restrict__ out,
-                                             BestPartial* __restrict__ partials) {
+                                             BestPartial* __restrict__ partials, const AngleEntry* angles,
+                                             char* ldsA, char* ldsB) {
   const double f = L.step_cells;
   double bs = -1.0e300;
   int64_t bf = INT64_MAX;
+  double lmax = -INFINITY;  // the fused finish (csm_tail.hpp): this lane's max, any NaN
+  bool lnan = false;
   const double yk = S.y0 + (oy + k) * f;  // :572
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -276,7 +280,9 @@ __device__ __forceinline__ void box_epilogue(const LevelWork& L, const ScanWork&
           bf = flat;
         }
       } else {
-        out[S.out_off + flat] = score;
+        tail::store_score(L, out + S.out_off + flat, score);
+        lnan |= score != score;
+        lmax = (score > lmax) ? score : lmax;
       }
     }
   }
@@ -291,6 +297,8 @@ __device__ __forceinline__ void box_epilogue(const LevelWork& L, const ScanWork&
       }
     }
     if (threadIdx.x == 0) partials[(int64_t)win * L.blocks_per_scan + a] = BestPartial{bs, bf};
+  } else if (L.tail.on) {
+    tail::finish(L, S, angles, out, a, lmax, lnan, ldsA, ldsB);
   }
 }
 
@@ -345,8 +353,9 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
   // are built per segment of kRunSeg beams (list, padding, then one scratch
   // slot per lane for the branch-free list writes).
   constexpr int kScratch = kRunSeg + 64 + 2 * D;
-  __shared__ int32_t run_off[kScratch + 64];
-  __shared__ int32_t run_cnt[kScratch + 64];
+  __shared__ __attribute__((aligned(16))) int32_t run_off[kScratch + 64];
+  __shared__ __attribute__((aligned(16))) int32_t run_cnt[kScratch + 64];
+  static_assert(sizeof(run_off) >= tail::kBytesA && sizeof(run_cnt) >= tail::kBytesB, "the fused finish's LDS");
   for (int s0 = 0; s0 < n_used; s0 += kRunSeg) {
     const int s1 = min(n_used, s0 + kRunSeg);
     const int nruns = B.build_runs(s0, s1, run_off, run_cnt, kScratch, slow);
@@ -394,7 +403,8 @@ __global__ __launch_bounds__(64) void score_box_kernel(LevelWork L, const ScanWo
     __syncthreads();  // the next segment rewrites the list
   }
   slow_beams<NS>(B, L, gi, slow, k, q, ox, oy, acc);
-  box_epilogue<NS, BEST>(L, S, ae, wt, a, act, k, q, ox, oy, nsf, acc, out, partials);
+  box_epilogue<NS, BEST>(L, S, ae, wt, a, act, k, q, ox, oy, nsf, acc, out, partials, angles,
+                         reinterpret_cast<char*>(run_off), reinterpret_cast<char*>(run_cnt));
 }
 
 // CSM_BOX_TRACE builds: s_memtime stamps of the pair kernel's phases for a
@@ -487,6 +497,7 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
   __shared__ __attribute__((aligned(16))) int32_t pair_off[kPairSlots];  // pair p: members 2p, 2p + 1
   __shared__ __attribute__((aligned(16))) uint8_t pair_cnt[kPairSlots / 2];
   __shared__ int32_t bin[64];  // counting sort by run count (1..64)
+  static_assert(sizeof(run_off) >= tail::kBytesA && sizeof(pair_off) >= tail::kBytesB, "the fused finish's LDS");
   for (int s0 = 0; s0 < n_used; s0 += kPairSeg) {
 #ifdef CSM_BOX_TRACE
     tq = BOX_STAMP();
@@ -624,7 +635,8 @@ __global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const S
 #ifdef CSM_BOX_TRACE
   tr[6] = BOX_STAMP();
 #endif
-  box_epilogue<NS, BEST>(L, S, ae, win, a, kk < NS, kk, q, 0, 0, NS, mine, out, partials);
+  box_epilogue<NS, BEST>(L, S, ae, win, a, kk < NS, kk, q, 0, 0, NS, mine, out, partials, angles,
+                         reinterpret_cast<char*>(run_off), reinterpret_cast<char*>(pair_off));
 #ifdef CSM_BOX_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   tr[7] = BOX_STAMP();

@@ -33,6 +33,7 @@
 #include <cstdlib>
 
 #include "csm_device.hpp"
+#include "csm_tail.hpp"
 #include "csm_internal.hpp"
 
 #pragma clang fp contract(off)
@@ -503,46 +504,6 @@ __device__ void sort_small(double* keys, uint16_t* vals, int base, int m, int de
 
 }  // namespace
 
-constexpr int kSysWriteThrough = 17;  // buffer cache policy sc0 | sc1: system-coherent, written through L2
-
-// One wave stores a window's FinishOut, assembled in LDS (src), to dst: the
-// pieces `lists` selects and the seal (kind = writer | lists << 2, and the
-// checksum of those pieces and the tag, csm_internal.hpp). Into host memory
-// (A.host_flag) as write-through sc0 sc1 stores, nothing left dirty in the
-// XCD's L2; plain stores otherwise (device memory, copied back after the launch).
-__device__ __forceinline__ void emit_sealed(const FinishArgs& A, const FinishOut* src, FinishOut* dst, int lists,
-                                            uint32_t writer, int lane) {
-  static_assert(sizeof(FinishOut) == 560 && offsetof(FinishOut, pos_idx) == 64 &&
-                    offsetof(FinishOut, ang_idx) == 144 && offsetof(FinishOut, pos_score) == 224 &&
-                    offsetof(FinishOut, ang_score) == 384 &&
-                    offsetof(FinishOut, seal_tag_kind) == 16 * kFinishSealPiece,
-                "FinishOut pieces: header 0-3, pos_idx 4-8, ang_idx 9-13, pos_score 14-23, ang_score 24-33, seal 34");
-  const int n_pieces = finish_n_pieces(lists);
-  const uint64_t tk = (uint64_t)(uint32_t)A.flag_value | ((uint64_t)(writer | (uint32_t)lists << 2) << 32);
-  const int pc = lane < n_pieces ? finish_piece(lane, lists) : kFinishSealPiece;
-  int4 piece = lane < n_pieces ? reinterpret_cast<const int4*>(src)[pc] : make_int4(0, 0, 0, 0);
-  uint64_t h = lane < n_pieces ? finish_piece_hash(pc, (uint32_t)piece.x, (uint32_t)piece.y, (uint32_t)piece.z,
-                                                   (uint32_t)piece.w)
-                               : 0ull;
-  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
-  h += finish_seal_share(tk);
-  if (lane == n_pieces) piece = make_int4((int32_t)(uint32_t)tk, (int32_t)(uint32_t)(tk >> 32), (int32_t)(uint32_t)h,
-                                          (int32_t)(uint32_t)(h >> 32));
-  if (lane > n_pieces) return;
-  if (A.host_flag) {
-    const uint64_t base = (uint64_t)(uintptr_t)dst;
-    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-    const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(((uint64_t)bhi << 32) | blo), (short)0, (int)sizeof(FinishOut), 0x00020000);
-    typedef int32_t v4i_t __attribute__((ext_vector_type(4)));
-    const v4i_t v = {piece.x, piece.y, piece.z, piece.w};
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, pc * 16, 0, kSysWriteThrough);
-  } else {
-    reinterpret_cast<int4*>(dst)[pc] = piece;
-  }
-}
-
 // The exact pass over one window (4 waves). Waves 1-3 return before the
 // list scans; the caller's barrier joins them. Inlined into finish_kernel
 // (as a call it took 211 VGPRs and scratch; inlined 129 and none, r04).
@@ -572,7 +533,7 @@ __device__ __forceinline__ void finish_window(const FinishArgs& A, const ScanWor
   uint16_t* rpos = reinterpret_cast<uint16_t*>(smem + Lo.rpos);
   Seg* stack = reinterpret_cast<Seg*>(smem + Lo.stack);
 
-  const double* sc = scores + (int64_t)w * A.n_cand;
+  const double* sc = scores + (int64_t)w * (A.score_stride ? A.score_stride : A.n_cand);
   // Load, and the limits of the partial sort: max, NaN, and the FindBest
   // prefix size (every element with DoubleEqual(s, max, 1e-2): the prefix is
   // exactly that set, in sorted order).
@@ -1075,20 +1036,12 @@ __device__ __forceinline__ void finish_fast_body(const FinishArgs& A, const Scan
   const int w = blockIdx.x;
   const int n = (int)A.n_cand;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const double* sc = scores + (int64_t)w * A.n_cand;
+  const double* sc = scores + (int64_t)w * (A.score_stride ? A.score_stride : A.n_cand);
   int32_t* need = A.need_exact + w;
   auto flag = [&]() {  // thread 0: the exact pass takes this window
     *need = 1;
     if (A.exact_list) A.exact_list[2 + atomicAdd(A.exact_list, 1)] = w;
-    if (A.host_fast_flag) {  // seal = pending (the exact pass owes it), written through to host memory
-      const uint64_t base = (uint64_t)(uintptr_t)(out + w);
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(uintptr_t)base, (short)0, (int)sizeof(FinishOut), 0x00020000);
-      const uint64_t tk = (uint64_t)(uint32_t)A.flag_value | ((uint64_t)kSealPending << 32);
-      typedef int32_t v2i_t __attribute__((ext_vector_type(2)));
-      const v2i_t v = {(int32_t)(uint32_t)tk, (int32_t)(uint32_t)(tk >> 32)};
-      __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)offsetof(FinishOut, seal_tag_kind), 0, kSysWriteThrough);
-    }
+    if (A.host_fast_flag) store_pending_seal(A, out + w);  // the exact pass owes it
   };
   // the scores, every load in flight (index clamped, value masked after)
   double v[V];
@@ -1393,7 +1346,7 @@ hipError_t launch_fast(const FinishArgs& A, const ScanWork* s, const AngleEntry*
 
 hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const AngleEntry* d_angles,
                          const double* d_scores, FinishOut* d_out, int32_t n_windows, hipStream_t stream,
-                         hipStream_t exact_stream, hipEvent_t ev_fast) {
+                         hipStream_t exact_stream, hipEvent_t ev_fast, bool fast_done) {
   const size_t lds = finish_lds_bytes(A.n_cand);
   if (A.n_cand <= 0 || A.n_cand > kFinishMaxCand || lds > 160 * 1024 || n_windows <= 0) return hipErrorInvalidValue;
   static bool attr_set = false;
@@ -1413,7 +1366,7 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
     hipError_t e = hipMemsetAsync(A.exact_list, 0, 2 * sizeof(int32_t), stream);  // {count 0, tag 0}
     if (e != hipSuccess) return e;
   }
-  if (A.need_exact && !A.order_out) {  // fast pass first; the exact pass only where it flagged
+  if (A.need_exact && !A.order_out && !fast_done) {  // fast pass first; the exact pass only where it flagged
     hipError_t e = launch_fast(A, d_scans, d_angles, d_scores, d_out, n_windows, stream);
     if (e != hipSuccess) return e;
   }

@@ -397,6 +397,8 @@ struct csm_ctx {
   int32_t key_sx = -1, key_sy = -1;
 
   csmh::DevBuf pts, scans, angles, scores, partials, best, fin;
+  csmh::DevBuf ang_max;  // the fused fast finish: per (window, angle) max score (csm_tail.hpp)
+  csmh::DevBuf win_ctr;  // ... and per window the waves arrived (zero between launches)
   csmh::DevBuf best_tiles;  // tiled box mode: one best per (window, tile) between the two reductions
   csmh::HostBuf h_search;   // csm_search_windows: pinned staging of the points and angle table
   bool staging_dirty = false;  // a search failed with copies out of its staging possibly in flight
@@ -570,7 +572,7 @@ struct csm_ctx {
   // the one kernel stream: a stream per part measured slower (two concurrent
   // box-kernel launches contend for L2, 1.01 -> 1.57 ms each; profiles/r01).
   struct Slot {
-    csmh::DevBuf scans, angles, scores, partials, best, fin;
+    csmh::DevBuf scans, angles, scores, partials, best, fin, ang_max, win_ctr;
     csmh::HostBuf h_scores, h_fin, h_angles, h_sw, h_angles_next, h_fin_sig;
     csmh::DevBuf fin_sig;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev_done = nullptr, ev_in = nullptr, ev_k = nullptr;
@@ -605,6 +607,8 @@ struct csm_ctx {
     std::swap(partials, a.partials);
     std::swap(best, a.best);
     std::swap(fin, a.fin);
+    std::swap(ang_max, a.ang_max);
+    std::swap(win_ctr, a.win_ctr);
     std::swap(h_scores, a.h_scores);
     std::swap(h_fin, a.h_fin);
     std::swap(h_angles, a.h_angles);

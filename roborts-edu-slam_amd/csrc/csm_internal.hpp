@@ -31,81 +31,13 @@ struct AngleEntry {
   double angle, cosine, sine;
 };
 
-// Launch-uniform description of one level.
-struct LevelWork {
-  int32_t n_angles;
-  int32_t n_space;
-  int64_t n_cand;          // n_angles * n_space^2 per window
-  int32_t blocks_per_scan;
-  int32_t n_scans;
-  double step_cells;       // space_step_factor = res / map_resolution (:548)
-  int32_t use_penalty;
-  int32_t pad0;
-  double dist_gain;        // kDistancePenaltyGain{Coarse,Fine} (:760-761)
-  double size;             // search_space_size (max_distance_bound of :734)
-  double mres;             // map_resolution (scale_factor of :733)
-  const float* grid;       // packed fp32 grid(s), row-major
-  int64_t grid_stride;     // floats between consecutive grids (submaps)
-  int32_t size_x, size_y;
-  float outside;
-  int32_t int_mode;        // 1: accumulate the fixed-point copy gridi exactly
-  const int32_t* gridi;    // value * 2^int_exp, exact (see csm_set_grid)
-  double int_scale;        // 2^-int_exp
-  int32_t outside_i;
-  int32_t n_cols;          // n_angles * n_space (column kernel)
-  int32_t ktiles;          // ceil(n_space / KT)
-  int32_t col_blocks;      // ceil(n_cols / 64)
-  int32_t pitch;           // gridi row pitch in cells (gridi_pitch(size_x))
-  int64_t gridi_stride;    // int32 cells between consecutive gridi grids (pitch * (size_y +
-                           // kGridiPadRows): each grid ends with zero rows)
-  int32_t tile_n;          // box kernel over a large window: tiles per axis (0: untiled)
-  int32_t tile_ns;         // ... and the window's own n_space (candidate indices are its)
-  // The finish's flagged-window list header (FinishArgs::exact_list[0..1]) of
-  // a host-signal launch: block 0 of the scoring kernel, which runs before the
-  // finish on the stream, stores {count 0, clear_tag} there as one 8-byte word
-  // (nullptr: nothing to clear). clear_tag is the launch's flag value: an
-  // exact pass left over from the slot's previous launch (it had nothing to
-  // do, or the host could not have gone on) finds another tag and exits.
-  int32_t* clear_word;
-  int32_t clear_tag;
-  // The palette copy of gridi (score_box_pair_kernel's source): every cell's index
-  // into pal_vals, the grid's distinct fixed-point values (pal_vals[0] = 0,
-  // the outside value), one byte per cell in gridi's layout (row pitch
-  // `pitch` bytes, pal_stride bytes per grid). pal_n = 0: no palette.
-  int32_t pal_n;
-  const uint8_t* pal_grid;
-  const int32_t* pal_vals;
-  int64_t pal_stride;
-  // The strip copies of the palette grid (score_box_pair_kernel, pal_n <=
-  // kPairMaxPal; csm_palette.hip strip_geom): bytes per strip, per copy and
-  // per grid of the stack.
-  const uint8_t* pal_strips;
-  int32_t strip_bytes;
-  int32_t strip_copy_bytes;
-  int64_t strip_grid_bytes;
-  // The strip copies of gridi (score_phase_kernel's strip form; csm_palette.hip
-  // istrip_geom): bytes per strip, per copy and per grid of the stack.
-  const int32_t* istrips;
-  int32_t istrip_bytes;
-  int32_t istrip_copy_bytes;
-  int64_t istrip_grid_bytes;
-};
-
-// Argmax partial: best score of a block and its flat candidate index.
-struct BestPartial {
-  double score;
-  int64_t flat;
-};
-
-constexpr int kBlock = 256;      // 4 waves
-constexpr int kChunk = 1024;     // beams staged in LDS per pass (16 KB)
-
 // ---- device finish (csm_finish.hip) -------------------------------------
 constexpr int kCovPoints = 20;          // kMaxVarianceUsePointSize (:1033)
 constexpr int64_t kFinishMaxCand = 10240;  // windows above this finish on the host (LDS: 160 KB)
 
 struct FinishArgs {
   int64_t n_cand;
+  int64_t score_stride;  // scores between consecutive windows (0: n_cand)
   int32_t n_space;
   // Covariance lists nobody reads (bit 0: positional, bit 1: angular). In the
   // 3-level driver a later level overwrites them (csm_api.cpp live_lists);
@@ -194,6 +126,93 @@ __host__ __device__ inline uint64_t finish_seal_share(uint64_t tag_kind) {
   return finish_piece_hash(kFinishSealPiece, (uint32_t)tag_kind, (uint32_t)(tag_kind >> 32), 0x5EA1u, 0u);
 }
 
+// The fused fast finish (r05, csm_tail.hpp): a scoring launch of the 3-level
+// driver finishes its windows itself. Each (window, angle) wave stores its
+// scores write-through and its angle's max, then counts in on its window; the
+// last to arrive runs the fast finish's decisions for the window and writes
+// its sealed FinishOut (or flags it for the exact pass, as before). The last
+// window of the level-part sets the host flags. No separate fast-pass launch.
+struct TailArgs {
+  int32_t on;
+  int32_t n_windows;   // windows of the level-part (every span of it)
+  int32_t* win_ctr;    // per window: waves arrived (the window's finisher resets it to 0)
+  int32_t* level_ctr;  // windows of the level-part finished (the last one resets it to 0)
+  double* ang_max;     // per (window, angle): the angle's max score, NaN if any score is NaN
+  FinishOut* out;      // FinishOut[n_windows] (pinned host memory with a host signal)
+  FinishArgs A;        // the fast finish's arguments (need_exact, exact_list, host flags, tag)
+};
+
+// Launch-uniform description of one level.
+struct LevelWork {
+  int32_t n_angles;
+  int32_t n_space;
+  int64_t n_cand;          // n_angles * n_space^2 per window
+  int32_t blocks_per_scan;
+  int32_t n_scans;
+  double step_cells;       // space_step_factor = res / map_resolution (:548)
+  int32_t use_penalty;
+  int32_t pad0;
+  double dist_gain;        // kDistancePenaltyGain{Coarse,Fine} (:760-761)
+  double size;             // search_space_size (max_distance_bound of :734)
+  double mres;             // map_resolution (scale_factor of :733)
+  const float* grid;       // packed fp32 grid(s), row-major
+  int64_t grid_stride;     // floats between consecutive grids (submaps)
+  int32_t size_x, size_y;
+  float outside;
+  int32_t int_mode;        // 1: accumulate the fixed-point copy gridi exactly
+  const int32_t* gridi;    // value * 2^int_exp, exact (see csm_set_grid)
+  double int_scale;        // 2^-int_exp
+  int32_t outside_i;
+  int32_t n_cols;          // n_angles * n_space (column kernel)
+  int32_t ktiles;          // ceil(n_space / KT)
+  int32_t col_blocks;      // ceil(n_cols / 64)
+  int32_t pitch;           // gridi row pitch in cells (gridi_pitch(size_x))
+  int64_t gridi_stride;    // int32 cells between consecutive gridi grids (pitch * (size_y +
+                           // kGridiPadRows): each grid ends with zero rows)
+  int32_t tile_n;          // box kernel over a large window: tiles per axis (0: untiled)
+  int32_t tile_ns;         // ... and the window's own n_space (candidate indices are its)
+  // The finish's flagged-window list header (FinishArgs::exact_list[0..1]) of
+  // a host-signal launch: block 0 of the scoring kernel, which runs before the
+  // finish on the stream, stores {count 0, clear_tag} there as one 8-byte word
+  // (nullptr: nothing to clear). clear_tag is the launch's flag value: an
+  // exact pass left over from the slot's previous launch (it had nothing to
+  // do, or the host could not have gone on) finds another tag and exits.
+  int32_t* clear_word;
+  int32_t clear_tag;
+  // The palette copy of gridi (score_box_pair_kernel's source): every cell's index
+  // into pal_vals, the grid's distinct fixed-point values (pal_vals[0] = 0,
+  // the outside value), one byte per cell in gridi's layout (row pitch
+  // `pitch` bytes, pal_stride bytes per grid). pal_n = 0: no palette.
+  int32_t pal_n;
+  const uint8_t* pal_grid;
+  const int32_t* pal_vals;
+  int64_t pal_stride;
+  // The strip copies of the palette grid (score_box_pair_kernel, pal_n <=
+  // kPairMaxPal; csm_palette.hip strip_geom): bytes per strip, per copy and
+  // per grid of the stack.
+  const uint8_t* pal_strips;
+  int32_t strip_bytes;
+  int32_t strip_copy_bytes;
+  int64_t strip_grid_bytes;
+  // The strip copies of gridi (score_phase_kernel's strip form; csm_palette.hip
+  // istrip_geom): bytes per strip, per copy and per grid of the stack.
+  const int32_t* istrips;
+  int32_t istrip_bytes;
+  int32_t istrip_copy_bytes;
+  int64_t istrip_grid_bytes;
+  // the fused fast finish (tail.on = 0: scores only; csm_tail.hpp)
+  TailArgs tail;
+};
+
+// Argmax partial: best score of a block and its flat candidate index.
+struct BestPartial {
+  double score;
+  int64_t flat;
+};
+
+constexpr int kBlock = 256;      // 4 waves
+constexpr int kChunk = 1024;     // beams staged in LDS per pass (16 KB)
+
 constexpr int kFinishWaveScratch = 640;  // bytes of per-wave scratch
 #ifndef CSM_FINISH_WAVES
 #define CSM_FINISH_WAVES 4
@@ -242,9 +261,12 @@ constexpr size_t finish_lds_bytes(int64_t n) { return finish_layout(n).total; }
 // The fast pass (when A.need_exact) and the exact pass on `stream`; with
 // exact_stream (and ev_fast, an event to record) the exact pass runs there,
 // after the fast pass.
+// fast_done: the scoring launches ran the fast pass's decisions themselves
+// (the fused finish, csm_tail.hpp): only the exact pass is launched.
 hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const AngleEntry* d_angles,
                          const double* d_scores, FinishOut* d_out, int32_t n_windows,
-                         hipStream_t stream, hipStream_t exact_stream = nullptr, hipEvent_t ev_fast = nullptr);
+                         hipStream_t stream, hipStream_t exact_stream = nullptr, hipEvent_t ev_fast = nullptr,
+                         bool fast_done = false);
 
 // Launchers (csm_kernels.hip). All enqueue on `stream` and return hipError_t.
 // Column kernel (v2): lane = one (theta, x) column of a window, KT rows (y)

@@ -200,14 +200,17 @@ bool int_mode_ok(const csm_ctx* c, const Dims& D, double f, const std::vector<Wi
   return true;
 }
 
+// stride: scores between consecutive windows (0: n_cand; the fused finish
+// pads each window to whole 128-byte lines, score_stride)
 void fill_scan_work(const Dims& D, const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
-                    const std::vector<int32_t>& grid_index, ScanWork* sw, size_t i0 = 0, size_t i1 = SIZE_MAX) {
+                    const std::vector<int32_t>& grid_index, ScanWork* sw, size_t i0 = 0, size_t i1 = SIZE_MAX,
+                    int64_t stride = 0) {
   for (size_t i = i0; i < std::min(i1, plans.size()); ++i) {
     const WindowPlan& W = plans[i];
     ScanWork& s = sw[i];
     s.pts_off = pt_offsets[i];
     s.angle_off = W.angle_off;
-    s.out_off = (int64_t)i * D.n_cand;
+    s.out_off = (int64_t)i * (stride ? stride : D.n_cand);
     s.n_used = W.n_used;
     s.step = W.step;
     s.divisor = (double)(W.use - 0);
@@ -216,7 +219,7 @@ void fill_scan_work(const Dims& D, const std::vector<WindowPlan>& plans, const s
     s.cx = W.center[0];
     s.cy = W.center[1];
     s.ct = W.center[2];
-    s.reserved = 0;
+    s.reserved = (int32_t)i;  // the window's index in its level (the fused finish's counters)
     s.grid_index = grid_index.empty() ? 0 : grid_index[i];
   }
 }
@@ -397,6 +400,17 @@ int run_windows_small(csm_ctx* c, const csm_param& P, const Dims& D, const Geome
   return wait_run(c, p);
 }
 
+// The fused fast finish (csm_tail.hpp); CSM_TAIL_FINISH=0 builds keep the
+// separate fast-pass launch (A/B).
+#ifndef CSM_TAIL_FINISH
+#define CSM_TAIL_FINISH 1
+#endif
+constexpr bool kTailFinish = CSM_TAIL_FINISH != 0;
+#ifndef CSM_TAIL_MAX_BEAMS
+#define CSM_TAIL_MAX_BEAMS 512
+#endif
+constexpr int kTailMaxBeams = CSM_TAIL_MAX_BEAMS;  // levels summing more beams keep the separate fast pass
+
 int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G,
                 const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
                 const AngleEntry* angles, size_t n_angle_entries,
@@ -486,7 +500,29 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   hipError_t e;
   if ((e = c->h_sw.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipHostMalloc(scans)");
   ScanWork* sw = (ScanWork*)c->h_sw.p;  // pinned staging
-  if (sp.score) fill_scan_work(D, plans, pt_offsets, grid_index, sw, (size_t)w0, (size_t)w1);
+  // Host-signal finish (the device finish with its fast pass): FinishOut goes
+  // straight to coherent pinned memory and the pass that ends last sets a flag
+  // the host spins on; the scoring kernel clears the flagged-window count.
+  const bool sig = c->host_signal && mode == Finish::kDevice && c->fast_finish;
+  // The fused fast finish (csm_tail.hpp): the level's scoring launches finish
+  // their windows themselves, no fast-pass launch. The same decision in every
+  // call of a level (its spans and its finish-only call): every window in
+  // fixed-point range and a kernel that carries the finish. Each window's
+  // scores then start on a 128-byte line of their own (no line is shared by
+  // two windows: a finisher's sc1 loads never find a line another window's
+  // finisher brought into its L2 before that window's scores were stored).
+  // Only for short scoring waves: each wave waits for its write-through score
+  // stores before counting in, which at B = 1081 costs the scoring launches
+  // as much as the separate fast pass costs (r05: +55 / +30 / +43 us on the
+  // box / phase / tiny launches against -32 / -31 / -29 us of fast passes);
+  // at B = 109 the host gets each level's signal ~50 us earlier and the step
+  // shortens.
+  int max_beams = 0;
+  for (const WindowPlan& W : plans) max_beams = std::max(max_beams, (int)W.n_used);
+  const bool tail = kTailFinish && sig && (box || phase || tiny) && max_beams <= kTailMaxBeams &&
+                    (whole ? use_int : int_mode_ok(c, D, f, plans, 0, (size_t)nw));
+  const int64_t stride = tail ? (D.n_cand + 15) / 16 * 16 : D.n_cand;
+  if (sp.score) fill_scan_work(D, plans, pt_offsets, grid_index, sw, (size_t)w0, (size_t)w1, stride);
   LevelWork L = make_level_work(c, P, D, G, nr, use_int);
   L.blocks_per_scan = box_tiled ? D.n_angles : (int32_t)bps;  // per (window, tile) when tiled
   L.tile_n = box_tiled ? tile_n : 0;
@@ -514,16 +550,14 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   L.ktiles = ktiles;
   L.col_blocks = (int32_t)col_blocks;
 
-  // Host-signal finish (the device finish with its fast pass): FinishOut goes
-  // straight to coherent pinned memory and the pass that ends last sets a flag
-  // the host spins on; the scoring kernel clears the flagged-window count.
-  const bool sig = c->host_signal && mode == Finish::kDevice && c->fast_finish;
   int32_t *d_done = nullptr, *d_need = nullptr, *d_list = nullptr;
   int32_t sig_tag = 0;
   if (sig) {
+    // done counter (0) | the fused finish's level counter (32) | need[nw] |
+    // list {count, tag, windows[nw]}
     const size_t o_need = 64, o_list = (o_need + (size_t)nw * 4 + 7) & ~(size_t)7;  // {count, tag}: 8 bytes
     const size_t dbytes = o_list + (size_t)(nw + 2) * 4;
-    if (dbytes > c->fin_sig.cap) {  // the done counter starts at zero; each launch leaves it at zero
+    if (dbytes > c->fin_sig.cap) {  // the counters start at zero; each launch leaves them at zero
       if ((e = c->fin_sig.ensure(dbytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(finish signal)");
       if ((e = hipMemsetAsync(c->fin_sig.p, 0, c->fin_sig.cap, c->stream)) != hipSuccess)
         return c->hip_fail(e, "hipMemsetAsync(finish signal)");
@@ -531,19 +565,80 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     d_done = (int32_t*)c->fin_sig.p;
     d_need = (int32_t*)((char*)c->fin_sig.p + o_need);
     d_list = (int32_t*)((char*)c->fin_sig.p + o_list);
-    L.clear_word = d_list;
-    // A fresh tag per scoring call, put on the list by its scoring kernel;
-    // the finish (the level's last call, which may score nothing itself) uses
-    // the slot's latest one as its flag value. The slot's previous exact pass
-    // (on x_stream) may still be queued when this launch's scoring and fast
-    // pass reuse the list: it had no windows (or the host would not have gone
-    // on), and it finds another tag.
-    if (sp.score) {
+    // The level's first scoring call's block 0 clears the list to {0, tag}
+    // (with the fused finish, the windows' finishers of every span append
+    // after it, csm_tail.hpp)
+    L.clear_word = (sp.score && w0 == 0) ? d_list : nullptr;
+    // A fresh tag per level: its first scoring call draws it, later spans and
+    // the finish (the level's last call, which may score nothing itself) use
+    // the slot's latest one as their flag value. The slot's previous exact
+    // pass (on x_stream) may still be queued when this level's scoring and
+    // fast pass reuse the list: it had no windows (or the host would not have
+    // gone on), and it finds another tag.
+    if (sp.score && w0 == 0) {
       c->list_tag = (int32_t)(++c->flag_seq & 0x7FFFFFFF);
       if (c->list_tag == 0) c->list_tag = (int32_t)(++c->flag_seq & 0x7FFFFFFF);
     }
     sig_tag = c->list_tag;
     L.clear_tag = sig_tag;
+  }
+  // the signalled finish's arguments (the fused finish's and the finish call's)
+  csm::FinishArgs SA{};
+  csm::FinishOut* sig_out = nullptr;
+  int32_t* sig_flag = nullptr;
+  int32_t* sig_fast = nullptr;
+  const int32_t* flags_h = nullptr;
+  int n_flags = 0;
+  if (sig) {
+    SA.n_cand = D.n_cand;
+    SA.score_stride = stride;
+    SA.n_space = D.n_space;
+    SA.step_cells = L.step_cells;
+    SA.lin_tol = P.search_space_resolution / G.mres;
+    SA.skip_lists = skip_lists | own_lists_skip(P.type);
+    SA.need_exact = d_need;
+    SA.exact_list = d_list;
+    SA.done_ctr = d_done;
+    SA.wide_windows = c->fast_wide_windows;
+    // FinishOut[nw] | need[nw] (profiling: the flags the host counts) | flag
+    const size_t out_need = ((size_t)nw * sizeof(csm::FinishOut) + 63) & ~(size_t)63;
+    const size_t out_flag = (out_need + (size_t)nw * sizeof(int32_t) + 63) & ~(size_t)63;
+    if (out_flag + 64 > c->h_fin_sig.cap) {
+      if ((e = c->h_fin_sig.ensure(std::max<size_t>(out_flag + 64, 64 * 1024), hipHostMallocCoherent)) != hipSuccess)
+        return c->hip_fail(e, "hipHostMalloc(finish signal)");
+      std::memset(c->h_fin_sig.p, 0, c->h_fin_sig.cap);
+    }
+    sig_out = (csm::FinishOut*)c->h_fin_sig.p;
+    sig_flag = (int32_t*)((char*)c->h_fin_sig.p + out_flag);
+    if (c->profiling) {  // the fast pass's flags to the host: finish:exact_windows
+      SA.need_exact = (int32_t*)((char*)c->h_fin_sig.p + out_need);
+      flags_h = SA.need_exact;
+      n_flags = nw;
+    }
+    SA.host_flag = sig_flag;
+    SA.flag_value = sig_tag;
+    SA.host_fast_flag = (c->early_complete && c->early_now) ? sig_flag + 8 : nullptr;  // same 64-byte slot
+    sig_fast = SA.host_fast_flag;
+  }
+  if (tail) {
+    L.tail.on = 1;
+    L.tail.n_windows = nw;
+    // the window counters: a buffer of their own, zeroed when it grows and
+    // left at zero by every window's finisher (need and the list, whose
+    // offsets move with nw, hold stale values)
+    if ((size_t)nw * sizeof(int32_t) > c->win_ctr.cap) {
+      if ((e = c->win_ctr.ensure((size_t)nw * sizeof(int32_t))) != hipSuccess)
+        return c->hip_fail(e, "hipMalloc(window counters)");
+      if ((e = hipMemsetAsync(c->win_ctr.p, 0, c->win_ctr.cap, c->stream)) != hipSuccess)
+        return c->hip_fail(e, "hipMemsetAsync(window counters)");
+    }
+    L.tail.win_ctr = (int32_t*)c->win_ctr.p;
+    L.tail.level_ctr = d_done + 8;
+    L.tail.out = sig_out;
+    L.tail.A = SA;
+    if ((e = c->ang_max.ensure((size_t)nw * (size_t)D.n_angles * sizeof(double))) != hipSuccess)
+      return c->hip_fail(e, "hipMalloc(angle maxima)");
+    L.tail.ang_max = (double*)c->ang_max.p;
   }
 
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
@@ -600,17 +695,13 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     c->span_gap = true;
   }
 
-  const int32_t* flags_h = nullptr;
-  int n_flags = 0;
-  csm::FinishOut* sig_out = nullptr;
-  int32_t* sig_flag = nullptr;
-  int32_t* sig_fast = nullptr;
   int32_t sig_value = 0;
   hipStream_t done_stream = c->d2h;
   double tl2 = 0.0;
   if (mode != Finish::kBest) {
     const size_t bytes = (size_t)nw * (size_t)D.n_cand * sizeof(double);
-    if ((e = c->scores.ensure(bytes)) != hipSuccess) return c->hip_fail(e, "hipMalloc(scores)");
+    if ((e = c->scores.ensure((size_t)nw * (size_t)stride * sizeof(double))) != hipSuccess)
+      return c->hip_fail(e, "hipMalloc(scores)");
     const ScanWork* d_sw = (const ScanWork*)c->scans.p + w0;
     if (!sp.score)
       e = hipSuccess;  // scored by earlier calls
@@ -651,40 +742,13 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       if ((e = hipMemcpyAsync(c->h_scores.p, c->scores.p, bytes, hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
         return c->hip_fail(e, "hipMemcpyAsync(scores)");
     } else if (sig) {
-      csm::FinishArgs A{};
-      A.n_cand = D.n_cand;
-      A.n_space = D.n_space;
-      A.step_cells = L.step_cells;
-      A.lin_tol = P.search_space_resolution / G.mres;
-      A.skip_lists = skip_lists | own_lists_skip(P.type);
-      A.need_exact = d_need;
-      A.exact_list = d_list;
-      A.done_ctr = d_done;
-      A.wide_windows = c->fast_wide_windows;
-      // FinishOut[nw] | need[nw] (profiling: the flags the host counts) | flag
-      const size_t out_need = ((size_t)nw * sizeof(csm::FinishOut) + 63) & ~(size_t)63;
-      const size_t out_flag = (out_need + (size_t)nw * sizeof(int32_t) + 63) & ~(size_t)63;
-      if (out_flag + 64 > c->h_fin_sig.cap) {
-        if ((e = c->h_fin_sig.ensure(std::max<size_t>(out_flag + 64, 64 * 1024), hipHostMallocCoherent)) != hipSuccess)
-          return c->hip_fail(e, "hipHostMalloc(finish signal)");
-        std::memset(c->h_fin_sig.p, 0, c->h_fin_sig.cap);
-      }
-      sig_out = (csm::FinishOut*)c->h_fin_sig.p;
-      sig_flag = (int32_t*)((char*)c->h_fin_sig.p + out_flag);
-      if (c->profiling) {  // the fast pass's flags to the host: finish:exact_windows
-        A.need_exact = (int32_t*)((char*)c->h_fin_sig.p + out_need);
-        flags_h = A.need_exact;
-        n_flags = nw;
-      }
-      A.host_flag = sig_flag;
-      A.flag_value = sig_tag;
-      A.host_fast_flag = (c->early_complete && c->early_now) ? sig_flag + 8 : nullptr;  // same 64-byte slot
-      sig_fast = A.host_fast_flag;
-      sig_value = A.flag_value;
+      sig_value = SA.flag_value;
       done_stream = c->x_stream ? c->x_stream : c->stream;
-      if ((e = csm::launch_finish(A, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
-                                  (const double*)c->scores.p, sig_out, nw, c->stream, done_stream, c->ev_fast)) !=
-          hipSuccess)
+      // with the fused finish the scoring launches did the fast pass's work:
+      // only the exact pass is launched, after them
+      if ((e = csm::launch_finish(SA, (const ScanWork*)c->scans.p, (const AngleEntry*)c->angles.p,
+                                  (const double*)c->scores.p, sig_out, nw, c->stream, done_stream, c->ev_fast,
+                                  tail)) != hipSuccess)
         return c->hip_fail(e, "finish_kernel");
       if (c->profiling && done_stream != c->stream && (e = hipEventRecord(c->ev_ft, c->stream)) != hipSuccess)
         return c->hip_fail(e, "hipEventRecord");
@@ -789,6 +853,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   p.timed = c->profiling;
   p.ev0 = c->ev0;
   p.ev1 = c->ev1;
+  // (with the fused finish the fast interval is empty: the scoring time holds it)
   p.ev_fast = (c->profiling && mode == Finish::kDevice && c->fast_finish && c->x_stream) ? c->ev_ft : nullptr;
   if (c->span_gap) {
     p.gap0 = c->ev_g0;

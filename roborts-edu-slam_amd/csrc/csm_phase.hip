@@ -36,6 +36,7 @@
 #include <cstdint>
 
 #include "csm_device.hpp"
+#include "csm_tail.hpp"
 #include "csm_internal.hpp"
 
 namespace csm {
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
   // exactly where an entry ends; the groups past the lists carry 2 * NP
   // (pair NP: a dummy row of psum nobody reads)
   __shared__ uint8_t gtag[kMaxGroups];
-  __shared__ int64_t psum[(NP + 1) * PC];  // per pair, box cell (row, column): the whole scan's sums
+  __shared__ __attribute__((aligned(16))) int64_t psum[(NP + 1) * PC];  // per pair, box cell (row, column): the whole scan's sums
+  static_assert(sizeof(psum) >= tail::kBytesA + tail::kBytesB, "the fused finish's LDS (csm_tail.hpp)");
   __shared__ int8_t oxs[NQ][kPhaseMaxSpace];
 
   const int bid = dev::xcd_remap(blockIdx.x, gridDim.x);
@@ -375,6 +377,8 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
 
   double bs = -1.0e300;
   int64_t bf = INT64_MAX;
+  double lmax = -INFINITY;  // the fused finish (csm_tail.hpp): this lane's max, any NaN
+  bool lnan = false;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int t = lane + 64 * r;
@@ -391,9 +395,16 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
           bf = flat;
         }
       } else {
-        out[S.out_off + flat] = score;
+        tail::store_score(L, out + S.out_off + flat, score);
+        lnan |= score != score;
+        lmax = (score > lmax) ? score : lmax;
       }
     }
+  }
+  if (!BEST && L.tail.on) {
+    __syncthreads();  // psum's last reads are done: the finisher's LDS
+    tail::finish(L, S, angles, out, a, lmax, lnan, reinterpret_cast<char*>(psum),
+                 reinterpret_cast<char*>(psum) + tail::kBytesA);
   }
   if (BEST) {
 #pragma unroll

@@ -24,6 +24,7 @@
 #include <cstdint>
 
 #include "csm_device.hpp"
+#include "csm_tail.hpp"
 #include "csm_internal.hpp"
 
 namespace csm {
@@ -128,6 +129,8 @@ __global__ __launch_bounds__(64) void score_tiny_kernel(LevelWork L, const ScanW
     }
   double bs = -1.0e300;
   int64_t bf = INT64_MAX;
+  double lmax = -INFINITY;  // the fused finish (csm_tail.hpp): this lane's max, any NaN
+  bool lnan = false;
   if (lane < NC) {
     const int j = lane / NS, k = lane - (lane / NS) * NS;
     const double accd = (double)(mine + (int64_t)n_used * L.outside_i) * L.int_scale;
@@ -137,8 +140,15 @@ __global__ __launch_bounds__(64) void score_tiny_kernel(LevelWork L, const ScanW
       bs = score;
       bf = flat;
     } else {
-      out[S.out_off + flat] = score;
+      tail::store_score(L, out + S.out_off + flat, score);
+      lnan = score != score;
+      lmax = score;
     }
+  }
+  if (!BEST && L.tail.on) {
+    __shared__ __attribute__((aligned(16))) char tail_a[tail::kBytesA];
+    __shared__ __attribute__((aligned(16))) char tail_b[tail::kBytesB];
+    tail::finish(L, S, angles, out, a, lmax, lnan, tail_a, tail_b);
   }
   if (BEST) {
 #pragma unroll

@@ -1188,23 +1188,25 @@ def world2000_bench():
     return w, b
 
 
-@pytest.mark.parametrize("quantised", [False, True])
-def test_timed_configuration_against_oracle(world2000_bench, quantised):
+@pytest.mark.parametrize("quantised,levels", [(False, "headline"), (True, "headline"), (False, "sim"), (True, "sim")])
+def test_timed_configuration_against_oracle(world2000_bench, quantised, levels):
     """The configuration bench.py times, with no CSM_* overrides: 4096 scans
     (two parts of 2048 windows), batches queued from pinned host memory
     (csm_load_scans_async) and submitted back to back with the library's
     submitted-batch defaults (first coarse launch whole, 50/50 part split,
     deferred last hand-off). Three different batches, each against the
     oracle bit for bit (scores, poses, covariances); on the 3-value map
-    every level's exact pass has windows."""
+    every level's exact pass has windows. Both beam rules: every beam (B =
+    1081, the headline) and the sim YAML's U = 100 (B = 109), whose levels
+    finish their windows inside the scoring launches (csm_tail.hpp)."""
     import roborts_csm
-    from roborts_csm.params import headline_levels
+    from roborts_csm.params import SIM_YAML_LEVELS, headline_levels
     w, b = world2000_bench
     grid = w.grid
     if quantised:
         grid = np.round(np.asarray(w.grid, dtype=np.float32) * 2.0).astype(np.float32) / np.float32(2.0)
     assert not any(k.startswith("CSM_") for k in os.environ), "the defaults are under test"
-    lv = headline_levels()
+    lv = headline_levels() if levels == "headline" else SIM_YAML_LEVELS
     n = b.init_poses.shape[0]
     eye = np.tile(np.eye(3).reshape(1, 9), (n, 1))
     rng = np.random.default_rng(11)
@@ -1240,6 +1242,12 @@ def test_timed_configuration_against_oracle(world2000_bench, quantised):
             assert np.array_equal(got[k][1], p2), (k, int(np.sum(np.any(got[k][1] != p2, axis=1))))
             assert np.array_equal(got[k][2], c2), (k, int(np.sum(np.any(got[k][2] != c2, axis=1))))
         assert st["score_box_pair_kernel<13,all>"]["launches"] >= 2 * len(scans), st.keys()
+        # the fused finish at B = 109 leaves no fast-pass time; B = 1081 keeps the fast pass
+        fast = sum(k["total_ms"] for nm, k in st.items() if nm.startswith("finish:fast<"))
+        if levels == "sim":
+            assert fast < 0.02 * len(scans) * 6, fast
+        else:
+            assert fast > 0.005 * len(scans) * 6, fast
         if quantised:
             ex = [k for nm, k in st.items() if nm.startswith("finish:exact_windows<")]
             assert len(ex) == 3 and all(k["scorings"] > 0 for k in ex), ex
