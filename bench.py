@@ -49,7 +49,7 @@ sys.path[:0] = [os.path.join(ROOT, "roborts-edu-slam_amd"), os.path.join(ROOT, "
 
 import numpy as np  # noqa: E402
 
-from bench_common import (COUNTERS_JSON, COUNTERS_LC_JSON, _cpu_model, _device,  # noqa: E402,F401
+from bench_common import (COUNTERS_B109_JSON, COUNTERS_JSON, COUNTERS_LC_JSON, _cpu_model, _device,  # noqa: E402,F401
                           _host_threads, host_cpu_share, load_counters, roofline, source_digest,
                           split_roofline, worlds_mod)
 from bench_host import adapter_bench, backend_bench, online_bench  # noqa: E402
@@ -706,6 +706,8 @@ def main():
                          "per-kernel averages equal to the timed steps' launches)")
     ap.add_argument("--counters-json", default=COUNTERS_JSON,
                     help="per-kernel PMC counters per launch (tools/pmc_roofline.sh -> tools/pmc_roofline.py)")
+    ap.add_argument("--counters-b109-json", default=COUNTERS_B109_JSON,
+                    help="the B=109 leg's PMC counters (tools/pmc_roofline.sh with --levels sim)")
     ap.add_argument("--no-b109", action="store_true",
                     help="config2: skip the reference-default B=109 (U=100) line beside the headline")
     ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
@@ -927,6 +929,8 @@ def main():
         dom109, avg109, info109 = dominant_kernel(stats109)
         b109["dominant_kernel"] = {"name": dom109["name"], "avg_ms": avg109,
                                    "share_of_step": dom109["total_ms"] * 1e-3 / e109, **info109}
+        b109["roofline"] = roofline(dom109["name"], avg109, dom109["algorithmic_bytes"] / dom109["launches"],
+                                    load_counters(args.counters_b109_json), args.counters_b109_json)
         b109["kernels"] = stats109
 
     # parity of the timed configuration itself: every rank checks its own

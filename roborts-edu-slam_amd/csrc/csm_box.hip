@@ -443,10 +443,21 @@ constexpr int kPairPD = 2;  // pairs of one slot per step
 #define CSM_PAIR_SEG 576
 #endif
 constexpr int kPairSeg = CSM_PAIR_SEG;
-static_assert(kPairSeg % 64 == 0 && kPairSeg >= 512, "whole 64-beam chunks; the sums' transpose reuses the list");
+static_assert(kPairSeg % 64 == 0 && (kPairSeg + 128) * 4 >= 16 * 16 * 8,
+              "whole 64-beam chunks; the sums' transpose (16 x 16 int64) reuses the run list");
 
+// waves per SIMD the pair kernel's register allocation aims for
+// (__launch_bounds__'s second argument on AMD: minimum waves per execution unit)
+#ifndef CSM_PAIR_WAVES
+#define CSM_PAIR_WAVES 4
+#endif
+#if CSM_PAIR_WAVES > 0
+#define CSM_PAIR_BOUNDS __launch_bounds__(64, CSM_PAIR_WAVES)
+#else
+#define CSM_PAIR_BOUNDS __launch_bounds__(64)
+#endif
 template <int NS, bool BEST>
-__global__ __launch_bounds__(64) void score_box_pair_kernel(LevelWork L, const ScanWork* __restrict__ scans,
+__global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWork* __restrict__ scans,
                                                             const double2* __restrict__ pts,
                                                             const AngleEntry* __restrict__ angles,
                                                             double* __restrict__ out,
