@@ -447,9 +447,12 @@ static_assert(kPairSeg % 64 == 0 && (kPairSeg + 128) * 4 >= 16 * 16 * 8,
               "whole 64-beam chunks; the sums' transpose (16 x 16 int64) reuses the run list");
 
 // waves per SIMD the pair kernel's register allocation aims for
-// (__launch_bounds__'s second argument on AMD: minimum waves per execution unit)
+// (__launch_bounds__'s second argument on AMD: minimum waves per execution unit);
+// 0: the compiler's choice (114 VGPRs). r05 A/B at B = 1081: 4 waves (98
+// VGPRs) made the kernel 0.632 -> 0.734 ms, seg 448 with 5 waves 0.687 ms
+// (profiles/r05/experiments/ab_pair_waves.txt)
 #ifndef CSM_PAIR_WAVES
-#define CSM_PAIR_WAVES 4
+#define CSM_PAIR_WAVES 0
 #endif
 #if CSM_PAIR_WAVES > 0
 #define CSM_PAIR_BOUNDS __launch_bounds__(64, CSM_PAIR_WAVES)
