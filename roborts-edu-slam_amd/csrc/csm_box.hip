@@ -96,8 +96,10 @@ struct BoxWave {
     ly = ae.sine * p.x + ae.cosine * p.y;  // :180
     const double tx = (lx + x_0) + 0.5;
     const double ty = (ly + y_0) + 0.5;
-    const double fx = tx - floor(tx);
-    const double fy = ty - floor(ty);
+    // v_fract_f64: tx - floor(tx), exact below 2^52; it differs (1 - 2^-53 for
+    // 1.0) only for tiny negative t, which the t >= 0 test rejects either way
+    const double fx = __builtin_amdgcn_fract(tx);
+    const double fy = __builtin_amdgcn_fract(ty);
     const bool clean = tx >= 0.0 && ty >= 0.0 && fx >= kBoxMargin && fx <= 1.0 - kBoxMargin &&
                        fy >= kBoxMargin && fy <= 1.0 - kBoxMargin;
     const double lim = -(double)nspan - kBoxMargin;
@@ -459,6 +461,28 @@ static_assert(kPairSeg % 64 == 0 && (kPairSeg + 128) * 4 >= 16 * 16 * 8,
 #else
 #define CSM_PAIR_BOUNDS __launch_bounds__(64)
 #endif
+// 8 x byte B of w (a pair code's byte offset in the 8-byte pair table): one
+// SDWA shift for every byte (the compiler folds byte 0 into the code's OR with
+// a mask and a separate shift, and the OR itself then into two instructions)
+template <int B>
+__device__ __forceinline__ uint32_t byte_x8(uint32_t w) {
+  static_assert(B >= 0 && B < 4, "a byte of a dword");
+  uint32_t r;
+  if constexpr (B == 0)
+    asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+        : "=v"(r) : "v"(w));
+  else if constexpr (B == 1)
+    asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+        : "=v"(r) : "v"(w));
+  else if constexpr (B == 2)
+    asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+        : "=v"(r) : "v"(w));
+  else
+    asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+        : "=v"(r) : "v"(w));
+  return r;
+}
+
 template <int NS, bool BEST>
 __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWork* __restrict__ scans,
                                                             const double2* __restrict__ pts,
@@ -495,9 +519,12 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
   const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)pg >> 32));
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(((uint64_t)phi << 32) | plo), (short)0, (int)L.strip_grid_bytes, 0x00020000);
-  // rows past the box read the last row again (no new lines) and add nothing
+  // rows past the box read the last row again (no new lines); their lanes'
+  // sums are never read (the exchange below takes rows k < NS only)
   const int krow = min(k, NS - 1) * 16;
-  const uint32_t kmask = k < NS ? 0xFFFFFFFFu : 0u;
+  // a box row piece's offset: 16-byte aligned when every row sits at byte 0
+  // of its strip row (kStripShift 1), its low bits the byte phase otherwise
+  constexpr int kPieceMask = kStripShift == 1 ? ~0 : ~15;
 
   double acc[NS];
 #pragma unroll
@@ -568,21 +595,20 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
     if (npad > 0) {
 #endif
       int4 offs = *reinterpret_cast<const int4*>(&pair_off[4 * slot]);  // (A0, B0, A1, B1)
-      uint32_t cnts = (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[2 * slot]) & kmask;
+      uint32_t cnts = (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[2 * slot]);
       v4i dA[kPairPD], dB[kPairPD];
-      dA[0] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.x & ~15), 0, 0);
+      dA[0] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.x & kPieceMask), 0, 0);
       __builtin_amdgcn_sched_barrier(0);  // issued in the order the loop consumes them
-      dB[0] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.y & ~15), 0, 0);
+      dB[0] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.y & kPieceMask), 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      dA[1] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.z & ~15), 0, 0);
+      dA[1] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.z & kPieceMask), 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      dB[1] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.w & ~15), 0, 0);
+      dB[1] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.w & kPieceMask), 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       for (int g = 0; g < npad; g += kStepPairs) {
         // the next step's pairs of this slot (the padding covers the last step's)
         const int4 noffs = *reinterpret_cast<const int4*>(&pair_off[2 * (g + kStepPairs) + 4 * slot]);
-        const uint32_t ncnts =
-            (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[g + kStepPairs + 2 * slot]) & kmask;
+        const uint32_t ncnts = (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[g + kStepPairs + 2 * slot]);
         const int curA[2] = {offs.x, offs.z}, curB[2] = {offs.y, offs.w};
         const int nxtA[2] = {noffs.x, noffs.z}, nxtB[2] = {noffs.y, noffs.w};
 #pragma unroll
@@ -608,10 +634,16 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
                    (__builtin_amdgcn_alignbyte(0u, (uint32_t)xb.w, sb) << sh);
           }
           const double c = (double)((cnts >> (8 * p)) & 0xFFu);
-          dA[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (nxtA[p] & ~15), 0, 0);
-          dB[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (nxtB[p] & ~15), 0, 0);
+          dA[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (nxtA[p] & kPieceMask), 0, 0);
+          dB[p] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (nxtB[p] & kPieceMask), 0, 0);
+          const char* tb = reinterpret_cast<const char*>(tab);
 #pragma unroll
-          for (int j = 0; j < NS; ++j) acc[j] = __builtin_fma(c, tab[(w[j >> 2] >> (8 * (j & 3))) & 0xFF], acc[j]);
+          for (int j = 0; j < NS; ++j) {
+            const uint32_t wj = w[j >> 2];
+            const uint32_t o = (j & 3) == 0 ? byte_x8<0>(wj) : (j & 3) == 1 ? byte_x8<1>(wj)
+                             : (j & 3) == 2 ? byte_x8<2>(wj) : byte_x8<3>(wj);
+            acc[j] = __builtin_fma(c, *reinterpret_cast<const double*>(tb + o), acc[j]);
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
         offs = noffs;

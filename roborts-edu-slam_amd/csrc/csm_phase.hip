@@ -160,8 +160,10 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
     const double tx = (lx + x_0) + 0.5;
     const double ty = (ly + y_0) + 0.5;
     bool ok = tx >= 0.0 && ty >= 0.0;
-    const double fx = tx - floor(tx);
-    const double fy = ty - floor(ty);
+    // v_fract_f64: tx - floor(tx), exact below 2^52; it differs (1 - 2^-53 for
+    // 1.0) only for tiny negative t, which the t >= 0 test rejects either way
+    const double fx = __builtin_amdgcn_fract(tx);
+    const double fy = __builtin_amdgcn_fract(ty);
     const int qx = bucket(fx, ok);
     const int qy = bucket(fy, ok);
     const bool live = cb + lane < lim;
