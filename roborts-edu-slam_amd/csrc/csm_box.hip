@@ -44,11 +44,13 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));
 
 // Rounding argument. Host: every |x_j|, |lx + x_j|, |t_j| < 2^24 cells
 // (use_int's R * 4 * pitch < 2^30, pitch >= 16). With T = lx + x0 + 0.5 (real)
-// and x_j = fl(x0 + j) = x0 + j + d_j, |d_j| <= 2^-29, the computed
+// and x_j = fl(x0 + j) = x0 + j + d_j, |d_j| <= 2^-29, the reference's
 // t_j = fl(fl(lx + x_j) + 0.5) = T + j + E_j with |E_j| <= 3 * 2^-29 < 2^-27.
-// If t_0 >= 0 and frac(t_0) is in [2^-20, 1 - 2^-20], T is more than
-// 2^-20 - 2^-27 > |E_j| from an integer, so trunc(t_j) = floor(T) + j =
-// trunc(t_0) + j for every j; the same for rows.
+// The kernels test t = fl(lx + fl(x0 + 0.5)) = T + E, |E| <= 2^-28 (one add
+// per beam and axis instead of two). If t >= 0 and frac(t) is in
+// [2^-20, 1 - 2^-20], T is positive and more than 2^-20 - 2^-28 > |E_j| from
+// an integer, so trunc(t_j) = floor(T) + j = trunc(t) + j for every j; the
+// same for rows.
 constexpr double kBoxMargin = 0x1p-20;
 
 // Beams per run-list segment: the list of one segment lives in LDS.
@@ -84,6 +86,10 @@ struct BoxWave {
   int cell_shift = 2;  // log2 bytes per cell: 2 for gridi (int32), 0 for the palette grid (bytes)
   int strip_bytes = 0, copy_bytes = 0;  // strip copies (offsets<true>): bytes per strip and per copy
   int nspan = 0;  // candidates per axis of the wave (box_test's far test; 0: off)
+  double hx = x_0 + 0.5, hy = y_0 + 0.5;  // box_test's t, one add per axis (see the rounding argument)
+  // a beam point's byte offset step: full-rate 24-bit multiplies (the host
+  // keeps every scan under 2^24 points: box_points_ok)
+  uint32_t step16 = (uint32_t)step * 16u;
 
   // The box test of one beam point; on success (ix0, iy0) is the box corner.
   // far: every cell the beam reads for this wave's candidates is off the
@@ -94,8 +100,8 @@ struct BoxWave {
                                            bool& far) const {
     lx = ae.cosine * p.x - ae.sine * p.y;  // :179
     ly = ae.sine * p.x + ae.cosine * p.y;  // :180
-    const double tx = (lx + x_0) + 0.5;
-    const double ty = (ly + y_0) + 0.5;
+    const double tx = lx + hx;  // the reference's (lx + x_0) + 0.5 within 2^-27 cells
+    const double ty = ly + hy;
     // v_fract_f64: tx - floor(tx), exact below 2^52; it differs (1 - 2^-53 for
     // 1.0) only for tiny negative t, which the t >= 0 test rejects either way
     const double fx = __builtin_amdgcn_fract(tx);
@@ -123,19 +129,26 @@ struct BoxWave {
     bool far;
     const bool clean = box_test(p, lx, ly, ix0, iy0, far);
     const bool live = cb + lane < n_used;
-    slow |= (uint64_t)(__builtin_amdgcn_ballot_w64(live && !clean && !far) != 0) << min(cb >> 6, 63);
+    const uint64_t rej = __builtin_amdgcn_ballot_w64(live && !clean && !far);
+    if (rej) slow |= 1ull << min(cb >> 6, 63);
     int o;
     if (STRIP) {  // (kStripShift: 4 or 1 cells between copies)
       constexpr int S = kStripShift, LS = S == 4 ? 2 : 0;
       const int c = (-(ix0 >> LS)) & (kStripCopies - 1);
       const int xs = (ix0 & ~(S - 1)) + S * c;
-      o = c * copy_bytes + (xs >> 4) * strip_bytes + iy0 * 16 + (ix0 & (S - 1));
+      // 24-bit products (box_pair_strips_ok: copies of whole 16-byte rows,
+      // copy_bytes / 16 and strip_bytes below 2^24)
+      o = (int)(__umul24((uint32_t)c, (uint32_t)copy_bytes >> 4) << 4) +
+          (int)__umul24((uint32_t)(xs >> 4), (uint32_t)strip_bytes) + iy0 * 16 + (ix0 & (S - 1));
     } else {
       o = iy0 * pitch4 + (ix0 << cell_shift);
     }
     return (live && clean && ix0 < sx && iy0 < sy) ? o : zero_off;
   }
-  __device__ __forceinline__ double2 point(int cb) const { return P[(int64_t)min(cb + lane, n_used - 1) * step]; }
+  __device__ __forceinline__ double2 point(int cb) const {
+    const uint32_t i = (uint32_t)min(cb + lane, n_used - 1);
+    return *reinterpret_cast<const double2*>(reinterpret_cast<const char*>(P) + __umul24(i, step16));
+  }
 
   // Run list of beams [s0, s1): consecutive beams with the same box corner
   // (common: at a few metres, neighbouring beams of a 0.25 deg scanner land in

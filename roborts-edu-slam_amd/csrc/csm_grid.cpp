@@ -215,7 +215,9 @@ int ensure_palette(csm_ctx* c) {
   c->pal_n = (m >= 1 && m <= csm::kPalMax) ? m : 0;
   c->pal_strips_ok = false;
   const csm::StripGeom SG = csm::strip_geom(c->info.size_x, c->info.size_y);
-  if (c->pair_kernel && c->pal_n >= 1 && c->pal_n <= csm::kPairMaxPal && SG.grid_bytes <= INT32_MAX) {
+  // (the pair kernel's strip offsets are 24-bit products: strips under 2^24 bytes)
+  if (c->pair_kernel && c->pal_n >= 1 && c->pal_n <= csm::kPairMaxPal && SG.grid_bytes <= INT32_MAX &&
+      SG.strip_bytes < (1 << 24)) {
     if ((e = c->pal_strips.ensure((size_t)SG.grid_bytes * (size_t)c->n_grids)) != hipSuccess)
       return c->hip_fail(e, "hipMalloc(palette strips)");
     const int64_t idx_stride = (int64_t)c->pitch * (c->info.size_y + csm::kGridiPadRows);

@@ -455,9 +455,12 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     rows_sq = csm::rows_pick_sq(D.n_space, (int)std::floor(span * (1.0 + 1e-9) + 1e-9) + 2);
     if (c->info.size_x < 4 * rows_sq) rows_sq = 0;
   }
+  // the box kernels' beam offsets are 24-bit products (BoxWave::point)
+  bool box_points_ok = true;
+  for (int w = w0; w < w1 && box_points_ok; ++w) box_points_ok = plans[(size_t)w].n_points < (1 << 24);
   // v6 box kernel: whole-cell window step (use_int bounds |t| < 2^24 cells,
   // which its rounding margin needs)
-  const bool box = use_int && c->box_kernel && f == 1.0 && csm::box_supported(D.n_space) &&
+  const bool box = use_int && box_points_ok && c->box_kernel && f == 1.0 && csm::box_supported(D.n_space) &&
                    c->pitch >= c->info.size_x + csm::kGridiPadCols;
   if (box) rows_sq = 0;
   // v11: the box read through the grid's palette (one byte per cell), pairs
@@ -472,7 +475,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   // v6 over 16 x 16 tiles: the argmax of a one-cell-step window wider than 16
   // (loop-closure windows), in place of the column kernel's dword gathers
   const int tile_n = (D.n_space + 15) / 16;
-  const bool box_tiled = !box && best_out && use_int && c->box_kernel && f == 1.0 && D.n_space > 16 &&
+  const bool box_tiled = !box && best_out && use_int && box_points_ok && c->box_kernel && f == 1.0 && D.n_space > 16 &&
                          c->pitch >= c->info.size_x + csm::kGridiPadCols &&
                          (int64_t)nw * tile_n * tile_n * D.n_angles <= INT32_MAX;
   if (box_tiled) rows_sq = 0;
