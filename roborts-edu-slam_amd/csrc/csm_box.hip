@@ -46,11 +46,15 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));
 // (use_int's R * 4 * pitch < 2^30, pitch >= 16). With T = lx + x0 + 0.5 (real)
 // and x_j = fl(x0 + j) = x0 + j + d_j, |d_j| <= 2^-29, the reference's
 // t_j = fl(fl(lx + x_j) + 0.5) = T + j + E_j with |E_j| <= 3 * 2^-29 < 2^-27.
-// The kernels test t = fl(lx + fl(x0 + 0.5)) = T + E, |E| <= 2^-28 (one add
-// per beam and axis instead of two). If t >= 0 and frac(t) is in
-// [2^-20, 1 - 2^-20], T is positive and more than 2^-20 - 2^-28 > |E_j| from
-// an integer, so trunc(t_j) = floor(T) + j = trunc(t) + j for every j; the
-// same for rows.
+// The kernels test t = fl(lx + h), h = fl(fl(x0 + 0.5) + pad) (one add per
+// beam and axis instead of two; pad: the columns the layout holds before the
+// grid's first, 0 but for the pair strips' kStripPadLo), t = T + pad + E with
+// |E| <= 2^-27. If t >= 0 and frac(t) is in [2^-20, 1 - 2^-20], T + pad is
+// positive and T more than 2^-20 - 2^-27 > |E_j| from an integer, so the
+// padded cell of candidate j is floor(T) + j + pad = trunc(t) + j. Without
+// padding that is the reference's trunc(t_j) + pad; with it, a t_j in (-1, 0)
+// (trunc 0) lands on column -1, which repeats column 0, and t_j < -1 on the
+// outside index. The same for rows.
 constexpr double kBoxMargin = 0x1p-20;
 
 // Beams per run-list segment: the list of one segment lives in LDS.
@@ -86,7 +90,10 @@ struct BoxWave {
   int cell_shift = 2;  // log2 bytes per cell: 2 for gridi (int32), 0 for the palette grid (bytes)
   int strip_bytes = 0, copy_bytes = 0;  // strip copies (offsets<true>): bytes per strip and per copy
   int nspan = 0;  // candidates per axis of the wave (box_test's far test; 0: off)
-  double hx = x_0 + 0.5, hy = y_0 + 0.5;  // box_test's t, one add per axis (see the rounding argument)
+  // cells before the grid's first that the layout holds (kStripPadLo in the
+  // pair strips): box corners and t are counted from column / row -pad
+  int pad = 0;
+  double hx = x_0 + 0.5 + pad, hy = y_0 + 0.5 + pad;  // box_test's t, one add per axis (rounding argument)
   // a beam point's byte offset step: full-rate 24-bit multiplies (the host
   // keeps every scan under 2^24 points: box_points_ok)
   uint32_t step16 = (uint32_t)step * 16u;
@@ -108,7 +115,7 @@ struct BoxWave {
     const double fy = __builtin_amdgcn_fract(ty);
     const bool clean = tx >= 0.0 && ty >= 0.0 && fx >= kBoxMargin && fx <= 1.0 - kBoxMargin &&
                        fy >= kBoxMargin && fy <= 1.0 - kBoxMargin;
-    const double lim = -(double)nspan - kBoxMargin;
+    const double lim = (double)(pad - nspan) - kBoxMargin;
     far = nspan > 0 && (tx <= lim || ty <= lim);
     ix0 = clean ? (int)tx : 0;
     iy0 = clean ? (int)ty : 0;
@@ -143,7 +150,7 @@ struct BoxWave {
     } else {
       o = iy0 * pitch4 + (ix0 << cell_shift);
     }
-    return (live && clean && ix0 < sx && iy0 < sy) ? o : zero_off;
+    return (live && clean && ix0 < sx + pad && iy0 < sy + pad) ? o : zero_off;
   }
   __device__ __forceinline__ double2 point(int cb) const {
     const uint32_t i = (uint32_t)min(cb + lane, n_used - 1);
@@ -516,9 +523,9 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
   const AngleEntry ae = angles[S.angle_off + a];
   const int lane = threadIdx.x;
   const int k = lane & 15, slot = lane >> 4;
-  const int zero_off = L.size_y * 16;  // copy 0, strip 0, first zero row
+  const int zero_off = (kStripPadLo + L.size_y) * 16;  // copy 0, strip 0, first zero row
   BoxWave B{S, ae, pts + S.pts_off, S.step, S.n_used, lane, L.size_x, L.size_y, 0, zero_off, S.x0 /* :569 */,
-            S.y0 /* :572 */, 0, L.strip_bytes, L.strip_copy_bytes, NS};
+            S.y0 /* :572 */, 0, L.strip_bytes, L.strip_copy_bytes, NS, kStripPadLo};
   const int n_used = S.n_used;
   // pair table: tab[a | b << sh] = V[a] + V[b]
   const int sh = L.pal_n <= 8 ? 3 : 4;

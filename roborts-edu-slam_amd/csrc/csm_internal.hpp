@@ -342,6 +342,15 @@ constexpr int kStripCopies = CSM_STRIP_COPIES;
 constexpr int kStripShift = kStripW / kStripCopies;
 static_assert(kStripCopies == 4 || kStripCopies == 16, "strip copies: 4 or 16");
 constexpr int kStripPadRows = 16;  // zero rows below the grid (box rows and the zero run's rows)
+// Columns and rows before the grid's first (pair strips): column -1 repeats
+// column 0 and row -1 row 0, the rest hold index 0 (the outside value). The
+// reference truncates toward zero, so a cell coordinate t in (-1, 0) reads
+// cell 0 and t <= -1 reads outside (occu_grid_map.h GetCell's bounds): with
+// this padding a box corner floor(t) >= -kStripPadLo reads what the reference
+// reads, and a beam whose box straddles the grid's low edge stays on the fast
+// path (r05: 10 % of the headline's waves had such beams, 0.8 % of beams,
+// each summed cell by cell before).
+constexpr int kStripPadLo = 16;
 struct StripGeom {
   int32_t rows, n_strips;
   int64_t strip_bytes, copy_bytes, grid_bytes;

@@ -164,9 +164,11 @@ __global__ __launch_bounds__(256) void pal_index_kernel(const int4* __restrict__
 }
 
 // Strip copies of the palette index grid (v11 pair box kernel): copy c holds
-// cell x of row y at byte (x + kStripShift c) of its strip row, strips kStripW bytes
-// wide with their rows contiguous (row y of strip t at (t * rows + y) * 16).
-// One thread writes one 16-byte strip row; cells off the grid are index 0.
+// cell x of row y at byte (x + kStripPadLo + kStripShift c) of its strip row,
+// strips kStripW bytes wide with their rows contiguous (row y of strip t at
+// (t * rows + kStripPadLo + y) * 16). One thread writes one 16-byte strip row;
+// cells off the grid are index 0 but for column -1 and row -1, which repeat
+// column 0 and row 0 (kStripPadLo).
 __global__ __launch_bounds__(256) void pal_strips_kernel(const uint8_t* __restrict__ idx, int pitch, int sx,
                                                          int sy, int rows, int n_strips, int64_t idx_stride,
                                                          int64_t grid_bytes, int n_grids, uint4* __restrict__ out) {
@@ -178,14 +180,14 @@ __global__ __launch_bounds__(256) void pal_strips_kernel(const uint8_t* __restri
     const int c = (int)(r / per_copy);
     const int64_t sr = r - (int64_t)c * per_copy;
     const int t = (int)(sr / rows);
-    const int y = (int)(sr - (int64_t)t * rows);
-    const uint8_t* src = idx + g * idx_stride + (int64_t)y * pitch;
+    const int y = (int)(sr - (int64_t)t * rows) - kStripPadLo;
+    const uint8_t* src = idx + g * idx_stride + (int64_t)max(y, 0) * pitch;
     uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if (y < sy) {
+    if (y >= -1 && y < sy) {
 #pragma unroll
       for (int b = 0; b < 16; ++b) {
-        const int x = kStripW * t + b - kStripShift * c;
-        const uint32_t v = (x >= 0 && x < sx) ? src[x] : 0u;
+        const int x = kStripW * t + b - kStripShift * c - kStripPadLo;
+        const uint32_t v = (x >= -1 && x < sx) ? src[max(x, 0)] : 0u;
         w[b >> 2] |= v << (8 * (b & 3));
       }
     }
@@ -247,9 +249,10 @@ hipError_t launch_build_istrips(const int32_t* gridi, int pitch, int size_x, int
 
 StripGeom strip_geom(int size_x, int size_y) {
   StripGeom G{};
-  G.rows = size_y + kStripPadRows;
-  // a box row piece starts at (ix & ~(S - 1)) + S c <= size_x - 1 + 16 - S in copy c (S = kStripShift)
-  G.n_strips = (size_x + 15 - kStripShift) / kStripW + 1;
+  G.rows = kStripPadLo + size_y + kStripPadRows;
+  // a box row piece starts at (ix & ~(S - 1)) + S c <= kStripPadLo + size_x - 1 + 16 - S
+  // in copy c (S = kStripShift, ix the padded column)
+  G.n_strips = (kStripPadLo + size_x + 15 - kStripShift) / kStripW + 1;
   G.strip_bytes = (int64_t)G.rows * kStripW;
   G.copy_bytes = G.strip_bytes * G.n_strips;
   G.grid_bytes = G.copy_bytes * kStripCopies;

@@ -203,3 +203,39 @@ def test_palette_follows_grid_refresh(f1, pair):
         assert _kernel(g, 0.3, pair) + "<13,all>" in st, st.keys()
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("pair", [True, False])
+def test_palette_low_edge_straddle(f1, pair):
+    """Windows whose boxes straddle the grid's low edges: the reference
+    truncates toward zero, so a cell coordinate in (-1, 0) reads row / column
+    0 and one at or below -1 the outside value. The pair kernel reads such
+    beams from the strips' low-side padding (column -1 repeating column 0,
+    row -1 repeating row 0); row 0 and column 0 hold values found nowhere else,
+    so a padding that repeated the wrong cells would change the scores."""
+    import roborts_csm
+    res = float(f1["resolution"])
+    rng = np.random.default_rng(23)
+    vals = np.array([0.3, 0.375, 0.5, 0.625, 0.75, 0.875, 1.0], dtype=np.float32)
+    g = rng.choice(vals[:5], size=f1["grid"].shape).astype(np.float32)
+    g[0, :] = vals[5]
+    g[:, 0] = vals[6]
+    g[0, 0] = np.float32(0.4375)
+    m = O.Map(g, res, tuple(f1["offset"]))
+    # beam endpoints a few cells around the pose (boxes of 13 x 13 around them)
+    pts = np.ascontiguousarray(rng.uniform(-14.0, 14.0, size=(700, 2)))
+    pts[:40] = np.round(pts[:40] * 4.0) / 4.0  # quarter cells: corners on x0 + 0.5 + k / 4
+    lv = _level(pts.shape[0])
+    cens = []
+    for i in range(12):
+        x = rng.uniform(-8.0, 14.0) if i % 3 else rng.uniform(150.0, 250.0)
+        y = rng.uniform(-8.0, 14.0) if i % 3 != 1 else rng.uniform(150.0, 250.0)
+        cens.append(np.array([x, y, rng.uniform(-np.pi, np.pi)]))
+    cens.append(np.array([6.0, 6.0, 0.0]))  # t on half cells: x0 + 0.5 integral
+    c = _ctx(**({} if pair else {"CSM_KERNEL": "v8"}))
+    try:
+        c.set_grid(roborts_csm.ScanMatchMap(g, res, tuple(f1["offset"]), 0, 1))
+        _check_windows(c, m, pts, lv, cens)
+        assert _kernel(g, 0.3, pair) + "<13,all>" in _stats(c)
+    finally:
+        c.close()
