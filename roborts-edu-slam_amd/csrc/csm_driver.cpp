@@ -503,29 +503,52 @@ int with_slot(csm_ctx* c, const PipeJob& J, int h, F&& f) {
 #ifndef CSM_WINDOW_ORDER  // 0: scan order (A/B builds)
 #define CSM_WINDOW_ORDER 1
 #endif
+// (ranked by a stable LSD radix sort of the 32-bit keys, ties in scan order:
+// std::sort of 2 x 2048 (key, scan) pairs took ~0.1 ms of the submit's way to
+// its first launch, r05)
 void window_order(const Geometry& G, const double* poses, int32_t n, std::vector<int32_t>& out) {
   out.resize((size_t)n);
-  std::vector<std::pair<uint64_t, int32_t>> key((size_t)n);
-  auto spread = [](uint64_t v) {  // 16 bits -> every other bit
+  thread_local std::vector<uint32_t> key, key2;
+  thread_local std::vector<int32_t> idx2;
+  key.resize((size_t)n);
+  key2.resize((size_t)n);
+  idx2.resize((size_t)n);
+  auto spread = [](uint32_t v) {  // 16 bits -> every other bit
     v &= 0xFFFF;
-    v = (v | (v << 8)) & 0x00FF00FFull;
-    v = (v | (v << 4)) & 0x0F0F0F0Full;
-    v = (v | (v << 2)) & 0x33333333ull;
-    v = (v | (v << 1)) & 0x55555555ull;
+    v = (v | (v << 8)) & 0x00FF00FFu;
+    v = (v | (v << 4)) & 0x0F0F0F0Fu;
+    v = (v | (v << 2)) & 0x33333333u;
+    v = (v | (v << 1)) & 0x55555555u;
     return v;
   };
   for (int32_t s = 0; s < n; ++s) {
     double m[3];
     G.to_map(poses + 3 * (size_t)s, m);
     const double qx = std::floor(m[0] / 64.0), qy = std::floor(m[1] / 64.0);
-    const uint64_t ix = (uint64_t)(int64_t)std::max(-32768.0, std::min(32767.0, qx)) + 32768;
-    const uint64_t iy = (uint64_t)(int64_t)std::max(-32768.0, std::min(32767.0, qy)) + 32768;
-    key[(size_t)s] = {spread(ix) | (spread(iy) << 1), s};
+    const uint32_t ix = (uint32_t)((int32_t)std::max(-32768.0, std::min(32767.0, qx)) + 32768);
+    const uint32_t iy = (uint32_t)((int32_t)std::max(-32768.0, std::min(32767.0, qy)) + 32768);
+    key[(size_t)s] = spread(ix) | (spread(iy) << 1);
   }
-  std::sort(key.begin(), key.end());
+  // rank[] in `out` (as scratch) then by 8-bit digits, least significant first
+  std::vector<int32_t>& idx = out;
+  for (int32_t s = 0; s < n; ++s) idx[(size_t)s] = s;
+  for (int shift = 0; shift < 32; shift += 8) {
+    size_t cnt[257] = {0};
+    for (int32_t i = 0; i < n; ++i) ++cnt[((key[(size_t)i] >> shift) & 0xFF) + 1];
+    for (int d = 0; d < 256; ++d) cnt[d + 1] += cnt[d];
+    for (int32_t i = 0; i < n; ++i) {
+      const size_t o = cnt[(key[(size_t)i] >> shift) & 0xFF]++;
+      key2[o] = key[(size_t)i];
+      idx2[o] = idx[(size_t)i];
+    }
+    key.swap(key2);
+    idx.swap(idx2);
+  }
+  // idx holds the ranked scans (4 swaps: back in `out`); rank m -> position (m % 8) * n / 8 + m / 8
+  idx2.assign(idx.begin(), idx.end());
   int32_t pos = 0;
   for (int x = 0; x < 8; ++x)
-    for (int32_t m = x; m < n; m += 8) out[(size_t)pos++] = key[(size_t)m].second;
+    for (int32_t m = x; m < n; m += 8) out[(size_t)pos++] = idx2[(size_t)m];
 }
 
 void job_setup(csm_ctx* c, PipeJob& J, int32_t n_scans, const int64_t* offsets, const csm_param* levels,
@@ -559,15 +582,7 @@ void job_setup(csm_ctx* c, PipeJob& J, int32_t n_scans, const int64_t* offsets, 
   J.resp.assign((size_t)n_scans, 0.0);
   for (auto& row : J.R)
     for (LevelRun& r : row) r.reset();
-  const Geometry G(c->info);
-  for (int h = 0; h < K; ++h) {
-    if (CSM_WINDOW_ORDER) {
-      window_order(G, poses + 3 * (size_t)J.first[h], J.count[h], J.order[h]);
-      J.R[0][h].order = J.R[1][h].order = J.order[h].data();
-    } else {
-      J.order[h].clear();
-    }
-  }
+  for (int h = 0; h < K; ++h) J.order[h].clear();  // (job_begin ranks each part's windows)
 }
 
 int job_skip(const csm_ctx* c, const PipeJob& J, int l) {
@@ -579,6 +594,10 @@ int job_skip(const csm_ctx* c, const PipeJob& J, int l) {
 int job_begin(csm_ctx* c, PipeJob& J, int h) {
   const int32_t s0 = J.first[h];
   J.R[0][h].tag = h;
+  if (CSM_WINDOW_ORDER) {  // here, not in job_setup: part 0's launch goes out before the other parts are ranked
+    window_order(Geometry(c->info), J.poses + 3 * (size_t)s0, J.count[h], J.order[h]);
+    J.R[0][h].order = J.R[1][h].order = J.order[h].data();
+  }
   return with_slot(c, J, h, [&] {
     const int32_t* g = J.scan_grid ? J.scan_grid + s0 : nullptr;
     if (h == 0)
