@@ -368,6 +368,11 @@ bool box_pair_supported(int ns);
 constexpr int kIStripCells = 8;
 constexpr int kIStripCopies = 2;
 constexpr int kIStripPadRows = 16;
+// columns and rows before the grid's first in the phase strips, as
+// kStripPadLo for the pair strips (column -1 repeats column 0, row -1 row 0,
+// the rest outside): a box straddling the low edge stays on the fast path
+// (r05: 6 % of the headline's fine-level waves summed such beams cell by cell)
+constexpr int kIStripPadLo = 16;
 StripGeom istrip_geom(int size_x, int size_y);
 hipError_t launch_build_istrips(const int32_t* gridi, int pitch, int size_x, int size_y, int64_t gridi_stride,
                                 int n_grids, int32_t* out, hipStream_t stream);

@@ -196,8 +196,10 @@ __global__ __launch_bounds__(256) void pal_strips_kernel(const uint8_t* __restri
 }
 
 // Strip copies of gridi (the phase kernel's strip form): copy c holds cell x
-// of row y at cell x + 4c of its 8-cell strip row. One thread per 16-byte half
-// row.
+// of row y at cell x + kIStripPadLo + 4c of its 8-cell strip row, row y at
+// strip row y + kIStripPadLo; column -1 repeats column 0 and row -1 row 0,
+// other cells off the grid are 0 (the outside value). One thread per 16-byte
+// half row.
 __global__ __launch_bounds__(256) void istrips_kernel(const int32_t* __restrict__ gi, int pitch, int sx, int sy,
                                                       int rows, int n_strips, int64_t gi_stride, int64_t grid_ints,
                                                       int n_grids, int4* __restrict__ out) {
@@ -210,14 +212,14 @@ __global__ __launch_bounds__(256) void istrips_kernel(const int32_t* __restrict_
     const int64_t hr = r - (int64_t)c * per_copy;  // half row within the copy
     const int64_t sr = hr >> 1;
     const int t = (int)(sr / rows);
-    const int y = (int)(sr - (int64_t)t * rows);
-    const int x0 = kIStripCells * t + 4 * (int)(hr & 1) - 4 * c;
-    const int32_t* src = gi + g * gi_stride + (int64_t)y * pitch;
+    const int y = (int)(sr - (int64_t)t * rows) - kIStripPadLo;
+    const int x0 = kIStripCells * t + 4 * (int)(hr & 1) - 4 * c - kIStripPadLo;
+    const int32_t* src = gi + g * gi_stride + (int64_t)max(y, 0) * pitch;
     int v[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int x = x0 + b;
-      v[b] = (y < sy && x >= 0 && x < sx) ? src[x] : 0;
+      v[b] = (y >= -1 && y < sy && x >= -1 && x < sx) ? src[max(x, 0)] : 0;
     }
     out[(g * grid_ints + (int64_t)c * per_copy * 4) / 4 + hr] = make_int4(v[0], v[1], v[2], v[3]);
   }
@@ -227,9 +229,10 @@ __global__ __launch_bounds__(256) void istrips_kernel(const int32_t* __restrict_
 
 StripGeom istrip_geom(int size_x, int size_y) {
   StripGeom G{};
-  G.rows = size_y + kIStripPadRows;
-  // a box row starts at cell (ix & ~3) + 4c <= size_x - 1 + 4 in copy c, phase <= 3
-  G.n_strips = (size_x + 3) / kIStripCells + 1;
+  G.rows = kIStripPadLo + size_y + kIStripPadRows;
+  // a box row starts at cell (ix & ~3) + 4c <= kIStripPadLo + size_x - 1 + 4 in
+  // copy c (ix the padded column), phase <= 3
+  G.n_strips = (kIStripPadLo + size_x + 3) / kIStripCells + 1;
   G.strip_bytes = (int64_t)G.rows * kIStripCells * 4;
   G.copy_bytes = G.strip_bytes * G.n_strips;
   G.grid_bytes = G.copy_bytes * kIStripCopies;

@@ -123,7 +123,11 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
   const int pitch4 = L.pitch * 4;
   constexpr int kRowB = kIStripCells * 4;   // strip row bytes
   static_assert(!ST || 4 * NPC <= kIStripCells + 4, "a box row's pieces stay within its strip row and the next");
-  const int zero_off = ST ? sy * kRowB : sy * pitch4;  // first of the zero rows (strip form: copy 0, strip 0)
+  // the strip form counts columns and rows from -kIStripPadLo (t and the box
+  // corner shifted by it: the padding holds what the reference's truncation
+  // reads there)
+  constexpr int kPad = ST ? kIStripPadLo : 0;
+  const int zero_off = ST ? (kPad + sy) * kRowB : sy * pitch4;  // first of the zero rows (strip form: copy 0, strip 0)
   const double2* __restrict__ P = pts + S.pts_off;
   const int step = S.step;
   const int n_used = S.n_used;
@@ -157,8 +161,8 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
   auto classify = [&](const double2 p, int cb, int lim, double& lx, double& ly, bool& rejected) -> int2 {
     lx = ae.cosine * p.x - ae.sine * p.y;  // :179
     ly = ae.sine * p.x + ae.cosine * p.y;  // :180
-    const double tx = (lx + x_0) + 0.5;
-    const double ty = (ly + y_0) + 0.5;
+    const double tx = (lx + x_0) + (0.5 + kPad);  // (a shift by kPad within 2^-28 cells)
+    const double ty = (ly + y_0) + (0.5 + kPad);
     bool ok = tx >= 0.0 && ty >= 0.0;
     // v_fract_f64: tx - floor(tx), exact below 2^52; it differs (1 - 2^-53 for
     // 1.0) only for tiny negative t, which the t >= 0 test rejects either way
@@ -170,12 +174,12 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
     // far: every candidate's cell is off the grid's low side on one axis
     // (t_j = t + j*f <= -1 for all j, with the rounding margin): the beam adds
     // the outside value (zero in gridi) everywhere and skips the exact pass
-    const double lim_far = -1.0 - (NS - 1) * f - 0x1p-20;
+    const double lim_far = kPad - 1.0 - (NS - 1) * f - 0x1p-20;
     const bool far = tx <= lim_far || ty <= lim_far;
     rejected = live && !ok && !far;
     const int ix0 = ok ? (int)tx : 0;
     const int iy0 = ok ? (int)ty : 0;
-    const bool use = live && ok && ix0 < sx && iy0 < sy;
+    const bool use = live && ok && ix0 < sx + kPad && iy0 < sy + kPad;
     int o;
     if (ST) {  // copy c = (ix0 / 4) mod 2 puts cells (ix0 & ~3) .. +7 in one strip row
       const int c = (ix0 >> 2) & 1;

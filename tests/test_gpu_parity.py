@@ -864,6 +864,48 @@ def test_phase_kernel_edge_beams(world2000, margin_log2):
         c.close()
 
 
+def test_phase_kernel_low_edge_straddle(world2000):
+    """Fine-level (v7 phase) windows whose boxes straddle the grid's low edges:
+    the reference truncates toward zero (a cell coordinate in (-1, 0) reads
+    row / column 0, one at or below -1 the outside value); the phase strips
+    hold that in their low-side padding (column -1 repeats column 0, row -1
+    row 0). Row 0 and column 0 carry values found nowhere else. Scores and
+    argmax against the oracle, over the strips and over gridi itself."""
+    w, _ = world2000
+    rng = np.random.default_rng(31)
+    vals = np.array([0.3, 0.375, 0.5, 0.625, 0.75], dtype=np.float32)
+    g = rng.choice(vals, size=(300, 300)).astype(np.float32)
+    g[0, :] = np.float32(0.875)
+    g[:, 0] = np.float32(1.0)
+    g[0, 0] = np.float32(0.4375)
+    res = w.resolution
+    m = O.Map(g, res, (0.0, 0.0))
+    from roborts_csm.params import SIM_YAML_LEVELS
+    pts = np.ascontiguousarray(rng.uniform(-7.0, 7.0, size=(600, 2)))
+    pts[:30] = np.round(pts[:30] * 5.0) / 5.0  # fifth cells: phases on bucket edges
+    lv = SIM_YAML_LEVELS[1].with_(use_point_size=pts.shape[0])
+    centers = [np.array([rng.uniform(-4.0, 8.0), rng.uniform(-4.0, 8.0), rng.uniform(-np.pi, np.pi)])
+               for _ in range(8)]
+    centers += [np.array([2.0, 150.0, 0.3]), np.array([150.0, 1.5, -1.0])]
+    ctxs = [_variant_ctx(None), _variant_ctx(None, CSM_PHASE_STRIPS="0")]
+    for c in ctxs:
+        c.set_grid(_map(g, res, (0.0, 0.0), version=1))
+        c.set_profiling(True)
+    try:
+        for cen in centers:
+            want = O.score_window(m, pts, lv, cen, 11 * 11 * 11)
+            s, flat = O.best_window(m, pts, lv, cen)
+            for c in ctxs:
+                assert np.array_equal(c.score_window(pts, lv, cen), want), cen
+                got = c.best_window(pts, lv, cen)
+                assert got.score == s and got.flat_index == flat, cen
+        names = {k["name"] for k in ctxs[0].kernel_stats()}
+        assert "score_phase_kernel<11,all>" in names and "grid:istrips" in names, names
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 @pytest.mark.parametrize("size,res", [(0.02, 0.01), (0.01, 0.01), (0.03, 0.01), (0.015, 0.005)])
 def test_tiny_kernel_edge_beams(world2000, size, res):
     """v8 tiny-window kernel (spans under one cell: the super-fine level, 3 x 3
