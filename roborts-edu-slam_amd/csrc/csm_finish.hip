@@ -924,6 +924,9 @@ __global__ __launch_bounds__(64 * kWaves) void finish_kernel(FinishArgs A, const
 // 256 candidates per pass), and the window's angle rows sit in LDS for the
 // sequential FindBest sums. T = 1024 for launches of few windows (the
 // reference's single-scan levels), 256 otherwise.
+#ifndef CSM_EXACT_GRID
+#define CSM_EXACT_GRID 512  // blocks of a listed exact pass (they walk the list of flagged windows)
+#endif
 constexpr int kFastCap = 512;      // compacted candidates of step 2
 constexpr int kFastNearCap = 512;  // compacted near-best candidates of step 3
 constexpr int kFastLevels = 8;     // thresholds best - {0.01, 0.02, ..., 0.64}, then everything > bound
@@ -1381,7 +1384,7 @@ hipError_t launch_finish(const FinishArgs& A, const ScanWork* d_scans, const Ang
   if (!A.host_flag) B.flag_value = 0;       // the tag the memset above left
   if (A.order_out) B.need_exact = nullptr;  // the permutation hook always sorts
   if (!listed) B.exact_list = nullptr;
-  const dim3 grid(listed ? std::min(n_windows, 512) : n_windows);
+  const dim3 grid(listed ? std::min(n_windows, CSM_EXACT_GRID) : n_windows);
   hipLaunchKernelGGL(finish_kernel, grid, dim3(64 * kWaves), lds, xs, B, d_scans, d_angles, d_scores, d_out);
   return hipGetLastError();
 }
