@@ -68,6 +68,44 @@ __device__ __forceinline__ double bcast_lane(double v, int l) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
+// Cross-lane sums without the LDS unit (ds_bpermute): DPP within a row of 16
+// lanes, v_permlane16_swap / v_permlane32_swap (CDNA4) across rows. For sums
+// whose order does not matter only: exact integers (the kernels' fixed-point
+// sums, also when held in doubles below 2^53).
+// Lane l's value plus lane (l ^ 16)'s / (l ^ 32)'s: a swap of x with itself
+// leaves (x, partner) in one of the two results and (partner, x) in the other
+// for every lane, so their sum is x + partner in every lane.
+template <bool ROWS32>
+__device__ __forceinline__ uint64_t swap_sum_u64(uint64_t u) {
+  const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+  if constexpr (ROWS32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return (((uint64_t)h[0] << 32) | l[0]) + (((uint64_t)h[1] << 32) | l[1]);
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return (((uint64_t)h[0] << 32) | l[0]) + (((uint64_t)h[1] << 32) | l[1]);
+  }
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t u) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+// The sum of v over the wave, in every lane (two's-complement int64: exact).
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+  uint64_t u = (uint64_t)v;
+  u += dpp_u64<0xB1>(u);   // quad_perm [1,0,3,2]: pairs
+  u += dpp_u64<0x4E>(u);   // quad_perm [2,3,0,1]: quads
+  u += dpp_u64<0x141>(u);  // row_half_mirror: 8 lanes
+  u += dpp_u64<0x140>(u);  // row_mirror: the row of 16
+  u = swap_sum_u64<false>(u);  // two rows
+  u = swap_sum_u64<true>(u);   // the wave
+  return (int64_t)u;
+}
+
 // CSM_TRACE_SMALL builds: wall-clock stamps (100 MHz) of the few-window
 // kernels' phases, min over blocks for slot 0 and max for the others
 // (tools/small_trace.py reads them through csm_debug_small_trace).

@@ -122,9 +122,7 @@ __global__ __launch_bounds__(64) void score_tiny_kernel(LevelWork L, const ScanW
   for (int j = 0; j < NS; ++j)
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
-      int64_t v = acc[j][k] + part[j][k];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      const int64_t v = dev::wave_sum_i64(acc[j][k] + part[j][k]);
       if (lane == j * NS + k) mine = v;
     }
   double bs = -1.0e300;
