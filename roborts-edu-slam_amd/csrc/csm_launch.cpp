@@ -689,6 +689,13 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   // (a signalled launch lets the host go on before its exact pass on
   // x_stream has retired; the list's tag, LevelWork::clear_tag, makes a stale
   // pass exit, so the slot's next scoring need not wait for it)
+  // An event recorded on the kernel stream right before every scoring launch
+  // (ev0 when it is timed): measured, not explained — without it an unprofiled
+  // config-2 step took 2.33-2.43 ms against 2.17-2.20 ms with it (r05,
+  // profiles/r05/experiments/ab_event_before_scoring.txt); the launch follows
+  // the stream's wait on the inputs' copy event (ev_in).
+  if (sp.score && !(c->profiling && w0 == 0) && (e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess)
+    return c->hip_fail(e, "hipEventRecord");
   if (c->profiling && sp.score && w0 == 0 && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess)
     return c->hip_fail(e, "hipEventRecord");
   // a later span: the gap since the first one ends here (only the first gap is

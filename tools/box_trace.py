@@ -24,6 +24,7 @@ import numpy as np  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scans", type=int, default=4096)
+    ap.add_argument("--use-point-size", type=int, default=0, help="the level's U (0: every beam; 100: B = 109)")
     a = ap.parse_args()
     import roborts_csm
     from roborts_csm import _lib, worlds
@@ -34,6 +35,8 @@ def main():
     w = worlds.make_world(2000, 2000, 0.05)
     b = worlds.make_scan_batch(w, a.scans, seed=7)
     lv = headline_levels()[0]
+    if a.use_point_size:
+        lv = lv.with_(use_point_size=a.use_point_size)
     c = roborts_csm.Context(0)
     c.set_grid(roborts_csm.ScanMatchMap(w.grid, w.resolution, w.offset, 0, 1))
     eye = np.tile(np.eye(3).reshape(1, 9), (b.init_poses.shape[0], 1))
