@@ -545,6 +545,7 @@ void window_order(const Geometry& G, const double* poses, int32_t n, std::vector
     idx.swap(idx2);
   }
   // idx holds the ranked scans (4 swaps: back in `out`); rank m -> position (m % 8) * n / 8 + m / 8
+  if (CSM_WINDOW_ORDER == 2) return;  // (A/B: contiguous Morton ranges, each XCD one region)
   idx2.assign(idx.begin(), idx.end());
   int32_t pos = 0;
   for (int x = 0; x < 8; ++x)
