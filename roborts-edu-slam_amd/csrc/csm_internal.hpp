@@ -392,6 +392,12 @@ struct PhaseTable {
   int32_t cells;                               // distinct offsets per axis: max ox + 1
   double lo[kPhaseMaxBuckets], hi[kPhaseMaxBuckets];  // bucket q: lo[q] <= phase <= hi[q]
   int8_t ox[kPhaseMaxBuckets][kPhaseMaxSpace]; // floor(phase + j*f) inside bucket q
+  // Buckets of equal width 1 / nq (f a multiple of 1 / nq, e.g. 0.4 cells: 5):
+  // bucket q = floor(phase * nq) when frac(phase * nq) is in [ulo, uhi]
+  // (phase_table: inside every bucket's [lo, hi] with room for the product's
+  // rounding), five comparisons a bucket fewer per beam and axis
+  int32_t uniform;
+  double ulo, uhi;
 };
 bool phase_supported(int ns, int cells, int nq);
 hipError_t launch_score_phase(const LevelWork& L, const PhaseTable& T, const ScanWork* d_scans, const double* d_pts,

@@ -179,6 +179,23 @@ bool phase_table(double f, int ns, int margin_log2, csm::PhaseTable& T) {
     T.nq++;
   }
   T.cells = cells;
+  if (T.nq > 0) {  // equal-width buckets: the fast form (PhaseTable::uniform)
+    const long double n = (long double)T.nq;
+    long double ulo = 0.0L, uhi = 1.0L;
+    bool uni = true;
+    for (int q = 0; q < T.nq && uni; ++q) {
+      const long double a = (long double)T.lo[q] * n - q, b = (long double)T.hi[q] * n - q;
+      uni = a > 0.0L && a < 0.25L && b > 0.75L && b < 1.0L;
+      ulo = std::max(ulo, a);
+      uhi = std::min(uhi, b);
+    }
+    // (phase * nq in fp64 is within 2^-50 of the real product: 1e-12 covers it)
+    if (uni && uhi - ulo > 0.5L) {
+      T.uniform = 1;
+      T.ulo = std::nextafter((double)(ulo + 1e-12L), 2.0);
+      T.uhi = std::nextafter((double)(uhi - 1e-12L), -1.0);
+    }
+  }
   return T.nq > 0;
 }
 

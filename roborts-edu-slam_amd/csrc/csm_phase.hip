@@ -168,8 +168,18 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
     // 1.0) only for tiny negative t, which the t >= 0 test rejects either way
     const double fx = __builtin_amdgcn_fract(tx);
     const double fy = __builtin_amdgcn_fract(ty);
-    const int qx = bucket(fx, ok);
-    const int qy = bucket(fy, ok);
+    int qx, qy;
+    if (T.uniform) {  // equal-width buckets (PhaseTable::uniform)
+      const double nqd = (double)T.nq;
+      const double sx_ = fx * nqd, sy_ = fy * nqd;
+      const double rx = __builtin_amdgcn_fract(sx_), ry = __builtin_amdgcn_fract(sy_);
+      qx = (int)(sx_ - rx);
+      qy = (int)(sy_ - ry);
+      ok = ok && rx >= T.ulo && rx <= T.uhi && ry >= T.ulo && ry <= T.uhi && qx < T.nq && qy < T.nq;
+    } else {
+      qx = bucket(fx, ok);
+      qy = bucket(fy, ok);
+    }
     const bool live = cb + lane < lim;
     // far: every candidate's cell is off the grid's low side on one axis
     // (t_j = t + j*f <= -1 for all j, with the rounding margin): the beam adds
