@@ -556,7 +556,12 @@ void job_setup(csm_ctx* c, PipeJob& J, int32_t n_scans, const int64_t* offsets, 
                int n_levels, double* poses, double* covs, double* sum, const int32_t* scan_grid, int K, int slot0,
                bool submitted = false) {
   J.K = K;
-  J.first_windows = submitted ? c->first_windows_submit : c->first_windows;
+  // submitted batches split their first span only when the coarse level sums
+  // many beams: below that the step is host-bound and the extra launch costs
+  // more than the shorter planning at the batch boundary (csm_host.hpp)
+  J.first_windows = !submitted ? c->first_windows
+                    : (n_levels > 0 && levels[0].use_point_size > c->first_windows_submit_min_use) ? c->first_windows_submit
+                                                                                                   : 0;
   const int permille = submitted ? c->part0_permille_submit : c->part0_permille;
   J.n_levels = n_levels;
   J.slot0 = slot0;

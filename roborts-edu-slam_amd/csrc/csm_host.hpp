@@ -587,9 +587,15 @@ struct csm_ctx {
   bool skip_dead_lists = true;  // live_lists (CSM_SKIP_DEAD_LISTS=0: every level fills both lists)
   int pipeline_parts = 2;    // parts in flight (CSM_PIPELINE_PARTS: 2..kMaxParts; 2 measured fastest)
   int first_windows = 128;   // level_begin_split: windows the first part's first launch takes (CSM_FIRST_WINDOWS; 0: one launch)
-  // submitted batches (the device has the previous batch's work queued): one
-  // launch (r04 A/B, 2 runs each: 0 10.77 / 10.98, 128 10.39 / 10.41 G scorings/s)
-  int first_windows_submit = 0;  // (CSM_FIRST_WINDOWS sets both)
+  // submitted batches (the device has the previous batch's work queued): a
+  // 512-window first span, so the batch boundary's host planning covers 512
+  // windows instead of the whole part (r05 A/B, 3 interleaved rounds, config-2
+  // ms/step: 0 2.165 / 2.185 / 2.170, 512 2.090 / 2.107 / 2.112, 768 2.105 /
+  // 2.111 / 2.115; r04's 128 was slower than one launch). Only for coarse
+  // levels of use_point_size > 512: B = 109 (use_point_size 100) is host-bound
+  // and measured 1.468 ms one launch against 1.495 split (6 rounds each).
+  int first_windows_submit = 512;  // (CSM_FIRST_WINDOWS sets both, CSM_FIRST_WINDOWS_SUBMIT this one)
+  int first_windows_submit_min_use = 512;
   int span_growth = 4;       // ... and each later span's growth
   void* pipe = nullptr;  // csm_driver.cpp PipeState: submitted batches (csm_scan_matchers_submit)
   bool split_last_handoff = true;  // the last part's hand-off to the last level in two spans
