@@ -97,15 +97,28 @@ def kernel_accounting(stats, elapsed_s: float, steps: int) -> dict:
             "kernel_scorings_per_s": scorings / (main_ms * 1e-3) if main_ms else None}
 
 
-def dominant_kernel(stats):
-    """The scoring or finish kernel with the most device time, and its average
-    launch time as rocprof sees it over whole-part dispatches
+def breakdown_note(elapsed_s: float, steps: int) -> dict:
+    """Where kernel_accounting's figures come from."""
+    return {"ms_per_step": elapsed_s / steps * 1e3, "steps": steps,
+            "how": "a second region of the same steps right after the timed one, HIP events around every "
+                   "launch (the timed region has them around the first level's scoring kernels only)"}
+
+
+def dominant_kernel(stats, timed_stats=None):
+    """The scoring or finish kernel with the most device time in `stats` (the
+    every-launch breakdown), and its average launch time from `timed_stats`
+    (the value's own region, when it timed that kernel) as rocprof sees it over
+    whole-part dispatches
     (`CSM_FIRST_WINDOWS=0`). The first part's coarse level goes out in spans
     ("span2:<name>", each with its own ramp and tail) and the parts differ in
     size (`CSM_PART0_PERMILLE`), so the time is the one-dispatch launches' bytes
     per ms at the mean launch's algorithmic bytes."""
     ks = [s for s in stats if s["name"].startswith(("score_", "finish_kernel"))]
     dom = max(ks, key=lambda s: s["total_ms"])
+    if timed_stats:
+        own = next((s for s in timed_stats if s["name"] == dom["name"]), None)
+        if own is not None:
+            stats, dom = timed_stats, own
     two = next((s for s in stats if s["name"] == "span2:" + dom["name"]), None)
     n1 = dom["launches"] - (two["launches"] if two else 0)
     info = {"launches": dom["launches"], "two_span_launches": two["launches"] if two else 0}
@@ -815,9 +828,12 @@ def main():
         if torch.cuda.is_available():
             torch.cuda.synchronize()
 
-    def timed(lv, warmup, steps, events=True):
+    def timed(lv, warmup, steps, events=2):
         """warmup untimed steps, then exactly `steps` timed ones between
-        barriers; returns (elapsed s, kernel stats, last step's outputs)."""
+        barriers; returns (elapsed s, kernel stats, last step's outputs).
+        events: csm_set_profiling's mode (2: HIP events around the first
+        level's scoring kernels only, the dominant kernel; 1: every launch and
+        finish, for the per-kernel breakdown)."""
         for _ in range(warmup):
             step(lv)
         settle()
@@ -835,7 +851,12 @@ def main():
         return el, st, tuple(np.array(a, copy=True) for a in res)
 
     # the A/B knob CSM_BENCH_NO_EVENTS=1 leaves the HIP events out to price their overhead
-    elapsed, stats, final = timed(levels, args.warmup, args.steps, os.environ.get("CSM_BENCH_NO_EVENTS") != "1")
+    # (CSM_BENCH_EVENTS=1 times every launch inside the value's region, as r05's first builds did)
+    ev_mode = 0 if os.environ.get("CSM_BENCH_NO_EVENTS") == "1" else int(os.environ.get("CSM_BENCH_EVENTS", "2"))
+    elapsed, stats_value, final = timed(levels, args.warmup, args.steps, ev_mode)
+    # the per-kernel breakdown: the same steps once more, every launch timed
+    # (its events add ~50 us of kernel-stream gaps a step, so not in `value`)
+    el_all, stats, _ = timed(levels, 5, args.steps, 1)
     poses = final[1]
     poses_resident = poses.copy()
 
@@ -915,7 +936,8 @@ def main():
     # B=109, driven exactly as the headline (submitted batches, HIP events)
     b109 = None
     if args.levels == "headline" and not args.no_b109:
-        e109, stats109, final109 = timed(SIM_YAML_LEVELS, args.warmup, args.steps)
+        e109, stats109_value, final109 = timed(SIM_YAML_LEVELS, args.warmup, args.steps, ev_mode)
+        e109_all, stats109, _ = timed(SIM_YAML_LEVELS, 5, args.steps, 1)
         if dist is not None:
             e = torch.tensor([e109], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
             dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -925,8 +947,9 @@ def main():
                 "ms_per_step": e109 / args.steps * 1e3, "beams_summed": _beams_summed(batch.offsets, 100),
                 "levels": "sim YAML (U=100 at every level: B=109)",
                 "batches": "submitted back to back, as the headline",
-                **kernel_accounting(stats109, e109, args.steps)}
-        dom109, avg109, info109 = dominant_kernel(stats109)
+                "breakdown": breakdown_note(e109_all, args.steps),
+                **kernel_accounting(stats109, e109_all, args.steps)}
+        dom109, avg109, info109 = dominant_kernel(stats109, stats109_value)
         b109["dominant_kernel"] = {"name": dom109["name"], "avg_ms": avg109,
                                    "share_of_step": dom109["total_ms"] * 1e-3 / e109, **info109}
         b109["roofline"] = roofline(dom109["name"], avg109, dom109["algorithmic_bytes"] / dom109["launches"],
@@ -974,12 +997,12 @@ def main():
         print(json.dumps({"ms_per_step": elapsed / args.steps * 1e3, "events": False}))
         return
     # device kernels only (kernel_accounting: no sub-interval or host phase twice)
-    dom, avg_ms, dom_info = dominant_kernel(stats)
+    dom, avg_ms, dom_info = dominant_kernel(stats, stats_value)
     rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"],
                   load_counters(args.counters_json), args.counters_json)
     rl["launch_time"] = dict(dom_info, source="HIP events on the kernel stream around each one-dispatch "
-                                              "launch of the timed steps")
-    acct = kernel_accounting(stats, elapsed, args.steps)
+                                              "launch of the dominant kernel in the timed steps")
+    acct = {"breakdown": breakdown_note(el_all, args.steps), **kernel_accounting(stats, el_all, args.steps)}
 
     err = np.hypot(*(poses[:, :2] - batch.true_poses[:, :2]).T)
     out = {
@@ -1017,6 +1040,7 @@ def main():
         "single_scan_latency_ms": float(np.median(lat) * 1e3) if lat else None,
         "median_pose_error_m": float(np.median(err)),
         "kernels": stats,
+        "kernels_timed_region": stats_value,
     }
     out["h2d_ms"] = h2d_ms
     if host_inputs is not None:

@@ -319,7 +319,10 @@ int csm_scan_matchers_batch_grids(csm_ctx* ctx, int32_t n_scans, const double* p
                                   double* covs, double* scores);
 
 /* --- measurement ---------------------------------------------------------- */
-/* Turn HIP-event timing of every scoring launch on/off (resets the stats). */
+/* HIP-event timing of scoring launches (resets the stats): 0 off, 1 every
+ * launch and its finish, 2 the 3-level drivers' first-level scoring kernels
+ * only (csm_scan_matchers_loaded / _submit: no events around their finish
+ * passes or later levels). */
 int csm_set_profiling(csm_ctx* ctx, int32_t on);
 /* Copy up to capacity stats; *count = number of distinct kernels seen. */
 int csm_kernel_stats(csm_ctx* ctx, csm_kernel_stat* out, int32_t capacity, int32_t* count);

@@ -618,12 +618,19 @@ int job_begin(csm_ctx* c, PipeJob& J, int h) {
 int job_handoff(csm_ctx* c, PipeJob& J, int l, int h) {
   const int32_t s0 = J.first[h];
   J.R[(l + 1) & 1][h].tag = (l + 1) * 8 + h;
-  return with_slot(c, J, h, [&] {
+  // csm_set_profiling(ctx, 2): the later levels' launches go out without
+  // timing events (their records cost ~50 us of kernel-stream gaps a config-2
+  // step, profiles/r05/experiments/ab_profile_first_level.txt)
+  const bool timed = c->profiling;
+  c->profiling = timed && !c->profile_first_level;
+  const int st = with_slot(c, J, h, [&] {
     return level_end_begin(c, J.R[l & 1][h], J.R[(l + 1) & 1][h], J.count[h], J.offsets + s0, J.levels[l + 1],
                            J.poses + 3 * (size_t)s0, J.covs + 9 * (size_t)s0, J.resp.data() + s0, J.sum + s0,
                            J.scan_grid ? J.scan_grid + s0 : nullptr, job_skip(c, J, l + 1),
                            c->split_last_handoff && h == J.K - 1 && l + 2 == J.n_levels);
   });
+  c->profiling = timed;
+  return st;
 }
 
 // Every level transition of J but the last part's last one, which is left to

@@ -553,6 +553,7 @@ struct csm_ctx {
 
   // per-kernel HIP-event timing (csm_set_profiling / csm_kernel_stats)
   bool profiling = false;
+  bool profile_first_level = false;  // csm_set_profiling(ctx, 2): the 3-level driver times its first level only
   bool stats_dump = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   hipEvent_t ev_ft = nullptr;    // profiling: the fast finish pass ended (timed; ev_fast is not)

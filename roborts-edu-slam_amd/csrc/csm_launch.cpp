@@ -722,6 +722,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     c->span_gap = true;
   }
 
+  // csm_set_profiling(ctx, 2) times the scoring kernel alone: the finish's
+  // events on the kernel stream would add gaps to the value's region
+  const bool time_fin = c->profiling && !c->profile_first_level;
   int32_t sig_value = 0;
   hipStream_t done_stream = c->d2h;
   double tl2 = 0.0;
@@ -777,9 +780,9 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                                   (const double*)c->scores.p, sig_out, nw, c->stream, done_stream, c->ev_fast,
                                   tail)) != hipSuccess)
         return c->hip_fail(e, "finish_kernel");
-      if (c->profiling && done_stream != c->stream && (e = hipEventRecord(c->ev_ft, c->stream)) != hipSuccess)
+      if (time_fin && done_stream != c->stream && (e = hipEventRecord(c->ev_ft, c->stream)) != hipSuccess)
         return c->hip_fail(e, "hipEventRecord");
-      if (c->profiling && (e = hipEventRecord(c->ev2, done_stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+      if (time_fin && (e = hipEventRecord(c->ev2, done_stream)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
     } else {
       csm::FinishArgs A{};
       A.n_cand = D.n_cand;
@@ -803,11 +806,11 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                                   (const double*)c->scores.p, (csm::FinishOut*)c->fin.p, nw, c->stream, fs,
                                   c->ev_fast)) != hipSuccess)
         return c->hip_fail(e, "finish_kernel");
-      if (c->profiling && fs != c->stream && (e = hipEventRecord(c->ev_ft, c->stream)) != hipSuccess)
+      if (time_fin && fs != c->stream && (e = hipEventRecord(c->ev_ft, c->stream)) != hipSuccess)
         return c->hip_fail(e, "hipEventRecord");
-      if (c->profiling && (e = hipEventRecord(c->ev2, fs)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
+      if (time_fin && (e = hipEventRecord(c->ev2, fs)) != hipSuccess) return c->hip_fail(e, "hipEventRecord");
       // with profiling on, the flags come back too: how many windows needed the exact sort
-      const size_t cbytes = fbytes + ((c->profiling && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
+      const size_t cbytes = fbytes + ((time_fin && A.need_exact) ? (size_t)nw * sizeof(int32_t) : 0);
       if ((e = hipEventRecord(c->ev_k, fs)) != hipSuccess || (e = hipStreamWaitEvent(c->d2h, c->ev_k, 0)) != hipSuccess)
         return c->hip_fail(e, "kernels event");
       if ((e = hipMemcpyAsync(c->h_fin.p, c->fin.p, cbytes, hipMemcpyDeviceToHost, c->d2h)) != hipSuccess)
@@ -876,12 +879,12 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   p.alg_bytes = alg_bytes;
   p.scorings = scorings;
   p.finish_bytes = (double)nw * (double)D.n_cand * 8.0;
-  p.device_finish = mode == Finish::kDevice;
+  p.device_finish = mode == Finish::kDevice && time_fin;
   p.timed = c->profiling;
   p.ev0 = c->ev0;
   p.ev1 = c->ev1;
   // (with the fused finish the fast interval is empty: the scoring time holds it)
-  p.ev_fast = (c->profiling && mode == Finish::kDevice && c->fast_finish && c->x_stream) ? c->ev_ft : nullptr;
+  p.ev_fast = (time_fin && mode == Finish::kDevice && c->fast_finish && c->x_stream) ? c->ev_ft : nullptr;
   if (c->span_gap) {
     p.gap0 = c->ev_g0;
     p.gap1 = c->ev_g1;

@@ -402,8 +402,11 @@ class Context:
         self._check(_lib.csm_get_host_plan(self._h, C.byref(p)))
         return p.as_dict()
 
-    def set_profiling(self, on: bool = True):
-        self._check(_lib.csm_set_profiling(self._h, 1 if on else 0))
+    def set_profiling(self, on=True):
+        """True/1: time every scoring launch and finish; 2: the 3-level
+        drivers' first-level scoring kernels only (csm.h csm_set_profiling);
+        False/0: off."""
+        self._check(_lib.csm_set_profiling(self._h, int(on) if on in (0, 1, 2) else (1 if on else 0)))
 
     def kernel_stats(self) -> list[dict]:
         cnt = C.c_int32(0)

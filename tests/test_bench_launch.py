@@ -87,6 +87,12 @@ def test_roofline_launch_time_and_kernel_accounting():
     assert dom["name"] == "score_box_pair_kernel<13,all>"
     # one-dispatch rate 0.8 GB / 0.4 ms = 2 GB/ms; the mean launch is 1.0 GB -> 0.5 ms
     assert abs(avg - 0.5) < 1e-12 and info["two_span_launches"] == 2
+    # the value's own region timed only the first level: its launches give the time
+    first = [dict(stats[0], total_ms=2 * (1.1 + 0.44)), dict(stats[1], total_ms=2.2)]
+    dom2, avg2, _ = bench.dominant_kernel(stats, first)
+    assert dom2["name"] == dom["name"] and abs(avg2 - 0.55) < 1e-12
+    # a timed region without that kernel falls back to the breakdown's
+    assert bench.dominant_kernel(stats, [stats[2]])[1] == avg
     acct = bench.kernel_accounting(stats, elapsed_s=4e-3, steps=2)
     assert abs(acct["kernel_stream_ms_per_step"] - (2.8 + 0.2) / 2) < 1e-12
     assert abs(acct["exact_finish_side_stream_ms_per_step"] - 0.4) < 1e-12

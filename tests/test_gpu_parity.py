@@ -1235,8 +1235,9 @@ def test_timed_configuration_against_oracle(world2000_bench, quantised, levels):
     """The configuration bench.py times, with no CSM_* overrides: 4096 scans
     (two parts of 2048 windows), batches queued from pinned host memory
     (csm_load_scans_async) and submitted back to back with the library's
-    submitted-batch defaults (first coarse launch whole, 50/50 part split,
-    deferred last hand-off). Three different batches, each against the
+    submitted-batch defaults (a 512-window first coarse span at B = 1081,
+    50/50 part split, deferred last hand-off). Three different batches, each
+    against the
     oracle bit for bit (scores, poses, covariances); on the 3-value map
     every level's exact pass has windows. Both beam rules: every beam (B =
     1081, the headline) and the sim YAML's U = 100 (B = 109), whose levels
@@ -1293,6 +1294,19 @@ def test_timed_configuration_against_oracle(world2000_bench, quantised, levels):
         if quantised:
             ex = [k for nm, k in st.items() if nm.startswith("finish:exact_windows<")]
             assert len(ex) == 3 and all(k["scorings"] > 0 for k in ex), ex
+        # the bench's timed region: events around the first level's scoring launches only
+        # (csm_set_profiling mode 2), the same results
+        c.set_profiling(2)
+        c.load_scans(scans[0], b.offsets)
+        again = (np.zeros(n), inits[0].copy(), eye.copy())
+        c.scan_matchers_submit(lv, again[1], again[2], again[0])
+        c.scan_matchers_wait()
+        st2 = {k["name"] for k in c.kernel_stats()}
+        c.set_profiling(False)
+        for g, e in zip(again, want[0]):
+            assert np.array_equal(g, e)
+        assert "score_box_pair_kernel<13,all>" in st2, st2
+        assert not any(nm.startswith(("score_phase", "score_tiny")) for nm in st2), st2
     finally:
         c.close()
         for p in pins:

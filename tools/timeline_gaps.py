@@ -3,7 +3,7 @@
 rocprofv3): the gaps between consecutive kernels of the queue the scoring
 kernels run on, summed by (kernel before, kernel after), per step.
 
-  python tools/timeline_gaps.py gpurun_out/prof/.../run_kernel_trace.csv [steps]
+  python tools/timeline_gaps.py gpurun_out/prof/.../run_kernel_trace.csv [steps] [parts]
 """
 import collections
 import csv
@@ -11,7 +11,7 @@ import sys
 
 
 def short(name):
-    for k in ("score_box_grouped_kernel", "score_box_kernel", "score_phase_kernel", "score_tiny_kernel",
+    for k in ("score_box_pair_kernel", "score_box_grouped_kernel", "score_box_kernel", "score_phase_kernel", "score_tiny_kernel",
               "finish_fast_kernel", "finish_kernel", "fillBuffer", "copyBuffer"):
         if k in name:
             return k
@@ -39,9 +39,13 @@ def main():
     busy = collections.Counter()
     n = 0
     t_total = 0.0
-    for a, b in zip(starts, starts[1:]):
-        n += 1
-        t_total += (int(seq[b]["Start_Timestamp"]) - int(seq[a]["Start_Timestamp"])) / 1e3
+    # steps: tiny-window launches / parts (a step's coarse launches can come
+    # in two spans and the parts interleave across batches)
+    parts = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    a, b = starts[0], starts[-1]
+    n = max(1, sum("score_tiny" in seq[i]["Kernel_Name"] for i in range(a, b)) // parts)
+    t_total = (int(seq[b]["Start_Timestamp"]) - int(seq[a]["Start_Timestamp"])) / 1e3
+    if True:
         for i in range(a, b):
             r, nx = seq[i], seq[i + 1]
             busy[short(r["Kernel_Name"])] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
