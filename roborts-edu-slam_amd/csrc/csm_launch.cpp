@@ -630,7 +630,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     }
     sig_out = (csm::FinishOut*)c->h_fin_sig.p;
     sig_flag = (int32_t*)((char*)c->h_fin_sig.p + out_flag);
-    if (c->profiling) {  // the fast pass's flags to the host: finish:exact_windows
+    if (c->profiling && !c->profile_first_level) {  // the fast pass's flags to the host: finish:exact_windows
       SA.need_exact = (int32_t*)((char*)c->h_fin_sig.p + out_need);
       flags_h = SA.need_exact;
       n_flags = nw;
