@@ -49,9 +49,9 @@ sys.path[:0] = [os.path.join(ROOT, "roborts-edu-slam_amd"), os.path.join(ROOT, "
 
 import numpy as np  # noqa: E402
 
-from bench_common import (COUNTERS_B109_JSON, COUNTERS_JSON, COUNTERS_LC_JSON, _cpu_model, _device,  # noqa: E402,F401
-                          _host_threads, host_cpu_share, load_counters, roofline, source_digest,
-                          split_roofline, worlds_mod)
+from bench_common import (COUNTERS_B109_JSON, COUNTERS_JSON, COUNTERS_LC_JSON, DETAIL_JSON,  # noqa: E402,F401
+                          _cpu_model, _device, _host_threads, emit, host_cpu_share, load_counters, roofline,
+                          source_digest, split_roofline, worlds_mod)
 from bench_host import adapter_bench, backend_bench, online_bench  # noqa: E402
 
 METRIC = "candidate-pose scorings/sec (1081-beam scan, 2000×2000 grid) at 1/2/4/8 GPUs"
@@ -604,9 +604,15 @@ def plumbing_bench(args, rank, world_size, dist, torch):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
         elapsed, units = float(e.item()), float(u.item())
+    # per-kernel tables of config 2's size, so the tests see the compact line
+    # hold its budget with the side file carrying the rest
+    kernels = [{"name": f"kernel<{i}>", "launches": 40, "total_ms": 1.0, "algorithmic_bytes": 0.0, "scorings": 0.0}
+               for i in range(64)]
     return {"metric": "plumbing", "value": units / elapsed, "unit": "steps/s", "n_gpus": world_size,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "rank_units": units}
+            "rank_units": units, "kernels": kernels, "kernels_timed_region": kernels[:20],
+            "b109": {"value": units / elapsed, "unit": "steps/s", "ms_per_step": elapsed / args.steps * 1e3,
+                     "kernels": kernels}}
 
 
 def build_info() -> dict:
@@ -725,6 +731,9 @@ def main():
                     help="config2: skip the reference-default B=109 (U=100) line beside the headline")
     ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
                     help="torch.distributed backend (auto: nccl = RCCL on a GPU box, gloo on CPU)")
+    ap.add_argument("--detail-json", default=DETAIL_JSON,
+                    help="config2 / plumbing: the whole result (per-kernel tables, breakdowns) goes here; "
+                         "the last stdout line is the compact headline ('' = no side file)")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = 30 if args.workload == "config2" else 5
@@ -775,7 +784,10 @@ def main():
                 out["loop_closure_rccl"] = leg
             out["world"] = world_info(dist)
             out["build"] = build_info()
-            print(json.dumps(out))
+            if args.workload == "plumbing":  # the config-2 line's emit path, side file included
+                emit(out, args.detail_json or None)
+            else:
+                print(json.dumps(out))
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
@@ -1059,8 +1071,10 @@ def main():
     out["host_threads"] = host
     out["world"] = world_info(dist)
     out["build"] = build_info()
-    print(json.dumps(out))
-    sys.stdout.flush()
+    # the per-kernel tables and breakdowns go to the side file; the last
+    # stdout line stays under LINE_BUDGET_BYTES (a 24 KB line
+    # was not parsed by the driver)
+    emit(out, args.detail_json or None)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

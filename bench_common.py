@@ -152,6 +152,100 @@ def roofline(kernel: str, avg_ms: float, algorithmic_bytes: float, counters, cou
 
 COUNTERS_SMALL_JSON = os.path.join(ROOT, "profiles", "r05", "counters_small.json")
 
+# The driver reads the LAST stdout line of a bounded tail: r05's 24 KB line
+# (per-kernel tables inlined) was not parsed. The final line keeps the headline
+# keys, the roofline, cpu_baseline, parity and a B=109 summary; everything
+# else goes to a side file (DETAIL_JSON) and is named in the line's "detail".
+LINE_BUDGET_BYTES = 6000
+DETAIL_JSON = os.path.join("gpurun_out", "bench_detail.json")
+_HEADLINE = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+             "scaling", "vs_baseline", "dtype", "data")
+_RL_KEYS = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "hbm_frac", "avg_launch_ms",
+            "algorithmic_bytes_per_launch", "algorithmic_GBs", "waves_per_simd", "wait_frac", "counters_source",
+            "counters_stale", "note")
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if d is not None and k in d}
+
+
+def compact_roofline(rl):
+    """The roofline object of the final line: the binding ceiling plus every
+    ceiling's fraction (the achieved/peak/unit of each stays in the detail)."""
+    if rl is None:
+        return None
+    out = _pick(rl, _RL_KEYS)
+    if rl.get("ceilings"):
+        out["ceiling_fracs"] = {k: v.get("frac") for k, v in rl["ceilings"].items()}
+    return out
+
+
+def _cpu(c):
+    return _pick(c, ("value", "unit", "cores", "kind", "sample"))
+
+
+def compact_line(out: dict, detail_path: str | None = None) -> dict:
+    """The driver-facing line of a config-2 result `out` (bench.py main)."""
+    line = _pick(out, _HEADLINE)
+    cfg = out.get("config") or {}
+    line["config"] = _pick(cfg, ("workload", "levels", "scans_per_gpu", "scorings_per_scan", "parallelism"))
+    if isinstance(cfg.get("beams_summed"), dict):
+        line["config"]["beams_summed"] = _pick(cfg["beams_summed"], ("mean", "use_point_size"))
+    line["roofline"] = compact_roofline(out.get("roofline"))
+    line["cpu_baseline"] = _cpu(out.get("cpu_baseline"))
+    if out.get("cpu_baseline_all_cores"):
+        line["cpu_baseline_all_cores"] = _pick(out["cpu_baseline_all_cores"], ("value", "unit", "cores", "kind"))
+    line["parity"] = _pick(out.get("parity"), ("scans_checked", "mismatches", "ranks"))
+    for k in ("kernel_stream_ms_per_step", "kernel_share_of_step", "single_scan_latency_ms", "median_pose_error_m"):
+        if k in out:
+            line[k] = out[k]
+    if out.get("value_host_inputs"):
+        line["value_host_inputs"] = _pick(out["value_host_inputs"], ("value", "ms_per_step", "same_result_as_resident"))
+    b = out.get("b109")
+    if b:
+        line["b109"] = dict(_pick(b, ("value", "unit", "ms_per_step", "kernel_stream_ms_per_step")),
+                            beams_summed=(b.get("beams_summed") or {}).get("mean"),
+                            roofline=compact_roofline(b.get("roofline")),
+                            parity=_pick(b.get("parity"), ("scans_checked", "mismatches", "ranks")),
+                            cpu_baseline=_cpu(b.get("cpu_baseline")))
+    lc = out.get("loop_closure_rccl")
+    if lc:
+        line["loop_closure_rccl"] = _pick(lc, ("status", "metric", "value", "unit", "ms_per_query", "n_devices",
+                                               "n_devices_requested", "command", "error"))
+        if isinstance(line["loop_closure_rccl"].get("error"), str):
+            line["loop_closure_rccl"]["error"] = line["loop_closure_rccl"]["error"][-600:]
+    for k in ("world", "build", "rank_units"):
+        if k in out:
+            line[k] = out[k]
+    if detail_path:
+        line["detail"] = detail_path
+    return line
+
+
+def emit(out: dict, detail_path: str | None = DETAIL_JSON, compact=compact_line) -> dict:
+    """Write the whole result to `detail_path` (best effort) and print the
+    compact line as the process's last stdout line."""
+    wrote = None
+    if detail_path:
+        try:
+            d = os.path.dirname(detail_path)
+            if d:
+                os.makedirs(d, exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump(out, f)
+            wrote = detail_path
+        except OSError:
+            wrote = None
+    line = compact(out, wrote)
+    s = json.dumps(line)
+    if len(s) > LINE_BUDGET_BYTES:  # never let the line outgrow the driver's tail again
+        for k in ("loop_closure_rccl", "value_host_inputs", "cpu_baseline_all_cores", "median_pose_error_m"):
+            line.pop(k, None)
+        s = json.dumps(line)
+    print(s)
+    sys.stdout.flush()
+    return line
+
 
 def split_roofline(stats, counters_path: str | None = None):
     """Roofline of the few-window path's dominant kernel from HIP-event stats

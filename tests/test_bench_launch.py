@@ -97,3 +97,54 @@ def test_roofline_launch_time_and_kernel_accounting():
     assert abs(acct["kernel_stream_ms_per_step"] - (2.8 + 0.2) / 2) < 1e-12
     assert abs(acct["exact_finish_side_stream_ms_per_step"] - 0.4) < 1e-12
     assert acct["kernel_share_of_step"] <= 1.0
+
+
+def test_compact_line_of_the_r05_result():
+    """the driver could not parse r05's 24 KB line. The
+    whole r05 config-2 result (tests/golden/bench_line_r05.json, the line the
+    r05 build printed) compacts to a last line under the budget that still
+    carries the headline keys, the roofline, cpu_baseline, parity and B=109."""
+    sys.path.insert(0, ROOT)
+    import bench_common as bc
+
+    with open(os.path.join(ROOT, "tests", "golden", "bench_line_r05.json")) as f:
+        full = json.load(f)
+    assert len(json.dumps(full)) > 20000
+    line = bc.compact_line(full, "gpurun_out/bench_detail.json")
+    s = json.dumps(line)
+    assert len(s) <= bc.LINE_BUDGET_BYTES, len(s)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
+              "roofline", "cpu_baseline", "parity", "b109", "build"):
+        assert k in line, k
+    assert line["value"] == full["value"] and line["ms_per_step"] == full["ms_per_step"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert line["roofline"][k] == full["roofline"][k]
+    assert line["cpu_baseline"] == {k: full["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind", "sample")}
+    assert line["parity"]["mismatches"] == 0 and line["parity"]["scans_checked"] > 0
+    b = line["b109"]
+    assert b["value"] == full["b109"]["value"] and b["roofline"]["frac"] == full["b109"]["roofline"]["frac"]
+    assert b["cpu_baseline"]["value"] == full["b109"]["cpu_baseline"]["value"] and b["parity"]["mismatches"] == 0
+    assert "kernels" not in line and "kernels_timed_region" not in line and "kernels" not in b
+
+
+def test_bench_plumbing_last_line_size_and_side_file(tmp_path):
+    """The plumbing mode runs the config-2 emit path: the last stdout line is
+    the compact one (under the budget, headline keys), the per-kernel tables
+    land in the side file."""
+    sys.path.insert(0, ROOT)
+    import bench_common as bc
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    detail = str(tmp_path / "detail.json")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "plumbing", "--steps", "3",
+                        "--detail-json", detail], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    last = [l for l in r.stdout.splitlines() if l.strip()][-1]
+    assert len(last) <= bc.LINE_BUDGET_BYTES
+    out = json.loads(last)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "b109", "world"):
+        assert k in out, k
+    assert "kernels" not in out and out["detail"] == detail
+    with open(detail) as f:
+        full = json.load(f)
+    assert len(full["kernels"]) == 64 and len(full["b109"]["kernels"]) == 64
