@@ -95,7 +95,7 @@ struct BoxWave {
   int pad = 0;
   double hx = x_0 + 0.5 + pad, hy = y_0 + 0.5 + pad;  // box_test's t, one add per axis (rounding argument)
   // a beam point's byte offset step: full-rate 24-bit multiplies (the host
-  // keeps every scan under 2^24 points: box_points_ok)
+  // keeps every scan under 2^24 points and step * 16 under 2^24: box_points_ok)
   uint32_t step16 = (uint32_t)step * 16u;
 
   // The box test of one beam point; on success (ix0, iy0) is the box corner.

@@ -10,10 +10,15 @@ namespace dev {
 
 // XCD-aware, bijective block remap (cdna_hip_programming.md T1): blocks that
 // share a logical neighbourhood (one window) land on one XCD's L2.
-// LevelWork::clear_word: block 0, lane 0 of a scoring kernel clears it.
+// LevelWork::clear_word: block 0, lane 0 of a scoring kernel clears it. An
+// agent-scope store: the fused finish's appends (csm_tail.hpp list_append) on
+// other XCDs wait for it and add to the same word inside this launch, so it
+// must not sit dirty in block 0's XCD L2 (a later write-back would also undo
+// their adds).
 __device__ __forceinline__ void clear_word(const LevelWork& L) {
   if (L.clear_word && blockIdx.x == 0 && threadIdx.x == 0)
-    *reinterpret_cast<uint64_t*>(L.clear_word) = (uint64_t)(uint32_t)L.clear_tag << 32;  // {count 0, tag}
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(L.clear_word), (uint64_t)(uint32_t)L.clear_tag << 32,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // {count 0, tag}
 }
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

@@ -563,6 +563,10 @@ struct csm_ctx {
   hipEvent_t ev_g0 = nullptr, ev_g1 = nullptr;
   bool span_gap = false;
   int32_t list_tag = 0;  // host signal: the tag of the slot's latest scoring call (run_windows)
+  // the fused finish: a level's first span is out but its last window's span
+  // is not (a level that failed on the host between them leaves level_ctr and
+  // the window counters part-counted; the slot's next tail level zeroes them)
+  bool tail_open = false;
   hipEvent_t ev_done = nullptr;  // end of a launch's work (async runs)
   hipEvent_t ev_in = nullptr;    // a launch's inputs are on the device
   hipEvent_t ev_k = nullptr;     // a launch's kernels are done
@@ -581,6 +585,7 @@ struct csm_ctx {
     hipEvent_t ev_fast = nullptr;
     bool span_gap = false;
     int32_t list_tag = 0;
+    bool tail_open = false;
   };
   static constexpr int kMaxParts = 4;
   Slot alt[kMaxParts - 1];
@@ -635,6 +640,7 @@ struct csm_ctx {
     std::swap(ev_g1, a.ev_g1);
     std::swap(span_gap, a.span_gap);
     std::swap(list_tag, a.list_tag);
+    std::swap(tail_open, a.tail_open);
   }
   // profiling: the pool's last job, as "pool:<what>" (total_ms = the first
   // worker's join latency, algorithmic_bytes = the caller's share of the items)

@@ -34,7 +34,8 @@ namespace {
 // LevelWork::clear_word: block 0, lane 0 of a scoring kernel clears it.
 __device__ __forceinline__ void clear_word(const LevelWork& L) {
   if (L.clear_word && blockIdx.x == 0 && threadIdx.x == 0)
-    *reinterpret_cast<uint64_t*>(L.clear_word) = (uint64_t)(uint32_t)L.clear_tag << 32;  // {count 0, tag}
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(L.clear_word), (uint64_t)(uint32_t)L.clear_tag << 32,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // {count 0, tag} (dev::clear_word)
 }
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

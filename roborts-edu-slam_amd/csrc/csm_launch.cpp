@@ -472,9 +472,15 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     rows_sq = csm::rows_pick_sq(D.n_space, (int)std::floor(span * (1.0 + 1e-9) + 1e-9) + 2);
     if (c->info.size_x < 4 * rows_sq) rows_sq = 0;
   }
-  // the box kernels' beam offsets are 24-bit products (BoxWave::point)
+  // the box kernels' beam offsets are 24-bit products (BoxWave::point: the
+  // point index and step * 16 each under 2^24). Over every window of the level,
+  // not this call's span: the fused-finish decision below depends on it and must
+  // be the same in every call of a level (level_ctr counts all of its windows).
   bool box_points_ok = true;
-  for (int w = w0; w < w1 && box_points_ok; ++w) box_points_ok = plans[(size_t)w].n_points < (1 << 24);
+  for (const WindowPlan& W : plans) {
+    box_points_ok = W.n_points < (1 << 24) && (int64_t)W.step * 16 < (1 << 24);
+    if (!box_points_ok) break;
+  }
   // v6 box kernel: whole-cell window step (use_int bounds |t| < 2^24 cells,
   // which its rounding margin needs)
   const bool box = use_int && box_points_ok && c->box_kernel && f == 1.0 && csm::box_supported(D.n_space) &&
@@ -659,6 +665,12 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if ((e = c->ang_max.ensure((size_t)nw * (size_t)D.n_angles * sizeof(double))) != hipSuccess)
       return c->hip_fail(e, "hipMalloc(angle maxima)");
     L.tail.ang_max = (double*)c->ang_max.p;
+    if (sp.score && w0 == 0 && c->tail_open) {  // an earlier level of this slot stopped between spans
+      if ((e = hipMemsetAsync(c->fin_sig.p, 0, c->fin_sig.cap, c->stream)) != hipSuccess ||
+          (e = hipMemsetAsync(c->win_ctr.p, 0, c->win_ctr.cap, c->stream)) != hipSuccess)
+        return c->hip_fail(e, "hipMemsetAsync(stale tail counters)");
+      c->tail_open = false;
+    }
   }
 
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
@@ -755,6 +767,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
       e = csm::launch_score_cols(L, d_sw, (const double*)c->pts.p, (const AngleEntry*)c->angles.p,
                                  (double*)c->scores.p, nullptr, kt, c->stream);
     if (e != hipSuccess) return c->hip_fail(e, "score kernel");
+    if (tail && sp.score) c->tail_open = w1 < nw;  // the level's last window is out: its counters close
     if (sp.score && c->profiling && (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess)
       return c->hip_fail(e, "hipEventRecord");
     if (sp.score && !sp.finish && w0 == 0 && c->profiling && (e = hipEventRecord(c->ev_g0, c->stream)) != hipSuccess)

@@ -148,19 +148,46 @@ int device_numa_node(int device) {
   return s.empty() ? -1 : std::atoi(s.c_str());
 }
 
-// The plan of a context on `device`, local rank `rank` of `world`: every
-// local rank's device is taken to be its rank (the one-process-per-GPU
-// launch, bench.py / torchrun's LOCAL_RANK), or `device` alone when the
-// ranks outnumber the visible devices.
+// The plan of a context on `device`, local rank `rank` of `world`. The local
+// ranks' NUMA nodes: CSM_LOCAL_NUMA (comma-separated, one per local rank) when
+// set; else, when every local rank's device is visible here, local rank r
+// drives device r (the one-process-per-GPU launch, bench.py / torchrun's
+// LOCAL_RANK). When the ranks outnumber the visible devices (each rank's
+// HIP_VISIBLE_DEVICES shows its own GPU only) the peers' nodes are unknown:
+// the plan then keeps this rank's node and thread share but pins nothing,
+// rather than guess which ranks share the node and pin them to overlapping or
+// too-small slices.
 void context_host_plan(int device, int rank, int world, csm_host_plan* out) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
   world = std::max(1, world);
   rank = std::min(std::max(0, rank), world - 1);
   std::vector<int32_t> numa((size_t)world, -1);
-  for (int r = 0; r < world && count > 0; ++r) numa[(size_t)r] = device_numa_node(r % count);
-  numa[(size_t)rank] = device_numa_node(device);
+  bool known = false;
+  if (const char* env = std::getenv("CSM_LOCAL_NUMA")) {
+    int r = 0;
+    for (const char* p = env; *p && r < world; ++r) {
+      numa[(size_t)r] = (int32_t)std::strtol(p, nullptr, 10);
+      while (*p && *p != ',') ++p;
+      if (*p == ',') ++p;
+    }
+    known = r == world;
+  }
+  if (!known && count >= world) {
+    for (int r = 0; r < world; ++r) numa[(size_t)r] = device_numa_node(r);
+    known = true;
+  }
+  if (!known) {
+    std::fill(numa.begin(), numa.end(), -1);
+    numa[(size_t)rank] = device_numa_node(device);
+  }
   host_plan(rank, world, numa.data(), cgroup_quota_cpus(), affinity_cpus(), out);
+  if (!known && world > 1) {
+    // this rank's node CPUs, shared with an unknown number of peers: the
+    // quota's per-rank share of threads, unpinned
+    out->n_cpus = 0;
+    out->threads = std::max(1, std::min(out->threads, (int)std::max<size_t>(1, affinity_cpus().size() / (size_t)world)));
+  }
 }
 
 // Pin the calling (worker) thread to a plan's CPUs; nothing when it has none.

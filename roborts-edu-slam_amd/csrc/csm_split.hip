@@ -48,7 +48,8 @@ __global__ __launch_bounds__(kT) void score_split_kernel(LevelWork L, SplitWork 
   CSM_TS_MIN(0);
   if (blockIdx.x == 0) {
     if (W.clear_word && tid == 0)
-      *reinterpret_cast<uint64_t*>(W.clear_word) = (uint64_t)(uint32_t)W.clear_tag << 32;  // {count 0, tag}
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(W.clear_word), (uint64_t)(uint32_t)W.clear_tag << 32,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // {count 0, tag} (dev::clear_word)
     if (W.inline_window) {
       if (tid == 0) *W.scans_out = W.sw;
       for (int t = tid; t < L.n_angles; t += kT) W.angles_out[t] = W.ang[t];

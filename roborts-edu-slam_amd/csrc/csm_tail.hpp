@@ -108,13 +108,19 @@ __device__ __forceinline__ double wave_max(double v) {
 }
 
 // Append window w to the exact pass's list. Block 0 of the launch clears the
-// header to {0, tag} as its first store (dev::clear_word); an append waits
-// until that clear is visible (in practice it always is: block 0 is dispatched
-// first and a window finishes only after all of its waves), then takes a slot
-// with one atomic add. (A compare-and-swap restart of the header per tag
-// serialised ~250 appends of a super-fine launch: 1.4 ms at B = 109.)
+// header to {0, tag} as its first store, agent-scope (dev::clear_word); an
+// append waits until that clear is visible (in practice it always is: block 0
+// is dispatched first and a window finishes only after all of its waves), then
+// takes a slot with one atomic add. (A compare-and-swap restart of the header
+// per tag serialised ~250 appends of a super-fine launch: 1.4 ms at B = 109.)
+// The wait is bounded (~2^20 sleeps, tens of ms): a clear that never arrives
+// is a broken invariant and traps the launch (an error the host sees) instead
+// of hanging it.
 __device__ __forceinline__ void list_append(int32_t* list, int32_t tag, int32_t w) {
-  while (__hip_atomic_load(list + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) __builtin_amdgcn_s_sleep(2);
+  for (int spins = 0; __hip_atomic_load(list + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag; ++spins) {
+    if (spins == (1 << 20)) __builtin_trap();
+    __builtin_amdgcn_s_sleep(2);
+  }
   const int at = __hip_atomic_fetch_add(list, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   list[2 + at] = w;
 }

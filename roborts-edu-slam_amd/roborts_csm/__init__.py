@@ -261,10 +261,16 @@ class Context:
         pts = np.ascontiguousarray(points_cells, dtype=np.float64).reshape(-1, 2)
         lv = (CsmParam * 3)(*[_as_param(l) for l in levels])
         sc = C.c_double(0.0)
-        self.__dict__.pop("_queued", None)  # csm_scan_matchers loads: queued batches are dropped
+        # csm_scan_matchers loads, dropping queued batches: their arrays stay
+        # referenced until the call (which waits for their uploads) returns
+        queued = self.__dict__.get("_queued")
         self._loaded = (pts, np.array([0, pts.shape[0]], dtype=np.int64))  # it is the loaded set now
-        self._check(_lib.csm_scan_matchers(self._h, _dptr(pts), pts.shape[0], lv, 1 if use_fine else 0,
-                                           _dptr(pose), _dptr(cov), C.byref(sc)))
+        try:
+            self._check(_lib.csm_scan_matchers(self._h, _dptr(pts), pts.shape[0], lv, 1 if use_fine else 0,
+                                               _dptr(pose), _dptr(cov), C.byref(sc)))
+        finally:
+            if queued is not None and self.__dict__.get("_queued") is queued:
+                self.__dict__.pop("_queued", None)
         return sc.value
 
     def scan_match_batch(self, points: np.ndarray, offsets: np.ndarray, param, poses, covs):
@@ -290,11 +296,15 @@ class Context:
         assert covs.dtype == np.float64 and covs.flags.c_contiguous and covs.size == 9 * n
         scores = np.zeros(n)
         lv = (CsmParam * 3)(*[_as_param(l) for l in levels])
-        self.__dict__.pop("_queued", None)  # a synchronous load: queued batches are dropped
+        queued = self.__dict__.get("_queued")  # a synchronous load drops queued batches (after the call)
         self._loaded = (pts, off)  # it is the loaded set now
-        self._check(_lib.csm_scan_matchers_batch(self._h, n, _dptr(pts), _i64ptr(off), lv,
-                                                 1 if use_fine else 0, _dptr(poses), _dptr(covs),
-                                                 _dptr(scores)))
+        try:
+            self._check(_lib.csm_scan_matchers_batch(self._h, n, _dptr(pts), _i64ptr(off), lv,
+                                                     1 if use_fine else 0, _dptr(poses), _dptr(covs),
+                                                     _dptr(scores)))
+        finally:
+            if queued is not None and self.__dict__.get("_queued") is queued:
+                self.__dict__.pop("_queued", None)
         return scores
 
     def load_scans(self, points, offsets):
@@ -302,8 +312,12 @@ class Context:
         pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 2)
         off = np.ascontiguousarray(offsets, dtype=np.int64)
         self._loaded = (pts, off)
-        self.__dict__.pop("_queued", None)  # the library drops queued batches too
-        self._check(_lib.csm_load_scans(self._h, off.size - 1, _dptr(pts), _i64ptr(off)))
+        queued = self.__dict__.get("_queued")  # the library drops queued batches too (after the call)
+        try:
+            self._check(_lib.csm_load_scans(self._h, off.size - 1, _dptr(pts), _i64ptr(off)))
+        finally:
+            if queued is not None and self.__dict__.get("_queued") is queued:
+                self.__dict__.pop("_queued", None)
 
     def load_scans_async(self, points, offsets):
         """Queue a batch (csm_load_scans_async): its upload runs beside the
