@@ -212,6 +212,8 @@ def compact_line(out: dict, detail_path: str | None = None) -> dict:
     if lc:
         line["loop_closure_rccl"] = _pick(lc, ("status", "metric", "value", "unit", "ms_per_query", "n_devices",
                                                "n_devices_requested", "command", "error"))
+        if isinstance(lc.get("verify"), dict):
+            line["loop_closure_rccl"]["same_as_one_device"] = lc["verify"].get("same_as_one_device")
         if isinstance(line["loop_closure_rccl"].get("error"), str):
             line["loop_closure_rccl"]["error"] = line["loop_closure_rccl"]["error"][-600:]
     for k in ("world", "build", "rank_units"):

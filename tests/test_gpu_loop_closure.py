@@ -179,12 +179,17 @@ def test_bench_lc_leg_one_device():
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import tempfile
+    detail = os.path.join(tempfile.mkdtemp(), "detail.json")
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--workload", "plumbing", "--lc-leg",
-                        "--gpus", "1", "--submaps", "24", "--lc-steps", "3", "--steps", "2"],
+                        "--gpus", "1", "--submaps", "24", "--lc-steps", "3", "--steps", "2", "--detail-json", detail],
                        capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    leg = d["loop_closure_rccl"]
+    short = d["loop_closure_rccl"]  # the compact line's summary of the leg
+    assert short["status"] == "ok" and short["n_devices"] == 1 and short["same_as_one_device"] is True, short
+    with open(detail) as f:  # the whole leg: the side file
+        leg = json.load(f)["loop_closure_rccl"]
     assert leg["status"] == "ok", leg
     assert leg["n_devices"] == 1 and leg["submaps_per_device"] == [24] and leg["steps"] == 3
     assert leg["verify"]["same_as_one_device"] is True, leg["verify"]
