@@ -35,12 +35,21 @@ struct LevelRun {
   // the order its windows take the scans in (nullptr: scan order; the
   // 3-level driver's spatial order, window_order)
   const int32_t* order = nullptr;
+  // the plan pass fills each window's ScanWork into the slot's pinned staging
+  // at the launch's score stride (run_windows then skips its serial fill, ~15
+  // us a 2048-window launch) and checks its fixed-point range (int_bad: some
+  // window is out of range; int_known: every window has been planned)
+  ScanWork* sw = nullptr;
+  int64_t sw_stride = 0;
+  int int_bad = 0;
+  bool int_known = false;
   // back to a fresh run, the vectors' capacity kept
   void reset() {
     P = csm_param{};
     D = Dims{};
     scan_of.clear();
-    plans.clear();
+    // (plans keep their elements: level_alloc value-initialises them only for
+    // a level launched in spans, whose unplanned windows the launch reads)
     pt_off.clear();
     grid.clear();
     angles = nullptr;
@@ -55,6 +64,10 @@ struct LevelRun {
     how = nullptr;
     err = 0;
     order = nullptr;
+    sw = nullptr;
+    sw_stride = 0;
+    int_bad = 0;
+    int_known = false;
   }
 };
 
@@ -105,6 +118,8 @@ int level_prepare(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm
   int st = window_dims(P, R.D);
   if (st != CSM_OK) return c->fail(st, "invalid search window parameters");
   R.scan_of.reserve((size_t)n_scans);
+  const bool ready = map_ready(c);
+  int last_n = -1;  // the beam rule's verdict for the last point count (scans mostly share one)
   for (int k = 0; k < n_scans; ++k) {
     const int s = R.order ? R.order[k] : k;
     if (reset) {
@@ -112,38 +127,17 @@ int level_prepare(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm
       if (argmax_flat) argmax_flat[s] = -1;
     }
     const int n = (int)(offsets[s + 1] - offsets[s]);
-    if (!map_ready(c) || n == 0) continue;  // :792-795
-    int step, use, n_used;
-    if (!beam_rule(n, P.use_point_size, step, use, n_used))
-      return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+    if (!ready || n == 0) continue;  // :792-795
+    if (n != last_n) {
+      int step, use, n_used;
+      if (!beam_rule(n, P.use_point_size, step, use, n_used))
+        return c->fail(CSM_ERR_INVALID_ARG, "use_point_size <= 1 with n_points >= 2*use_point_size");
+      last_n = n;
+    }
     R.scan_of.push_back(s);
     if (scan_grid) R.grid.push_back(scan_grid[s]);
   }
   return CSM_OK;
-}
-
-// Room for the level's plans and angle rows (pinned: uploaded by DMA).
-int level_alloc(csm_ctx* c, const int64_t* offsets, LevelRun& R, HostBuf& rows) {
-  const int nw = (int)R.scan_of.size();
-  R.plans.assign((size_t)nw, WindowPlan{});
-  R.pt_off.resize((size_t)nw);
-  for (int i = 0; i < nw; ++i) R.pt_off[(size_t)i] = offsets[R.scan_of[(size_t)i]];
-  const hipError_t he = rows.ensure((size_t)nw * (size_t)R.D.n_angles * sizeof(AngleEntry));
-  if (he != hipSuccess) return c->hip_fail(he, "hipHostMalloc(angles)");
-  R.rows = (AngleEntry*)rows.p;
-  R.angles = R.rows;
-  return CSM_OK;
-}
-
-// Plan window i of a prepared level around the scan's current pose: host
-// libm cos/sin per angle (AngleSearchLookUpTable::UpdateLookUpTable :154-172).
-void level_plan_one(LevelRun& R, const Geometry& G, const int64_t* offsets, const double* poses, int i) {
-  const int s = R.scan_of[(size_t)i];
-  double center[3];
-  G.to_map(poses + 3 * s, center);
-  WindowPlan& W = R.plans[(size_t)i];
-  plan_window_into(R.P, R.D, G, (int)(offsets[s + 1] - offsets[s]), center, R.rows + (size_t)i * (size_t)R.D.n_angles, W);
-  W.angle_off = (int64_t)i * R.D.n_angles;
 }
 
 // Device finish for the front-end windows (and enough of them to fill the
@@ -153,12 +147,61 @@ bool level_device_finish(const csm_ctx* c, const Dims& D, int nw) {
          nw >= c->device_finish_min;
 }
 
+// Room for the level's plans and angle rows (pinned: uploaded by DMA).
+// spans: the level goes out in spans, so its launches read window plans not
+// planned yet (zeroed, as the kernel choice expects); otherwise every plan is
+// written before the launch and the old ones are only resized (value-initialising
+// 2048 plans cost ~20 us of the serial chain, r06).
+int level_alloc(csm_ctx* c, const int64_t* offsets, LevelRun& R, HostBuf& rows, bool spans) {
+  const int nw = (int)R.scan_of.size();
+  if (spans)
+    R.plans.assign((size_t)nw, WindowPlan{});
+  else
+    R.plans.resize((size_t)nw);
+  R.pt_off.resize((size_t)nw);
+  for (int i = 0; i < nw; ++i) R.pt_off[(size_t)i] = offsets[R.scan_of[(size_t)i]];
+  hipError_t he = rows.ensure((size_t)nw * (size_t)R.D.n_angles * sizeof(AngleEntry));
+  if (he != hipSuccess) return c->hip_fail(he, "hipHostMalloc(angles)");
+  R.rows = (AngleEntry*)rows.p;
+  R.angles = R.rows;
+  // this slot's ScanWork staging (run_windows uploads it from c->h_sw; the
+  // slot's previous launch has read it: its level was joined before this plan)
+  if ((he = c->h_sw.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(he, "hipHostMalloc(scans)");
+  R.sw = (ScanWork*)c->h_sw.p;
+  R.sw_stride = score_stride(c, R.D, level_device_finish(c, R.D, nw) ? Finish::kDevice : Finish::kScoresToHost);
+  R.int_bad = 0;
+  R.int_known = false;
+  return CSM_OK;
+}
+
+// Plan window i of a prepared level around the scan's current pose: host
+// libm cos/sin per angle (AngleSearchLookUpTable::UpdateLookUpTable :154-172).
+// Its ScanWork goes straight into the slot's staging, and its fixed-point
+// range is checked (LevelRun::sw, int_bad).
+void level_plan_one(const csm_ctx* c, LevelRun& R, const Geometry& G, const int64_t* offsets, const double* poses,
+                    int i) {
+  const int s = R.scan_of[(size_t)i];
+  double center[3];
+  G.to_map(poses + 3 * s, center);
+  WindowPlan& W = R.plans[(size_t)i];
+  plan_window_into(R.P, R.D, G, (int)(offsets[s + 1] - offsets[s]), center, R.rows + (size_t)i * (size_t)R.D.n_angles, W);
+  W.angle_off = (int64_t)i * R.D.n_angles;
+  if (R.sw)
+    fill_scan_work_one(R.D, W, R.pt_off[(size_t)i], R.grid.empty() ? 0 : R.grid[(size_t)i], (size_t)i, R.sw_stride,
+                       R.sw[i]);
+  if (!int_mode_window_ok(c, R.D, R.P.search_space_resolution / G.mres, W))
+    __atomic_store_n(&R.int_bad, 1, __ATOMIC_RELAXED);
+}
+
 // Enqueue a planned level, or a span of it (nothing waits).
 int level_launch(csm_ctx* c, LevelRun& R, WinSpan sp = WinSpan{}) {
   const int nw = (int)R.scan_of.size();
   const Dims& D = R.D;
   const Geometry G(c->info);
   R.dev = level_device_finish(c, D, nw);
+  sp.sw_ready = R.sw;
+  sp.sw_stride = R.sw_stride;
+  sp.int_all = R.int_known && !__atomic_load_n(&R.int_bad, __ATOMIC_RELAXED);
   const int st = run_windows(c, R.P, D, G, R.plans, R.pt_off, R.angles, (size_t)nw * (size_t)D.n_angles, R.grid,
                              nullptr, R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend, R.skip_lists, sp);
   if (st != CSM_OK || !sp.finish) return st;
@@ -175,10 +218,12 @@ int level_begin(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const csm_p
   const int nw = (int)R.scan_of.size();
   if (nw == 0) return CSM_OK;
   const double t0 = now_ms();
-  if ((st = level_alloc(c, offsets, R, c->h_angles)) != CSM_OK) return st;
+  if ((st = level_alloc(c, offsets, R, c->h_angles, false)) != CSM_OK) return st;
   const Geometry G(c->info);
   const int threads = (nw >= 64) ? c->host_threads : 1;
-  c->parallel_for(nw, threads, [&](int i) { level_plan_one(R, G, offsets, poses, i); });
+  if (c->profiling) c->account("host:plan:alloc", (float)(now_ms() - t0), 0.0, 0.0);
+  c->parallel_for(nw, threads, [&](int i) { level_plan_one(c, R, G, offsets, poses, i); });
+  R.int_known = true;
   if (threads > 1) c->account_pool("plan");
   const double t1 = now_ms();
   if ((st = level_launch(c, R)) != CSM_OK) return st;
@@ -210,7 +255,7 @@ int level_begin_split(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const
   if (first <= 0 || nw < 2 * first || !level_device_finish(c, R.D, nw))
     return level_begin(c, n_scans, offsets, P, poses, responses, nullptr, R, scan_grid, skip_lists);
   const double t0 = now_ms();
-  if ((st = level_alloc(c, offsets, R, c->h_angles)) != CSM_OK) return st;
+  if ((st = level_alloc(c, offsets, R, c->h_angles, true)) != CSM_OK) return st;
   const Geometry G(c->info);
   if (c->profiling) c->account("host:first:prepare+alloc", (float)(now_ms() - t_in), 0.0, 0.0);
   int w0 = 0;
@@ -218,7 +263,8 @@ int level_begin_split(csm_ctx* c, int32_t n_scans, const int64_t* offsets, const
     // the last span takes the rest when it would leave less than a span behind
     const int w1 = (nw - w0 <= 2 * sz) ? nw : w0 + (int)sz;
     const double tp = now_ms();
-    c->parallel_for(w1 - w0, c->host_threads, [&](int i) { level_plan_one(R, G, offsets, poses, w0 + i); });
+    c->parallel_for(w1 - w0, c->host_threads, [&](int i) { level_plan_one(c, R, G, offsets, poses, w0 + i); });
+    R.int_known = w1 == nw;
     c->account_pool("plan");
     if (c->profiling && w0 == 0) c->account("host:first:plan", (float)(now_ms() - tp), 0.0, 0.0);
     if ((st = level_launch(c, R, WinSpan{w0, w1, true, false})) != CSM_OK) return st;
@@ -367,8 +413,10 @@ int level_end(csm_ctx* c, LevelRun& R, double* poses, double* covs, double* resp
 int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const int64_t* offsets,
                     const csm_param& P, double* poses, double* covs, double* responses, double* sum,
                     const int32_t* scan_grid, int skip_lists, bool split = false) {
+  const double tq = c->profiling ? now_ms() : 0.0;
   int st = level_prepare(c, n_scans, offsets, P, responses, nullptr, N, scan_grid, skip_lists, false);
   if (st != CSM_OK) return st;
+  if (c->profiling) c->account("host:transition:prepare", (float)(now_ms() - tq), 0.0, 0.0);
   const int nw = (int)R.scan_of.size();
   if (N.scan_of != R.scan_of || nw == 0) {  // not the same windows: one after the other
     if ((st = level_end(c, R, poses, covs, responses, nullptr)) != CSM_OK) return st;
@@ -379,17 +427,17 @@ int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const
   if ((st = early ? level_wait_fast(c, R) : level_join(c, R)) != CSM_OK) return st;
   const double t2 = now_ms();
   std::swap(c->h_angles, c->h_angles_next);
-  if ((st = level_alloc(c, offsets, N, c->h_angles)) != CSM_OK) return st;
+  split = split && early && nw >= c->split_handoff_min && level_device_finish(c, N.D, nw);
+  if ((st = level_alloc(c, offsets, N, c->h_angles, split)) != CSM_OK) return st;
   const Geometry G(c->info);
   const int threads = (nw >= 64) ? c->host_threads : 1;
   auto one = [&](int i, bool defer) {
     if (!level_complete_one(R, G, poses, covs, responses, nullptr, i, defer)) return false;
     const int s = R.scan_of[(size_t)i];
     sum[s] += responses[s];
-    level_plan_one(N, G, offsets, poses, i);
+    level_plan_one(c, N, G, offsets, poses, i);
     return true;
   };
-  split = split && early && nw >= c->split_handoff_min && level_device_finish(c, N.D, nw);
   if (split) {  // [0, h) completed, planned and scored while [h, nw) is completed and planned
     const int h = nw / 2;
     std::vector<int> owed((size_t)nw);
@@ -414,6 +462,7 @@ int level_end_begin(csm_ctx* c, LevelRun& R, LevelRun& N, int32_t n_scans, const
     c->parallel_for(nw, threads, [&](int i) { one(i, false); });
   }
   if ((st = level_check(c, R)) != CSM_OK) return st;
+  N.int_known = true;  // every window of N planned
   if (threads > 1) c->account_pool("complete+plan");
   const double t3 = now_ms();
   if (split) {

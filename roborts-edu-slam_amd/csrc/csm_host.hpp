@@ -710,7 +710,19 @@ enum class Finish { kScoresToHost, kDevice, kBest };
 struct WinSpan {
   int w0 = 0, w1 = -1;  // w1 < 0: every window
   bool score = true, finish = true;
+  // the caller's plan pass filled the windows' ScanWork into the slot's
+  // staging (c->h_sw, this pointer) at sw_stride, and found every window of
+  // the level in fixed-point range (int_all): run_windows skips both loops
+  const ScanWork* sw_ready = nullptr;
+  int64_t sw_stride = 0;
+  bool int_all = false;
 };
+
+bool signalled_finish(const csm_ctx* c, Finish mode);
+int64_t score_stride(const csm_ctx* c, const Dims& D, Finish mode);
+bool int_mode_window_ok(const csm_ctx* c, const Dims& D, double f, const WindowPlan& W);
+void fill_scan_work_one(const Dims& D, const WindowPlan& W, int64_t pt_off, int32_t grid, size_t i, int64_t stride,
+                        ScanWork& s);
 
 // csm_grid.cpp
 int ensure_int_grid(csm_ctx* c);

@@ -200,45 +200,64 @@ bool phase_table(double f, int ns, int margin_log2, csm::PhaseTable& T) {
 }
 
 
-// Exact fixed-point accumulation for these windows: grid eligible, beams
-// bounded, no offset wrap (every endpoint within 2^30 bytes of a row).
+// Exact fixed-point accumulation for one window: beams bounded, no offset
+// wrap (every endpoint within 2^30 bytes of a row); the context's grid must
+// be eligible too (c->int_ok).
+bool int_mode_window_ok(const csm_ctx* c, const Dims& D, double f, const WindowPlan& W) {
+  const double far = (double)(D.n_space - 1) * f;
+  const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
+                               std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
+  const double R = c->pts_maxabs * (1.0 + 1e-9) + span + 2.0;
+  if (!(R * 4.0 * (double)c->pitch < std::ldexp(1.0, 30))) return false;
+  return !((double)W.n_used * c->int_max_abs * std::ldexp(1.0, c->int_exp) > std::ldexp(1.0, 53));
+}
+
+// ... for windows [i0, i1)
 bool int_mode_ok(const csm_ctx* c, const Dims& D, double f, const std::vector<WindowPlan>& plans, size_t i0 = 0,
                  size_t i1 = SIZE_MAX) {
   if (!c->int_ok) return false;
-  for (size_t i = i0; i < std::min(i1, plans.size()); ++i) {
-    const WindowPlan& W = plans[i];
-    const double far = (double)(D.n_space - 1) * f;
-    const double span = std::max(std::max(std::fabs(W.x0), std::fabs(W.x0 + far)),
-                                 std::max(std::fabs(W.y0), std::fabs(W.y0 + far)));
-    const double R = c->pts_maxabs * (1.0 + 1e-9) + span + 2.0;
-    if (!(R * 4.0 * (double)c->pitch < std::ldexp(1.0, 30))) return false;
-    if ((double)W.n_used * c->int_max_abs * std::ldexp(1.0, c->int_exp) > std::ldexp(1.0, 53)) return false;
-  }
+  for (size_t i = i0; i < std::min(i1, plans.size()); ++i)
+    if (!int_mode_window_ok(c, D, f, plans[i])) return false;
   return true;
 }
 
-// stride: scores between consecutive windows (0: n_cand; the fused finish
-// pads each window to whole 128-byte lines, score_stride)
+void fill_scan_work_one(const Dims& D, const WindowPlan& W, int64_t pt_off, int32_t grid, size_t i, int64_t stride,
+                        ScanWork& s) {
+  s.pts_off = pt_off;
+  s.angle_off = W.angle_off;
+  s.out_off = (int64_t)i * (stride ? stride : D.n_cand);
+  s.n_used = W.n_used;
+  s.step = W.step;
+  s.divisor = (double)(W.use - 0);
+  s.x0 = W.x0;
+  s.y0 = W.y0;
+  s.cx = W.center[0];
+  s.cy = W.center[1];
+  s.ct = W.center[2];
+  s.reserved = (int32_t)i;  // the window's index in its level (the fused finish's counters)
+  s.grid_index = grid;
+}
+
+// stride: scores between consecutive windows (0: n_cand; the signalled device
+// finish pads each window to whole 128-byte lines, score_stride)
 void fill_scan_work(const Dims& D, const std::vector<WindowPlan>& plans, const std::vector<int64_t>& pt_offsets,
                     const std::vector<int32_t>& grid_index, ScanWork* sw, size_t i0 = 0, size_t i1 = SIZE_MAX,
                     int64_t stride = 0) {
-  for (size_t i = i0; i < std::min(i1, plans.size()); ++i) {
-    const WindowPlan& W = plans[i];
-    ScanWork& s = sw[i];
-    s.pts_off = pt_offsets[i];
-    s.angle_off = W.angle_off;
-    s.out_off = (int64_t)i * (stride ? stride : D.n_cand);
-    s.n_used = W.n_used;
-    s.step = W.step;
-    s.divisor = (double)(W.use - 0);
-    s.x0 = W.x0;
-    s.y0 = W.y0;
-    s.cx = W.center[0];
-    s.cy = W.center[1];
-    s.ct = W.center[2];
-    s.reserved = (int32_t)i;  // the window's index in its level (the fused finish's counters)
-    s.grid_index = grid_index.empty() ? 0 : grid_index[i];
-  }
+  for (size_t i = i0; i < std::min(i1, plans.size()); ++i)
+    fill_scan_work_one(D, plans[i], pt_offsets[i], grid_index.empty() ? 0 : grid_index[i], i, stride, sw[i]);
+}
+
+bool signalled_finish(const csm_ctx* c, Finish mode) {
+  return c->host_signal && mode == Finish::kDevice && c->fast_finish;
+}
+
+// Scores between consecutive windows of a launch: whole 128-byte lines per
+// window with the host-signal device finish (the fused finish needs them: no
+// line shared by two windows' finishers, csm_tail.hpp; the other signalled
+// passes read through FinishArgs::score_stride), n_cand otherwise (the scores
+// go to the host contiguous).
+int64_t score_stride(const csm_ctx* c, const Dims& D, Finish mode) {
+  return signalled_finish(c, mode) ? (D.n_cand + 15) / 16 * 16 : D.n_cand;
 }
 
 LevelWork make_level_work(const csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G, int nw,
@@ -439,10 +458,13 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const int w0 = sp.w1 < 0 ? 0 : sp.w0, w1 = sp.w1 < 0 ? nw : sp.w1;
   const int nr = w1 - w0;  // windows scored by this call
   const bool whole = w0 == 0 && w1 == nw && sp.score && sp.finish;
+  const double tp0 = c->profiling ? now_ms() : 0.0;  // host cost of the launch before its inputs (host:launch:prep)
   if (!c->deferred.empty()) {  // the events below are recorded again
     const int fst = flush_deferred(c);
     if (fst != CSM_OK) return fst;
   }
+  const double tp1 = c->profiling ? now_ms() : 0.0;  // (the deferred event reads are profiling's own cost)
+  if (c->profiling) c->account("host:launch:flush_events", (float)(tp1 - tp0), 0.0, 0.0);
   if (!whole) {
     bool ok = mode == Finish::kDevice && (sp.score || sp.finish) && 0 <= w0 && w0 < w1 && w1 <= nw &&
               n_angle_entries == (size_t)nw * (size_t)D.n_angles;
@@ -458,7 +480,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   const int64_t col_blocks = (n_cols + 63) / 64;
   if (n_cols >= INT32_MAX) return c->fail(CSM_ERR_UNSUPPORTED, "window too large for one launch");
   const double f = P.search_space_resolution / G.mres;
-  const bool use_int = int_mode_ok(c, D, f, plans, (size_t)w0, (size_t)w1);
+  // (sp.int_all: the plan pass found every window of the level in range)
+  const bool use_int = (sp.int_all && c->int_ok) || int_mode_ok(c, D, f, plans, (size_t)w0, (size_t)w1);
   if (whole && mode != Finish::kBest && use_int && small_launch(c, D, nw))
     return run_windows_small(c, P, D, G, plans, pt_offsets, angles, n_angle_entries, grid_index,
                              mode == Finish::kDevice, pend, skip_lists);
@@ -529,7 +552,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   // Host-signal finish (the device finish with its fast pass): FinishOut goes
   // straight to coherent pinned memory and the pass that ends last sets a flag
   // the host spins on; the scoring kernel clears the flagged-window count.
-  const bool sig = c->host_signal && mode == Finish::kDevice && c->fast_finish;
+  const bool sig = signalled_finish(c, mode);
   // The fused fast finish (csm_tail.hpp): the level's scoring launches finish
   // their windows themselves, no fast-pass launch. The same decision in every
   // call of a level (its spans and its finish-only call): every window in
@@ -546,9 +569,12 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   int max_beams = 0;
   for (const WindowPlan& W : plans) max_beams = std::max(max_beams, (int)W.n_used);
   const bool tail = kTailFinish && sig && (box || phase || tiny) && max_beams <= kTailMaxBeams &&
-                    (whole ? use_int : int_mode_ok(c, D, f, plans, 0, (size_t)nw));
-  const int64_t stride = tail ? (D.n_cand + 15) / 16 * 16 : D.n_cand;
-  if (sp.score) fill_scan_work(D, plans, pt_offsets, grid_index, sw, (size_t)w0, (size_t)w1, stride);
+                    (whole ? use_int : (sp.int_all && c->int_ok) || int_mode_ok(c, D, f, plans, 0, (size_t)nw));
+  const int64_t stride = score_stride(c, D, mode);
+  // the plan pass may have filled this call's ScanWork already (WinSpan::sw_ready:
+  // level_plan_one, into this slot's staging, at this stride)
+  if (sp.score && !(sp.sw_ready && sp.sw_stride == stride && (const void*)sp.sw_ready == (const void*)sw))
+    fill_scan_work(D, plans, pt_offsets, grid_index, sw, (size_t)w0, (size_t)w1, stride);
   LevelWork L = make_level_work(c, P, D, G, nr, use_int);
   L.blocks_per_scan = box_tiled ? D.n_angles : (int32_t)bps;  // per (window, tile) when tiled
   L.tile_n = box_tiled ? tile_n : 0;
@@ -676,6 +702,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   if ((e = c->scans.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(e, "hipMalloc(scans)");
   if ((e = c->angles.ensure(n_angle_entries * sizeof(AngleEntry))) != hipSuccess) return c->hip_fail(e, "hipMalloc(angles)");
   const double tl0 = c->profiling ? now_ms() : 0.0;  // host cost of the launch, by phase
+  if (c->profiling) c->account("host:launch:prep", (float)(tl0 - tp1), 0.0, 0.0);
   if (sp.score) {  // this call's windows and angle rows
     const size_t a0 = whole ? 0 : (size_t)w0 * D.n_angles;
     const size_t na = whole ? n_angle_entries : (size_t)nr * D.n_angles;

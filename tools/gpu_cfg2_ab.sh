@@ -8,7 +8,7 @@ for cfg in "$@"; do
   env $cfg timeout -k 10 300 python bench.py --no-cpu --no-latency --no-b109 > gpurun_out/cfg2ab.json 2> gpurun_out/cfg2ab.err || exit $?
   python3 -c "
 import json
-d = json.loads(open('gpurun_out/cfg2ab.json').read().strip().splitlines()[-1])
+d = json.load(open('gpurun_out/bench_detail.json'))  # the whole result (the last stdout line is the compact one)
 print('[$cfg]', round(d['value'] / 1e9, 3), 'G', round(d['ms_per_step'], 3), 'ms share', round(d['kernel_share_of_step'], 3))
 steps = d['steps']
 for k in d['kernels']:
