@@ -473,32 +473,74 @@ def lc_cpu_baseline(bases, pts, param, pose, seconds, per_submap):
             "host_cpu_share": host_cpu_share()}
 
 
+def willow_map(grid_cells: int, seed: int):
+    """Config 4's map: the reference's willow map (1165x945, padded by 200
+    cells to 1565x1345), or with grid_cells > 0 a grid_cells^2 @5cm grid tiled
+    from config 2's 2000^2 synthetic world (the HBM-stress variant of SURVEY
+    8d: 16384^2 = 1 GiB of fp32). Returns (world, scan batch, tile side)."""
+    from roborts_csm import worlds
+    if grid_cells <= 0:
+        w = worlds.willow_world()
+        return w, None, 0
+    base = worlds.make_world(2000, 2000, 0.05, seed=20261015)
+    reps = -(-grid_cells // 2000)
+    grid = np.ascontiguousarray(np.tile(base.grid, (reps, reps))[:grid_cells, :grid_cells])
+    return worlds.World(grid, None, base.resolution, base.offset), base, 2000
+
+
 def willow_bench(args, rank, world_size, dist, torch):
     """Config 4: the reference's willow map (1165x945, padded
-    by 200 cells to 1565x1345), one argmax-only window per query scan,
-    +-pi at 0.0349 (181 angles), every beam summed (U = 1081). The window
-    edge is --window-m (the whole-map window of the survey is ~78 m: 181 x
-    1566^2 candidates, minutes per query; scale it here). Queries are
-    independent: weak scaling, one replica per GPU."""
+    by 200 cells to 1565x1345), argmax-only windows, +-pi at 0.0349 (181
+    angles), every beam summed (U = 1081). The window is --window-m metres
+    around each query scan's initial pose, or with --whole-map the whole
+    padded map (1566^2 cells around the map's centre: 181 x 1566^2 = 444 M
+    candidates per query, the survey's definition). --grid-cells N: an N x N
+    grid tiled from config 2's world instead, one scan per step searched in
+    --windows windows spread over every tile (the 1 GiB HBM-stress grid at
+    16384). Queries are independent: weak scaling, one replica per GPU."""
     import roborts_csm
     from roborts_csm import worlds
     from roborts_csm.params import CorrelationScanMatchParam
-    w = worlds.willow_world()
-    batch = worlds.make_scan_batch(w, max(1, args.steps + args.warmup), seed=31 + rank)
-    param = CorrelationScanMatchParam(args.window_m, 0.05, math.pi, 0.0349, 0.5, 1081, 0, False, 0)
+    w, base, tile = willow_map(args.grid_cells, 20261015)
+    batch = worlds.make_scan_batch(base if base is not None else w, max(1, args.steps + args.warmup), seed=31 + rank)
+    sy, sx = w.grid.shape
+    window_m = max(sx, sy) * w.resolution if args.whole_map else args.window_m
+    param = CorrelationScanMatchParam(window_m, 0.05, math.pi, 0.0349, 0.5, 1081, 0, False, 0)
     na, ns = roborts_csm.window_dims(param)
     ctx = roborts_csm.Context(_device())
     ctx.set_grid(roborts_csm.ScanMatchMap(w.grid, w.resolution, w.offset, 0, 1))
     from roborts_csm.loop_closure import world_to_map
+    n_win = args.windows if tile else 1
+    rng = np.random.default_rng(7 + rank)
+    reps = -(-sx // tile) if tile else 1
 
+    def centers(k):
+        """Query k's window centres (map cells): the scan's initial pose, in
+        n_win tiles drawn over the whole grid (the same map around it in every
+        tile); the map's centre with --whole-map."""
+        c = world_to_map(batch.init_poses[k], w.resolution, w.offset)
+        if args.whole_map:
+            c = np.array([sx / 2.0, sy / 2.0, c[2]])
+        if not tile:
+            return c.reshape(1, 3)
+        t = rng.integers(0, reps, size=(n_win, 2))
+        out = np.tile(c, (n_win, 1))
+        out[:, 0] += t[:, 0] * tile
+        out[:, 1] += t[:, 1] * tile
+        return out
+    qc = [centers(k) for k in range(args.steps + args.warmup)]
     last = {}
 
     def query(k, search=args.search):
         pts = batch.points_cells[batch.offsets[k]:batch.offsets[k + 1]]
-        c = world_to_map(batch.init_poses[k], w.resolution, w.offset)
+        c = qc[k]
         if search == "exhaustive":
-            return ctx.best_window(pts, param, c)
-        b, _, st = ctx.search_windows(pts, param, [0], c.reshape(1, 3), max_depth=args.depth)
+            if c.shape[0] == 1:
+                return ctx.best_window(pts, param, c[0])
+            sc, fl, x, y, a = ctx.best_windows(pts, param, np.zeros(c.shape[0], np.int32), c)
+            i = int(np.lexsort((np.arange(sc.size), -sc))[0])  # max score, then the lowest window
+            return roborts_csm.CsmBest(sc[i], fl[i], x[i], y[i], a[i])
+        b, _, st = ctx.search_windows(pts, param, [0] * c.shape[0], c, max_depth=args.depth)
         last.update(st)
         return b
 
@@ -534,7 +576,7 @@ def willow_bench(args, rank, world_size, dist, torch):
                 b1, b2 = query(k, "exhaustive"), query(k)
                 same = same and b1.score == b2.score and b1.flat_index == b2.flat_index
             search["same_answer_as_exhaustive"] = bool(same)
-    local = float(na * ns * ns * args.steps)
+    local = float(na * ns * ns * n_win * args.steps)
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     if dist is not None:
         t = torch.tensor([elapsed, local], dtype=torch.float64, device=dev)
@@ -558,27 +600,39 @@ def willow_bench(args, rank, world_size, dist, torch):
         th = _host_threads()
         O.set_threads(th)
         om = O.Map(w.grid, w.resolution, w.offset)
+        # a bounded sample: windows of more than 30 M candidates (the whole
+        # map: ~2 min of all cores per query) are sampled by a 20 m window
+        # around the same centre (the oracle's rate per candidate, all beams)
+        cp, cna, cns = param, na, ns
+        if na * ns * ns > 30e6:
+            cp = CorrelationScanMatchParam(20.0, 0.05, math.pi, 0.0349, 0.5, 1081, 0, False, 0)
+            cna, cns = roborts_csm.window_dims(cp)
         tc = time.perf_counter()
         m = 0
         while m < 1 or time.perf_counter() - tc < args.cpu_seconds:
             q = m % args.steps  # the timed queries, cycled
             pts = batch.points_cells[batch.offsets[q]:batch.offsets[q + 1]]
-            O.best_window(om, pts, param, world_to_map(batch.init_poses[q], w.resolution, w.offset))
+            O.best_window(om, pts, cp, qc[q][0])
             m += 1
         dtc = time.perf_counter() - tc
         O.set_threads(1)
-        cpu = {"value": m * na * ns * ns / dtc, "unit": "scorings/s", "cores": th, "kind": "port",
-               "sample": f"{m} of the same queries ({na}x{ns}^2 candidates, all beams), {dtc:.1f} s, oracle "
-                         f"best_window with {th} threads (OpenMP over theta) on {_cpu_model()}"}
+        cpu = {"value": m * cna * cns * cns / dtc, "unit": "scorings/s", "cores": th, "kind": "port",
+               "sample": f"{m} of the same queries ({cna}x{cns}^2 candidates"
+                         f"{' (a 20 m window around the same centre)' if cp is not param else ''}, all beams), "
+                         f"{dtc:.1f} s, oracle best_window with {th} threads (OpenMP over theta) on {_cpu_model()}"}
     met, unit = _metric(args.search)
     return {
         "metric": met, "value": total / elapsed, "unit": unit, "n_gpus": world_size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "willow-full-0.05 occupancy (tests/golden/willow_walls.npz) with the blur splat; "
-                "ray-cast scans at free poses",
-        "config": {"workload": f"config4: willow 1565x1345 @5cm, {args.window_m} m / +-pi window "
-                               f"({na}x{ns}^2 candidates), all beams", "search": args.search,
+        "data": ("willow-full-0.05 occupancy (tests/golden/willow_walls.npz) with the blur splat; "
+                 "ray-cast scans at free poses") if not tile else
+                (f"{sx}x{sy} @5cm grid tiled from config 2's 2000x2000 synthetic world ({sx * sy * 4 / 2**30:.2f} GiB "
+                 f"fp32); ray-cast scans of that world, each searched in {n_win} windows over random tiles"),
+        "config": {"workload": (f"config4: {'willow 1565x1345' if not tile else f'{sx}x{sy} tiled'} @5cm, "
+                                f"{'whole-map ' if args.whole_map else ''}{window_m:.2f} m / +-pi window "
+                                f"({na}x{ns}^2 candidates) x {n_win} windows, all beams"),
+                   "search": args.search, "windows_per_query": n_win,
                    "mean_beams": beams / args.steps, "parallelism": f"replicas x{world_size}"},
         "roofline": rl, "search": search,
         "kernels": stats, "cpu_baseline": cpu,
@@ -695,6 +749,11 @@ def main():
     ap.add_argument("--attach-backend", action="store_true",
                     help="online: run the back end's per-vertex jobs in a thread beside the front end (config 5)")
     ap.add_argument("--window-m", type=float, default=20.0, help="willow: window edge (m)")
+    ap.add_argument("--whole-map", action="store_true",
+                    help="willow: the window is the whole map around its centre (SURVEY 8d config 4)")
+    ap.add_argument("--grid-cells", type=int, default=0,
+                    help="willow: an N x N grid tiled from config 2's world instead (16384: the 1 GiB HBM stress)")
+    ap.add_argument("--windows", type=int, default=64, help="willow --grid-cells: windows per query scan")
     ap.add_argument("--submaps", type=int, default=512, help="loop_closure: submaps in total")
     ap.add_argument("--search", choices=["pyramid", "exhaustive"], default="pyramid",
                     help="loop_closure / willow: the admissible multi-resolution search (csm_search_windows) "

@@ -229,6 +229,8 @@ class ThreadPool {
     uint32_t ep;
     start_ns_ = now_ns();
     first_join_ns_.store(0, std::memory_order_relaxed);
+    last_join_ns_.store(0, std::memory_order_relaxed);
+    busy_ns_.store(0, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> lk(mu_);
       job_ = &job;
@@ -251,11 +253,20 @@ class ThreadPool {
     last_caller_share_ = (double)mine / n;
     const int64_t j = first_join_ns_.load(std::memory_order_relaxed);
     last_join_us_ = j ? (double)(j - start_ns_) * 1e-3 : -1.0;
+    const int64_t jl = last_join_ns_.load(std::memory_order_relaxed);
+    last_last_join_us_ = jl ? (double)(jl - start_ns_) * 1e-3 : -1.0;
+    last_wall_us_ = (double)(now_ns() - start_ns_) * 1e-3;
+    last_busy_us_ = (double)busy_ns_.load(std::memory_order_relaxed) * 1e-3;
   }
   // the last job: the caller's share of the items, and when the first worker
   // joined it (us after the notify; -1: none did) — profiling only
   double last_caller_share() const { return last_caller_share_; }
   double last_join_us() const { return last_join_us_; }
+  // profiling: when the last worker joined (us after the notify), the job's
+  // wall time, and the time all threads spent inside items (summed)
+  double last_last_join_us() const { return last_last_join_us_; }
+  double last_wall_us() const { return last_wall_us_; }
+  double last_busy_us() const { return last_busy_us_; }
 
  private:
   static int64_t now_ns() {
@@ -268,12 +279,15 @@ class ThreadPool {
     for (;;) {
       if ((uint32_t)(c >> 32) != ep || (int64_t)(c & 0xffffffffu) >= n) return ran;
       if (!claim_.compare_exchange_weak(c, c + (uint64_t)chunk, std::memory_order_acq_rel)) continue;
+      const int64_t tj = now_ns();
       if (worker && ran == 0) {
         int64_t zero = 0;
-        first_join_ns_.compare_exchange_strong(zero, now_ns(), std::memory_order_relaxed);
+        first_join_ns_.compare_exchange_strong(zero, tj, std::memory_order_relaxed);
+        last_join_ns_.store(tj, std::memory_order_relaxed);  // (racy max: profiling only)
       }
       const int i0 = (int)(c & 0xffffffffu), i1 = std::min(n, i0 + chunk);
       for (int i = i0; i < i1; ++i) job(i);
+      busy_ns_.fetch_add(now_ns() - tj, std::memory_order_relaxed);
       ran += i1 - i0;
       done_.fetch_add(i1 - i0, std::memory_order_release);
       c = claim_.load(std::memory_order_acquire);
@@ -318,8 +332,9 @@ class ThreadPool {
   std::atomic<int> done_{0};
   bool stop_ = false;
   int64_t start_ns_ = 0;
-  std::atomic<int64_t> first_join_ns_{0};
-  double last_caller_share_ = 0.0, last_join_us_ = -1.0;
+  std::atomic<int64_t> first_join_ns_{0}, last_join_ns_{0}, busy_ns_{0};
+  double last_caller_share_ = 0.0, last_join_us_ = -1.0, last_last_join_us_ = -1.0, last_wall_us_ = 0.0,
+         last_busy_us_ = 0.0;
 };
 
 inline double now_ms() {
@@ -649,6 +664,10 @@ struct csm_ctx {
     char nm[48];
     std::snprintf(nm, sizeof(nm), "pool:%s", what);
     account(nm, (float)(std::max(0.0, pool->last_join_us()) * 1e-3), pool->last_caller_share(), 0.0);
+    // wall time of the job (total_ms), the last worker's join (bytes, us), the
+    // items' time summed over threads (scorings, us)
+    std::snprintf(nm, sizeof(nm), "pool:%s:wall", what);
+    account(nm, (float)(pool->last_wall_us() * 1e-3), std::max(0.0, pool->last_last_join_us()), pool->last_busy_us());
   }
   std::vector<csmh::PendingRun> deferred;  // signalled launches whose timings are read later (flush_deferred)
   std::vector<csm_kernel_stat> stats;

@@ -329,3 +329,40 @@ def test_config4_willow_20m():
         finally:
             O.set_threads(1)
         assert b.score == s2 and b.flat_index == f2
+
+
+def test_config4_willow_whole_map():
+    """BASELINE config 4 as SURVEY 8d defines it: the whole padded willow map
+    as the window (1566^2 cells around the map's centre x 181 angles = 444 M
+    candidates), every beam summed. The admissible search equals the
+    exhaustive argmax; the oracle (a whole-map oracle query is ~2 min of all
+    cores, so not here) confirms the winner's score bit for bit by scoring
+    that one candidate (a window of one position and one angle at the
+    winner's pose: the same cell lattice, the same angle value, so the same
+    host sincos); the exhaustive kernels are checked element-wise against the
+    oracle on smaller windows in the tests above."""
+    import roborts_csm
+    from roborts_csm import worlds
+    from roborts_csm.loop_closure import world_to_map
+    from roborts_csm.params import CorrelationScanMatchParam
+    w = worlds.willow_world()
+    sy, sx = w.grid.shape
+    batch = worlds.make_scan_batch(w, 1, seed=31)
+    pts = batch.points_cells[batch.offsets[0]:batch.offsets[1]]
+    p = CorrelationScanMatchParam(max(sx, sy) * w.resolution, 0.05, math.pi, 0.0349, 0.5, 1081, 0, False, 0)
+    na, ns = roborts_csm.window_dims(p)
+    assert na == 181 and ns >= max(sx, sy)
+    center = np.array([sx / 2.0, sy / 2.0, world_to_map(batch.init_poses[0], w.resolution, w.offset)[2]])
+    with roborts_csm.Context(0) as c:
+        c.set_grid(roborts_csm.ScanMatchMap(w.grid, w.resolution, w.offset, 0, 1))
+        got = c.best_window(pts, p, center)
+        b, win, st = c.search_windows(pts, p, [0], center.reshape(1, 3))
+        assert win == 0 and b.score == got.score and b.flat_index == got.flat_index
+        assert (b.x, b.y, b.angle) == (got.x, got.y, got.angle)
+        assert got.score > 0.5  # the scan found its place in the map
+        one = CorrelationScanMatchParam(0.0, 0.05, 0.0, 0.0349, 0.5, 1081, 0, False, 0)
+        assert roborts_csm.window_dims(one) == (1, 1)
+        at = np.array([got.x, got.y, got.angle])
+        g1 = c.best_window(pts, one, at)
+    s1, f1 = O.best_window(O.Map(w.grid, w.resolution, w.offset), pts, one, at)
+    assert f1 == 0 and s1 == got.score and g1.score == got.score
