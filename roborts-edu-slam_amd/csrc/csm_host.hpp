@@ -396,6 +396,7 @@ struct csm_ctx {
   float outside = 0.3f;  // kMapUnknownCellProb (slam/slam_processor.h:264)
   int host_threads = 1;
   csm_host_plan host_plan{};  // where the pool runs (csm_placement.cpp)
+  bool score_marker = true;   // the event recorded before each scoring launch (CSM_SCORE_MARKER=0: A/B)
   std::unique_ptr<csmh::ThreadPool> pool;
   template <class F>
   void parallel_for(int n, int threads, F&& fn) {

@@ -750,7 +750,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
   // config-2 step took 2.33-2.43 ms against 2.17-2.20 ms with it (r05,
   // profiles/r05/experiments/ab_event_before_scoring.txt); the launch follows
   // the stream's wait on the inputs' copy event (ev_in).
-  if (sp.score && !(c->profiling && w0 == 0) && (e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess)
+  if (sp.score && c->score_marker && !(c->profiling && w0 == 0) &&
+      (e = hipEventRecord(c->ev_k, c->stream)) != hipSuccess)
     return c->hip_fail(e, "hipEventRecord");
   if (c->profiling && sp.score && w0 == 0 && (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess)
     return c->hip_fail(e, "hipEventRecord");

@@ -144,6 +144,10 @@ struct PyrStats {
   // bytes (one int16 pooled value per node and beam)
   double top_ms = 0.0, top_bytes = 0.0;
   char top_name[48] = {0};
+  // PyrInputs::timed: the bound launches (pyr_bound_kernel, incumbent probes
+  // excluded) per depth, HIP events around each: launches and summed ms
+  int32_t bound_launches[kPyrMaxDepth + 1] = {};
+  double bound_ms[kPyrMaxDepth + 1] = {};
   double build_ms = 0.0;                 // pooled levels built (0 when cached)
 };
 

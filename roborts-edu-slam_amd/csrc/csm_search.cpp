@@ -91,6 +91,11 @@ struct PyramidSearch::Impl {
   BestPartial* h_inc() const { return (BestPartial*)(h_counts + 2); }
   unsigned long long* h_scored() const { return (unsigned long long*)(h_inc() + 1); }
   hipEvent_t ev_top[2] = {nullptr, nullptr};  // PyrInputs::timed
+  // PyrInputs::timed: an event pair around each bound launch (depth, pair)
+  static constexpr int kBoundEvents = 256;
+  std::vector<hipEvent_t> ev_bound;
+  std::vector<int> ev_bound_depth;
+  int n_ev_bound = 0;
   int64_t cap = (int64_t)1 << 25;
   // per level: the capacity of its node list, min(cap, the nodes the level
   // has at all), and that count; a level whose children always fit its list
@@ -114,6 +119,8 @@ struct PyramidSearch::Impl {
   ~Impl() {
     if (h_counts) (void)hipHostFree(h_counts);
     for (hipEvent_t e : ev_top)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev_bound)
       if (e) (void)hipEventDestroy(e);
   }
   hipError_t mark_top(int i, hipStream_t stream) {
@@ -209,8 +216,24 @@ struct PyramidSearch::Impl {
   // nodes (n on the host, or *n_dev), at most `upper` of them
   hipError_t bound(int d, const uint64_t* list, double* out, int64_t n, const unsigned long long* n_dev,
                    int64_t upper) {
-    return launch_pyr_bound(in.L, lev[d], d, in.scans, in.angles, in.pts, in.n_used, in.step, list, n, n_dev, upper,
-                            out, (PyrPartial*)partials.p, scored_dev() + d, in.stream);
+    const bool timed = in.timed && n_ev_bound < kBoundEvents;
+    hipError_t e;
+    if (timed) {
+      if (ev_bound.size() < (size_t)2 * kBoundEvents) ev_bound.resize((size_t)2 * kBoundEvents, nullptr);
+      ev_bound_depth.resize(kBoundEvents);
+      for (int k = 0; k < 2; ++k)
+        if (!ev_bound[2 * n_ev_bound + k] && (e = hipEventCreate(&ev_bound[2 * n_ev_bound + k])) != hipSuccess)
+          return e;
+      if ((e = hipEventRecord(ev_bound[2 * n_ev_bound], in.stream)) != hipSuccess) return e;
+    }
+    if ((e = launch_pyr_bound(in.L, lev[d], d, in.scans, in.angles, in.pts, in.n_used, in.step, list, n, n_dev, upper,
+                              out, (PyrPartial*)partials.p, scored_dev() + d, in.stream)) != hipSuccess)
+      return e;
+    if (timed) {
+      if ((e = hipEventRecord(ev_bound[2 * n_ev_bound + 1], in.stream)) != hipSuccess) return e;
+      ev_bound_depth[(size_t)n_ev_bound++] = d;
+    }
+    return hipSuccess;
   }
 
   // Score the leaves of the best nodes of n_partials block partials exactly
@@ -330,6 +353,7 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
   PyrStats local;
   I.st = stats ? stats : &local;
   *I.st = PyrStats{};
+  I.n_ev_bound = 0;
   I.st->depth = x.depth;
   I.in = x;
   hipError_t e;
@@ -422,6 +446,15 @@ hipError_t PyramidSearch::run(const PyrInputs& x, BestPartial* best, PyrStats* s
     if ((e = hipEventElapsedTime(&ms, I.ev_top[0], I.ev_top[1])) != hipSuccess) return fail(e, "hipEventElapsedTime");
     I.st->top_ms = ms;
   }
+  for (int k = 0; k < I.n_ev_bound; ++k) {
+    float ms = 0.f;
+    if ((e = hipEventElapsedTime(&ms, I.ev_bound[2 * k], I.ev_bound[2 * k + 1])) != hipSuccess)
+      return fail(e, "hipEventElapsedTime");
+    const int d = I.ev_bound_depth[(size_t)k];
+    I.st->bound_ms[d] += ms;
+    I.st->bound_launches[d] += 1;
+  }
+  I.n_ev_bound = 0;
   I.st->nodes[D] += top_scored;
   return hipSuccess;
 }
