@@ -706,8 +706,13 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
 #ifdef CSM_BOX_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   tr[7] = BOX_STAMP();
+#ifdef CSM_BOX_TRACE_XCD  // per-XCD balance (tools/box_trace.py --xcd): the dispatch slot and the exit wall clock
+  tr[10] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+  tr[11] = (unsigned long long)blockIdx.x;
+#else
   tr[10] = (unsigned long long)n_used;
   tr[11] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID
+#endif
   if (bid % 61 == 0 && lane == 0) {
     const int i = atomicAdd(&g_box_trace_n, 1);
     if (i < kBoxTraceWaves)

@@ -25,6 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scans", type=int, default=4096)
     ap.add_argument("--use-point-size", type=int, default=0, help="the level's U (0: every beam; 100: B = 109)")
+    ap.add_argument("--xcd", action="store_true",
+                    help="a CSM_BOX_TRACE_XCD build: per-XCD (blockIdx % 8) summed wave life and last exit")
     a = ap.parse_args()
     import roborts_csm
     from roborts_csm import _lib, worlds
@@ -61,6 +63,18 @@ def main():
            "beams": float(t[:, 10].mean()), "kernel_span_cycles": float(span),
            "sampled_waves_alive_mean": float(life.sum() / span) if span > 0 else None,
            "life_p10_p50_p90": [float(np.percentile(life, q)) for q in (10, 50, 90)]}
+    if a.xcd:  # the samples are the last launch's (each iteration resets them)
+        x = t[:, 11].astype(np.int64) % 8
+        ex = t[:, 10]
+        last = np.ones(n, bool)
+        per = {}
+        for k in range(8):
+            m = (x == k) & last
+            per[k] = {"waves": int(m.sum()), "life_sum": float(life[m].sum()),
+                      "last_exit_us": float((ex[m].max() - ex[last].min()) / 100.0) if m.any() else None}
+        ls = [v["life_sum"] for v in per.values()]
+        out["per_xcd"] = per
+        out["xcd_life_max_over_mean"] = float(max(ls) / (sum(ls) / 8)) if sum(ls) else None
     print(json.dumps(out), flush=True)
     c.close()
 
