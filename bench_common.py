@@ -101,6 +101,8 @@ def roofline(kernel: str, avg_ms: float, algorithmic_bytes: float, counters, cou
            "algorithmic_note": "4 B per summed beam per candidate (SURVEY 8d); served from L2/MALL and "
                                "deduplicated on chip, so not an HBM rate"}
     ks = (counters or {}).get("kernels", {}).get(kernel)
+    if ks is None and kernel.endswith(",tiles>"):  # the tiled box argmax: rocprof's name has no tile flag
+        ks = (counters or {}).get("kernels", {}).get(kernel[:-len(",tiles>")] + ">")
     if ks is None:
         out.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
                     "traffic": None, "note": f"no PMC counters for {kernel} in {counters_path}"})

@@ -52,6 +52,10 @@ def _short(name: str) -> str:
         i = name.index(key) + len(key)
         args = [a.strip() for a in name[i:name.index(">", i)].split(",")]
         return f"pyr_topbox_kernel<{args[0]},{args[1]}>"
+    key = "pyr_bound_kernel<"
+    if key in name:  # <typename T>: the search's level passes (csm_api.cpp accounts them per depth)
+        i = name.index(key) + len(key)
+        return f"pyr_bound_kernel<{name[i:name.index('>', i)].strip()}>"
     key = "score_tiny_kernel<"
     if key in name:  # <int NS, bool BEST>
         i = name.index(key) + len(key)
