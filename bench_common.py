@@ -15,11 +15,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 # fp64 arithmetic: FP64 vector peak = half the FP32 rate).
 HBM_PEAK_GBS = 8000.0
 N_CU, N_SIMD, CLK_GHZ = 256, 1024, 2.4
-COUNTERS_JSON = os.path.join(ROOT, "profiles", "r05", "counters.json")
+COUNTERS_JSON = os.path.join(ROOT, "profiles", "r06", "counters.json")
 # the reference-default beam rule's leg (B = 109: the same kernels, other counters)
-COUNTERS_B109_JSON = os.path.join(ROOT, "profiles", "r05", "counters_b109.json")
+COUNTERS_B109_JSON = os.path.join(ROOT, "profiles", "r06", "counters_b109.json")
 # the loop-closure / willow legs' counters (tools/pmc_topbox.sh: the search's top-level kernel)
-COUNTERS_LC_JSON = os.path.join(ROOT, "profiles", "r05", "counters_lc.json")
+COUNTERS_LC_JSON = os.path.join(ROOT, "profiles", "r06", "counters_lc.json")
 
 
 def _cpu_model() -> str:
@@ -152,7 +152,7 @@ def roofline(kernel: str, avg_ms: float, algorithmic_bytes: float, counters, cou
     return out
 
 
-COUNTERS_SMALL_JSON = os.path.join(ROOT, "profiles", "r05", "counters_small.json")
+COUNTERS_SMALL_JSON = os.path.join(ROOT, "profiles", "r06", "counters_small.json")
 
 # The driver reads the LAST stdout line of a bounded tail: r05's 24 KB line
 # (per-kernel tables inlined) was not parsed. The final line keeps the headline
