@@ -174,6 +174,16 @@ int csm_set_grid_device(csm_ctx* ctx, const float* device_prob,
  * n_space = Round(size/res)+1 (:538). */
 int csm_window_dims(const csm_param* param, int32_t* n_angles, int32_t* n_space);
 
+/* The angle rows' cos/sin as the 3-level driver computes them on the device
+ * (AngleSearchLookUpTable::UpdateLookUpTable correlate_scan_matcher.h:171-172,
+ * one glibc sincos per angle as GCC compiles it): glibc 2.35's sincos restated
+ * for the GPU over the table of the libm this process has mapped, so each
+ * result equals the host's sincos(x[i]) bit for bit. Arguments outside the
+ * restated domain (|x| >= 105414350, not finite) are computed by the host.
+ * CSM_ERR_UNSUPPORTED when the host's libm did not pass the table checks (the
+ * driver then keeps the host sincos). Host buffers of n doubles. */
+int csm_sincos_device(csm_ctx* ctx, const double* x, int64_t n, double* sin_out, double* cos_out);
+
 /* --- drop-in entry points (host buffers) -------------------------------- */
 /* BasedCorrelationScanMatch::ScanMatch. points_xy: n_points (x, y) pairs in
  * map-cell units, sensor frame (RangeDataContainer after CreateFrom with the

@@ -673,4 +673,11 @@ void oracle_std_sort_order(const double* keys, int64_t n, int64_t* order) {
   std::sort(v.begin(), v.end(), CandGreater());
   for (int64_t i = 0; i < n; ++i) order[i] = v[(size_t)i].flat;
 }
+
+// The host libm's sincos over x[0..n) (AngleSearchLookUpTable :171-172 as
+// GCC compiles it): the checker of the device's angle rows (csm_sincos_device).
+void oracle_sincos_batch(const double* x, int64_t n, double* s, double* c) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) ref_sincos(x[i], &s[i], &c[i]);
+}
 }

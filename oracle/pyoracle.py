@@ -65,6 +65,7 @@ def _load():
         "oracle_map_to_world": (None, [C.POINTER(OracleMap), _dp, _dp]),
         "oracle_best_window": (C.c_double, [C.POINTER(OracleMap), _dp, C.c_int, C.c_void_p, _dp, _i64p]),
         "oracle_std_sort_order": (None, [_dp, C.c_int64, _i64p]),
+        "oracle_sincos_batch": (None, [_dp, C.c_int64, _dp, _dp]),
         "oracle_set_threads": (None, [C.c_int]),
     }
     for k, (r, a) in sig.items():
@@ -205,6 +206,15 @@ def std_sort_order(keys) -> np.ndarray:
     out = np.empty(k.size, dtype=np.int64)
     _lib.oracle_std_sort_order(k.ctypes.data_as(_dp), k.size, out.ctypes.data_as(_i64p))
     return out
+
+
+def sincos_batch(x):
+    """(sin x, cos x) from the host libm's sincos, element by element."""
+    a = np.ascontiguousarray(x, dtype=np.float64)
+    s = np.empty_like(a)
+    c = np.empty_like(a)
+    _lib.oracle_sincos_batch(a.ctypes.data_as(_dp), a.size, s.ctypes.data_as(_dp), c.ctypes.data_as(_dp))
+    return s, c
 
 
 # ---- occupancy-grid map building (SURVEY.md 8f rows f1, f4; map_oracle.cpp) ----

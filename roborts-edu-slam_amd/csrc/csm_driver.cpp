@@ -43,6 +43,9 @@ struct LevelRun {
   int64_t sw_stride = 0;
   int int_bad = 0;
   bool int_known = false;
+  // the rows' cos/sin are left to the launch (csm_trig.hip): a device finish
+  // (the host finish reads them), not the few-window path (its own copy)
+  bool dev_trig = false;
   // back to a fresh run, the vectors' capacity kept
   void reset() {
     P = csm_param{};
@@ -68,6 +71,7 @@ struct LevelRun {
     sw_stride = 0;
     int_bad = 0;
     int_known = false;
+    dev_trig = false;
   }
 };
 
@@ -168,9 +172,11 @@ int level_alloc(csm_ctx* c, const int64_t* offsets, LevelRun& R, HostBuf& rows, 
   // slot's previous launch has read it: its level was joined before this plan)
   if ((he = c->h_sw.ensure((size_t)nw * sizeof(ScanWork))) != hipSuccess) return c->hip_fail(he, "hipHostMalloc(scans)");
   R.sw = (ScanWork*)c->h_sw.p;
-  R.sw_stride = score_stride(c, R.D, level_device_finish(c, R.D, nw) ? Finish::kDevice : Finish::kScoresToHost);
+  const bool dev = level_device_finish(c, R.D, nw);
+  R.sw_stride = score_stride(c, R.D, dev ? Finish::kDevice : Finish::kScoresToHost);
   R.int_bad = 0;
   R.int_known = false;
+  R.dev_trig = c->device_trig && dev && !small_launch(c, R.D, nw) && libm_sincos_table() != nullptr;
   return CSM_OK;
 }
 
@@ -184,7 +190,8 @@ void level_plan_one(const csm_ctx* c, LevelRun& R, const Geometry& G, const int6
   double center[3];
   G.to_map(poses + 3 * s, center);
   WindowPlan& W = R.plans[(size_t)i];
-  plan_window_into(R.P, R.D, G, (int)(offsets[s + 1] - offsets[s]), center, R.rows + (size_t)i * (size_t)R.D.n_angles, W);
+  plan_window_into(R.P, R.D, G, (int)(offsets[s + 1] - offsets[s]), center, R.rows + (size_t)i * (size_t)R.D.n_angles, W,
+                   !R.dev_trig);
   W.angle_off = (int64_t)i * R.D.n_angles;
   if (R.sw)
     fill_scan_work_one(R.D, W, R.pt_off[(size_t)i], R.grid.empty() ? 0 : R.grid[(size_t)i], (size_t)i, R.sw_stride,
@@ -202,6 +209,7 @@ int level_launch(csm_ctx* c, LevelRun& R, WinSpan sp = WinSpan{}) {
   sp.sw_ready = R.sw;
   sp.sw_stride = R.sw_stride;
   sp.int_all = R.int_known && !__atomic_load_n(&R.int_bad, __ATOMIC_RELAXED);
+  sp.dev_trig = R.dev_trig;
   const int st = run_windows(c, R.P, D, G, R.plans, R.pt_off, R.angles, (size_t)nw * (size_t)D.n_angles, R.grid,
                              nullptr, R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend, R.skip_lists, sp);
   if (st != CSM_OK || !sp.finish) return st;

@@ -397,6 +397,11 @@ struct csm_ctx {
   int host_threads = 1;
   csm_host_plan host_plan{};  // where the pool runs (csm_placement.cpp)
   bool score_marker = true;   // the event recorded before each scoring launch (CSM_SCORE_MARKER=0: A/B)
+  // The 3-level driver's angle rows: cos/sin on the device (csm_trig.hip,
+  // glibc's sincos restated; CSM_DEVICE_TRIG=0: the host's ::sincos), when
+  // the host's libm passed libm_sincos_table()'s checks
+  bool device_trig = true;
+  csmh::DevBuf trig_tab;      // libm's sincos table on this device (uploaded on first use)
   std::unique_ptr<csmh::ThreadPool> pool;
   template <class F>
   void parallel_for(int n, int threads, F&& fn) {
@@ -736,10 +741,19 @@ struct WinSpan {
   const ScanWork* sw_ready = nullptr;
   int64_t sw_stride = 0;
   bool int_all = false;
+  // the plan left the rows' cos/sin to the device (plan_window_into host_trig
+  // false): the launch computes them after the rows' copy (csm_trig.hip)
+  bool dev_trig = false;
 };
+
+// glibc's sincos table from this process's libm, or nullptr when it was not
+// found or the restated sincos did not equal ::sincos on the check's
+// arguments (csm_launch.cpp; libm_sincos_table.hpp). Located once.
+const double* libm_sincos_table();
 
 bool signalled_finish(const csm_ctx* c, Finish mode);
 int64_t score_stride(const csm_ctx* c, const Dims& D, Finish mode);
+bool small_launch(const csm_ctx* c, const Dims& D, int nw);
 bool int_mode_window_ok(const csm_ctx* c, const Dims& D, double f, const WindowPlan& W);
 void fill_scan_work_one(const Dims& D, const WindowPlan& W, int64_t pt_off, int32_t grid, size_t i, int64_t stride,
                         ScanWork& s);
@@ -765,7 +779,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                 Finish mode = Finish::kScoresToHost, PendingRun* pend = nullptr, int skip_lists = 0,
                 WinSpan sp = WinSpan{});
 bool plan_window_into(const csm_param& P, const Dims& D, const Geometry& G, int n_points,
-                      const double center[3], AngleEntry* out, WindowPlan& W);
+                      const double center[3], AngleEntry* out, WindowPlan& W, bool host_trig = true);
 bool plan_window(const csm_param& P, const Dims& D, const Geometry& G, int n_points,
                  const double center[3], std::vector<AngleEntry>& angles, WindowPlan& W);
 bool plan_windows_shared(const csm_param& P, const Dims& D, const Geometry& G, int n_points, int n_windows,

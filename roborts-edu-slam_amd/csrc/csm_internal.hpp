@@ -425,6 +425,10 @@ struct SplitWork {
 };
 hipError_t launch_score_split(const LevelWork& L, const SplitWork& W, const ScanWork* d_scans, const double* d_pts,
                               const AngleEntry* d_angles, double* d_out, hipStream_t stream);
+// csm_trig.hip: rows[i].cosine / .sine = glibc sincos(rows[i].angle), bit-equal
+// to the host's (libm_sincos.hpp; d_tab: libm's 440-double table); rows whose
+// angle is outside the restated domain are left as they are.
+hipError_t launch_angle_trig(AngleEntry* d_rows, int64_t n, const double* d_tab, hipStream_t stream);
 // gridi layout: row pitch = round4(size_x + kGridiPadCols) cells, size_y +
 // kGridiPadRows rows; every cell outside [0,size_x) x [0,size_y) is zero, so a
 // 16 x 16 box whose corner lies on the grid never leaves the buffer.

@@ -4,6 +4,7 @@
 // launch with its device finish (run_windows, run_windows_small), the joins
 // and the per-launch HIP-event accounting.
 #include "csm_host.hpp"
+#include "libm_sincos_table.hpp"
 
 namespace csmh {
 
@@ -715,6 +716,21 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if ((e = hipMemcpyAsync((AngleEntry*)c->angles.p + a0, angles + a0, na * sizeof(AngleEntry), hipMemcpyHostToDevice,
                             is)) != hipSuccess)
       return c->hip_fail(e, "hipMemcpyAsync(angles)");
+    if (sp.dev_trig) {  // the rows' cos/sin (the plan left them to the device)
+      const double* tab = libm_sincos_table();
+      if (!tab) return c->fail(CSM_ERR_UNSUPPORTED, "run_windows: device trig without the libm table");
+      if (!c->trig_tab.p) {
+        if ((e = c->trig_tab.ensure(csm::libm::kSincosTableDoubles * sizeof(double))) != hipSuccess)
+          return c->hip_fail(e, "hipMalloc(sincos table)");
+        if ((e = hipMemcpyAsync(c->trig_tab.p, tab, csm::libm::kSincosTableDoubles * sizeof(double),
+                                hipMemcpyHostToDevice, is)) != hipSuccess)
+          return c->hip_fail(e, "hipMemcpyAsync(sincos table)");
+      }
+      if ((e = csm::launch_angle_trig((AngleEntry*)c->angles.p + a0, (int64_t)na, (const double*)c->trig_tab.p, is)) !=
+          hipSuccess)
+        return c->hip_fail(e, "angle_trig_kernel");
+      if (c->profiling) c->account("host:trig_rows", 0.0f, (double)na * sizeof(AngleEntry), 0.0);  // launches: levels
+    }
     if ((e = hipEventRecord(c->ev_in, c->h2d)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->ev_in, 0)) != hipSuccess)
       return c->hip_fail(e, "inputs event");
   }
@@ -948,7 +964,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
 // :154-172 and ScanMatch :538-548) for a window centred at `center` (map coords).
 // Writes D.n_angles rows at `out`; the caller sets W.angle_off.
 bool plan_window_into(const csm_param& P, const Dims& D, const Geometry& G, int n_points,
-                      const double center[3], AngleEntry* out, WindowPlan& W) {
+                      const double center[3], AngleEntry* out, WindowPlan& W, bool host_trig) {
   W.center[0] = center[0];
   W.center[1] = center[1];
   W.center[2] = center[2];
@@ -963,9 +979,23 @@ bool plan_window_into(const csm_param& P, const Dims& D, const Geometry& G, int 
   for (int a = 0; a < D.n_angles; ++a) {
     AngleEntry& ae = out[a];
     ae.angle = start + a * P.search_angle_resolution;
-    csm::host_sincos(ae.angle, &ae.sine, &ae.cosine);
+    // (!host_trig: the launch's angle_trig_kernel writes cos/sin, except where
+    // the restated sincos does not reach)
+    if (host_trig || !csm::libm::sincos_device_ok(ae.angle)) csm::host_sincos(ae.angle, &ae.sine, &ae.cosine);
   }
   return true;
+}
+
+const double* libm_sincos_table() {
+  struct Table {
+    bool ok = false;
+    double t[csm::libm::kSincosTableDoubles];
+    Table() {
+      ok = csm::libm::locate_sincos_table(t) && csm::libm::check_sincos(t, 4096, 0x7a61ull) == 0;
+    }
+  };
+  static const Table tab;
+  return tab.ok ? tab.t : nullptr;
 }
 
 bool plan_window(const csm_param& P, const Dims& D, const Geometry& G, int n_points,

@@ -180,6 +180,16 @@ class Context:
         if st != _abi.CSM_OK:
             raise CsmError(st, _lib.csm_last_error(self._h).decode())
 
+    def sincos_device(self, x):
+        """(sin x, cos x) computed on the GPU as the 3-level driver's angle rows
+        are (csm_sincos_device: glibc's sincos restated, bit-equal to the host's)."""
+        a = np.ascontiguousarray(x, dtype=np.float64).ravel()
+        s = np.empty_like(a)
+        c = np.empty_like(a)
+        self._check(_lib.csm_sincos_device(self._h, a.ctypes.data_as(_abi._dp), a.size,
+                                           s.ctypes.data_as(_abi._dp), c.ctypes.data_as(_abi._dp)))
+        return s, c
+
     def set_outside_value(self, v: float):
         self._check(_lib.csm_set_outside_value(self._h, C.c_float(v)))
 

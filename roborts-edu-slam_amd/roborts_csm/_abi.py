@@ -25,7 +25,7 @@ EXPORTED = (
     "csm_create", "csm_destroy", "csm_last_error", "csm_abi_version", "csm_build_digest",
     "csm_set_outside_value", "csm_set_grid", "csm_set_grid_device", "csm_update_grid_cells",
     "csm_update_grid_rows",
-    "csm_window_dims", "csm_scan_match", "csm_scan_matchers",
+    "csm_window_dims", "csm_sincos_device", "csm_scan_match", "csm_scan_matchers",
     "csm_scan_match_batch", "csm_scan_matchers_batch", "csm_score_window",
     "csm_best_window", "csm_load_scans", "csm_scan_matchers_loaded", "csm_scan_matchers_submit", "csm_scan_matchers_wait", "csm_load_scans_async",
     "csm_host_alloc", "csm_host_free",
@@ -220,6 +220,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "csm_update_grid_rows": (C.c_int, [_ctx, C.c_void_p, C.c_int64, C.POINTER(CsmMapInfo), C.c_int64,
                                            C.c_int32, C.c_int32]),
         "csm_window_dims": (C.c_int, [C.POINTER(CsmParam), _i32p, _i32p]),
+        "csm_sincos_device": (C.c_int, [_ctx, _dp, C.c_int64, _dp, _dp]),
         "csm_scan_match": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), _dp, _dp, _dp, _i64p]),
         "csm_scan_matchers": (C.c_int, [_ctx, _dp, C.c_int32, C.POINTER(CsmParam), C.c_int32, _dp, _dp, _dp]),
         "csm_scan_match_batch": (C.c_int, [_ctx, C.c_int32, _dp, _i64p, C.POINTER(CsmParam), _dp, _dp, _dp, _i64p]),
