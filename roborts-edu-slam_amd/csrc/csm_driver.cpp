@@ -3,6 +3,7 @@
 // driver (scan_matchers.h:179-289): levels planned, launched, joined and
 // completed per part, with the parts of a resident batch in flight together.
 #include "csm_host.hpp"
+#include "libm_sincos.hpp"
 
 namespace csmh {
 
@@ -46,6 +47,9 @@ struct LevelRun {
   // the rows' cos/sin are left to the launch (csm_trig.hip): a device finish
   // (the host finish reads them), not the few-window path (its own copy)
   bool dev_trig = false;
+  // some window has an angle outside the restated sincos's domain: its launch
+  // copies the host's rows (the kernel fills the others in place)
+  int trig_bad = 0;
   // back to a fresh run, the vectors' capacity kept
   void reset() {
     P = csm_param{};
@@ -72,6 +76,7 @@ struct LevelRun {
     int_bad = 0;
     int_known = false;
     dev_trig = false;
+    trig_bad = 0;
   }
 };
 
@@ -177,6 +182,7 @@ int level_alloc(csm_ctx* c, const int64_t* offsets, LevelRun& R, HostBuf& rows, 
   R.int_bad = 0;
   R.int_known = false;
   R.dev_trig = c->device_trig && dev && !small_launch(c, R.D, nw) && libm_sincos_table() != nullptr;
+  R.trig_bad = 0;
   return CSM_OK;
 }
 
@@ -190,8 +196,12 @@ void level_plan_one(const csm_ctx* c, LevelRun& R, const Geometry& G, const int6
   double center[3];
   G.to_map(poses + 3 * s, center);
   WindowPlan& W = R.plans[(size_t)i];
-  plan_window_into(R.P, R.D, G, (int)(offsets[s + 1] - offsets[s]), center, R.rows + (size_t)i * (size_t)R.D.n_angles, W,
-                   !R.dev_trig);
+  AngleEntry* rows = R.rows + (size_t)i * (size_t)R.D.n_angles;
+  plan_window_into(R.P, R.D, G, (int)(offsets[s + 1] - offsets[s]), center, rows, W, !R.dev_trig);
+  // (the angles grow with their index: both ends inside the domain, all are)
+  if (R.dev_trig && R.D.n_angles > 0 &&
+      !(csm::libm::sincos_device_ok(rows[0].angle) && csm::libm::sincos_device_ok(rows[R.D.n_angles - 1].angle)))
+    __atomic_store_n(&R.trig_bad, 1, __ATOMIC_RELAXED);
   W.angle_off = (int64_t)i * R.D.n_angles;
   if (R.sw)
     fill_scan_work_one(R.D, W, R.pt_off[(size_t)i], R.grid.empty() ? 0 : R.grid[(size_t)i], (size_t)i, R.sw_stride,
@@ -210,6 +220,7 @@ int level_launch(csm_ctx* c, LevelRun& R, WinSpan sp = WinSpan{}) {
   sp.sw_stride = R.sw_stride;
   sp.int_all = R.int_known && !__atomic_load_n(&R.int_bad, __ATOMIC_RELAXED);
   sp.dev_trig = R.dev_trig;
+  sp.rows_gen = R.dev_trig && !__atomic_load_n(&R.trig_bad, __ATOMIC_RELAXED);
   const int st = run_windows(c, R.P, D, G, R.plans, R.pt_off, R.angles, (size_t)nw * (size_t)D.n_angles, R.grid,
                              nullptr, R.dev ? Finish::kDevice : Finish::kScoresToHost, &R.pend, R.skip_lists, sp);
   if (st != CSM_OK || !sp.finish) return st;

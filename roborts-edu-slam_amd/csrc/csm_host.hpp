@@ -744,6 +744,9 @@ struct WinSpan {
   // the plan left the rows' cos/sin to the device (plan_window_into host_trig
   // false): the launch computes them after the rows' copy (csm_trig.hip)
   bool dev_trig = false;
+  // ... and every window of the span has its angles inside the restated
+  // domain: the device builds the rows whole from the ScanWork, no rows' copy
+  bool rows_gen = false;
 };
 
 // glibc's sincos table from this process's libm, or nullptr when it was not

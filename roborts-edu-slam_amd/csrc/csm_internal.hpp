@@ -429,6 +429,11 @@ hipError_t launch_score_split(const LevelWork& L, const SplitWork& W, const Scan
 // to the host's (libm_sincos.hpp; d_tab: libm's 440-double table); rows whose
 // angle is outside the restated domain are left as they are.
 hipError_t launch_angle_trig(AngleEntry* d_rows, int64_t n, const double* d_tab, hipStream_t stream);
+// csm_trig.hip: the rows of windows d_sw[0..nw) whole (angle, cos, sin) from
+// each window's ct: θ_a = (ct - offset) + a * ares, at rows[S.angle_off + a];
+// every θ inside the restated domain (the caller checks).
+hipError_t launch_angle_rows(const ScanWork* d_sw, int nw, int n_angles, double offset, double ares, AngleEntry* d_rows,
+                             const double* d_tab, hipStream_t stream);
 // gridi layout: row pitch = round4(size_x + kGridiPadCols) cells, size_y +
 // kGridiPadRows rows; every cell outside [0,size_x) x [0,size_y) is zero, so a
 // 16 x 16 box whose corner lies on the grid never leaves the buffer.

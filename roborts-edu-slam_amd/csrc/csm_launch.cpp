@@ -713,7 +713,8 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     if ((e = hipMemcpyAsync((ScanWork*)c->scans.p + w0, sw + w0, (size_t)nr * sizeof(ScanWork), hipMemcpyHostToDevice,
                             is)) != hipSuccess)
       return c->hip_fail(e, "hipMemcpyAsync(scans)");
-    if ((e = hipMemcpyAsync((AngleEntry*)c->angles.p + a0, angles + a0, na * sizeof(AngleEntry), hipMemcpyHostToDevice,
+    if (!(sp.dev_trig && sp.rows_gen) &&
+        (e = hipMemcpyAsync((AngleEntry*)c->angles.p + a0, angles + a0, na * sizeof(AngleEntry), hipMemcpyHostToDevice,
                             is)) != hipSuccess)
       return c->hip_fail(e, "hipMemcpyAsync(angles)");
     if (sp.dev_trig) {  // the rows' cos/sin (the plan left them to the device)
@@ -726,10 +727,15 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
                                 hipMemcpyHostToDevice, is)) != hipSuccess)
           return c->hip_fail(e, "hipMemcpyAsync(sincos table)");
       }
-      if ((e = csm::launch_angle_trig((AngleEntry*)c->angles.p + a0, (int64_t)na, (const double*)c->trig_tab.p, is)) !=
-          hipSuccess)
-        return c->hip_fail(e, "angle_trig_kernel");
-      if (c->profiling) c->account("host:trig_rows", 0.0f, (double)na * sizeof(AngleEntry), 0.0);  // launches: levels
+      if (sp.rows_gen)  // the rows whole from the windows' ScanWork (copied above)
+        e = csm::launch_angle_rows((const ScanWork*)c->scans.p + w0, nr, D.n_angles, (P.search_angle_offset * 2) / 2,
+                                   P.search_angle_resolution, (AngleEntry*)c->angles.p, (const double*)c->trig_tab.p, is);
+      else
+        e = csm::launch_angle_trig((AngleEntry*)c->angles.p + a0, (int64_t)na, (const double*)c->trig_tab.p, is);
+      if (e != hipSuccess) return c->hip_fail(e, "angle rows kernel");
+      // launches: the launches with device rows; bytes: the rows' copy saved
+      if (c->profiling) c->account(sp.rows_gen ? "host:trig_rows:gen" : "host:trig_rows", 0.0f,
+                                   (double)na * sizeof(AngleEntry), 0.0);
     }
     if ((e = hipEventRecord(c->ev_in, c->h2d)) != hipSuccess || (e = hipStreamWaitEvent(c->stream, c->ev_in, 0)) != hipSuccess)
       return c->hip_fail(e, "inputs event");

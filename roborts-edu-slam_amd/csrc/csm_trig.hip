@@ -29,6 +29,40 @@ __global__ __launch_bounds__(256) void angle_trig_kernel(AngleEntry* __restrict_
   rows[i].sine = s;
 }
 
+// The rows whole, from each window's ScanWork: θ_a = (ct - offset) + a·ares
+// in plan_window_into's operations (csm_launch.cpp; correlate_scan_matcher.h
+// :161-168), then its sincos. Every row of the launch must be inside the
+// restated domain (the plan checks each window's end angles). Replaces the
+// rows' host-to-device copy (24 bytes a row).
+__global__ __launch_bounds__(256) void angle_rows_kernel(const ScanWork* __restrict__ sw, int64_t n, int n_angles,
+                                                         double offset, double ares, AngleEntry* __restrict__ rows,
+                                                         const double* __restrict__ tab) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t w = i / n_angles;
+  const int a = (int)(i - w * n_angles);
+  const ScanWork& S = sw[w];
+  const double start = S.ct - offset;
+  const double th = start + a * ares;
+  double s, c;
+  libm::sincos(th, tab, &s, &c);
+  AngleEntry& r = rows[S.angle_off + a];
+  r.angle = th;
+  r.cosine = c;
+  r.sine = s;
+}
+
+hipError_t launch_angle_rows(const ScanWork* d_sw, int nw, int n_angles, double offset, double ares, AngleEntry* d_rows,
+                             const double* d_tab, hipStream_t stream) {
+  const int64_t n = (int64_t)nw * n_angles;
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = (n + 255) / 256;
+  if (blocks > INT32_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(angle_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, d_sw, n, n_angles, offset, ares,
+                     d_rows, d_tab);
+  return hipGetLastError();
+}
+
 hipError_t launch_angle_trig(AngleEntry* d_rows, int64_t n, const double* d_tab, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   const int64_t blocks = (n + 255) / 256;

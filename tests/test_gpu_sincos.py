@@ -113,7 +113,7 @@ def test_driver_rows_device_equal_host(world2000, parts):
             s = c.scan_matchers_batch(b.points_cells, b.offsets, headline_levels(), poses, covs)
             st = {k["name"]: k["launches"] for k in c.kernel_stats()}
             c.set_profiling(False)
-            out[trig] = (s, poses, covs, st.get("host:trig_rows", 0))
+            out[trig] = (s, poses, covs, st.get("host:trig_rows", 0) + st.get("host:trig_rows:gen", 0))
         finally:
             c.close()
     assert out["1"][3] >= 2 * int(parts) and out["0"][3] == 0
@@ -123,3 +123,30 @@ def test_driver_rows_device_equal_host(world2000, parts):
     s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells, b.offsets, headline_levels(), b.init_poses,
                                        np.tile(np.eye(3).reshape(1, 9), (b.init_poses.shape[0], 1)))
     assert np.array_equal(out["1"][0], s2) and np.array_equal(out["1"][1], p2) and np.array_equal(out["1"][2], c2)
+
+
+def test_driver_rows_outside_domain(world2000):
+    """Scans whose pose angle lies beyond the restated sincos's domain (|theta|
+    >= 105414350 rad, glibc's __branred range): their launches copy the host's
+    rows and the kernel fills the rest in place; the results are the oracle's."""
+    import roborts_csm
+    from roborts_csm.params import headline_levels
+    w, b = world2000
+    init = b.init_poses.copy()
+    init[::5, 2] += 1.2e8  # every fifth scan far outside (the same direction modulo 2 pi, roughly)
+    c = _ctx_env(CSM_PIPELINE="16", CSM_PIPELINE_PARTS="2", CSM_SMALL="0")
+    try:
+        c.set_grid(roborts_csm.ScanMatchMap(w.grid, float(w.resolution), tuple(w.offset), 0, 1))
+        poses = np.ascontiguousarray(init.copy())
+        covs = np.tile(np.eye(3).reshape(1, 9), (poses.shape[0], 1))
+        c.set_profiling(True)
+        s = c.scan_matchers_batch(b.points_cells, b.offsets, headline_levels(), poses, covs)
+        st = {k["name"]: k["launches"] for k in c.kernel_stats()}
+        c.set_profiling(False)
+    finally:
+        c.close()
+    assert st.get("host:trig_rows", 0) > 0
+    m = O.Map(w.grid, w.resolution, w.offset)
+    s2, p2, c2 = O.scan_matchers_batch(m, b.points_cells, b.offsets, headline_levels(), init,
+                                       np.tile(np.eye(3).reshape(1, 9), (init.shape[0], 1)))
+    assert _bits_equal(s, s2) and _bits_equal(poses, p2) and _bits_equal(covs, c2)
