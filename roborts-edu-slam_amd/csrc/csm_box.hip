@@ -503,7 +503,15 @@ __device__ __forceinline__ uint32_t byte_x8(uint32_t w) {
   return r;
 }
 
-template <int NS, bool BEST>
+// The run-free form (NORUN) for short scans: at the reference's default beam
+// rule (every 10th beam, B = 109) neighbouring beams rarely share a box corner
+// (104 runs for 108 beams, profiles/r06/experiments/box_trace_b109.txt), so
+// the run list and its counting sort (17 % of a wave there) buy nothing.
+// NORUN pairs consecutive beams, each with count 1: pair p is beams 2p and
+// 2p + 1 of the segment, in beam order. The sums are the same exact integers.
+constexpr int kPairNoRunBeams = 128;
+
+template <int NS, bool BEST, bool NORUN = false>
 __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWork* __restrict__ scans,
                                                             const double2* __restrict__ pts,
                                                             const AngleEntry* __restrict__ angles,
@@ -564,6 +572,28 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
     tq = BOX_STAMP();
     if (s0 == 0) tr[1] = tq;
 #endif
+    int npad;
+    if constexpr (NORUN) {
+      // beam i of the segment's box offset at pair_off[i]; past the segment,
+      // through the look-ahead step's pairs, the zero run
+      const int s1 = min(n_used, s0 + kPairSeg);
+      npad = ((s1 - s0 + 1) / 2 + kStepPairs - 1) / kStepPairs * kStepPairs;
+      const int s_end = s0 + 2 * (npad + kStepPairs);
+      for (int cb = s0; cb < s_end; cb += 128) {
+        const double2 p0 = B.point(cb), p1 = B.point(cb + 64);
+        const int o0 = B.offsets<true>(p0, cb, slow);
+        const int o1 = B.offsets<true>(p1, cb + 64, slow);
+        pair_off[cb - s0 + lane] = cb + lane < s1 ? o0 : zero_off;
+        if (cb + 64 < s_end) pair_off[cb + 64 - s0 + lane] = cb + 64 + lane < s1 ? o1 : zero_off;
+      }
+      __syncthreads();
+#ifdef CSM_BOX_TRACE
+      tr[2] += BOX_STAMP() - tq;
+      tq = BOX_STAMP();
+      tr[8] += s1 - s0;
+      tr[9] += npad;
+#endif
+    } else {
     const int nruns = B.build_runs<CSM_PAIR_PF, uint8_t, true, CSM_PAIR_ILP != 0>(
         s0, min(n_used, s0 + kPairSeg), run_off, run_cnt, kScratch, slow);
     bin[lane] = 0;
@@ -590,7 +620,7 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
     if (h & 1) pair_off[base + h] = zero_off;  // the odd bin's last run pairs with the zero run
     // whole steps, then one step of empty pairs (zero runs, count 0) that the
     // look-ahead reads of the last step take
-    const int npad = (npairs + kStepPairs - 1) / kStepPairs * kStepPairs;
+    npad = (npairs + kStepPairs - 1) / kStepPairs * kStepPairs;
     for (int p = npairs + lane; p < npad + kStepPairs; p += 64) {
       pair_off[2 * p] = zero_off;
       pair_off[2 * p + 1] = zero_off;
@@ -609,13 +639,14 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
     tq = BOX_STAMP();
     tr[9] += npad;
 #endif
+    }
 #if defined(CSM_PAL_DIAG) && CSM_PAL_DIAG >= 1  // timing diagnostic (wrong scores): the run lists only
     if (false) {
 #else
     if (npad > 0) {
 #endif
       int4 offs = *reinterpret_cast<const int4*>(&pair_off[4 * slot]);  // (A0, B0, A1, B1)
-      uint32_t cnts = (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[2 * slot]);
+      uint32_t cnts = NORUN ? 0x0101u : (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[2 * slot]);
       v4i dA[kPairPD], dB[kPairPD];
       dA[0] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, krow + (offs.x & kPieceMask), 0, 0);
       __builtin_amdgcn_sched_barrier(0);  // issued in the order the loop consumes them
@@ -628,7 +659,8 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
       for (int g = 0; g < npad; g += kStepPairs) {
         // the next step's pairs of this slot (the padding covers the last step's)
         const int4 noffs = *reinterpret_cast<const int4*>(&pair_off[2 * (g + kStepPairs) + 4 * slot]);
-        const uint32_t ncnts = (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[g + kStepPairs + 2 * slot]);
+        const uint32_t ncnts =
+            NORUN ? 0x0101u : (uint32_t)*reinterpret_cast<const uint16_t*>(&pair_cnt[g + kStepPairs + 2 * slot]);
         const int curA[2] = {offs.x, offs.z}, curB[2] = {offs.y, offs.w};
         const int nxtA[2] = {noffs.x, noffs.z}, nxtB[2] = {noffs.y, noffs.w};
 #pragma unroll
@@ -724,8 +756,14 @@ __global__ CSM_PAIR_BOUNDS void score_box_pair_kernel(LevelWork L, const ScanWor
 template <int NS>
 hipError_t launch_pair(const LevelWork& L, const ScanWork* s, const double2* p, const AngleEntry* an, double* out,
                        BestPartial* part, unsigned nblk, hipStream_t stream) {
-  if (part)
+  const bool norun = L.max_n_used > 0 && L.max_n_used <= kPairNoRunBeams;
+  if (part && norun)
+    hipLaunchKernelGGL((score_box_pair_kernel<NS, true, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+  else if (part)
     hipLaunchKernelGGL((score_box_pair_kernel<NS, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
+  else if (norun)
+    hipLaunchKernelGGL((score_box_pair_kernel<NS, false, true>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out,
+                       part);
   else
     hipLaunchKernelGGL((score_box_pair_kernel<NS, false>), dim3(nblk), dim3(64), 0, stream, L, s, p, an, out, part);
   return hipGetLastError();

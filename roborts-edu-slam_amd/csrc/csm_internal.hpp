@@ -202,6 +202,9 @@ struct LevelWork {
   int64_t istrip_grid_bytes;
   // the fused fast finish (tail.on = 0: scores only; csm_tail.hpp)
   TailArgs tail;
+  // the largest n_used of the level's windows (0: unknown); the pair kernel
+  // takes its run-free form at or below kPairNoRunBeams (csm_box.hip)
+  int32_t max_n_used;
 };
 
 // Argmax partial: best score of a block and its flat candidate index.

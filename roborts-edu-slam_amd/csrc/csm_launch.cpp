@@ -578,6 +578,7 @@ int run_windows(csm_ctx* c, const csm_param& P, const Dims& D, const Geometry& G
     fill_scan_work(D, plans, pt_offsets, grid_index, sw, (size_t)w0, (size_t)w1, stride);
   LevelWork L = make_level_work(c, P, D, G, nr, use_int);
   L.blocks_per_scan = box_tiled ? D.n_angles : (int32_t)bps;  // per (window, tile) when tiled
+  L.max_n_used = max_beams;
   L.tile_n = box_tiled ? tile_n : 0;
   if (box_pair) {
     L.pal_n = c->pal_n;

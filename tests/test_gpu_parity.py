@@ -402,18 +402,21 @@ def test_kernel_variants_agree(f1, grid_kind):
         c.close()
 
 
-def test_box_kernel_edge_beams(world2000):
+@pytest.mark.parametrize("thin", [1, 10])
+def test_box_kernel_edge_beams(world2000, thin):
     """v6 box kernel (one-cell window step) on its margin cases: beams whose
     (lx + x0) + 0.5 is an exact integer (points at the origin, window with
     x0 + 0.5 integral), beams off the grid's low edge (negative t, where the
     reference's truncation is not a floor) and past its high edges, and windows
     whose x0 + j crosses a power of two (inexact steps) -- all scores and the
-    argmax against the oracle and against the v4 row kernel."""
+    argmax against the oracle and against the v4 row kernel. thin = 10: every
+    10th beam plus the edge beams, 116 in all, the pair kernel's run-free
+    short-scan form (kPairNoRunBeams)."""
     import roborts_csm
     from roborts_csm.params import SIM_YAML_LEVELS
     w, b = world2000
     m = O.Map(w.grid, w.resolution, w.offset)
-    pts = b.points_cells[b.offsets[0]:b.offsets[1]]
+    pts = b.points_cells[b.offsets[0]:b.offsets[1]][::thin]
     extra = np.array([[0.0, 0.0], [0.0, 0.0], [1.0, -2.0], [-1500.0, 3.0], [2.0, -1500.0],
                       [900.0, 900.0], [-3000.0, -3000.0], [0.25, 0.0]])
     pts = np.ascontiguousarray(np.concatenate([pts, extra]))
