@@ -32,11 +32,11 @@ def _short(name: str) -> str:
             i = name.index(key) + len(key)
             ns, sq, best = [a.strip() for a in name[i:name.index(">", i)].split(",")][:3]
             return f"{key[:-1]}<{ns},{sq},{'best' if best == 'true' else 'all'}>"
-    for key in ("score_box_palette_kernel<", "score_box_pair_kernel<"):  # <int NS, bool BEST>: v10, v11
+    for key in ("score_box_palette_kernel<", "score_box_pair_kernel<"):  # <int NS, bool BEST[, bool NORUN]>: v10, v11
         if key in name:
             i = name.index(key) + len(key)
             args = [a.strip() for a in name[i:name.index(">", i)].split(",")]
-            return f"{key[:-1]}<{args[0]},{'best' if args[-1] == 'true' else 'all'}>"
+            return f"{key[:-1]}<{args[0]},{'best' if args[1] == 'true' else 'all'}>"
     key = "score_box_grouped_kernel<"
     if key in name:  # <int NS, bool BEST>: the v9 box kernel, accounted as score_box_kernel
         i = name.index(key) + len(key)
