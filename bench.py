@@ -1069,8 +1069,11 @@ def main():
         return
     # device kernels only (kernel_accounting: no sub-interval or host phase twice)
     dom, avg_ms, dom_info = dominant_kernel(stats, stats_value)
-    rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"],
-                  load_counters(args.counters_json), args.counters_json)
+    # a B = 109 run prices its launches with the B = 109 counters (the kernels
+    # share names with the B = 1081 ones; the pair kernel even changes form)
+    cj = (args.counters_b109_json if args.levels == "sim" and args.counters_json == COUNTERS_JSON
+          else args.counters_json)
+    rl = roofline(dom["name"], avg_ms, dom["algorithmic_bytes"] / dom["launches"], load_counters(cj), cj)
     rl["launch_time"] = dict(dom_info, source="HIP events on the kernel stream around each one-dispatch "
                                               "launch of the dominant kernel in the timed steps")
     acct = {"breakdown": breakdown_note(el_all, args.steps), **kernel_accounting(stats, el_all, args.steps)}
