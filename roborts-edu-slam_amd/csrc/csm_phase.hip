@@ -74,7 +74,13 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));
 // beam's 5 rows are 160 contiguous bytes of one strip instead of 5 rows of the
 // row-major grid, so a load instruction's lanes touch about half the 64-byte
 // segments (the texture-address unit's cost per instruction follows them).
-template <int NS, int C, int NQ, bool BEST, bool ST>
+// KCH: 64-beam chunks classified per segment, all in flight at once. kChunks
+// (a 576-beam segment) for full scans; 2 for short ones (levels of <= 128
+// beams, kPhaseShortBeams: the reference's default every-10th-beam rule), which
+// would otherwise load and classify seven dead chunks per wave.
+constexpr int kPhaseShortBeams = 128;
+
+template <int NS, int C, int NQ, bool BEST, bool ST, int KCH = kChunks>
 __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelWork L, PhaseTable T,
                                                          const ScanWork* __restrict__ scans,
                                                          const double2* __restrict__ pts,
@@ -89,7 +95,7 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
   static_assert(LPS <= 64 && NP <= 64 && NS <= kPhaseMaxSpace && NQ <= kPhaseMaxBuckets, "layout");
   static_assert(2 * NP + 1 < 256, "group tags are bytes");
   // padded lists, whole kD blocks of groups and two blocks of issue-ahead slack
-  constexpr int kList = kSeg + NP * (SL - 1) + 3 * SL * kD + 64;
+  constexpr int kList = 64 * KCH + NP * (SL - 1) + 3 * SL * kD + 64;  // a segment is 64 * KCH beams
   constexpr int kMaxGroups = kList / SL + 1;
   __shared__ int32_t list[kList];
   __shared__ int32_t cursor[NP];
@@ -226,18 +232,19 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
   const int lane_cell = cv * C + 4 * ch;  // this lane's first box cell in a pair's sums
 
   uint64_t slow = 0;  // bit c: 64-beam chunk c holds a rejected beam (bit 63: some chunk >= 63)
-  for (int s0 = 0; s0 < n_used; s0 += kSeg) {
-    const int s1 = min(n_used, s0 + kSeg);
+  static_assert(KCH >= 1 && KCH <= kChunks, "segments of at most kSeg beams");
+  for (int s0 = 0; s0 < n_used; s0 += 64 * KCH) {
+    const int s1 = min(n_used, s0 + 64 * KCH);
     // 1a. every point of the segment in flight at once, then classify into
     // registers (offset, pair) and count per pair
-    double2 pq[kChunks];
+    double2 pq[KCH];
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u) pq[u] = point(s0 + 64 * u + lane);
+    for (int u = 0; u < KCH; ++u) pq[u] = point(s0 + 64 * u + lane);
     if (lane < NP) cursor[lane] = 0;
     __syncthreads();
-    int offr[kChunks], pairr[kChunks];
+    int offr[KCH], pairr[KCH];
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u) {
+    for (int u = 0; u < KCH; ++u) {
       const int cb = s0 + 64 * u;
       double lx, ly;
       bool rej;
@@ -278,7 +285,7 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
     __syncthreads();
     // 1c. scatter box corners into their pair's list
 #pragma unroll
-    for (int u = 0; u < kChunks; ++u)
+    for (int u = 0; u < KCH; ++u)
       if (pairr[u] >= 0) list[atomicAdd(&cursor[pairr[u]], 1)] = offr[u];
     __syncthreads();
     // 2. gather: group g = list entries g*SL .. g*SL + SL - 1 (slot s takes
@@ -436,16 +443,24 @@ __global__ __launch_bounds__(64, CSM_PHASE_WAVES) void score_phase_kernel(LevelW
   }
 }
 
+template <int NS, int C, int NQ, bool ST, int KCH>
+hipError_t launch_phase_k(const LevelWork& L, const PhaseTable& T, const ScanWork* s, const double2* p,
+                          const AngleEntry* an, double* out, BestPartial* part, unsigned nblk, hipStream_t stream) {
+  if (part)
+    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, true, ST, KCH>), dim3(nblk), dim3(64), 0, stream, L, T, s, p,
+                       an, out, part);
+  else
+    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, false, ST, KCH>), dim3(nblk), dim3(64), 0, stream, L, T, s, p,
+                       an, out, part);
+  return hipGetLastError();
+}
+
 template <int NS, int C, int NQ, bool ST>
 hipError_t launch_phase(const LevelWork& L, const PhaseTable& T, const ScanWork* s, const double2* p,
                         const AngleEntry* an, double* out, BestPartial* part, unsigned nblk, hipStream_t stream) {
-  if (part)
-    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, true, ST>), dim3(nblk), dim3(64), 0, stream, L, T, s, p, an,
-                       out, part);
-  else
-    hipLaunchKernelGGL((score_phase_kernel<NS, C, NQ, false, ST>), dim3(nblk), dim3(64), 0, stream, L, T, s, p, an,
-                       out, part);
-  return hipGetLastError();
+  if (L.max_n_used > 0 && L.max_n_used <= kPhaseShortBeams)
+    return launch_phase_k<NS, C, NQ, ST, kPhaseShortBeams / 64>(L, T, s, p, an, out, part, nblk, stream);
+  return launch_phase_k<NS, C, NQ, ST, kChunks>(L, T, s, p, an, out, part, nblk, stream);
 }
 
 }  // namespace

@@ -820,8 +820,8 @@ def test_dead_covariance_lists_skipped_exactly(world2000, order, use_fine):
             c.close()
 
 
-@pytest.mark.parametrize("margin_log2", [None, "5"])
-def test_phase_kernel_edge_beams(world2000, margin_log2):
+@pytest.mark.parametrize("margin_log2,thin", [(None, 1), ("5", 1), (None, 10), ("5", 10)])
+def test_phase_kernel_edge_beams(world2000, margin_log2, thin):
     """v7 phase kernel (sub-cell window step) on its margin cases: beams whose
     phase sits on or near a bucket edge (origin points with window phases at
     the breakpoints 0, 0.2, 0.4, ...), beams off the grid's low edge (negative
@@ -829,12 +829,14 @@ def test_phase_kernel_edge_beams(world2000, margin_log2):
     2^-20 margin and with a 1/32 margin that sends ~half the beams down the exact
     path. All scores and the argmax against the oracle and the v4 row kernel;
     the phase kernel over the strip copies of gridi (default) and over gridi
-    itself (CSM_PHASE_STRIPS=0)."""
+    itself (CSM_PHASE_STRIPS=0). thin = 10: every 10th beam plus the edge
+    beams, 119 in all: the short-scan form (kPhaseShortBeams, two chunks a
+    segment)."""
     import roborts_csm
     from roborts_csm.params import SIM_YAML_LEVELS
     w, b = world2000
     m = O.Map(w.grid, w.resolution, w.offset)
-    pts = b.points_cells[b.offsets[0]:b.offsets[1]]
+    pts = b.points_cells[b.offsets[0]:b.offsets[1]][::thin]
     extra = np.array([[0.0, 0.0], [0.0, 0.0], [1.0, -2.0], [-1500.0, 3.0], [2.0, -1500.0],
                       [900.0, 900.0], [-3000.0, -3000.0], [0.25, 0.0], [0.2, 0.6], [-0.4, 0.8]])
     pts = np.ascontiguousarray(np.concatenate([pts, extra]))
